@@ -1,0 +1,118 @@
+/*
+ * neo_hip.h — C-ABI drop-in boundary of the MI355X (gfx950) FFT + UPOLS hot path.
+ *
+ * libneo_hip.so exports exactly these symbols. Plain pointers, sizes and int
+ * status codes only (no HIP / torch / C++ types in the signatures), so the
+ * reference's C++ headers (include/neo/fft.hpp, include/neo/convolution.hpp in
+ * this repo), its pybind11 module or any FFI can bind them.
+ *
+ * Conventions shared with the reference (paths relative to neo-dsp's tree):
+ *   - complex data is interleaved float {re, im} = std::complex<float>
+ *     (src/neo/complex/scalar_complex.hpp:14-114);
+ *   - direction: -1 = forward e^{-2 pi i nk/N}, +1 = backward
+ *     (src/neo/fft/direction.hpp:8-12); transforms are UNNORMALIZED
+ *     (src/neo/fft/reference/c2c_dit2_plan.hpp:81-95);
+ *   - r2c writes N/2+1 bins; c2r reads N/2+1 bins, ignores the imaginary parts of
+ *     the DC and Nyquist bins and does not scale
+ *     (src/neo/fft/fallback/fallback_rfft_plan.hpp:27-55);
+ *   - UPOLS filters are uniform_partition's [C][P][B+1] layout
+ *     (src/neo/convolution/uniform_partition.hpp:12-26).
+ * Every function returns NEO_HIP_OK (0) or a nonzero status; neo_hip_last_error()
+ * then holds a message (thread-local). Construction errors map to the
+ * reference's std::runtime_error (c2c_dit2_plan.hpp:97-104).
+ */
+#ifndef NEO_HIP_H
+#define NEO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define NEO_HIP_API __attribute__((visibility("default")))
+#else
+#define NEO_HIP_API
+#endif
+
+enum neo_hip_status {
+    NEO_HIP_OK = 0,
+    NEO_HIP_EINVAL = 1,   /* bad argument (order > max_order, null pointer, shape) */
+    NEO_HIP_ERUNTIME = 2, /* HIP runtime / kernel failure */
+    NEO_HIP_ENOMEM = 3,   /* device allocation failed */
+    NEO_HIP_ENODEV = 4    /* no such GPU */
+};
+
+enum neo_hip_fft_kind { NEO_HIP_C2C = 0, NEO_HIP_R2C = 1, NEO_HIP_C2R = 2 };
+
+typedef struct neo_hip_fft_plan neo_hip_fft_plan;
+typedef struct neo_hip_upols neo_hip_upols;
+
+/* -- library ------------------------------------------------------------ */
+NEO_HIP_API const char* neo_hip_last_error(void);
+NEO_HIP_API int neo_hip_version(void);
+NEO_HIP_API int neo_hip_device_count(int* count);
+
+/* -- FFT plans ------------------------------------------------------------
+ * Replaces fft_plan<complex<float>> = c2c_dit2_plan (src/neo/fft/fft.hpp:36-52,
+ * c2c_dit2_plan.hpp:21-104) and rfft_plan<float> = fallback_rfft_plan
+ * (src/neo/fft/rfft.hpp:15-23, fallback_rfft_plan.hpp:14-61), batched.
+ * max order 27 (c2c_dit2_plan.hpp:58-61); order > 27 -> NEO_HIP_EINVAL. */
+NEO_HIP_API int neo_hip_fft_max_order(void);
+NEO_HIP_API int neo_hip_fft_plan_create(int order, int64_t batch, int kind, int device, neo_hip_fft_plan** plan);
+NEO_HIP_API int neo_hip_fft_plan_destroy(neo_hip_fft_plan* plan);
+/* Device pointers, asynchronous on `stream` (hipStream_t, NULL = the plan's
+ * own stream). c2c: in/out [batch][N] complex (in == out allowed).
+ * r2c: in [batch][N] float, out [batch][N/2+1] complex.
+ * c2r: in [batch][N/2+1] complex, out [batch][N] float. `direction` is used by
+ * c2c only (r2c is forward, c2r backward, as in fallback_rfft_plan). */
+NEO_HIP_API int neo_hip_fft_execute(neo_hip_fft_plan* plan, const void* in, void* out, int direction, void* stream);
+/* Host pointers, synchronous (staging through the plan's device buffers). */
+NEO_HIP_API int neo_hip_fft_execute_host(neo_hip_fft_plan* plan, const void* in, void* out, int direction);
+
+/* -- UPOLS convolver --------------------------------------------------------
+ * Replaces C instances of upols_convolver<complex<float>> (one per channel,
+ * src/neo/convolution/dense_convolver.hpp:19-20;
+ * uniform_partitioned_convolver.hpp:13-65; overlap_save.hpp:84-112;
+ * fdl_index.hpp:23-36) as driven by dense_convolve / DenseConvolution
+ * (extra/plugin/src/dsp/DenseConvolution.hpp:35,39-70). `block` = B must be a
+ * power of two in [16, 4096]; output block t corresponds to input block t
+ * (zero latency). Channels are independent. */
+NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, int device, neo_hip_upols** h);
+NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h);
+/* filter [C][P][B+1] complex (uniform_partition layout), host or device memory;
+ * like uniform_partitioned_convolver::filter() it also resets all state. */
+NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, int is_device);
+/* normalize_impulse + uniform_partition of ir [C][L] float straight into the
+ * convolver (setup path, DenseConvolution.cpp:78-108); host or device memory. */
+NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int64_t length, int normalize, int is_device);
+/* one block for all channels, in place: io [C][B] float (host: synchronous). */
+NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_device, void* stream);
+/* one block, device pointers, channel c at in + c*ld_in / out + c*ld_out
+ * (in == out allowed); asynchronous on `stream`. */
+NEO_HIP_API int neo_hip_upols_process_device(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
+                                             int64_t ld_out, void* stream);
+/* nblocks consecutive blocks: channel c samples at in + c*ld + t*B. */
+NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, float* out, int64_t ld,
+                                             int64_t nblocks, void* stream);
+NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
+/* MAC-kernel timing with HIP events recorded on the launch stream (for the
+ * roofline in bench.py): enable, then read the accumulated ms / launch count. */
+NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable);
+NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches);
+NEO_HIP_API int neo_hip_upols_info(neo_hip_upols* h, int* channels, int* block, int* partitions, int* splits);
+
+/* -- setup path (uniform_partition.hpp:12-26, normalize_impulse.hpp:11-33) -- */
+NEO_HIP_API int neo_hip_num_partitions(int64_t length, int block, int64_t* partitions);
+/* ir [C][L] float -> out [C][P][B+1] complex; host or device pointers. */
+NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t length, int block, void* out,
+                                          int is_device, int device);
+/* in place on ir [C][L]: scale all channels by min_c 1/sqrt(sum ir[c]^2). */
+NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t length, int is_device, int device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NEO_HIP_H */

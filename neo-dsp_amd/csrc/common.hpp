@@ -1,0 +1,95 @@
+// common.hpp — host-side plumbing shared by the neo_hip C-ABI translation units:
+// the thread-local last-error latch, HIP status checks and twiddle tables.
+#pragma once
+
+#include "../../include/neo_hip.h"
+#include "fft_device.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+namespace neo_hip {
+
+std::string& last_error_slot();
+
+inline int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    last_error_slot() = buf;
+    return code;
+}
+
+#define NEO_HIP_CHECK(expr)                                                                          \
+    do {                                                                                             \
+        hipError_t _e = (expr);                                                                      \
+        if (_e != hipSuccess)                                                                        \
+            return ::neo_hip::fail(NEO_HIP_ERUNTIME, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                                   __FILE__, __LINE__);                                              \
+    } while (0)
+
+// Kernel launches: check the launch status immediately (catches bad configs).
+#define NEO_HIP_LAUNCH_CHECK() NEO_HIP_CHECK(hipGetLastError())
+
+// Scoped hipSetDevice that restores the caller's device.
+struct device_guard {
+    int prev = -1;
+    int rc = NEO_HIP_OK;
+    explicit device_guard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) {
+            if (hipSetDevice(dev) != hipSuccess) rc = fail(NEO_HIP_ENODEV, "hipSetDevice(%d) failed", dev);
+        }
+    }
+    ~device_guard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// Two-level forward twiddle table for an FFT of size n (see twiddle<> in
+// fft_device.hpp): [0,64) = W^e, [64, 64+n/64) = W^(64h), W = exp(-2*pi*i/n),
+// computed in double and rounded once to float.
+inline std::vector<cf> make_twiddle_table(int64_t n)
+{
+    const int64_t lo = 64, hi = n <= 64 ? 0 : n / 64;
+    std::vector<cf> t(static_cast<size_t>(lo + hi));
+    for (int64_t e = 0; e < lo; ++e) {
+        const double a = -2.0 * M_PI * double(e % (n > 0 ? n : 1)) / double(n > 0 ? n : 1);
+        t[size_t(e)] = {float(std::cos(a)), float(std::sin(a))};
+    }
+    for (int64_t h = 0; h < hi; ++h) {
+        const double a = -2.0 * M_PI * double(64 * h) / double(n);
+        t[size_t(lo + h)] = {float(std::cos(a)), float(std::sin(a))};
+    }
+    return t;
+}
+
+// Split table for the global-memory passes of large transforms: e = hi*2^lo_bits + lo.
+inline std::vector<cf> make_split_table(int order, int lo_bits)
+{
+    const int64_t n = int64_t(1) << order, nlo = int64_t(1) << lo_bits, nhi = n >> lo_bits;
+    std::vector<cf> t(static_cast<size_t>(nlo + nhi));
+    for (int64_t e = 0; e < nlo; ++e) {
+        const double a = -2.0 * M_PI * double(e) / double(n);
+        t[size_t(e)] = {float(std::cos(a)), float(std::sin(a))};
+    }
+    for (int64_t h = 0; h < nhi; ++h) {
+        const double a = -2.0 * M_PI * double(h * nlo) / double(n);
+        t[size_t(nlo + h)] = {float(std::cos(a)), float(std::sin(a))};
+    }
+    return t;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace neo_hip

@@ -1,0 +1,495 @@
+// fft.hip — batched c2c / r2c / c2r FFT plans for MI355X (gfx950), C-ABI part.
+//
+// Replaces neo's fft_plan (c2c_dit2_plan, src/neo/fft/reference/c2c_dit2_plan.hpp:21-104)
+// and rfft_plan (fallback_rfft_plan, src/neo/fft/fallback/fallback_rfft_plan.hpp:14-61).
+//
+// Sizes N <= 4096 (c2c) / N <= 8192 (real): one kernel, one pass over HBM — each
+// workgroup loads whole transforms into registers (lane t owns t + m*T, coalesced),
+// runs the Stockham passes through LDS and stores the natural-order result.
+// Larger sizes: global-memory Stockham radix-16 passes (ping-pong scratch).
+#include "common.hpp"
+#include "fft_device_real.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+
+namespace neo_hip {
+
+constexpr int kMaxOrder = 27;   // c2c_dit2_plan.hpp:58-61
+constexpr int kLdsMaxOrder = 12;  // N <= 4096 complex points per LDS transform
+
+__host__ __device__ constexpr int pick_e(int n) { return n >= 16 ? 16 : (n < 1 ? 1 : n); }
+
+// ---------------------------------------------------------------------------
+// c2c, whole transforms in LDS. FPB transforms per 256-lane block for small N.
+// ---------------------------------------------------------------------------
+template<int N, int DIR>
+__global__ __launch_bounds__(256) void k_c2c_lds(const cf* __restrict__ in, cf* __restrict__ out,
+                                                 const cf* __restrict__ twg, int64_t batch)
+{
+    constexpr int E = pick_e(N), T = N / E, FPB = T >= 256 ? 1 : 256 / T;
+    constexpr int TWL = twiddle_len<N>(), LL = lds_len(N);
+    __shared__ cf smem[FPB * LL + TWL];
+    cf* tw = smem + FPB * LL;
+    const int tid = threadIdx.x, f = tid / T, t = tid % T;
+    for (int i = tid; i < TWL; i += FPB * T) tw[i] = twg[i];
+    const int64_t g = int64_t(blockIdx.x) * FPB + f;
+    const bool active = g < batch;
+    cf v[E];
+    if (active) {
+        const cf* src = in + g * N;
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = src[t + m * T];
+    }
+    __syncthreads();
+    stockham<N, E, DIR>(v, smem + f * LL, tw, t, active);
+    if (active) {
+        cf* dst = out + g * N;
+#pragma unroll
+        for (int m = 0; m < E; ++m) dst[t + m * T] = v[m];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// r2c / c2r of N = 2M reals, whole transforms in LDS (unpacked N/2+1 bins).
+// ---------------------------------------------------------------------------
+template<int M>
+__global__ __launch_bounds__(256) void k_r2c_lds(const float* __restrict__ in, cf* __restrict__ out,
+                                                 const cf* __restrict__ twg, int64_t batch)
+{
+    constexpr int E = pick_e(M), T = M / E, FPB = T >= 256 ? 1 : 256 / T;
+    constexpr int TW1 = twiddle_len<M>(), TW2 = twiddle_len<2 * M>(), LL = lds_len(M);
+    __shared__ cf smem[FPB * LL + TW1 + TW2];
+    cf* tw1 = smem + FPB * LL;
+    cf* tw2 = tw1 + TW1;
+    const int tid = threadIdx.x, f = tid / T, t = tid % T;
+    for (int i = tid; i < TW1 + TW2; i += FPB * T) tw1[i] = twg[i];
+    const int64_t g = int64_t(blockIdx.x) * FPB + f;
+    const bool active = g < batch;
+    cf* lds = smem + f * LL;
+    cf v[E];
+    if (active) {
+        const cf* src = reinterpret_cast<const cf*>(in + g * 2 * M);  // z[n] = x[2n] + i x[2n+1]
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = src[t + m * T];
+    }
+    __syncthreads();
+    stockham<M, E, -1>(v, lds, tw1, t, active);
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) lds[lpad(t + m * T)] = v[m];
+    }
+    __syncthreads();
+    if (active) {
+        cf* dst = out + g * (M + 1);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int k = t + m * T;
+            const cf x = r2c_split<M>(lds, tw2, k);
+            if (k == 0) {
+                dst[0] = {x.x, 0.0f};
+                dst[M] = {x.y, 0.0f};
+            } else {
+                dst[k] = x;
+            }
+        }
+    }
+}
+
+template<int M>
+__global__ __launch_bounds__(256) void k_c2r_lds(const cf* __restrict__ in, float* __restrict__ out,
+                                                 const cf* __restrict__ twg, int64_t batch)
+{
+    constexpr int E = pick_e(M), T = M / E, FPB = T >= 256 ? 1 : 256 / T;
+    constexpr int TW1 = twiddle_len<M>(), TW2 = twiddle_len<2 * M>(), LL = lds_len(M + 1);
+    __shared__ cf smem[FPB * LL + TW1 + TW2];
+    cf* tw1 = smem + FPB * LL;
+    cf* tw2 = tw1 + TW1;
+    const int tid = threadIdx.x, f = tid / T, t = tid % T;
+    for (int i = tid; i < TW1 + TW2; i += FPB * T) tw1[i] = twg[i];
+    const int64_t g = int64_t(blockIdx.x) * FPB + f;
+    const bool active = g < batch;
+    cf* lds = smem + f * LL;
+    if (active) {
+        const cf* src = in + g * (M + 1);
+        for (int k = t; k <= M; k += T) lds[lpad(k)] = src[k];
+    }
+    __syncthreads();
+    cf v[E];
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int k = t + m * T;
+            v[m] = c2r_join<M>(lds[lpad(k)], lds[lpad(k == 0 ? M : M - k)], tw2, k);
+        }
+    }
+    __syncthreads();
+    stockham<M, E, +1>(v, lds, tw1, t, active);
+    if (active) {
+        cf* dst = reinterpret_cast<cf*>(out + g * 2 * M);
+#pragma unroll
+        for (int m = 0; m < E; ++m) dst[t + m * T] = v[m];
+    }
+}
+
+// order-0 real transforms (N = 1): X[0] = x[0]; x[0] = Re X[0]
+__global__ void k_r2c_order0(const float* in, cf* out, int64_t batch)
+{
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < batch) out[i] = {in[i], 0.0f};
+}
+__global__ void k_c2r_order0(const cf* in, float* out, int64_t batch)
+{
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < batch) out[i] = in[i].x;
+}
+
+// ---------------------------------------------------------------------------
+// Large transforms: one global-memory Stockham pass of radix R.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ cf split_twiddle(const cf* tw, int lo_bits, int64_t e)
+{
+    const int64_t mask = (int64_t(1) << lo_bits) - 1;
+    return cmul(tw[(int64_t(1) << lo_bits) + (e >> lo_bits)], tw[e & mask]);
+}
+
+template<int R, int DIR>
+__global__ __launch_bounds__(256) void k_pass(const cf* __restrict__ in, cf* __restrict__ out,
+                                              const cf* __restrict__ tw, int lo_bits, int64_t n, int64_t ns,
+                                              int64_t total)
+{
+    const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (gid >= total) return;
+    const int64_t nb = n / R;
+    const int64_t b = gid / nb, j = gid - b * nb;
+    in += b * n;
+    out += b * n;
+    cf v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
+    const int64_t jm = j & (ns - 1);
+    if (ns > 1) {
+        const int64_t step = jm * (n / (ns * R));
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+            cf w = split_twiddle(tw, lo_bits, step * r);
+            if (DIR > 0) w.y = -w.y;
+            v[r] = cmul(v[r], w);
+        }
+    }
+    dft<R, DIR>(v);
+    const int64_t base = (j / ns) * ns * R + jm;
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[base + r * ns] = v[r];
+}
+
+// r2c split / c2r join for large sizes (global memory, one bin per lane).
+__global__ void k_r2c_split_global(const cf* __restrict__ z, cf* __restrict__ out, const cf* __restrict__ tw,
+                                   int lo_bits, int64_t m, int64_t batch)
+{
+    const int64_t gid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (gid >= batch * m) return;
+    const int64_t b = gid / m, k = gid - b * m;
+    const cf* zr = z + b * m;
+    cf* dst = out + b * (m + 1);
+    const cf zk = zr[k];
+    if (k == 0) {
+        dst[0] = {zk.x + zk.y, 0.0f};
+        dst[m] = {zk.x - zk.y, 0.0f};
+        return;
+    }
+    const cf zc = cconj(zr[m - k]);
+    const cf fe = cscale(cadd(zk, zc), 0.5f);
+    const cf d = csub(zk, zc);
+    const cf fo = {0.5f * d.y, -0.5f * d.x};
+    dst[k] = cadd(fe, cmul(split_twiddle(tw, lo_bits, k), fo));
+}
+
+__global__ void k_c2r_join_global(const cf* __restrict__ x, cf* __restrict__ z, const cf* __restrict__ tw,
+                                  int lo_bits, int64_t m, int64_t batch)
+{
+    const int64_t gid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (gid >= batch * m) return;
+    const int64_t b = gid / m, k = gid - b * m;
+    const cf* xr = x + b * (m + 1);
+    cf a, c;
+    if (k == 0) {
+        a = {xr[0].x, 0.0f};
+        c = {xr[m].x, 0.0f};
+    } else {
+        a = xr[k];
+        c = cconj(xr[m - k]);
+    }
+    cf w = split_twiddle(tw, lo_bits, k);
+    w.y = -w.y;
+    const cf fe = cadd(a, c);
+    const cf fo = cmul(csub(a, c), w);
+    z[b * m + k] = {fe.x - fo.y, fe.y + fo.x};
+}
+
+}  // namespace neo_hip
+
+using namespace neo_hip;
+
+struct neo_hip_fft_plan {
+    int order = 0, kind = 0, device = 0;
+    int64_t batch = 0, n = 0;
+    hipStream_t stream = nullptr;
+    cf* d_tw = nullptr;      // LDS path: table(n) [c2c] or table(M) ++ table(2M) [real]
+    cf* d_split = nullptr;   // large path: split table of the inner c2c size
+    int lo_bits = 0;
+    cf* d_split2 = nullptr;  // large real path: split table of size 2M (join/split twiddles)
+    int lo_bits2 = 0;
+    cf* d_scratch[3] = {nullptr, nullptr, nullptr};
+    void* d_in = nullptr;    // staging for neo_hip_fft_execute_host
+    void* d_out = nullptr;
+    size_t in_bytes = 0, out_bytes = 0;
+};
+
+namespace {
+
+using plan_t = neo_hip_fft_plan;
+
+// inner complex FFT order of a plan (c2c: order, real: order-1)
+int inner_order(const plan_t* p) { return p->kind == NEO_HIP_C2C ? p->order : p->order - 1; }
+
+template<int DIR>
+int launch_c2c_lds(int order, const cf* in, cf* out, const cf* tw, int64_t batch, hipStream_t s)
+{
+#define NEO_C2C_CASE(ORD)                                                                            \
+    case ORD: {                                                                                      \
+        constexpr int N = 1 << ORD, E = pick_e(N), T = N / E, FPB = T >= 256 ? 1 : 256 / T;          \
+        const int64_t blocks = (batch + FPB - 1) / FPB;                                              \
+        hipLaunchKernelGGL((k_c2c_lds<N, DIR>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s, in, out, tw, \
+                           batch);                                                                   \
+        break;                                                                                       \
+    }
+    switch (order) {
+        NEO_C2C_CASE(0) NEO_C2C_CASE(1) NEO_C2C_CASE(2) NEO_C2C_CASE(3) NEO_C2C_CASE(4) NEO_C2C_CASE(5)
+        NEO_C2C_CASE(6) NEO_C2C_CASE(7) NEO_C2C_CASE(8) NEO_C2C_CASE(9) NEO_C2C_CASE(10) NEO_C2C_CASE(11)
+        NEO_C2C_CASE(12)
+        default: return fail(NEO_HIP_EINVAL, "c2c lds: bad order %d", order);
+    }
+#undef NEO_C2C_CASE
+    NEO_HIP_LAUNCH_CHECK();
+    return NEO_HIP_OK;
+}
+
+int launch_real_lds(int kind, int m_order, const void* in, void* out, const cf* tw, int64_t batch, hipStream_t s)
+{
+#define NEO_REAL_CASE(ORD)                                                                            \
+    case ORD: {                                                                                       \
+        constexpr int M = 1 << ORD, E = pick_e(M), T = M / E, FPB = T >= 256 ? 1 : 256 / T;           \
+        const int64_t blocks = (batch + FPB - 1) / FPB;                                               \
+        if (kind == NEO_HIP_R2C)                                                                      \
+            hipLaunchKernelGGL((k_r2c_lds<M>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s,            \
+                               static_cast<const float*>(in), static_cast<cf*>(out), tw, batch);      \
+        else                                                                                          \
+            hipLaunchKernelGGL((k_c2r_lds<M>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s,            \
+                               static_cast<const cf*>(in), static_cast<float*>(out), tw, batch);      \
+        break;                                                                                        \
+    }
+    switch (m_order) {
+        NEO_REAL_CASE(0) NEO_REAL_CASE(1) NEO_REAL_CASE(2) NEO_REAL_CASE(3) NEO_REAL_CASE(4) NEO_REAL_CASE(5)
+        NEO_REAL_CASE(6) NEO_REAL_CASE(7) NEO_REAL_CASE(8) NEO_REAL_CASE(9) NEO_REAL_CASE(10)
+        NEO_REAL_CASE(11) NEO_REAL_CASE(12)
+        default: return fail(NEO_HIP_EINVAL, "real lds: bad order %d", m_order);
+    }
+#undef NEO_REAL_CASE
+    NEO_HIP_LAUNCH_CHECK();
+    return NEO_HIP_OK;
+}
+
+// Large c2c: radix-16 passes (remainder radix last), ping-pong through scratch
+// so that `in == out` is safe; the last pass writes `out`.
+int run_c2c_global(const plan_t* p, int order, const cf* in, cf* out, int dir, hipStream_t s)
+{
+    const int64_t n = int64_t(1) << order;
+    std::vector<int> radix;
+    for (int rem = order; rem > 0;) {
+        const int r = rem >= 4 ? 4 : rem;
+        radix.push_back(1 << r);
+        rem -= r;
+    }
+    const int K = int(radix.size());
+    const cf* src = in;
+    int64_t ns = 1;
+    for (int i = 0; i < K; ++i) {
+        cf* dst = (i == K - 1) ? out : p->d_scratch[i & 1];
+        const int R = radix[size_t(i)];
+        const int64_t total = p->batch * (n / R);
+        const unsigned blocks = unsigned((total + 255) / 256);
+#define NEO_PASS(RR)                                                                                     \
+    if (dir < 0)                                                                                         \
+        hipLaunchKernelGGL((k_pass<RR, -1>), dim3(blocks), dim3(256), 0, s, src, dst, p->d_split, p->lo_bits, \
+                           n, ns, total);                                                                \
+    else                                                                                                 \
+        hipLaunchKernelGGL((k_pass<RR, +1>), dim3(blocks), dim3(256), 0, s, src, dst, p->d_split, p->lo_bits, \
+                           n, ns, total);
+        switch (R) {
+            case 16: NEO_PASS(16) break;
+            case 8: NEO_PASS(8) break;
+            case 4: NEO_PASS(4) break;
+            case 2: NEO_PASS(2) break;
+            default: return fail(NEO_HIP_ERUNTIME, "bad radix");
+        }
+#undef NEO_PASS
+        NEO_HIP_LAUNCH_CHECK();
+        src = dst;
+        ns *= R;
+    }
+    return NEO_HIP_OK;
+}
+
+int upload(cf** dst, const std::vector<cf>& v)
+{
+    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dst), v.size() * sizeof(cf)));
+    NEO_HIP_CHECK(hipMemcpy(*dst, v.data(), v.size() * sizeof(cf), hipMemcpyHostToDevice));
+    return NEO_HIP_OK;
+}
+
+void free_plan(plan_t* p)
+{
+    if (!p) return;
+    (void)hipFree(p->d_tw);
+    (void)hipFree(p->d_split);
+    (void)hipFree(p->d_split2);
+    for (auto* s : p->d_scratch) (void)hipFree(s);
+    (void)hipFree(p->d_in);
+    (void)hipFree(p->d_out);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+}  // namespace
+
+extern "C" {
+
+NEO_HIP_API int neo_hip_fft_max_order(void) { return kMaxOrder; }
+
+NEO_HIP_API int neo_hip_fft_plan_create(int order, int64_t batch, int kind, int device, neo_hip_fft_plan** out)
+{
+    if (!out) return fail(NEO_HIP_EINVAL, "plan pointer is null");
+    *out = nullptr;
+    if (order < 0 || order > kMaxOrder)
+        return fail(NEO_HIP_EINVAL, "unsupported order '%d' (max_order %d)", order, kMaxOrder);
+    if (batch < 1) return fail(NEO_HIP_EINVAL, "batch must be >= 1");
+    if (kind != NEO_HIP_C2C && kind != NEO_HIP_R2C && kind != NEO_HIP_C2R)
+        return fail(NEO_HIP_EINVAL, "bad fft kind %d", kind);
+    device_guard g(device);
+    if (g.rc) return g.rc;
+    auto* p = new plan_t{};
+    p->order = order;
+    p->kind = kind;
+    p->batch = batch;
+    p->n = int64_t(1) << order;
+    (void)hipGetDevice(&p->device);
+    int rc = NEO_HIP_OK;
+    auto bail = [&](int code) {
+        free_plan(p);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
+    const int io = inner_order(p);
+    if (io >= 0 && io <= kLdsMaxOrder) {
+        std::vector<cf> t = make_twiddle_table(int64_t(1) << io);
+        if (kind != NEO_HIP_C2C) {
+            std::vector<cf> t2 = make_twiddle_table(int64_t(2) << io);
+            t.insert(t.end(), t2.begin(), t2.end());
+        }
+        if ((rc = upload(&p->d_tw, t))) return bail(rc);
+    } else if (io > kLdsMaxOrder) {
+        p->lo_bits = (io + 1) / 2;
+        if ((rc = upload(&p->d_split, make_split_table(io, p->lo_bits)))) return bail(rc);
+        const int64_t inner = int64_t(1) << io;
+        const int nscratch = kind == NEO_HIP_C2C ? 2 : 3;
+        for (int i = 0; i < nscratch; ++i)
+            if (hipMalloc(reinterpret_cast<void**>(&p->d_scratch[i]), size_t(inner * batch) * sizeof(cf)) != hipSuccess)
+                return bail(fail(NEO_HIP_ENOMEM, "scratch allocation failed"));
+        if (kind != NEO_HIP_C2C) {
+            p->lo_bits2 = (io + 2) / 2;
+            if ((rc = upload(&p->d_split2, make_split_table(io + 1, p->lo_bits2)))) return bail(rc);
+        }
+    }
+    const size_t cbytes = size_t(p->n) * sizeof(cf), rbytes = size_t(p->n) * sizeof(float);
+    const size_t hbytes = size_t(p->n / 2 + 1) * sizeof(cf);
+    p->in_bytes = size_t(batch) * (kind == NEO_HIP_C2C ? cbytes : kind == NEO_HIP_R2C ? rbytes : hbytes);
+    p->out_bytes = size_t(batch) * (kind == NEO_HIP_C2C ? cbytes : kind == NEO_HIP_R2C ? hbytes : rbytes);
+    *out = p;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_fft_plan_destroy(neo_hip_fft_plan* p)
+{
+    if (!p) return NEO_HIP_OK;
+    device_guard g(p->device);
+    free_plan(p);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_fft_execute(neo_hip_fft_plan* p, const void* in, void* out, int direction, void* stream)
+{
+    if (!p || !in || !out) return fail(NEO_HIP_EINVAL, "null plan or buffer");
+    if (p->kind == NEO_HIP_C2C && direction != -1 && direction != 1)
+        return fail(NEO_HIP_EINVAL, "direction must be -1 (forward) or +1 (backward)");
+    device_guard g(p->device);
+    if (g.rc) return g.rc;
+    hipStream_t s = stream ? as_stream(stream) : p->stream;
+    const int io = inner_order(p);
+    if (p->kind == NEO_HIP_C2C) {
+        const cf* ci = static_cast<const cf*>(in);
+        cf* co = static_cast<cf*>(out);
+        if (io <= kLdsMaxOrder)
+            return direction < 0 ? launch_c2c_lds<-1>(io, ci, co, p->d_tw, p->batch, s)
+                                 : launch_c2c_lds<+1>(io, ci, co, p->d_tw, p->batch, s);
+        return run_c2c_global(p, io, ci, co, direction, s);
+    }
+    if (io < 0) {  // order 0 real transform
+        const unsigned blocks = unsigned((p->batch + 255) / 256);
+        if (p->kind == NEO_HIP_R2C)
+            hipLaunchKernelGGL(k_r2c_order0, dim3(blocks), dim3(256), 0, s, static_cast<const float*>(in),
+                               static_cast<cf*>(out), p->batch);
+        else
+            hipLaunchKernelGGL(k_c2r_order0, dim3(blocks), dim3(256), 0, s, static_cast<const cf*>(in),
+                               static_cast<float*>(out), p->batch);
+        NEO_HIP_LAUNCH_CHECK();
+        return NEO_HIP_OK;
+    }
+    if (io <= kLdsMaxOrder) return launch_real_lds(p->kind, io, in, out, p->d_tw, p->batch, s);
+    const int64_t m = int64_t(1) << io, total = m * p->batch;
+    const unsigned blocks = unsigned((total + 255) / 256);
+    cf* z = p->d_scratch[2];
+    if (p->kind == NEO_HIP_R2C) {
+        int rc = run_c2c_global(p, io, static_cast<const cf*>(in), z, -1, s);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_r2c_split_global, dim3(blocks), dim3(256), 0, s, z, static_cast<cf*>(out), p->d_split2,
+                           p->lo_bits2, m, p->batch);
+        NEO_HIP_LAUNCH_CHECK();
+        return NEO_HIP_OK;
+    }
+    hipLaunchKernelGGL(k_c2r_join_global, dim3(blocks), dim3(256), 0, s, static_cast<const cf*>(in), z, p->d_split2,
+                       p->lo_bits2, m, p->batch);
+    NEO_HIP_LAUNCH_CHECK();
+    return run_c2c_global(p, io, z, static_cast<cf*>(out), +1, s);
+}
+
+NEO_HIP_API int neo_hip_fft_execute_host(neo_hip_fft_plan* p, const void* in, void* out, int direction)
+{
+    if (!p || !in || !out) return fail(NEO_HIP_EINVAL, "null plan or buffer");
+    device_guard g(p->device);
+    if (g.rc) return g.rc;
+    if (!p->d_in) {
+        NEO_HIP_CHECK(hipMalloc(&p->d_in, p->in_bytes));
+        NEO_HIP_CHECK(hipMalloc(&p->d_out, p->out_bytes));
+    }
+    NEO_HIP_CHECK(hipMemcpyAsync(p->d_in, in, p->in_bytes, hipMemcpyHostToDevice, p->stream));
+    int rc = neo_hip_fft_execute(p, p->d_in, p->d_out, direction, p->stream);
+    if (rc) return rc;
+    NEO_HIP_CHECK(hipMemcpyAsync(out, p->d_out, p->out_bytes, hipMemcpyDeviceToHost, p->stream));
+    NEO_HIP_CHECK(hipStreamSynchronize(p->stream));
+    return NEO_HIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,759 @@
+// upols.hip — multichannel uniformly-partitioned overlap-save convolution on MI355X.
+//
+// Replaces C instances of neo's upols_convolver<complex<float>>
+// (src/neo/convolution/dense_convolver.hpp:19-20) stepped by dense_convolve /
+// DenseConvolution (extra/plugin/src/dsp/DenseConvolution.hpp:39-70). One block
+// step for all channels is two kernels:
+//
+//   k_upols_mac  grid C x S. Workgroup (c, s) accumulates filter partitions
+//                p in [p0, p1) of channel c:  acc[k] += H[c][p][k] * FDL[c][(w-p) mod P][k]
+//                (fdl_index.hpp:23-36 ring order; dense_filter.hpp:30-35 MAC).
+//                The s == 0 workgroup first runs the overlap-save r2c of
+//                [previous block | new block] (overlap_save.hpp:90-103) as a packed
+//                B-point complex FFT in LDS, inserts it as FDL row w
+//                (dense_fdl.hpp:27-30) and uses it for p = 0 straight from LDS.
+//                Streams 16 B per bin per partition from HBM: the roofline kernel.
+//   k_upols_out  grid C. Sums the S partial spectra (fixed order), runs the c2r
+//                (fallback_rfft_plan.hpp:38-55) as a packed inverse FFT in LDS,
+//                scales by 1/2B and writes the last B samples (overlap_save.hpp:104-111).
+//
+// Device layout (HBM), all packed rows of B complex with bin 0 = {DC, Nyquist}
+// (both purely real for real signals, so the fold is exact):
+//   H    [C][P][B]   filter partitions (uniform_partition.hpp layout, packed)
+//   FDL  [C][P][B]   frequency-domain delay line (ring, write position w)
+//   prev [C][B]      previous input block (first half of the overlap-save window)
+//   part [C][S][B]   per-split partial spectra
+#include "common.hpp"
+#include "fft_device_real.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace neo_hip {
+
+__host__ __device__ constexpr int upols_e(int b) { return b >= 16 ? 16 : b; }
+
+template<int B>
+struct upols_cfg {
+    static constexpr int E = upols_e(B);                 // FFT elements per lane
+    static constexpr int T = B / E;                      // FFT lanes
+    static constexpr int Q = B / 2;                      // float4 (2 bins) per row
+    static constexpr int QT = Q < 256 ? Q : 256;         // lanes per row group
+    static constexpr int RPI = 256 / QT;                 // rows in flight per iteration
+    static constexpr int VPT = Q / QT;                   // float4 per lane per row
+    static constexpr int U = VPT >= 4 ? 1 : 4 / VPT;     // row unroll
+    static constexpr int TW1 = twiddle_len<B>();
+    static constexpr int TW2 = twiddle_len<2 * B>();
+    static constexpr int LL = lds_len(B);
+};
+
+struct acc4 {  // 4 partial products per bin keep the packed bin 0 exact
+    float rr, ii, ri, ir;
+};
+
+__device__ __forceinline__ void mac2(acc4& a0, acc4& a1, float4 h, float4 x)
+{
+    a0.rr = fmaf(h.x, x.x, a0.rr);
+    a0.ii = fmaf(h.y, x.y, a0.ii);
+    a0.ri = fmaf(h.x, x.y, a0.ri);
+    a0.ir = fmaf(h.y, x.x, a0.ir);
+    a1.rr = fmaf(h.z, x.z, a1.rr);
+    a1.ii = fmaf(h.w, x.w, a1.ii);
+    a1.ri = fmaf(h.z, x.w, a1.ri);
+    a1.ir = fmaf(h.w, x.z, a1.ir);
+}
+
+// acc4 -> packed complex bin: bin 0 = {DC, Nyquist} (products of real values),
+// other bins = the complex product sum.
+__device__ __forceinline__ cf finish(const acc4& a, bool bin0)
+{
+    return bin0 ? cf{a.rr, a.ii} : cf{a.rr - a.ii, a.ri + a.ir};
+}
+
+// Load the overlap-save window [prev | in] of channel c as the packed complex
+// sequence z[n] = w[2n] + i w[2n+1] (lane t owns n = t + m*T), forward FFT, and
+// leave the natural-order spectrum Z in `fft` (lpad'ed).
+template<int B>
+__device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, const cf* tw1, int tid)
+{
+    using K = upols_cfg<B>;
+    const bool active = tid < K::T;
+    cf v[K::E];
+    if (active) {
+        const cf* pz = reinterpret_cast<const cf*>(prev_c);
+        const cf* iz = reinterpret_cast<const cf*>(in_c);
+#pragma unroll
+        for (int m = 0; m < K::E; ++m) {
+            const int n = tid + m * K::T;
+            v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+        }
+    }
+    __syncthreads();  // twiddles staged by the caller
+    stockham<B, K::E, -1>(v, fft, tw1, tid, active);
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < K::E; ++m) fft[lpad(tid + m * K::T)] = v[m];
+    }
+    __syncthreads();
+}
+
+template<int B>
+__global__ __launch_bounds__(256) void k_upols_mac(const float* __restrict__ in, int64_t ld_in,
+                                                   float* __restrict__ prev, const cf* __restrict__ H,
+                                                   cf* __restrict__ fdl, cf* __restrict__ part,
+                                                   const int* __restrict__ wp_dev, const cf* __restrict__ twg, int P,
+                                                   int S, int rows)
+{
+    using K = upols_cfg<B>;
+    __shared__ cf xnew[B];
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    __shared__ float4 red[K::RPI > 1 ? 256 * 2 * K::VPT : 1];
+
+    const int tid = threadIdx.x;
+    const int c = blockIdx.x / S, s = blockIdx.x - c * S;
+    const int p0 = s * rows, p1 = min(P, p0 + rows);
+    const int w = *wp_dev;
+    const int64_t crow = int64_t(c) * P * B;  // channel base in H / FDL (complex units)
+
+    if (s == 0) {
+        for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+        const float* in_c = in + int64_t(c) * ld_in;
+        float* prev_c = prev + int64_t(c) * B;
+        window_fft<B>(prev_c, in_c, fft, tw, tid);
+        cf* row = fdl + crow + int64_t(w) * B;
+        for (int k = tid; k < B; k += 256) {
+            const cf x = r2c_split<B>(fft, tw + K::TW1, k);
+            xnew[k] = x;
+            row[k] = x;
+        }
+        // the window's second half becomes the next call's first half
+        for (int i = tid; i < B / 4; i += 256)
+            reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
+        __syncthreads();
+    }
+
+    const int rs = tid / K::QT, q0 = tid - rs * K::QT;
+    acc4 a[2 * K::VPT];
+#pragma unroll
+    for (int v = 0; v < 2 * K::VPT; ++v) a[v] = {0.f, 0.f, 0.f, 0.f};
+
+    const float4* H4 = reinterpret_cast<const float4*>(H + crow);
+    const float4* F4 = reinterpret_cast<const float4*>(fdl + crow);
+    int pstart = p0;
+    if (p0 == 0) {
+        if (rs == 0) {
+            const float4* Xn = reinterpret_cast<const float4*>(xnew);
+#pragma unroll
+            for (int v = 0; v < K::VPT; ++v) {
+                const int q = q0 + v * K::QT;
+                mac2(a[2 * v], a[2 * v + 1], H4[q], Xn[q]);
+            }
+        }
+        pstart = 1;
+    }
+    // main loop: U row-groups in flight, no bounds checks inside
+    int p = pstart + rs;
+    for (; p + (K::U - 1) * K::RPI < p1; p += K::U * K::RPI) {
+        float4 hv[K::U][K::VPT], xv[K::U][K::VPT];
+#pragma unroll
+        for (int u = 0; u < K::U; ++u) {
+            const int pp = p + u * K::RPI;
+            const int fr = w >= pp ? w - pp : w - pp + P;
+#pragma unroll
+            for (int v = 0; v < K::VPT; ++v) {
+                const int q = q0 + v * K::QT;
+                hv[u][v] = H4[int64_t(pp) * K::Q + q];
+                xv[u][v] = F4[int64_t(fr) * K::Q + q];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < K::U; ++u)
+#pragma unroll
+            for (int v = 0; v < K::VPT; ++v) mac2(a[2 * v], a[2 * v + 1], hv[u][v], xv[u][v]);
+    }
+    for (; p < p1; p += K::RPI) {
+        const int fr = w >= p ? w - p : w - p + P;
+#pragma unroll
+        for (int v = 0; v < K::VPT; ++v) {
+            const int q = q0 + v * K::QT;
+            mac2(a[2 * v], a[2 * v + 1], H4[int64_t(p) * K::Q + q], F4[int64_t(fr) * K::Q + q]);
+        }
+    }
+
+    if constexpr (K::RPI > 1) {
+        // fold the row groups (fixed order -> deterministic)
+#pragma unroll
+        for (int v = 0; v < K::VPT; ++v) {
+            red[(tid * K::VPT + v) * 2 + 0] = make_float4(a[2 * v].rr, a[2 * v].ii, a[2 * v].ri, a[2 * v].ir);
+            red[(tid * K::VPT + v) * 2 + 1] =
+                make_float4(a[2 * v + 1].rr, a[2 * v + 1].ii, a[2 * v + 1].ri, a[2 * v + 1].ir);
+        }
+        __syncthreads();
+        if (rs != 0) return;
+        for (int g = 1; g < K::RPI; ++g) {
+#pragma unroll
+            for (int v = 0; v < K::VPT; ++v) {
+                const int idx = ((g * K::QT + q0) * K::VPT + v) * 2;
+                const float4 r0 = red[idx], r1 = red[idx + 1];
+                a[2 * v].rr += r0.x; a[2 * v].ii += r0.y; a[2 * v].ri += r0.z; a[2 * v].ir += r0.w;
+                a[2 * v + 1].rr += r1.x; a[2 * v + 1].ii += r1.y; a[2 * v + 1].ri += r1.z; a[2 * v + 1].ir += r1.w;
+            }
+        }
+    }
+    float4* out = reinterpret_cast<float4*>(part + (int64_t(c) * S + s) * B);
+#pragma unroll
+    for (int v = 0; v < K::VPT; ++v) {
+        const int q = q0 + v * K::QT;
+        const cf b0 = finish(a[2 * v], q == 0), b1 = finish(a[2 * v + 1], false);
+        out[q] = make_float4(b0.x, b0.y, b1.x, b1.y);
+    }
+}
+
+template<int B>
+__global__ __launch_bounds__(256) void k_upols_out(const cf* __restrict__ part, float* __restrict__ out, int64_t ld_out,
+                                                   int* __restrict__ wp_dev, const cf* __restrict__ twg, int P, int S)
+{
+    using K = upols_cfg<B>;
+    __shared__ cf X[B];
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    const int tid = threadIdx.x, c = blockIdx.x;
+    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+    const float4* p4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * B);
+    for (int q = tid; q < K::Q; q += 256) {
+        float4 sum = p4[q];
+        for (int s = 1; s < S; ++s) {
+            const float4 t = p4[int64_t(s) * K::Q + q];
+            sum.x += t.x; sum.y += t.y; sum.z += t.z; sum.w += t.w;
+        }
+        reinterpret_cast<float4*>(X)[q] = sum;
+    }
+    __syncthreads();
+    const bool active = tid < K::T;
+    cf v[K::E];
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < K::E; ++m) {
+            const int k = tid + m * K::T;
+            const cf x0 = X[0];
+            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
+                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
+        }
+    }
+    stockham<B, K::E, +1>(v, fft, tw, tid, active);
+    if (active) {
+        const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108
+        cf* o = reinterpret_cast<cf*>(out + int64_t(c) * ld_out);
+#pragma unroll
+        for (int m = K::E / 2; m < K::E; ++m) {  // samples [B, 2B) of the window
+            const int n = tid + m * K::T;
+            o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+        }
+    }
+    if (c == 0 && tid == 0) {
+        const int w = *wp_dev + 1;  // fdl_index.hpp:35-37
+        *wp_dev = w >= P ? 0 : w;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// setup path
+// ---------------------------------------------------------------------------
+// uniform_partition (uniform_partition.hpp:12-26 -> stft.hpp:56-99): partition p
+// of channel c = rfft_2B(ir[c][pB : pB+B] zero-padded to 2B). Packed output
+// [C][P][B] (UPOLS layout) or unpacked [C][P][B+1] (reference layout).
+template<int B, bool PACKED>
+__global__ __launch_bounds__(256) void k_partition(const float* __restrict__ ir, int64_t L, int P,
+                                                   cf* __restrict__ out, const cf* __restrict__ twg)
+{
+    using K = upols_cfg<B>;
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    const int tid = threadIdx.x;
+    const int64_t cp = blockIdx.x;
+    const int64_t c = cp / P, p = cp - c * P;
+    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+    const bool active = tid < K::T;
+    const float* seg = ir + c * L + p * B;
+    const int64_t cnt = min(int64_t(B), L - p * B);
+    cf v[K::E];
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < K::E; ++m) {
+            const int n = tid + m * K::T;  // z[n] = (w[2n], w[2n+1]); w = segment | zeros
+            const float a = 2 * n < cnt ? seg[2 * n] : 0.f;
+            const float b = 2 * n + 1 < cnt ? seg[2 * n + 1] : 0.f;
+            v[m] = {a, b};
+        }
+    }
+    __syncthreads();
+    stockham<B, K::E, -1>(v, fft, tw, tid, active);
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < K::E; ++m) fft[lpad(tid + m * K::T)] = v[m];
+    }
+    __syncthreads();
+    if constexpr (PACKED) {
+        cf* row = out + cp * B;
+        for (int k = tid; k < B; k += 256) row[k] = r2c_split<B>(fft, tw + K::TW1, k);
+    } else {
+        cf* row = out + cp * (B + 1);
+        for (int k = tid; k < B; k += 256) {
+            const cf x = r2c_split<B>(fft, tw + K::TW1, k);
+            if (k == 0) {
+                row[0] = {x.x, 0.f};
+                row[B] = {x.y, 0.f};
+            } else {
+                row[k] = x;
+            }
+        }
+    }
+}
+
+// filter [C][P][B+1] (reference layout) -> packed [C][P][B]
+__global__ void k_pack_filter(const cf* __restrict__ in, cf* __restrict__ out, int B, int64_t rows)
+{
+    const int64_t gid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (gid >= rows * B) return;
+    const int64_t r = gid / B, k = gid - r * B;
+    const cf* src = in + r * (B + 1);
+    out[gid] = k == 0 ? cf{src[0].x, src[B].x} : src[k];
+}
+
+// normalize_energy_factor (normalize_energy.hpp:17-44) with the reference's exact
+// rounding: sequential float sum of x*x (multiply, then add; no FMA), then
+// 1/sqrt. One lane per channel.
+__global__ void k_energy_factor(const float* __restrict__ ir, int64_t L, int C, float* __restrict__ factor)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float* x = ir + int64_t(c) * L;
+    float e = 0.0f;
+    for (int64_t i = 0; i < L; ++i) e = __fadd_rn(e, __fmul_rn(x[i], x[i]));
+    factor[c] = e == 0.0f ? 1.0f : __fdiv_rn(1.0f, __fsqrt_rn(e));
+}
+
+// normalize_impulse.hpp:21-30: min factor over channels, then scale everything
+__global__ void k_scale_min(float* __restrict__ ir, int64_t n, const float* __restrict__ factor, int C)
+{
+    __shared__ float fmin_s;
+    if (threadIdx.x == 0) {
+        float f = factor[0];
+        for (int c = 1; c < C; ++c) f = fminf(f, factor[c]);
+        fmin_s = f;
+    }
+    __syncthreads();
+    const float f = fmin_s;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+        ir[i] = __fmul_rn(ir[i], f);
+}
+
+}  // namespace neo_hip
+
+using namespace neo_hip;
+
+struct neo_hip_upols {
+    int device = 0, C = 0, B = 0, P = 0, S = 1, rows = 1;
+    hipStream_t stream = nullptr;
+    cf* H = nullptr;
+    cf* fdl = nullptr;
+    cf* part = nullptr;
+    float* prev = nullptr;
+    int* wp = nullptr;
+    cf* tw = nullptr;
+    float* io = nullptr;       // device staging for host-pointer process()
+    float* io_host = nullptr;  // pinned staging
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    double mac_ms = 0.0;
+    int64_t launches = 0;
+};
+
+namespace {
+
+using upols_t = neo_hip_upols;
+
+bool valid_block(int b) { return b >= 16 && b <= 4096 && (b & (b - 1)) == 0; }
+
+#define NEO_UPOLS_DISPATCH(B_, BODY) \
+    switch (B_) {                    \
+        case 16: { constexpr int BB = 16; BODY; break; }     \
+        case 32: { constexpr int BB = 32; BODY; break; }     \
+        case 64: { constexpr int BB = 64; BODY; break; }     \
+        case 128: { constexpr int BB = 128; BODY; break; }   \
+        case 256: { constexpr int BB = 256; BODY; break; }   \
+        case 512: { constexpr int BB = 512; BODY; break; }   \
+        case 1024: { constexpr int BB = 1024; BODY; break; } \
+        case 2048: { constexpr int BB = 2048; BODY; break; } \
+        case 4096: { constexpr int BB = 4096; BODY; break; } \
+        default: return fail(NEO_HIP_EINVAL, "unsupported block size %d", B_); \
+    }
+
+int64_t partitions_for(int64_t L, int B)
+{
+    // stft.hpp:21-25 with overlap 0: idiv(L - B, B) + 1 (= ceil(L/B) for L >= B);
+    // the reference underflows for L < B, we clamp to one partition.
+    if (L <= B) return 1;
+    return (L - B + B - 1) / B + 1;
+}
+
+int upload_tw(cf** d, int B)
+{
+    std::vector<cf> t = make_twiddle_table(B);
+    std::vector<cf> t2 = make_twiddle_table(2 * int64_t(B));
+    t.insert(t.end(), t2.begin(), t2.end());
+    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(d), t.size() * sizeof(cf)));
+    NEO_HIP_CHECK(hipMemcpy(*d, t.data(), t.size() * sizeof(cf), hipMemcpyHostToDevice));
+    return NEO_HIP_OK;
+}
+
+int reset_state(upols_t* h, hipStream_t s)
+{
+    NEO_HIP_CHECK(hipMemsetAsync(h->fdl, 0, size_t(h->C) * h->P * h->B * sizeof(cf), s));
+    NEO_HIP_CHECK(hipMemsetAsync(h->prev, 0, size_t(h->C) * h->B * sizeof(float), s));
+    NEO_HIP_CHECK(hipMemsetAsync(h->wp, 0, sizeof(int), s));
+    return NEO_HIP_OK;
+}
+
+void destroy(upols_t* h)
+{
+    if (!h) return;
+    for (auto& e : h->events) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    (void)hipFree(h->H);
+    (void)hipFree(h->fdl);
+    (void)hipFree(h->part);
+    (void)hipFree(h->prev);
+    (void)hipFree(h->wp);
+    (void)hipFree(h->tw);
+    (void)hipFree(h->io);
+    if (h->io_host) (void)hipHostFree(h->io_host);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+// normalize (optional) + partition ir [C][L] (device) into packed or unpacked rows.
+int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s)
+{
+    const int64_t P = partitions_for(L, B);
+    const int64_t blocks = int64_t(C) * P;
+    if (blocks > 0x7fffffff) return fail(NEO_HIP_EINVAL, "too many partitions");
+    if (packed) {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_partition<BB, true>), dim3(unsigned(blocks)), dim3(256), 0, s,
+                                                 d_ir, L, int(P), out, tw))
+    } else {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_partition<BB, false>), dim3(unsigned(blocks)), dim3(256), 0, s,
+                                                 d_ir, L, int(P), out, tw))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    return NEO_HIP_OK;
+}
+
+int normalize_device(float* d_ir, int C, int64_t L, hipStream_t s)
+{
+    if (C < 1) return NEO_HIP_OK;
+    float* factor = nullptr;
+    NEO_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&factor), size_t(C) * sizeof(float), s));
+    hipLaunchKernelGGL(k_energy_factor, dim3(unsigned((C + 63) / 64)), dim3(64), 0, s, d_ir, L, C, factor);
+    NEO_HIP_LAUNCH_CHECK();
+    const int64_t n = int64_t(C) * L;
+    const unsigned blocks = unsigned(std::min<int64_t>((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_scale_min, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, d_ir, n, factor, C);
+    NEO_HIP_LAUNCH_CHECK();
+    NEO_HIP_CHECK(hipFreeAsync(factor, s));
+    return NEO_HIP_OK;
+}
+
+int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
+{
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (h->timing) {
+        NEO_HIP_CHECK(hipEventCreate(&ev.first));
+        NEO_HIP_CHECK(hipEventCreate(&ev.second));
+        NEO_HIP_CHECK(hipEventRecord(ev.first, s));
+    }
+    const unsigned grid = unsigned(h->C) * unsigned(h->S);
+    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_mac<BB>), dim3(grid), dim3(256), 0, s, in, ld_in, h->prev,
+                                                h->H, h->fdl, h->part, h->wp, h->tw, h->P, h->S, h->rows))
+    NEO_HIP_LAUNCH_CHECK();
+    if (h->timing) {
+        NEO_HIP_CHECK(hipEventRecord(ev.second, s));
+        h->events.push_back(ev);
+    }
+    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_out<BB>), dim3(unsigned(h->C)), dim3(256), 0, s, h->part,
+                                                out, ld_out, h->wp, h->tw, h->P, h->S))
+    NEO_HIP_LAUNCH_CHECK();
+    return NEO_HIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+NEO_HIP_API int neo_hip_num_partitions(int64_t length, int block, int64_t* partitions)
+{
+    if (!partitions || block < 1 || length < 0) return fail(NEO_HIP_EINVAL, "bad arguments");
+    *partitions = partitions_for(length, block);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
+{
+    if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
+    *out = nullptr;
+    if (channels < 1) return fail(NEO_HIP_EINVAL, "channels must be >= 1");
+    if (!valid_block(block)) return fail(NEO_HIP_EINVAL, "block must be a power of two in [16, 4096], got %d", block);
+    if (partitions < 1) return fail(NEO_HIP_EINVAL, "partitions must be >= 1");
+    device_guard g(device);
+    if (g.rc) return g.rc;
+    auto* h = new upols_t{};
+    (void)hipGetDevice(&h->device);
+    h->C = channels;
+    h->B = block;
+    h->P = partitions;
+    // splits per channel: aim for ~2048 workgroups (8 per CU), <= 64 partial slabs
+    const int target = 2048;
+    int S = std::max(1, std::min({(target + channels - 1) / channels, partitions, 64}));
+    h->rows = (partitions + S - 1) / S;
+    h->S = (partitions + h->rows - 1) / h->rows;
+    const size_t rowbytes = size_t(block) * sizeof(cf);
+    const size_t nrows = size_t(channels) * size_t(partitions);
+    auto bail = [&](int code) {
+        destroy(h);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
+    if (hipMalloc(reinterpret_cast<void**>(&h->H), nrows * rowbytes) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&h->fdl), nrows * rowbytes) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&h->part), size_t(channels) * h->S * rowbytes) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&h->prev), size_t(channels) * block * sizeof(float)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&h->wp), sizeof(int)) != hipSuccess)
+        return bail(fail(NEO_HIP_ENOMEM, "device allocation of %zu bytes failed", 2 * nrows * rowbytes));
+    int rc = upload_tw(&h->tw, block);
+    if (rc) return bail(rc);
+    if (hipMemset(h->H, 0, nrows * rowbytes) != hipSuccess) return bail(fail(NEO_HIP_ERUNTIME, "memset failed"));
+    if ((rc = reset_state(h, h->stream))) return bail(rc);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(NEO_HIP_ERUNTIME, "sync failed"));
+    *out = h;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h)
+{
+    if (!h) return NEO_HIP_OK;
+    device_guard g(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    destroy(h);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_info(neo_hip_upols* h, int* channels, int* block, int* partitions, int* splits)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    if (channels) *channels = h->C;
+    if (block) *block = h->B;
+    if (partitions) *partitions = h->P;
+    if (splits) *splits = h->S;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    device_guard g(h->device);
+    int rc = reset_state(h, h->stream);
+    if (rc) return rc;
+    NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, int is_device)
+{
+    if (!h || !filter) return fail(NEO_HIP_EINVAL, "null handle or filter");
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    const int64_t rows = int64_t(h->C) * h->P;
+    const size_t bytes = size_t(rows) * size_t(h->B + 1) * sizeof(cf);
+    const cf* src = static_cast<const cf*>(filter);
+    cf* tmp = nullptr;
+    if (!is_device) {
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp), bytes));
+        NEO_HIP_CHECK(hipMemcpyAsync(tmp, filter, bytes, hipMemcpyHostToDevice, h->stream));
+        src = tmp;
+    }
+    const int64_t total = rows * h->B;
+    hipLaunchKernelGGL(k_pack_filter, dim3(unsigned((total + 255) / 256)), dim3(256), 0, h->stream, src, h->H, h->B,
+                       rows);
+    int rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "pack kernel launch failed");
+    if (!rc) rc = reset_state(h, h->stream);
+    if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
+    if (tmp) (void)hipFree(tmp);
+    return rc;
+}
+
+NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int64_t length, int normalize,
+                                          int is_device)
+{
+    if (!h || !ir || length < 1) return fail(NEO_HIP_EINVAL, "null handle/ir or empty impulse");
+    if (partitions_for(length, h->B) != h->P)
+        return fail(NEO_HIP_EINVAL, "impulse of %lld taps gives %lld partitions, convolver has %d", (long long)length,
+                    (long long)partitions_for(length, h->B), h->P);
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    const size_t bytes = size_t(h->C) * size_t(length) * sizeof(float);
+    float* d = nullptr;
+    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), bytes));
+    int rc = NEO_HIP_OK;
+    if (hipMemcpyAsync(d, ir, bytes, is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream) !=
+        hipSuccess)
+        rc = fail(NEO_HIP_ERUNTIME, "impulse copy failed");
+    if (!rc && normalize) rc = normalize_device(d, h->C, length, h->stream);
+    if (!rc) rc = partition_device(d, h->C, length, h->B, true, h->H, h->tw, h->stream);
+    if (!rc) rc = reset_state(h, h->stream);
+    if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
+    (void)hipFree(d);
+    return rc;
+}
+
+NEO_HIP_API int neo_hip_upols_process_device(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
+                                             int64_t ld_out, void* stream)
+{
+    if (!h || !in || !out) return fail(NEO_HIP_EINVAL, "null handle or buffer");
+    if (ld_in < h->B || ld_out < h->B) return fail(NEO_HIP_EINVAL, "leading dimension smaller than the block");
+    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15 || (ld_in | ld_out) & 3)
+        return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    return launch_step(h, in, ld_in, out, ld_out, stream ? as_stream(stream) : h->stream);
+}
+
+NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, float* out, int64_t ld, int64_t nblocks,
+                                             void* stream)
+{
+    if (!h || !in || !out) return fail(NEO_HIP_EINVAL, "null handle or buffer");
+    if (ld < nblocks * h->B) return fail(NEO_HIP_EINVAL, "ld < nblocks * block");
+    for (int64_t t = 0; t < nblocks; ++t) {
+        int rc = neo_hip_upols_process_device(h, in + t * h->B, ld, out + t * h->B, ld, stream);
+        if (rc) return rc;
+    }
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_device, void* stream)
+{
+    if (!h || !io) return fail(NEO_HIP_EINVAL, "null handle or buffer");
+    if (io_is_device) return neo_hip_upols_process_device(h, io, h->B, io, h->B, stream);
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    hipStream_t s = stream ? as_stream(stream) : h->stream;
+    const size_t bytes = size_t(h->C) * h->B * sizeof(float);
+    if (!h->io) {
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->io), bytes));
+        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->io_host), bytes, hipHostMallocDefault));
+    }
+    std::copy(io, io + size_t(h->C) * h->B, h->io_host);
+    NEO_HIP_CHECK(hipMemcpyAsync(h->io, h->io_host, bytes, hipMemcpyHostToDevice, s));
+    int rc = launch_step(h, h->io, h->B, h->io, h->B, s);
+    if (rc) return rc;
+    NEO_HIP_CHECK(hipMemcpyAsync(h->io_host, h->io, bytes, hipMemcpyDeviceToHost, s));
+    NEO_HIP_CHECK(hipStreamSynchronize(s));
+    std::copy(h->io_host, h->io_host + size_t(h->C) * h->B, io);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    h->timing = enable != 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    device_guard g(h->device);
+    for (auto& e : h->events) {
+        NEO_HIP_CHECK(hipEventSynchronize(e.second));
+        float ms = 0.f;
+        NEO_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
+        h->mac_ms += ms;
+        ++h->launches;
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    h->events.clear();
+    if (mac_ms) *mac_ms = h->mac_ms;
+    if (launches) *launches = h->launches;
+    h->mac_ms = 0.0;
+    h->launches = 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t length, int block, void* out,
+                                          int is_device, int device)
+{
+    if (!ir || !out || channels < 1 || length < 1) return fail(NEO_HIP_EINVAL, "bad arguments");
+    if (!valid_block(block)) return fail(NEO_HIP_EINVAL, "block must be a power of two in [16, 4096], got %d", block);
+    device_guard g(device);
+    if (g.rc) return g.rc;
+    const int64_t P = partitions_for(length, block);
+    const size_t in_bytes = size_t(channels) * size_t(length) * sizeof(float);
+    const size_t out_bytes = size_t(channels) * size_t(P) * size_t(block + 1) * sizeof(cf);
+    hipStream_t s = nullptr;
+    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    cf* tw = nullptr;
+    const float* d_ir = ir;
+    float* tmp_in = nullptr;
+    cf* d_out = static_cast<cf*>(out);
+    int rc = upload_tw(&tw, block);
+    if (!rc && !is_device) {
+        if (hipMalloc(reinterpret_cast<void**>(&tmp_in), in_bytes) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&d_out), out_bytes) != hipSuccess)
+            rc = fail(NEO_HIP_ENOMEM, "allocation failed");
+        else if (hipMemcpyAsync(tmp_in, ir, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+            rc = fail(NEO_HIP_ERUNTIME, "copy failed");
+        d_ir = tmp_in;
+    }
+    if (!rc) rc = partition_device(d_ir, channels, length, block, false, d_out, tw, s);
+    if (!rc && !is_device && hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
+    if (!is_device) {
+        (void)hipFree(tmp_in);
+        (void)hipFree(d_out);
+    }
+    (void)hipFree(tw);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t length, int is_device, int device)
+{
+    if (!ir || channels < 0 || length < 0) return fail(NEO_HIP_EINVAL, "bad arguments");
+    if (channels == 0 || length == 0) return NEO_HIP_OK;
+    device_guard g(device);
+    if (g.rc) return g.rc;
+    hipStream_t s = nullptr;
+    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const size_t bytes = size_t(channels) * size_t(length) * sizeof(float);
+    float* d = ir;
+    int rc = NEO_HIP_OK;
+    if (!is_device) {
+        if (hipMalloc(reinterpret_cast<void**>(&d), bytes) != hipSuccess) rc = fail(NEO_HIP_ENOMEM, "alloc failed");
+        else if (hipMemcpyAsync(d, ir, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+            rc = fail(NEO_HIP_ERUNTIME, "copy failed");
+    }
+    if (!rc) rc = normalize_device(d, channels, length, s);
+    if (!rc && !is_device && hipMemcpyAsync(ir, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
+    if (!is_device && d) (void)hipFree(d);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,25 @@
+"""neo (MI355X): the FFT + UPOLS hot path of neo-dsp on HIP/gfx950.
+
+`import neo` mirrors the reference's Python package entry points that exist on
+this path (extra/python/src/neo/__init__.py, neo/fft/__init__.py); the compute
+is libneo_hip.so (include/neo_hip.h). Put `<repo>/neo-dsp_amd` on sys.path.
+"""
+from . import _native
+from . import convolution
+from . import fft
+from .convolution import (UpolsConvolver, dense_convolve, normalize_impulse, num_partitions,
+                          split_upols_convolver, uniform_partition, upols_convolver)
+
+__version__ = "0.1.0"
+
+__all__ = [
+    "fft",
+    "convolution",
+    "UpolsConvolver",
+    "upols_convolver",
+    "split_upols_convolver",
+    "uniform_partition",
+    "normalize_impulse",
+    "num_partitions",
+    "dense_convolve",
+]

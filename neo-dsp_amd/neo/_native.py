@@ -1,0 +1,95 @@
+"""ctypes binding of libneo_hip.so (the C-ABI in include/neo_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU
+is visible, calls raise. The library is built in-tree by
+`make -C neo-dsp_amd` (or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libneo_hip.so"))
+
+NEO_HIP_OK = 0
+NEO_HIP_EINVAL = 1
+NEO_HIP_ERUNTIME = 2
+NEO_HIP_ENOMEM = 3
+NEO_HIP_ENODEV = 4
+
+C2C, R2C, C2R = 0, 1, 2
+
+# every symbol declared in include/neo_hip.h: (name, restype, argtypes)
+_vp, _i, _i64, _fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_float)
+SIGNATURES = {
+    "neo_hip_last_error": (ctypes.c_char_p, []),
+    "neo_hip_version": (_i, []),
+    "neo_hip_device_count": (_i, [ctypes.POINTER(_i)]),
+    "neo_hip_fft_max_order": (_i, []),
+    "neo_hip_fft_plan_create": (_i, [_i, _i64, _i, _i, ctypes.POINTER(_vp)]),
+    "neo_hip_fft_plan_destroy": (_i, [_vp]),
+    "neo_hip_fft_execute": (_i, [_vp, _vp, _vp, _i, _vp]),
+    "neo_hip_fft_execute_host": (_i, [_vp, _vp, _vp, _i]),
+    "neo_hip_upols_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "neo_hip_upols_destroy": (_i, [_vp]),
+    "neo_hip_upols_set_filter": (_i, [_vp, _vp, _i]),
+    "neo_hip_upols_set_impulse": (_i, [_vp, _vp, _i64, _i, _i]),
+    "neo_hip_upols_process": (_i, [_vp, _vp, _i, _vp]),
+    "neo_hip_upols_process_device": (_i, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "neo_hip_upols_process_blocks": (_i, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    "neo_hip_upols_reset": (_i, [_vp]),
+    "neo_hip_upols_set_timing": (_i, [_vp, _i]),
+    "neo_hip_upols_timing": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
+    "neo_hip_upols_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
+    "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),
+    "neo_hip_normalize_impulse": (_i, [_vp, _i, _i64, _i, _i]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NeoHipError(RuntimeError):
+    """Raised for any nonzero neo_hip status (maps the reference's std::runtime_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"neo_hip error {code}: {msg}")
+        self.code = code
+
+
+def load(path: str = LIB_PATH):
+    """Load libneo_hip.so and bind every exported symbol; raises if absent."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise ImportError(
+                    f"{path} not found: build the HIP library first (make -C neo-dsp_amd); "
+                    "there is no CPU fallback")
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != NEO_HIP_OK:
+        msg = load().neo_hip_last_error()
+        raise NeoHipError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = load().neo_hip_device_count(ctypes.byref(n))
+    return n.value if rc == NEO_HIP_OK else 0
+
+
+def require_gpu() -> None:
+    if device_count() < 1:
+        raise NeoHipError(NEO_HIP_ENODEV, "no HIP device visible; neo_hip has no CPU fallback")

@@ -1,0 +1,232 @@
+"""neo.convolution on MI355X: UPOLS convolvers, uniform_partition, normalize_impulse.
+
+Mirrors the reference's C++ convolution API (the reference binds no UPOLS in
+Python; extra/python/src/main.cpp:227-234 only lists the `upols` method enum):
+  - uniform_partition      src/neo/convolution/uniform_partition.hpp:12-26
+  - normalize_impulse      src/neo/convolution/normalize_impulse.hpp:11-33
+  - upols_convolver        src/neo/convolution/dense_convolver.hpp:19-20 +
+                           uniform_partitioned_convolver.hpp:13-65
+  - split_upols_convolver  dense_convolver.hpp:38-42 (same math, SoA on the CPU;
+                           one device layout here)
+  - dense_convolve         extra/plugin/src/dsp/DenseConvolution.hpp:39-70
+Everything runs on the GPU through libneo_hip.so; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native
+
+__all__ = [
+    "num_partitions",
+    "uniform_partition",
+    "normalize_impulse",
+    "UpolsConvolver",
+    "upols_convolver",
+    "split_upols_convolver",
+    "dense_convolve",
+]
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch") and hasattr(x, "is_cuda")
+
+
+def _ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def num_partitions(length: int, block: int) -> int:
+    """P = ceil(L / B) (stft.hpp:21-25 with overlap 0; clamped to 1 for L < B)."""
+    p = ctypes.c_int64()
+    _native.check(_native.load().neo_hip_num_partitions(int(length), int(block), ctypes.byref(p)))
+    return p.value
+
+
+def uniform_partition(impulse_response, block_size: int, device: int = 0) -> np.ndarray:
+    """[C][L] float32 -> [C][P][B+1] complex64: rfft_2B of each zero-padded B-sample partition."""
+    ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
+    C, L = ir.shape
+    P = num_partitions(L, block_size)
+    out = np.empty((C, P, block_size + 1), dtype=np.complex64)
+    _native.check(_native.load().neo_hip_uniform_partition(_ptr(ir), C, L, int(block_size), _ptr(out), 0, int(device)))
+    return out
+
+
+def normalize_impulse(impulse_response, device: int = 0):
+    """In place: scale every channel by min_c 1/sqrt(sum(ir[c]^2)), rounded exactly like the
+    reference's sequential float sum. Accepts a float32 ndarray (rank 1 or 2) or CUDA tensor."""
+    if _is_torch(impulse_response):
+        t = impulse_response
+        C, L = (1, t.shape[0]) if t.dim() == 1 else tuple(t.shape)
+        _native.check(_native.load().neo_hip_normalize_impulse(ctypes.c_void_p(t.data_ptr()), C, L, 1,
+                                                               t.device.index or 0))
+        return t
+    a = impulse_response
+    if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous):
+        raise TypeError("normalize_impulse works in place on a C-contiguous float32 array")
+    C, L = (1, a.shape[0]) if a.ndim == 1 else a.shape
+    _native.check(_native.load().neo_hip_normalize_impulse(_ptr(a), C, L, 0, int(device)))
+    return a
+
+
+class UpolsConvolver:
+    """C independent UPOLS convolvers stepped together (one launch pair per block).
+
+    State lives in HBM: filter [C][P][B] and FDL [C][P][B] (packed bins),
+    previous block [C][B]. Blocks are processed in place, zero latency
+    (output block t corresponds to input block t, overlap_save.hpp:84-112).
+    """
+
+    def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0):
+        lib = _native.load()
+        h = ctypes.c_void_p()
+        _native.check(lib.neo_hip_upols_create(int(channels), int(block_size), int(partitions), int(device),
+                                               ctypes.byref(h)))
+        self._h = h
+        self.channels, self.block_size, self.partitions, self.device = channels, block_size, partitions, device
+
+    # -- setup ------------------------------------------------------------
+    def filter(self, partitions) -> None:
+        """uniform_partitioned_convolver::filter(): [C][P][B+1] complex64 (host array or
+        CUDA tensor); resets FDL, window and write position."""
+        if _is_torch(partitions):
+            _native.check(_native.load().neo_hip_upols_set_filter(self._h, ctypes.c_void_p(partitions.data_ptr()), 1))
+            return
+        H = np.ascontiguousarray(partitions, dtype=np.complex64)
+        if H.ndim == 2:
+            H = H[None]
+        if H.shape != (self.channels, self.partitions, self.block_size + 1):
+            raise ValueError(f"filter shape {H.shape} != {(self.channels, self.partitions, self.block_size + 1)}")
+        _native.check(_native.load().neo_hip_upols_set_filter(self._h, _ptr(H), 0))
+
+    def set_impulse(self, impulse_response, normalize: bool = True) -> None:
+        """normalize_impulse (optional) + uniform_partition straight into the device filter."""
+        if _is_torch(impulse_response):
+            t = impulse_response
+            _native.check(_native.load().neo_hip_upols_set_impulse(self._h, ctypes.c_void_p(t.data_ptr()),
+                                                                   t.shape[-1], int(normalize), 1))
+            return
+        ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
+        if ir.shape[0] != self.channels:
+            raise ValueError("impulse channel count mismatch")
+        _native.check(_native.load().neo_hip_upols_set_impulse(self._h, _ptr(ir), ir.shape[1], int(normalize), 0))
+
+    def reset(self) -> None:
+        _native.check(_native.load().neo_hip_upols_reset(self._h))
+
+    # -- processing ---------------------------------------------------------
+    def __call__(self, block, stream: int = 0):
+        """Process one block [C][B] in place (float32 ndarray or CUDA tensor)."""
+        if _is_torch(block):
+            import torch
+
+            assert block.dtype == torch.float32 and block.is_contiguous()
+            s = stream or torch.cuda.current_stream(block.device).cuda_stream
+            _native.check(_native.load().neo_hip_upols_process(self._h, ctypes.c_void_p(block.data_ptr()), 1,
+                                                               ctypes.c_void_p(s)))
+            return block
+        if not (isinstance(block, np.ndarray) and block.dtype == np.float32 and block.flags.c_contiguous):
+            raise TypeError("block must be a C-contiguous float32 array")
+        if block.size != self.channels * self.block_size:
+            raise ValueError("block must hold channels * block_size samples")
+        _native.check(_native.load().neo_hip_upols_process(self._h, _ptr(block), 0, None))
+        return block
+
+    def process_device(self, in_ptr: int, ld_in: int, out_ptr: int, ld_out: int, stream: int = 0) -> None:
+        _native.check(_native.load().neo_hip_upols_process_device(self._h, ctypes.c_void_p(in_ptr), int(ld_in),
+                                                                  ctypes.c_void_p(out_ptr), int(ld_out),
+                                                                  ctypes.c_void_p(stream)))
+
+    def process_blocks(self, signal, out=None, stream: int = 0):
+        """Run consecutive blocks of a CUDA tensor [C][nblocks*B] (out may alias signal)."""
+        import torch
+
+        out = signal if out is None else out
+        nb = signal.shape[-1] // self.block_size
+        s = stream or torch.cuda.current_stream(signal.device).cuda_stream
+        _native.check(_native.load().neo_hip_upols_process_blocks(self._h, ctypes.c_void_p(signal.data_ptr()),
+                                                                  ctypes.c_void_p(out.data_ptr()), signal.shape[-1],
+                                                                  nb, ctypes.c_void_p(s)))
+        return out
+
+    # -- instrumentation ------------------------------------------------------
+    def set_timing(self, enable: bool) -> None:
+        _native.check(_native.load().neo_hip_upols_set_timing(self._h, int(enable)))
+
+    def timing(self):
+        """(accumulated MAC-kernel ms, launches) since the last call."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        _native.check(_native.load().neo_hip_upols_timing(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    @property
+    def splits(self) -> int:
+        s = ctypes.c_int()
+        _native.check(_native.load().neo_hip_upols_info(self._h, None, None, None, ctypes.byref(s)))
+        return s.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _native.load().neo_hip_upols_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class upols_convolver:
+    """Single-channel drop-in for upols_convolver<complex<float>>: default-constructible,
+    filter([P][B+1]) then __call__(block[B]) in place."""
+
+    def __init__(self, device: int = 0):
+        self._impl = None
+        self._device = device
+
+    def filter(self, filt) -> None:
+        H = np.ascontiguousarray(filt, dtype=np.complex64)
+        if H.ndim != 2:
+            raise ValueError("filter must be [P][B+1]")
+        P, bins = H.shape
+        impl = self._impl
+        if impl is None or (impl.partitions, impl.block_size) != (P, bins - 1):
+            impl = UpolsConvolver(1, bins - 1, P, self._device)
+        impl.filter(H[None])
+        self._impl = impl
+
+    def __call__(self, block):
+        if self._impl is None:
+            raise RuntimeError("filter() must be called first")
+        return self._impl(block)
+
+
+split_upols_convolver = upols_convolver
+
+
+def dense_convolve(signal, impulse_response, block_size: int, device: int = 0) -> np.ndarray:
+    """dense_convolve<upols_convolver> (DenseConvolution.hpp:39-70): normalize the IR matrix,
+    partition it, run every block (tail zero-padded) and return the output truncated to N."""
+    sig = np.ascontiguousarray(np.atleast_2d(np.asarray(signal, dtype=np.float32)))
+    ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
+    C, N = sig.shape
+    if ir.shape[0] != C:
+        raise ValueError("signal and impulse response channel counts differ")
+    P = num_partitions(ir.shape[1], block_size)
+    conv = UpolsConvolver(C, block_size, P, device)
+    conv.set_impulse(ir, normalize=True)
+    nb = -(-N // block_size)
+    out = np.empty_like(sig)
+    block = np.zeros((C, block_size), dtype=np.float32)
+    for t in range(nb):
+        lo, hi = t * block_size, min(N, (t + 1) * block_size)
+        block[:] = 0.0
+        block[:, : hi - lo] = sig[:, lo:hi]
+        conv(block)
+        out[:, lo:hi] = block[:, : hi - lo]
+    conv.close()
+    return out

@@ -1,0 +1,149 @@
+"""neo.fft on MI355X — mirrors the reference's Python facade.
+
+Reference: extra/python/src/neo/fft/__init__.py:22-31 (fft/ifft) over
+extra/python/src/main.cpp:129-167 (power-of-two sizes only, RuntimeError
+otherwise; unnormalized transforms scaled per `norm`). Here every transform runs
+on the GPU through libneo_hip.so (include/neo_hip.h); there is no CPU path.
+
+Extensions over the reference (documented in INTEGRATION.md): arrays of rank > 1
+are transformed along the last axis as one batched launch; torch CUDA tensors are
+transformed in device memory on torch's current stream; rfft/irfft are exposed.
+Plans are cached per (kind, order, batch, device) instead of rebuilt per call
+(main.cpp:147).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .. import _native
+from ._plan import FFTPlan, get_plan
+
+__all__ = ["fft", "ifft", "rfft", "irfft", "FFTPlan", "get_plan", "next_order", "size", "max_order"]
+
+_NORMS = ("backward", "ortho", "forward")
+
+
+def max_order() -> int:
+    return int(_native.load().neo_hip_fft_max_order())
+
+
+def size(order: int) -> int:
+    """neo::fft::size (src/neo/fft/order.hpp:26-30)."""
+    return 1 << order
+
+
+def next_order(n: int) -> int:
+    """neo::fft::next_order = log2(bit_ceil(n)) (src/neo/fft/order.hpp:32-37)."""
+    n = int(n)
+    return 0 if n <= 1 else (n - 1).bit_length()
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch") and hasattr(x, "is_cuda")
+
+
+def _check_size(n: int) -> int:
+    if n < 1 or (n & (n - 1)) != 0:
+        raise RuntimeError(f"unsupported size: {n}")  # main.cpp:137-139
+    return n.bit_length() - 1
+
+
+def _fit(x: np.ndarray, n: int) -> np.ndarray:
+    if x.shape[-1] == n:
+        return x
+    if x.shape[-1] > n:
+        return x[..., :n]
+    pad = [(0, 0)] * (x.ndim - 1) + [(0, n - x.shape[-1])]
+    return np.pad(x, pad)
+
+
+def _scale(norm: str, n: int, inverse: bool) -> float:
+    if norm not in _NORMS:
+        raise ValueError(f"invalid norm {norm!r}")
+    if norm == "ortho":
+        return 1.0 / np.sqrt(n)
+    if (norm == "backward") == inverse:
+        return 1.0 / n
+    return 1.0
+
+
+def _c2c(x, n, norm, direction):
+    inverse = direction > 0
+    if _is_torch(x):
+        import torch
+
+        if x.dtype != torch.complex64:
+            raise TypeError("neo_hip transforms complex64 (float32) data")
+        if n is not None and n != x.shape[-1]:
+            raise ValueError("device tensors: n must equal the last dimension")
+        n = x.shape[-1]
+        order = _check_size(n)
+        xc = x.resolve_conj().contiguous()
+        out = torch.empty_like(xc)
+        batch = xc.numel() // n if n else 0
+        plan = get_plan(_native.C2C, order, batch, xc.device.index or 0)
+        plan.execute_device(xc.data_ptr(), out.data_ptr(), direction,
+                            torch.cuda.current_stream(xc.device).cuda_stream)
+        s = _scale(norm, n, inverse)
+        return out if s == 1.0 else out.mul_(s)
+    a = np.asarray(x)
+    if a.dtype != np.complex64:
+        if a.dtype == np.complex128 or not np.iscomplexobj(a) and a.dtype.kind not in "fiub":
+            raise TypeError("neo_hip transforms complex64 (float32) data; complex128 is not supported on the GPU path")
+        a = a.astype(np.complex64)
+    if a.ndim == 0:
+        raise ValueError("input must have at least one dimension")
+    n = a.shape[-1] if n is None else int(n)
+    order = _check_size(n)
+    a = np.ascontiguousarray(_fit(a, n))
+    batch = a.size // n
+    out = np.empty_like(a)
+    plan = get_plan(_native.C2C, order, batch, 0)
+    plan.execute_host(a, out, direction)
+    s = _scale(norm, n, inverse)
+    if s != 1.0:
+        out *= np.float32(s)
+    return out
+
+
+def fft(x, n=None, norm="backward"):
+    """1-D forward DFT along the last axis (e^{-2 pi i nk/N})."""
+    return _c2c(x, n, norm, -1)
+
+
+def ifft(x, n=None, norm="backward"):
+    """1-D inverse DFT along the last axis; `backward` norm scales by 1/N."""
+    return _c2c(x, n, norm, +1)
+
+
+def rfft(x, n=None, norm="backward"):
+    """Real-input forward DFT: N/2+1 bins (fallback_rfft_plan semantics, packed on the GPU)."""
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+    n = a.shape[-1] if n is None else int(n)
+    order = _check_size(n)
+    a = np.ascontiguousarray(_fit(a, n))
+    batch = a.size // n
+    out = np.empty(a.shape[:-1] + (n // 2 + 1,), dtype=np.complex64)
+    get_plan(_native.R2C, order, batch, 0).execute_host(a, out, -1)
+    s = _scale(norm, n, False)
+    if s != 1.0:
+        out *= np.float32(s)
+    return out
+
+
+def irfft(x, n=None, norm="backward"):
+    """Inverse of rfft: reads N/2+1 bins (Im of DC/Nyquist ignored), returns N reals."""
+    a = np.asarray(x, dtype=np.complex64)
+    n = 2 * (a.shape[-1] - 1) if n is None else int(n)
+    order = _check_size(n)
+    need = n // 2 + 1
+    a = np.ascontiguousarray(_fit(a, need))
+    batch = a.size // need
+    out = np.empty(a.shape[:-1] + (n,), dtype=np.float32)
+    get_plan(_native.C2R, order, batch, 0).execute_host(a, out, +1)
+    s = _scale(norm, n, True)
+    if s != 1.0:
+        out *= np.float32(s)
+    return out

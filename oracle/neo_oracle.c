@@ -1,0 +1,477 @@
+/*
+ * neo_oracle.c — CPU restatement of neo-dsp's FFT + UPOLS hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. Nothing in the product (neo-dsp_amd/, include/)
+ * links, loads or calls this file; only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg do, and only as the checker / CPU baseline.
+ *
+ * Parity status: the reference itself is unbuildable in this image (its CMake
+ * FetchContent-pulls Kokkos mdspan, xsimd, Catch2; none is vendored), so
+ * oracle/_ref does not exist. This restatement is pinned instead by
+ *   (1) every known-answer / round-trip / identity test the reference's own
+ *       suite holds for this path (restated in tests/test_oracle.py), and
+ *   (2) float64 numpy/scipy truth (np.fft, direct convolution) on the golden
+ *       inputs (tests/golden/make_golden.py).
+ *
+ * Arithmetic mirrors the reference's default Linux configuration (no IPP/MKL,
+ * no xsimd): fft_plan = c2c_dit2_plan<complex<float>, c2c_dit2_v3>,
+ * rfft_plan = fallback_rfft_plan. Compile with -ffp-contract=off so that the
+ * complex multiply (ac-bd, ad+bc) is rounded exactly like std::complex<float>
+ * on x86-64 without FMA.
+ */
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORACLE_MAX_ORDER 27 /* c2c_dit2_plan.hpp:58-61 max_order() */
+
+/* ------------------------------------------------------------------------ */
+/* twiddles: src/neo/fft/twiddle.hpp:17-29 (angle computed in float)          */
+/* ------------------------------------------------------------------------ */
+static void twiddle_f(size_t size, size_t index, int dir, float* re, float* im)
+{
+    const float sign   = dir < 0 ? -1.0f : 1.0f;        /* direction::forward = -1 */
+    const float two_pi = (float)(3.14159265358979323846 * 2.0);
+    const float angle  = sign * two_pi * (float)index / (float)size;
+    *re = cosf(angle); /* std::polar<float>(1, angle) */
+    *im = sinf(angle);
+}
+
+/* twiddle.hpp:33-44 fill_twiddle_lut_radix2: lut[i] = twiddle(2*lut_size, i) */
+void oracle_twiddle_lut(int order, int dir, float* lut)
+{
+    const size_t n = (size_t)1 << order;
+    for (size_t i = 0; i < n / 2; ++i) twiddle_f(n, i, dir, &lut[2 * i], &lut[2 * i + 1]);
+}
+
+/* ------------------------------------------------------------------------ */
+/* bit reversal: src/neo/fft/reference/bitrevorder.hpp:19-32,65-77           */
+/* ------------------------------------------------------------------------ */
+static uint32_t bitrev_u32(uint32_t i, int order)
+{
+    uint32_t r = 0;
+    for (int j = 0; j < order; ++j) r |= ((i >> j) & 1u) << (order - 1 - j);
+    return r;
+}
+
+void oracle_bitrev(int order, float* x)
+{
+    const uint32_t n = 1u << order;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t j = bitrev_u32(i, order);
+        if (i < j) {
+            float t0 = x[2 * i], t1 = x[2 * i + 1];
+            x[2 * i] = x[2 * j]; x[2 * i + 1] = x[2 * j + 1];
+            x[2 * j] = t0;       x[2 * j + 1] = t1;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* radix-2 DIT: src/neo/fft/reference/kernel/c2c_dit2.hpp:122-168 (v3)        */
+/* ------------------------------------------------------------------------ */
+static void dit2_v3(int order, float* x, const float* tw)
+{
+    const size_t n = (size_t)1 << order;
+    /* stage 0, no twiddle (:133-146) */
+    for (size_t k = 0; k < n; k += 2) {
+        const float ar = x[2 * k], ai = x[2 * k + 1];
+        const float br = x[2 * k + 2], bi = x[2 * k + 3];
+        x[2 * k] = ar + br;       x[2 * k + 1] = ai + bi;
+        x[2 * k + 2] = ar - br;   x[2 * k + 3] = ai - bi;
+    }
+    /* stages 1..order-1 (:148-166) */
+    for (int stage = 1; stage < order; ++stage) {
+        const size_t len = (size_t)1 << stage, stride = len * 2;
+        const size_t tws = (size_t)1 << (order - stage - 1);
+        for (size_t k = 0; k < n; k += stride) {
+            for (size_t p = 0; p < len; ++p) {
+                const float wr = tw[2 * (p * tws)], wi = tw[2 * (p * tws) + 1];
+                const size_t i1 = k + p, i2 = k + p + len;
+                const float xr = x[2 * i2], xi = x[2 * i2 + 1];
+                const float tr = wr * xr - wi * xi; /* std::complex<float> operator* */
+                const float ti = wr * xi + wi * xr;
+                const float ar = x[2 * i1], ai = x[2 * i1 + 1];
+                x[2 * i1] = ar + tr; x[2 * i1 + 1] = ai + ti;
+                x[2 * i2] = ar - tr; x[2 * i2 + 1] = ai - ti;
+            }
+        }
+    }
+}
+
+/* c2c_dit2_plan::operator() (c2c_dit2_plan.hpp:81-95): bitrev, then kernel with
+ * the forward or backward LUT; in place; unnormalized. Returns -1 on bad order
+ * (the plan constructor throws, :97-104). */
+int oracle_fft_c2c(int order, int dir, float* x)
+{
+    if (order < 0 || order > ORACLE_MAX_ORDER) return -1;
+    if (order == 0) return 0;
+    const size_t n = (size_t)1 << order;
+    float* lut = (float*)malloc(sizeof(float) * n); /* n/2 complex */
+    if (!lut) return -2;
+    oracle_twiddle_lut(order, dir, lut);
+    oracle_bitrev(order, x);
+    dit2_v3(order, x, lut);
+    free(lut);
+    return 0;
+}
+
+/* batched convenience for the tests: `batch` contiguous transforms */
+int oracle_fft_c2c_batch(int order, int dir, float* x, size_t batch)
+{
+    const size_t n = (size_t)1 << order;
+    for (size_t b = 0; b < batch; ++b) {
+        int rc = oracle_fft_c2c(order, dir, x + 2 * n * b);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* fallback_rfft_plan: src/neo/fft/fallback/fallback_rfft_plan.hpp:27-55      */
+/* ------------------------------------------------------------------------ */
+int oracle_rfft(int order, const float* in, float* out /* n/2+1 complex */)
+{
+    const size_t n = (size_t)1 << order;
+    float* buf = (float*)calloc(2 * n, sizeof(float));
+    if (!buf) return -2;
+    for (size_t i = 0; i < n; ++i) { buf[2 * i] = in[i]; buf[2 * i + 1] = 0.0f; }
+    int rc = oracle_fft_c2c(order, -1, buf);
+    if (rc == 0) memcpy(out, buf, sizeof(float) * 2 * (n / 2 + 1));
+    free(buf);
+    return rc;
+}
+
+/* c2r: copy bins, Hermitian fill buf[i] = conj(buf[n-i]) for i >= n/2+1,
+ * backward c2c, take .real(); no 1/n. */
+int oracle_irfft(int order, const float* in /* n/2+1 complex */, float* out /* n */)
+{
+    const size_t n = (size_t)1 << order, coeffs = n / 2 + 1;
+    float* buf = (float*)calloc(2 * n, sizeof(float));
+    if (!buf) return -2;
+    memcpy(buf, in, sizeof(float) * 2 * coeffs);
+    for (size_t i = coeffs; i < n; ++i) {
+        buf[2 * i] = buf[2 * (n - i)];
+        buf[2 * i + 1] = -buf[2 * (n - i) + 1];
+    }
+    int rc = oracle_fft_c2c(order, +1, buf);
+    if (rc == 0) for (size_t i = 0; i < n; ++i) out[i] = buf[2 * i];
+    free(buf);
+    return rc;
+}
+
+/* rfft_deinterleave: src/neo/fft/rfft.hpp:41-62 */
+void oracle_rfft_deinterleave(size_t n, const float* dft, float* x, float* y)
+{
+    x[0] = dft[0]; x[1] = 0.0f;
+    y[0] = dft[1]; y[1] = 0.0f;
+    for (size_t k = 1; k < n / 2 + 1; ++k) {
+        const float zr = dft[2 * k], zi = dft[2 * k + 1];
+        const float nr = dft[2 * (n - k)], ni = -dft[2 * (n - k) + 1];
+        x[2 * k] = (zr + nr) * 0.5f;
+        x[2 * k + 1] = (zi + ni) * 0.5f;
+        /* ((zk - znk) * i) * 0.5 : (a+bi)*i = -b + ai */
+        const float dr = zr - nr, di = zi - ni;
+        y[2 * k] = (dr * 0.0f - di * -1.0f) * 0.5f;
+        y[2 * k + 1] = (dr * -1.0f + di * 0.0f) * 0.5f;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* multiply_add: src/neo/algorithm/multiply_add.hpp:279-301 (interleaved)     */
+/* and :328-368 / :60-68 (split): out = x*y + z                              */
+/* ------------------------------------------------------------------------ */
+void oracle_multiply_add(const float* x, const float* y, const float* z, float* out, size_t n)
+{
+    for (size_t i = 0; i < n; ++i) {
+        const float xr = x[2 * i], xi = x[2 * i + 1], yr = y[2 * i], yi = y[2 * i + 1];
+        const float pr = xr * yr - xi * yi, pi = xr * yi + xi * yr;
+        out[2 * i] = pr + z[2 * i];
+        out[2 * i + 1] = pi + z[2 * i + 1];
+    }
+}
+
+void oracle_split_multiply_add(const float* xr, const float* xi, const float* yr, const float* yi,
+                               const float* zr, const float* zi, float* outr, float* outi, size_t n)
+{
+    for (size_t i = 0; i < n; ++i) {
+        const float a = xr[i], b = xi[i], c = yr[i], d = yi[i];
+        outr[i] = (a * c - b * d) + zr[i];
+        outi[i] = (a * d + b * c) + zi[i];
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* normalize_impulse: src/neo/convolution/normalize_impulse.hpp:11-33 and     */
+/* src/neo/algorithm/normalize_energy.hpp:17-44 ([C][L], min factor)          */
+/* ------------------------------------------------------------------------ */
+static float energy_factor(const float* x, size_t n)
+{
+    float e = 0.0f;
+    for (size_t i = 0; i < n; ++i) e += x[i] * x[i];
+    if (e == 0.0f) return 1.0f;
+    return 1.0f / sqrtf(e);
+}
+
+void oracle_normalize_impulse(float* ir, size_t channels, size_t length)
+{
+    if (channels < 1) return;
+    float f = energy_factor(ir, length);
+    for (size_t c = 1; c < channels; ++c) {
+        const float g = energy_factor(ir + c * length, length);
+        if (g < f) f = g;
+    }
+    for (size_t i = 0; i < channels * length; ++i) ir[i] *= f;
+}
+
+/* ------------------------------------------------------------------------ */
+/* uniform_partition: src/neo/convolution/uniform_partition.hpp:12-26 →       */
+/* stft(frame=B, transform=2B, overlap=0, rectangular) stft.hpp:56-99.        */
+/* P = ceil(L/B) (stft.hpp:21-25 with overlap 0); out [C][P][B+1] complex.    */
+/* ------------------------------------------------------------------------ */
+size_t oracle_num_partitions(size_t length, size_t block)
+{
+    if (length <= block) return 1; /* the reference wraps for L < B; we clamp */
+    return (length - block + block - 1) / block + 1;
+}
+
+int oracle_uniform_partition(const float* ir, size_t channels, size_t length, size_t block, float* out)
+{
+    const size_t P = oracle_num_partitions(length, block), bins = block + 1;
+    int order = 0;
+    while (((size_t)1 << order) < 2 * block) ++order;
+    const size_t n = (size_t)1 << order;
+    float* in = (float*)malloc(sizeof(float) * n);
+    if (!in) return -2;
+    for (size_t c = 0; c < channels; ++c) {
+        for (size_t p = 0; p < P; ++p) {
+            const size_t s = p * block;
+            const size_t cnt = (length - s) < block ? (length - s) : block;
+            memset(in, 0, sizeof(float) * n);
+            for (size_t i = 0; i < cnt; ++i) in[i] = ir[c * length + s + i] * 1.0f; /* window = 1 */
+            int rc = oracle_rfft(order, in, out + 2 * bins * (c * P + p));
+            if (rc) { free(in); return rc; }
+        }
+    }
+    free(in);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* upols_convolver = uniform_partitioned_convolver<overlap_save, dense_fdl,  */
+/* dense_filter> (dense_convolver.hpp:19-20; uniform_partitioned_convolver   */
+/* .hpp:37-65; overlap_save.hpp:84-112; fdl_index.hpp:23-36)                 */
+/* ------------------------------------------------------------------------ */
+typedef struct oracle_upols {
+    size_t B, P, bins, n;
+    int order;
+    size_t write_pos;
+    float* H;       /* [P][bins] complex */
+    float* fdl;     /* [P][bins] complex */
+    float* acc;     /* [bins] complex */
+    float* window;  /* [n] real */
+    float* cbuf;    /* [n] complex: the overlap stage's complex buffer */
+    float* rbuf;    /* [n] real */
+    int split;      /* 1: split_upols_convolver (dense_split_fdl/filter) */
+    float* Hs;      /* split filter [2][P][bins] */
+    float* fdls;    /* split fdl [2][P][bins] */
+    float* accs;    /* split accumulator [2][bins] */
+} oracle_upols;
+
+oracle_upols* oracle_upols_create(size_t P, size_t bins, const float* H, int split)
+{
+    oracle_upols* u = (oracle_upols*)calloc(1, sizeof(oracle_upols));
+    if (!u) return NULL;
+    u->B = bins - 1; u->P = P; u->bins = bins; u->split = split;
+    int order = 0;
+    /* overlap_save.hpp:53: next_order(B + F - 1) with F = B */
+    while (((size_t)1 << order) < 2 * u->B - 1) ++order;
+    u->order = order; u->n = (size_t)1 << order;
+    u->H = (float*)malloc(sizeof(float) * 2 * P * bins);
+    u->fdl = (float*)calloc(2 * P * bins, sizeof(float));
+    u->acc = (float*)calloc(2 * bins, sizeof(float));
+    u->window = (float*)calloc(u->n, sizeof(float));
+    u->cbuf = (float*)calloc(2 * u->n, sizeof(float));
+    u->rbuf = (float*)calloc(u->n, sizeof(float));
+    memcpy(u->H, H, sizeof(float) * 2 * P * bins);
+    if (split) {
+        u->Hs = (float*)malloc(sizeof(float) * 2 * P * bins);
+        u->fdls = (float*)calloc(2 * P * bins, sizeof(float));
+        u->accs = (float*)calloc(2 * bins, sizeof(float));
+        for (size_t i = 0; i < P * bins; ++i) {
+            u->Hs[i] = H[2 * i];
+            u->Hs[P * bins + i] = H[2 * i + 1];
+        }
+    }
+    return u;
+}
+
+void oracle_upols_destroy(oracle_upols* u)
+{
+    if (!u) return;
+    free(u->H); free(u->fdl); free(u->acc); free(u->window); free(u->cbuf); free(u->rbuf);
+    free(u->Hs); free(u->fdls); free(u->accs);
+    free(u);
+}
+
+static void upols_callback(oracle_upols* u, float* coeffs /* bins complex, in place */)
+{
+    const size_t P = u->P, bins = u->bins, w = u->write_pos;
+    if (!u->split) {
+        memset(u->acc, 0, sizeof(float) * 2 * bins);                      /* fill(acc, 0) */
+        memcpy(u->fdl + 2 * bins * w, coeffs, sizeof(float) * 2 * bins);  /* dense_fdl::insert */
+        for (size_t s = 0; s < P; ++s) {
+            const size_t f = (w + P - s) % P;                             /* fdl_index.hpp:29 */
+            oracle_multiply_add(u->fdl + 2 * bins * s, u->H + 2 * bins * f, u->acc, u->acc, bins);
+        }
+        memcpy(coeffs, u->acc, sizeof(float) * 2 * bins);
+    } else {
+        memset(u->accs, 0, sizeof(float) * 2 * bins);
+        for (size_t i = 0; i < bins; ++i) {
+            u->fdls[w * bins + i] = coeffs[2 * i];
+            u->fdls[P * bins + w * bins + i] = coeffs[2 * i + 1];
+        }
+        for (size_t s = 0; s < P; ++s) {
+            const size_t f = (w + P - s) % P;
+            oracle_split_multiply_add(u->fdls + s * bins, u->fdls + P * bins + s * bins,
+                                      u->Hs + f * bins, u->Hs + P * bins + f * bins,
+                                      u->accs, u->accs + bins, u->accs, u->accs + bins, bins);
+        }
+        for (size_t i = 0; i < bins; ++i) {
+            coeffs[2 * i] = u->accs[i];
+            coeffs[2 * i + 1] = u->accs[bins + i];
+        }
+    }
+    if (++u->write_pos >= P) u->write_pos = 0;
+}
+
+/* one block of B samples, in place (overlap_save::operator(), :84-112) */
+int oracle_upols_process(oracle_upols* u, float* block)
+{
+    const size_t B = u->B, n = u->n;
+    /* slide_window_left + copy block -> window[n-B, n) */
+    memmove(u->window, u->window + B, sizeof(float) * (n - B));
+    memcpy(u->window + (n - B), block, sizeof(float) * B);
+    /* rfft(window -> cbuf[0:n/2+1]); the plan's internal buffer is separate */
+    int rc = oracle_rfft(u->order, u->window, u->cbuf);
+    if (rc) return rc;
+    upols_callback(u, u->cbuf);
+    rc = oracle_irfft(u->order, u->cbuf, u->rbuf);
+    if (rc) return rc;
+    const float scale = 1.0f / (float)n;
+    for (size_t i = 0; i < n; ++i) u->rbuf[i] *= scale;
+    memcpy(block, u->rbuf + (n - B), sizeof(float) * B);
+    return 0;
+}
+
+/* run `num_blocks` consecutive blocks of one channel (signal in place) */
+int oracle_upols_run(oracle_upols* u, float* signal, size_t num_blocks)
+{
+    for (size_t b = 0; b < num_blocks; ++b) {
+        int rc = oracle_upols_process(u, signal + b * u->B);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+/* no-op-callback overlap_save (overlap_test.cpp:21-53): the identity stage */
+int oracle_overlap_save_identity(size_t block, float* signal, size_t num_blocks)
+{
+    int order = 0;
+    while (((size_t)1 << order) < 2 * block - 1) ++order;
+    const size_t n = (size_t)1 << order;
+    float* window = (float*)calloc(n, sizeof(float));
+    float* cbuf = (float*)calloc(2 * n, sizeof(float));
+    float* rbuf = (float*)calloc(n, sizeof(float));
+    int rc = 0;
+    for (size_t b = 0; b < num_blocks && rc == 0; ++b) {
+        float* blk = signal + b * block;
+        memmove(window, window + block, sizeof(float) * (n - block));
+        memcpy(window + (n - block), blk, sizeof(float) * block);
+        rc = oracle_rfft(order, window, cbuf);
+        if (!rc) rc = oracle_irfft(order, cbuf, rbuf);
+        const float scale = 1.0f / (float)n;
+        for (size_t i = 0; i < n; ++i) rbuf[i] *= scale;
+        memcpy(blk, rbuf + (n - block), sizeof(float) * block);
+    }
+    free(window); free(cbuf); free(rbuf);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* multichannel harness: dense_convolve<upols_convolver>                     */
+/* (extra/plugin/src/dsp/DenseConvolution.hpp:39-70). signal/out [C][N];     */
+/* partitions [C][P][B+1] (already normalized+partitioned). Blocks outer,    */
+/* channels inner; the tail block zero-padded, output truncated to N.        */
+/* threads > 1 partitions channels across pthreads (the harness's choice).   */
+/* ------------------------------------------------------------------------ */
+#include <pthread.h>
+
+typedef struct {
+    const float* signal; float* out; const float* parts;
+    size_t C, N, P, B, c0, c1; int rc;
+} dc_job;
+
+static void* dc_worker(void* arg)
+{
+    dc_job* j = (dc_job*)arg;
+    const size_t bins = j->B + 1;
+    float* block = (float*)malloc(sizeof(float) * j->B);
+    for (size_t c = j->c0; c < j->c1 && j->rc == 0; ++c) {
+        oracle_upols* u = oracle_upols_create(j->P, bins, j->parts + 2 * bins * j->P * c, 0);
+        if (!u) { j->rc = -2; break; }
+        for (size_t i = 0; i < j->N; i += j->B) {
+            const size_t cnt = (j->N - i) < j->B ? (j->N - i) : j->B;
+            memset(block, 0, sizeof(float) * j->B);
+            memcpy(block, j->signal + c * j->N + i, sizeof(float) * cnt);
+            j->rc = oracle_upols_process(u, block);
+            memcpy(j->out + c * j->N + i, block, sizeof(float) * cnt);
+        }
+        oracle_upols_destroy(u);
+    }
+    free(block);
+    return NULL;
+}
+
+int oracle_dense_convolve(const float* signal, float* out, const float* parts,
+                          size_t C, size_t N, size_t P, size_t B, int threads)
+{
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > C) threads = (int)C;
+    pthread_t tid[256];
+    dc_job jobs[256];
+    if (threads > 256) threads = 256;
+    for (int t = 0; t < threads; ++t) {
+        jobs[t] = (dc_job){signal, out, parts, C, N, P, B, C * t / threads, C * (t + 1) / threads, 0};
+        if (threads == 1) dc_worker(&jobs[t]);
+        else pthread_create(&tid[t], NULL, dc_worker, &jobs[t]);
+    }
+    int rc = 0;
+    for (int t = 0; t < threads; ++t) {
+        if (threads > 1) pthread_join(tid[t], NULL);
+        if (jobs[t].rc) rc = jobs[t].rc;
+    }
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* splitmix64 -> U[-1,1) float32 (the documented generator)      */
+/* ------------------------------------------------------------------------ */
+static uint64_t splitmix64(uint64_t* s)
+{
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void oracle_noise(uint64_t seed, float* out, size_t n)
+{
+    uint64_t s = seed;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t r = splitmix64(&s) >> 40; /* 24 random bits */
+        out[i] = (float)r * (2.0f / 16777216.0f) - 1.0f;
+    }
+}

@@ -1,0 +1,83 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly
+the symbols include/neo_hip.h declares, validates arguments before touching a
+device, and the Python mirror binds every one of them."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "neo_hip.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"NEO_HIP_API\s+[^;(]*?\b(neo_hip_\w+)\s*\(", txt)))
+
+
+def test_header_declares_api():
+    syms = declared_symbols()
+    assert "neo_hip_fft_plan_create" in syms and "neo_hip_upols_process" in syms
+    assert len(syms) >= 20
+
+
+def test_library_exports_every_declared_symbol():
+    import neo
+
+    lib = neo._native.LIB_PATH
+    assert os.path.exists(lib), "build libneo_hip.so first (make -C neo-dsp_amd)"
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (neo_hip_\w+)", out))
+    assert set(declared_symbols()) == exported
+    # and the Python binding covers them all
+    assert set(neo._native.SIGNATURES) == exported
+    neo._native.load()
+
+
+def test_host_validation_without_gpu():
+    import neo
+
+    lib = neo._native.load()
+    h = ctypes.c_void_p()
+    assert lib.neo_hip_fft_plan_create(28, 1, 0, 0, ctypes.byref(h)) == neo._native.NEO_HIP_EINVAL
+    assert b"unsupported order" in lib.neo_hip_last_error()
+    assert lib.neo_hip_fft_plan_create(4, 0, 0, 0, ctypes.byref(h)) == neo._native.NEO_HIP_EINVAL
+    assert lib.neo_hip_upols_create(1, 500, 3, 0, ctypes.byref(h)) == neo._native.NEO_HIP_EINVAL
+    assert lib.neo_hip_upols_create(0, 512, 3, 0, ctypes.byref(h)) == neo._native.NEO_HIP_EINVAL
+    assert lib.neo_hip_fft_max_order() == 27
+    assert lib.neo_hip_version() >= 100
+    with pytest.raises(neo._native.NeoHipError):
+        neo.fft.FFTPlan(0, 28)
+
+
+def test_num_partitions_matches_reference_formula(oracle):
+    import neo
+
+    for L, B in [(4096, 128), (4095, 128), (480000, 512), (480000, 256), (96000, 512), (1, 64), (64, 64), (65, 64)]:
+        assert neo.num_partitions(L, B) == oracle.num_partitions(L, B)
+    assert neo.num_partitions(480000, 512) == 938 and neo.num_partitions(480000, 256) == 1875
+    assert neo.num_partitions(96000, 512) == 188
+
+
+def test_python_fft_helpers():
+    import neo
+
+    assert neo.fft.next_order(1024) == 10 and neo.fft.next_order(1025) == 11 and neo.fft.next_order(1) == 0
+    assert neo.fft.size(12) == 4096
+    with pytest.raises(RuntimeError):
+        neo.fft._check_size(12)
+
+
+def test_no_cpu_fallback_without_gpu():
+    """The product path fails loudly when no device is present (this container)."""
+    import neo
+
+    if neo._native.device_count() > 0:
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        neo.fft.fft(np.zeros(8, np.complex64))
+    with pytest.raises(RuntimeError):
+        neo.UpolsConvolver(1, 128, 2)

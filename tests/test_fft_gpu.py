@@ -1,0 +1,160 @@
+"""GPU parity of the FFT path (libneo_hip.so via the C-ABI) against the CPU
+restatement of c2c_dit2_plan / fallback_rfft_plan and the golden fixtures.
+
+Tolerance (BASELINE.json north_star, float32): peak-normalized max error
+max|y - ref| / max|ref| <= 1e-5, plus the reference's own allclose abs 1e-5
+(src/neo/algorithm/allclose.hpp:36-39) on round trips."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import peak_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def cnoise(oracle, seed, shape):
+    n = int(np.prod(shape))
+    return oracle.noise(seed, 2 * n).view(np.complex64).reshape(shape)
+
+
+@pytest.mark.parametrize("order", range(0, 15))
+@pytest.mark.parametrize("direction", [-1, 1])
+def test_c2c_vs_oracle(neo_gpu, oracle, order, direction):
+    x = cnoise(oracle, 100 + order, (3, 1 << order))
+    ref = oracle.fft(x, direction)
+    y = neo_gpu.fft.fft(x) if direction < 0 else neo_gpu.fft.ifft(x, norm="forward")
+    assert peak_err(y, ref) <= TOL
+
+
+@pytest.mark.parametrize("order", [15, 16, 17, 20])
+def test_c2c_large_vs_oracle(neo_gpu, oracle, order):
+    x = cnoise(oracle, 200 + order, (1 << order,))
+    for d in (-1, 1):
+        ref = oracle.fft(x, d)
+        y = neo_gpu.fft.fft(x) if d < 0 else neo_gpu.fft.ifft(x, norm="forward")
+        assert peak_err(y, ref) <= TOL
+
+
+@pytest.mark.parametrize("order", list(range(2, 15)) + [16, 18])
+def test_round_trip(neo_gpu, oracle, order):
+    """fft_test.cpp:79-91: fft -> ifft -> scale(1/N) == x within abs 1e-5."""
+    x = cnoise(oracle, 300 + order, (1 << order,))
+    y = neo_gpu.fft.ifft(neo_gpu.fft.fft(x))
+    assert np.abs(y - x).max() <= 1e-5
+
+
+def test_known_answer(neo_gpu):
+    """rfft_test.cpp:170-186: FFT([1,2,3,4]) = [10, -2+2i, -2, -2-2i]; impulse -> ones."""
+    y = neo_gpu.fft.fft(np.array([1, 2, 3, 4], np.complex64))
+    np.testing.assert_allclose(y, [10, -2 + 2j, -2, -2 - 2j], atol=1e-6)
+    for order in range(2, 9):
+        imp = np.zeros(1 << order, np.complex64)
+        imp[0] = 1
+        np.testing.assert_allclose(neo_gpu.fft.fft(imp), np.ones(1 << order), atol=1e-6)
+
+
+def test_python_api_contract(neo_gpu):
+    """extra/python/test/test.py:10-18 and main.cpp:135-139."""
+    for n in [4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096]:
+        assert neo_gpu.fft.fft(np.zeros(n, np.complex64)).shape == (n,)
+        imp = np.zeros(n, np.complex64)
+        imp[0] = 1
+        assert np.allclose(neo_gpu.fft.ifft(neo_gpu.fft.fft(imp.copy())), imp)
+    with pytest.raises(RuntimeError):
+        neo_gpu.fft.fft(np.zeros(12, np.complex64))
+    with pytest.raises(RuntimeError):
+        neo_gpu.fft.FFTPlan(0, 28)  # order > max_order throws (fft_test.cpp:62-67)
+    x = np.arange(8).astype(np.complex64)
+    np.testing.assert_allclose(neo_gpu.fft.fft(x, norm="ortho"), np.fft.fft(x, norm="ortho"), atol=1e-5)
+    np.testing.assert_allclose(neo_gpu.fft.fft(x, norm="forward"), np.fft.fft(x, norm="forward"), atol=1e-6)
+
+
+def test_golden_c2c(neo_gpu):
+    g = np.load(os.path.join(GOLD, "c2c_1024_seed1.npz"))
+    assert peak_err(neo_gpu.fft.fft(g["x"]), g["fwd"]) <= TOL
+    assert peak_err(neo_gpu.fft.ifft(g["fwd"], norm="forward"), g["bwd"]) <= TOL
+    g = np.load(os.path.join(GOLD, "c2c_4096x8_seed2.npz"))
+    assert peak_err(neo_gpu.fft.fft(g["x"]), g["fwd"]) <= TOL
+
+
+@pytest.mark.parametrize("order", list(range(0, 15)) + [15, 17])
+def test_rfft_irfft_vs_oracle(neo_gpu, oracle, order):
+    n = 1 << order
+    x = oracle.noise(400 + order, 2 * n).reshape(2, n)
+    R = neo_gpu.fft.rfft(x)
+    ref = oracle.rfft(x)
+    assert R.shape == (2, n // 2 + 1)
+    assert peak_err(R, ref) <= TOL
+    back = neo_gpu.fft.irfft(R, n, norm="forward")  # unnormalized c2r
+    assert peak_err(back, oracle.irfft(ref, n)) <= TOL
+    # round trip rfft_test.cpp:40-71
+    assert np.abs(back / n - x).max() <= 1e-5
+
+
+def test_irfft_ignores_dc_nyquist_imag(neo_gpu, oracle):
+    """fallback_rfft_plan c2r takes .real() of a Hermitian-filled buffer: Im(DC), Im(Nyq) drop out."""
+    n = 256
+    X = oracle.rfft(oracle.noise(7, n))
+    X2 = X.copy()
+    X2[0] += 0.5j
+    X2[-1] -= 0.25j
+    a = neo_gpu.fft.irfft(X, n, norm="forward")
+    b = neo_gpu.fft.irfft(X2, n, norm="forward")
+    assert peak_err(b, oracle.irfft(X2, n)) <= TOL
+    assert np.abs(a - b).max() <= 1e-5 * np.abs(a).max()
+
+
+@pytest.mark.parametrize("order", [4, 5, 6, 7, 8])
+def test_rfft_deinterleave_cross_check(neo_gpu, oracle, order):
+    """rfft_test.cpp:80-126: two reals packed into one c2c, split by rfft_deinterleave,
+    equal two rffts (pins bin layout and sign convention against c2c)."""
+    n = 1 << order
+    a, b = oracle.noise(500, n), oracle.noise(501, n)
+    z = neo_gpu.fft.fft((a + 1j * b).astype(np.complex64))
+    ca, cb = oracle.rfft_deinterleave(z)
+    assert np.abs(ca - neo_gpu.fft.rfft(a)).max() <= 1e-5 * n
+    assert np.abs(cb - neo_gpu.fft.rfft(b)).max() <= 1e-5 * n
+
+
+def test_golden_rfft(neo_gpu):
+    for n in (512, 1024):
+        g = np.load(os.path.join(GOLD, f"rfft_{n}_seed3.npz"))
+        assert peak_err(neo_gpu.fft.rfft(g["x"]), g["r2c"]) <= TOL
+        assert peak_err(neo_gpu.fft.irfft(g["r2c"], n, norm="forward"), g["c2r"]) <= TOL
+
+
+def test_inplace_device(neo_gpu, oracle):
+    torch = pytest.importorskip("torch")
+    x = cnoise(oracle, 600, (16, 4096))
+    t = torch.from_numpy(x).cuda()
+    plan = neo_gpu.fft.get_plan(0, 12, 16)
+    plan.execute_device(t.data_ptr(), t.data_ptr(), -1, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert peak_err(t.cpu().numpy(), oracle.fft(x)) <= TOL
+
+
+def test_c2_full_shape_properties(neo_gpu, oracle):
+    """C2 (4096 x 65536) at full size: spot rows vs the oracle, the round trip, Parseval,
+    and linearity hold on every transform (size-independent checks)."""
+    torch = pytest.importorskip("torch")
+    B, N = 65536, 4096
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = (torch.rand((B, N, 2), generator=g, device="cuda") * 2 - 1).contiguous()
+    xc = torch.view_as_complex(x)
+    y = neo_gpu.fft.fft(xc)
+    rows = [0, 1, 4095, 32768, 65535]
+    for r in rows:
+        ref = oracle.fft(xc[r].cpu().numpy())
+        assert peak_err(y[r].cpu().numpy(), ref) <= TOL
+    e_x = (xc.abs() ** 2).sum(dim=1).double()
+    e_y = (y.abs() ** 2).sum(dim=1).double() / N
+    assert torch.max(torch.abs(e_y / e_x - 1)).item() < 1e-5
+    back = neo_gpu.fft.ifft(y)
+    assert torch.max(torch.abs(back - xc)).item() < 1e-5
+    y2 = neo_gpu.fft.fft(xc * 2 + xc.conj())
+    lin = y * 2 + neo_gpu.fft.fft(xc.conj())
+    assert (torch.max(torch.abs(y2 - lin)) / torch.max(torch.abs(lin))).item() < 1e-5

@@ -1,0 +1,191 @@
+"""GPU parity of the UPOLS path (libneo_hip.so via the C-ABI) against the CPU
+restatement of upols_convolver / dense_convolve and the golden fixtures.
+
+Tolerance (BASELINE.json north_star: <= 1e-5 rel, float32) read as SURVEY §8(a):
+max|y - y_ref| / max|y_ref| <= 1e-5 (peak-normalized), plus the reference's
+per-sample abs 1e-5 on the identity tests (uniform_partitioned_convolver_test.cpp:74)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import peak_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def identity_impulse(B, n):
+    """generate_identity_impulse (src/neo/testing/testing.hpp:74-82)."""
+    h = np.zeros((n, B + 1), np.complex64)
+    h[0] = 1
+    return h
+
+
+@pytest.mark.parametrize("B", [128, 256, 512, 1024])
+def test_identity_ir(neo_gpu, oracle, B):
+    """uniform_partitioned_convolver_test.cpp:35-75: identity IR, 20 noise blocks, out == in."""
+    sig = oracle.noise(11, B * 20)
+    conv = neo_gpu.upols_convolver()
+    conv.filter(identity_impulse(B, 3))
+    out = sig.copy()
+    for i in range(0, len(out), B):
+        blk = np.ascontiguousarray(out[i:i + B])
+        conv(blk)
+        out[i:i + B] = blk
+    assert np.abs(out - sig).max() <= 1e-5
+
+
+@pytest.mark.parametrize("B,L,C,nb", [(512, 4096, 1, 40), (256, 2560, 2, 40), (128, 1000, 3, 30),
+                                      (16, 100, 2, 20), (64, 64, 1, 10), (1024, 5000, 2, 12),
+                                      (2048, 9000, 1, 6), (4096, 12000, 1, 5), (32, 7, 1, 8)])
+def test_random_ir_vs_oracle(neo_gpu, oracle, B, L, C, nb):
+    ir = np.stack([oracle.noise(20 + c, L) for c in range(C)])
+    irn = oracle.normalize_impulse(ir)
+    parts = oracle.uniform_partition(irn, B)
+    sig = np.stack([oracle.noise(30 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts)
+    got = neo_gpu.dense_convolve(sig, ir, B)
+    assert peak_err(got, ref) <= TOL
+    assert np.abs(got - ref).max() <= 1e-5
+
+
+@pytest.mark.parametrize("name", ["upols_b512_l4096_seed5", "upols_b256_l2560_2ch_seed6",
+                                  "upols_b512_l96000_seed7"])
+def test_golden_upols(neo_gpu, name):
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    B = 256 if "b256" in name else 512
+    got = neo_gpu.dense_convolve(g["signal"], g["ir"], B)
+    assert peak_err(got, g["out"]) <= TOL
+    assert np.abs(got - g["out"]).max() <= 1e-5
+
+
+def test_uniform_partition_vs_oracle(neo_gpu, oracle):
+    g = np.load(os.path.join(GOLD, "partition_seed4.npz"))
+    H = neo_gpu.uniform_partition(g["ir"][None], 256)
+    assert H.shape == (1, 12, 257)
+    assert peak_err(H, g["H"]) <= TOL
+    H2 = neo_gpu.uniform_partition(g["ir2_norm"], 128)
+    assert peak_err(H2, g["H2"]) <= TOL
+    # uniform_partition_test.cpp:8-37 shapes
+    for C, L in [(1, 4096), (2, 4096), (2, 4095)]:
+        assert neo_gpu.uniform_partition(np.zeros((C, L), np.float32), 128).shape == (C, 32, 129)
+
+
+def test_normalize_impulse_bit_exact(neo_gpu, oracle):
+    """Sequential float energy (normalize_energy.hpp:21-33): the GPU rounds identically."""
+    ir = np.stack([oracle.noise(50 + c, 48000) * (c + 1) for c in range(4)]).astype(np.float32)
+    ref = oracle.normalize_impulse(ir)
+    got = ir.copy()
+    neo_gpu.normalize_impulse(got)
+    assert np.array_equal(got, ref)
+    # normalize_impulse_test.cpp:13-56 known answers
+    v = np.zeros(33, np.float32)
+    v[0] = 2
+    neo_gpu.normalize_impulse(v)
+    assert v[0] == pytest.approx(1.0)
+    v[0] = v[1] = 2
+    neo_gpu.normalize_impulse(v)
+    assert v[0] == pytest.approx(0.707106782) and v[1] == pytest.approx(0.707106782)
+    m = np.zeros((33, 66), np.float32)
+    m[0, 0] = 2
+    neo_gpu.normalize_impulse(m)
+    assert m[0, 0] == pytest.approx(1.0)
+
+
+def test_ring_order_delay(neo_gpu, oracle):
+    """fdl_index ring (fdl_index.hpp:23-36): a filter whose only nonzero partition is p
+    delays the input by exactly p blocks."""
+    B, P = 128, 5
+    sig = oracle.noise(60, B * 16)
+    for p in range(P):
+        H = np.zeros((P, B + 1), np.complex64)
+        H[p] = 1
+        c = neo_gpu.UpolsConvolver(1, B, P)
+        c.filter(H[None])
+        out = np.empty_like(sig)
+        for t in range(16):
+            blk = np.ascontiguousarray(sig[t * B:(t + 1) * B][None])
+            c(blk)
+            out[t * B:(t + 1) * B] = blk[0]
+        expect = np.concatenate([np.zeros(p * B, np.float32), sig[: len(sig) - p * B]])
+        assert np.abs(out - expect).max() <= 1e-5, p
+
+
+def test_set_filter_equals_set_impulse_and_reset(neo_gpu, oracle):
+    B, L, C = 256, 3000, 3
+    ir = np.stack([oracle.noise(70 + c, L) for c in range(C)])
+    P = neo_gpu.num_partitions(L, B)
+    a = neo_gpu.UpolsConvolver(C, B, P)
+    b = neo_gpu.UpolsConvolver(C, B, P)
+    a.set_impulse(ir, normalize=True)
+    b.filter(oracle.uniform_partition(oracle.normalize_impulse(ir), B))
+    blocks = [np.ascontiguousarray(np.stack([oracle.noise(80 + 10 * t + c, B) for c in range(C)])) for t in range(12)]
+    ya = [a(x.copy()) for x in blocks]
+    yb = [b(x.copy()) for x in blocks]
+    assert max(np.abs(p - q).max() for p, q in zip(ya, yb)) <= 1e-5
+    a.reset()
+    ya2 = [a(x.copy()) for x in blocks]
+    assert max(np.abs(p - q).max() for p, q in zip(ya, ya2)) == 0.0  # deterministic after reset
+
+
+def test_errors(neo_gpu):
+    with pytest.raises(RuntimeError):
+        neo_gpu.UpolsConvolver(1, 500, 4)  # not a power of two
+    with pytest.raises(RuntimeError):
+        neo_gpu.UpolsConvolver(0, 512, 4)
+    c = neo_gpu.UpolsConvolver(2, 128, 3)
+    with pytest.raises(ValueError):
+        c.filter(np.zeros((2, 4, 129), np.complex64))
+    with pytest.raises(RuntimeError):
+        c.set_impulse(np.zeros((2, 1000), np.float32))  # 8 partitions != 3
+
+
+def test_device_blocks_match_host_blocks(neo_gpu, oracle):
+    torch = pytest.importorskip("torch")
+    B, L, C, nb = 512, 20000, 4, 24
+    ir = np.stack([oracle.noise(90 + c, L) for c in range(C)])
+    sig = np.stack([oracle.noise(95 + c, B * nb) for c in range(C)])
+    ref = neo_gpu.dense_convolve(sig, ir, B)
+    P = neo_gpu.num_partitions(L, B)
+    conv = neo_gpu.UpolsConvolver(C, B, P)
+    conv.set_impulse(torch.from_numpy(ir).cuda(), normalize=True)
+    t = torch.from_numpy(sig).cuda()
+    out = torch.empty_like(t)
+    conv.process_blocks(t, out)
+    torch.cuda.synchronize()
+    assert np.abs(out.cpu().numpy() - ref).max() == 0.0
+    conv.reset()
+    conv.process_blocks(t)  # in place
+    torch.cuda.synchronize()
+    assert np.abs(t.cpu().numpy() - ref).max() == 0.0
+
+
+@pytest.mark.parametrize("C,B,L", [(256, 256, 480000), (256, 512, 480000)])
+def test_full_size_properties(neo_gpu, oracle, C, B, L):
+    """C4 / C5-per-GPU shapes at full size: (a) three channels spot-checked against the
+    oracle over the first blocks, (b) linearity over the whole multichannel state."""
+    torch = pytest.importorskip("torch")
+    nb = 6
+    g = torch.Generator(device="cuda").manual_seed(C + B)
+    ir = (torch.rand((C, L), generator=g, device="cuda") * 2 - 1).contiguous()
+    x = (torch.rand((C, B * nb), generator=g, device="cuda") * 2 - 1).contiguous()
+    y = (torch.rand((C, B * nb), generator=g, device="cuda") * 2 - 1).contiguous()
+    P = neo_gpu.num_partitions(L, B)
+    conv = neo_gpu.UpolsConvolver(C, B, P)
+    conv.set_impulse(ir, normalize=True)
+    ox = conv.process_blocks(x.clone())
+    conv.reset()
+    oy = conv.process_blocks(y.clone())
+    conv.reset()
+    oxy = conv.process_blocks((0.5 * x + y).contiguous())
+    torch.cuda.synchronize()
+    lin = 0.5 * ox + oy
+    assert (torch.max(torch.abs(oxy - lin)) / torch.max(torch.abs(lin))).item() <= 1e-5
+    irh = oracle.normalize_impulse(ir.cpu().numpy())
+    xh = x.cpu().numpy()
+    for c in (0, C // 2, C - 1):
+        parts = oracle.uniform_partition(irh[c:c + 1], B)
+        ref = oracle.dense_convolve(xh[c:c + 1], parts)
+        assert peak_err(ox[c].cpu().numpy(), ref[0]) <= TOL
