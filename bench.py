@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""bench.py — MI355X throughput of neo's UPOLS convolver (and FFT) hot path.
+
+Headline (BASELINE.json metric "Msamples/sec UPOLS convolver (block=512,
+IR=10s@48k); achieved HBM GB/s"): configs[4], the 2048-channel UPOLS sharded by
+channel across GPUs — 256 channels per GPU, B = 512, L = 480000 taps (P = 938).
+At N = 1 that is one GPU's shard; at N GPUs, N x 256 channels (weak scaling; the
+channels are independent, so there is no collective on the data path — torch
+.distributed (gloo) only carries the timing barrier and the max-over-ranks).
+
+A "step" = one block of B samples through the whole convolver for every channel
+(r2c + FDL insert + partitioned MAC + c2r), inputs already resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c4|c3|c2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "neo-dsp_amd")]
+
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    # name: (channels per GPU, block, taps)
+    "c5": (256, 512, 480000),  # headline: 2048 ch / 8 GPUs, B=512, IR 10 s @ 48 kHz
+    "c4": (256, 256, 480000),  # 256 ch, B=256, IR 10 s @ 48 kHz
+    "c3": (1, 512, 96000),     # 1 ch, B=512, IR 2 s @ 48 kHz
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS) + ["c2"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_pmc_traffic(workload: str):
+    """HBM bytes per MAC launch from the committed rocprofv3 --pmc summary (separate
+    passes; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+                return float(d["hbm_bytes_per_launch"])
+        except (OSError, ValueError):
+            continue
+    return None
+
+
+def cpu_baseline_upols(C, B, L, threads):
+    """The oracle's restatement of dense_convolve<upols_convolver> (kind "port") on a
+    bounded sample of the same workload, on this box's host cores."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    cs, nb = 64, 160  # 64 channels x 160 blocks ~ 10 CPU-seconds at ~1 ms per channel-block
+    cs = min(cs, max(C, 1) * 64)
+    ir = np.stack([O.noise(8 + c, L) for c in range(cs)])
+    parts = O.uniform_partition(O.normalize_impulse(ir), B)
+    sig = np.stack([O.noise(7000 + c, B * nb) for c in range(cs)])
+    th = max(1, min(threads, cs))
+    t0 = time.perf_counter()
+    O.dense_convolve(sig, parts, threads=th)
+    dt = time.perf_counter() - t0
+    return {"value": cs * nb * B / dt / 1e6, "unit": "Msamples/s", "cores": th, "kind": "port",
+            "sample": f"{cs} ch x {nb} blocks of B={B}, L={L} (P={parts.shape[1]}), oracle dense_convolve "
+                      f"(c2c_dit2 r2c/c2r + scalar complex MAC), {th} threads, {dt:.2f} s wall"}
+
+
+def cpu_baseline_fft(threads):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    nb = 1024
+    x = O.noise(2, 2 * 4096 * nb).view(np.complex64).reshape(nb, 4096)
+    t0 = time.perf_counter()
+    O.fft(x)
+    dt = time.perf_counter() - t0
+    return {"value": nb * 4096 / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": f"{nb} of the 65536 4096-pt transforms, oracle c2c_dit2 (bitrev + radix-2), 1 thread, "
+                      f"{dt:.2f} s; scales linearly with batch"}
+
+
+def run_upols(args, world, rank, local):
+    import torch
+    import neo
+
+    C, B, L = WORKLOADS[args.workload]
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    P = neo.num_partitions(L, B)
+    conv = neo.UpolsConvolver(C, B, P, device=local)
+    g = torch.Generator(device=dev).manual_seed(8 + rank)
+    ir = torch.rand((C, L), generator=g, device=dev).mul_(2).sub_(1)  # synthetic white-noise IR
+    conv.set_impulse(ir, normalize=True)
+    del ir
+    nblk = args.warmup + args.steps
+    x = torch.rand((C, nblk * B), generator=g, device=dev).mul_(2).sub_(1)
+    y = torch.empty_like(x)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ld = x.shape[1]
+    xp, yp = x.data_ptr(), y.data_ptr()
+
+    for t in range(args.warmup):
+        conv.process_device(xp + 4 * t * B, ld, yp + 4 * t * B, ld, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    conv.timing()  # drain
+    conv.set_timing(True)
+    t0 = time.perf_counter()
+    for t in range(args.warmup, nblk):
+        conv.process_device(xp + 4 * t * B, ld, yp + 4 * t * B, ld, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    conv.set_timing(False)
+    mac_ms, launches = conv.timing()
+    assert torch.isfinite(y[:, args.warmup * B:]).all().item()
+    elapsed = max_over_ranks(t1 - t0, world)
+    mac_avg_ms = max_over_ranks(mac_ms / max(launches, 1), world)
+
+    samples = world * C * B * args.steps
+    bytes_mac = C * (16 * P * B + 20 * B)  # filter + FDL stream (packed bins) + FDL row write + in/prev
+    achieved = bytes_mac / (mac_avg_ms * 1e-3) / 1e9
+    res = {
+        "metric": "Msamples/sec UPOLS convolver (block=512, IR=10s@48k); achieved HBM GB/s",
+        "value": samples / elapsed / 1e6,
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (U[-1,1) white-noise input and IR, torch.rand on device)",
+        "config": {"workload": f"UPOLS {args.workload}: {C} ch/GPU x {world} GPU, B={B}, L={L} taps (P={P}), "
+                               f"channel-sharded",
+                   "channels_per_gpu": C, "channels_total": C * world, "block": B, "taps": L, "partitions": P,
+                   "splits": conv.splits, "parallelism": f"channel-shard x{world} (no collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": load_pmc_traffic(args.workload),
+                     "kernel": f"k_upols_mac<{B}>", "kernel_avg_ms": mac_avg_ms,
+                     "algorithmic_bytes_per_launch": bytes_mac},
+        "effective_hbm_gbs_step": bytes_mac * world / (elapsed / args.steps) / 1e9 / world,
+    }
+    if args.workload == "c3":
+        res["roofline"]["note"] = "working set L2/MALL-resident: effective GB/s, launch-latency bound"
+    return res
+
+
+def run_fft(args, world, rank, local):
+    import torch
+    import neo
+
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    N, batch = 4096, 65536
+    g = torch.Generator(device=dev).manual_seed(2 + rank)
+    x = torch.view_as_complex(torch.rand((batch, N, 2), generator=g, device=dev).mul_(2).sub_(1))
+    y = torch.empty_like(x)
+    plan = neo.fft.FFTPlan(0, 12, batch, device=local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(args.warmup):
+        plan.execute_device(x.data_ptr(), y.data_ptr(), -1, stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record()
+        plan.execute_device(x.data_ptr(), y.data_ptr(), -1, stream)
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    kms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    elapsed = max_over_ranks(t1 - t0, world)
+    kms = max_over_ranks(kms, world)
+    bytes_launch = 16 * N * batch
+    achieved = bytes_launch / (kms * 1e-3) / 1e9
+    return {
+        "metric": "Msamples/sec batched c2c FFT 4096 x 65536 (complex points per transform)",
+        "value": world * N * batch * args.steps / elapsed / 1e6,
+        "unit": "Msamples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (U[-1,1) complex, torch.rand on device)",
+        "config": {"workload": "C2 batched c2c FFT, N=4096, batch 65536 per GPU, out of place",
+                   "parallelism": f"batch-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": load_pmc_traffic("c2"),
+                     "kernel": "k_c2c_lds<4096,-1>", "kernel_avg_ms": kms, "algorithmic_bytes_per_launch": bytes_launch},
+    }
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    if args.workload == "c2":
+        res = run_fft(args, world, rank, local)
+    else:
+        res = run_upols(args, world, rank, local)
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            C, B, L = WORKLOADS.get(args.workload, (0, 0, 0))
+            res["cpu_baseline"] = (cpu_baseline_fft(args.cpu_threads) if args.workload == "c2"
+                                   else cpu_baseline_upols(C, B, L, args.cpu_threads))
+            try:
+                import platform
+
+                model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")]
+                res["cpu_baseline"]["host_cpu"] = (model[0] if model else platform.processor())
+            except OSError:
+                pass
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -62,8 +62,8 @@ NEO_HIP_API int neo_hip_device_count(int* count);
 NEO_HIP_API int neo_hip_fft_max_order(void);
 NEO_HIP_API int neo_hip_fft_plan_create(int order, int64_t batch, int kind, int device, neo_hip_fft_plan** plan);
 NEO_HIP_API int neo_hip_fft_plan_destroy(neo_hip_fft_plan* plan);
-/* Device pointers, asynchronous on `stream` (hipStream_t, NULL = the plan's
- * own stream). c2c: in/out [batch][N] complex (in == out allowed).
+/* Device pointers, asynchronous on `stream` (a hipStream_t; NULL = the HIP
+ * null stream, which is also torch's default stream). c2c: in/out [batch][N] complex (in == out allowed).
  * r2c: in [batch][N] float, out [batch][N/2+1] complex.
  * c2r: in [batch][N/2+1] complex, out [batch][N] float. `direction` is used by
  * c2c only (r2c is forward, c2r backward, as in fallback_rfft_plan). */
@@ -87,10 +87,12 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
 /* normalize_impulse + uniform_partition of ir [C][L] float straight into the
  * convolver (setup path, DenseConvolution.cpp:78-108); host or device memory. */
 NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int64_t length, int normalize, int is_device);
-/* one block for all channels, in place: io [C][B] float (host: synchronous). */
+/* one block for all channels, in place: io [C][B] float. Host memory: staged
+ * through pinned buffers, synchronous (own stream if `stream` is NULL). Device
+ * memory: same as process_device on `stream`. */
 NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_device, void* stream);
 /* one block, device pointers, channel c at in + c*ld_in / out + c*ld_out
- * (in == out allowed); asynchronous on `stream`. */
+ * (in == out allowed); asynchronous on `stream` (NULL = HIP null stream). */
 NEO_HIP_API int neo_hip_upols_process_device(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
                                              int64_t ld_out, void* stream);
 /* nblocks consecutive blocks: channel c samples at in + c*ld + t*B. */

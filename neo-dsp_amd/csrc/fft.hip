@@ -390,7 +390,7 @@ NEO_HIP_API int neo_hip_fft_plan_create(int order, int64_t batch, int kind, int 
         free_plan(p);
         return code;
     };
-    if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&p->stream, hipStreamDefault) != hipSuccess)
         return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
     const int io = inner_order(p);
     if (io >= 0 && io <= kLdsMaxOrder) {
@@ -436,7 +436,7 @@ NEO_HIP_API int neo_hip_fft_execute(neo_hip_fft_plan* p, const void* in, void* o
         return fail(NEO_HIP_EINVAL, "direction must be -1 (forward) or +1 (backward)");
     device_guard g(p->device);
     if (g.rc) return g.rc;
-    hipStream_t s = stream ? as_stream(stream) : p->stream;
+    hipStream_t s = as_stream(stream);  // NULL = the HIP null stream (torch's default stream)
     const int io = inner_order(p);
     if (p->kind == NEO_HIP_C2C) {
         const cf* ci = static_cast<const cf*>(in);

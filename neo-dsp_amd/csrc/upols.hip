@@ -105,10 +105,10 @@ __global__ __launch_bounds__(256) void k_upols_mac(const float* __restrict__ in,
                                                    int S, int rows)
 {
     using K = upols_cfg<B>;
-    __shared__ cf xnew[B];
+    __shared__ __attribute__((aligned(16))) cf xnew[B];
     __shared__ cf fft[K::LL];
     __shared__ cf tw[K::TW1 + K::TW2];
-    __shared__ float4 red[K::RPI > 1 ? 256 * 2 * K::VPT : 1];
+    __shared__ __attribute__((aligned(16))) float4 red[K::RPI > 1 ? 256 * 2 * K::VPT : 1];
 
     const int tid = threadIdx.x;
     const int c = blockIdx.x / S, s = blockIdx.x - c * S;
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void k_upols_out(const cf* __restrict__ part, 
                                                    int* __restrict__ wp_dev, const cf* __restrict__ twg, int P, int S)
 {
     using K = upols_cfg<B>;
-    __shared__ cf X[B];
+    __shared__ __attribute__((aligned(16))) cf X[B];
     __shared__ cf fft[K::LL];
     __shared__ cf tw[K::TW1 + K::TW2];
     const int tid = threadIdx.x, c = blockIdx.x;
@@ -525,7 +525,7 @@ NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, in
         destroy(h);
         return code;
     };
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamDefault) != hipSuccess)
         return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
     if (hipMalloc(reinterpret_cast<void**>(&h->H), nrows * rowbytes) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->fdl), nrows * rowbytes) != hipSuccess ||
@@ -565,6 +565,7 @@ NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h)
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     device_guard g(h->device);
+    NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
     int rc = reset_state(h, h->stream);
     if (rc) return rc;
     NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
@@ -576,6 +577,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
     if (!h || !filter) return fail(NEO_HIP_EINVAL, "null handle or filter");
     device_guard g(h->device);
     if (g.rc) return g.rc;
+    NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
     const int64_t rows = int64_t(h->C) * h->P;
     const size_t bytes = size_t(rows) * size_t(h->B + 1) * sizeof(cf);
     const cf* src = static_cast<const cf*>(filter);
@@ -604,6 +606,7 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
                     (long long)partitions_for(length, h->B), h->P);
     device_guard g(h->device);
     if (g.rc) return g.rc;
+    NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
     const size_t bytes = size_t(h->C) * size_t(length) * sizeof(float);
     float* d = nullptr;
     NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), bytes));
@@ -628,7 +631,7 @@ NEO_HIP_API int neo_hip_upols_process_device(neo_hip_upols* h, const float* in, 
         return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
     device_guard g(h->device);
     if (g.rc) return g.rc;
-    return launch_step(h, in, ld_in, out, ld_out, stream ? as_stream(stream) : h->stream);
+    return launch_step(h, in, ld_in, out, ld_out, as_stream(stream));  // NULL = HIP null stream
 }
 
 NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, float* out, int64_t ld, int64_t nblocks,
@@ -649,7 +652,7 @@ NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_dev
     if (io_is_device) return neo_hip_upols_process_device(h, io, h->B, io, h->B, stream);
     device_guard g(h->device);
     if (g.rc) return g.rc;
-    hipStream_t s = stream ? as_stream(stream) : h->stream;
+    hipStream_t s = stream ? as_stream(stream) : h->stream;  // host I/O: own stream unless given
     const size_t bytes = size_t(h->C) * h->B * sizeof(float);
     if (!h->io) {
         NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->io), bytes));
@@ -704,7 +707,8 @@ NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t
     const size_t in_bytes = size_t(channels) * size_t(length) * sizeof(float);
     const size_t out_bytes = size_t(channels) * size_t(P) * size_t(block + 1) * sizeof(cf);
     hipStream_t s = nullptr;
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
+    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
     cf* tw = nullptr;
     const float* d_ir = ir;
     float* tmp_in = nullptr;
@@ -738,7 +742,8 @@ NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t lengt
     device_guard g(device);
     if (g.rc) return g.rc;
     hipStream_t s = nullptr;
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
+    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
     const size_t bytes = size_t(channels) * size_t(length) * sizeof(float);
     float* d = ir;
     int rc = NEO_HIP_OK;

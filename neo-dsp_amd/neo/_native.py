@@ -65,6 +65,14 @@ def load(path: str = LIB_PATH):
     global _lib
     with _lock:
         if _lib is None:
+            # One HIP runtime per process: torch bundles its own libamdhip64.so (same
+            # soname, libamdhip64.so.7). Importing torch first makes libneo_hip.so bind
+            # to that copy; loading ours first would map a second HIP/HSA runtime.
+            if os.environ.get("NEO_HIP_NO_TORCH") != "1":
+                try:
+                    import torch  # noqa: F401
+                except ImportError:
+                    pass
             if not os.path.exists(path):
                 raise ImportError(
                     f"{path} not found: build the HIP library first (make -C neo-dsp_amd); "

@@ -106,7 +106,7 @@ def test_ring_order_delay(neo_gpu, oracle):
         c.filter(H[None])
         out = np.empty_like(sig)
         for t in range(16):
-            blk = np.ascontiguousarray(sig[t * B:(t + 1) * B][None])
+            blk = sig[t * B:(t + 1) * B][None].copy()  # a view would be processed in place
             c(blk)
             out[t * B:(t + 1) * B] = blk[0]
         expect = np.concatenate([np.zeros(p * B, np.float32), sig[: len(sig) - p * B]])
