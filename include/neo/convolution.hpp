@@ -1,0 +1,221 @@
+// SPDX-License-Identifier: MIT
+// neo/convolution.hpp — neo::convolution UPOLS API on MI355X (gfx950).
+//
+// Same names and semantics as the reference's src/neo/convolution/*:
+//   fdl_index                 fdl_index.hpp:12-41 (host ring bookkeeping)
+//   uniform_partition         uniform_partition.hpp:12-26  -> [C][P][B+1] complex<float>
+//   normalize_impulse         normalize_impulse.hpp:11-33  (bit-exact rounding on the GPU)
+//   upols_convolver           dense_convolver.hpp:19-20 + uniform_partitioned_convolver.hpp:13-65
+//   split_upols_convolver     dense_convolver.hpp:38-42 (same math; one device layout)
+// plus the GPU-shaped entry the plugin and CLI loops map onto: upols_multichannel,
+// C channels stepped by one launch pair per block ([C][B] in, [C][P][B+1] filter),
+// and dense_convolve (extra/plugin/src/dsp/DenseConvolution.hpp:39-70).
+#pragma once
+
+#include <neo/fft.hpp>
+#include <neo/hip/detail.hpp>
+
+#include <algorithm>
+#include <complex>
+#include <concepts>
+#include <cstddef>
+#include <memory>
+#include <vector>
+
+namespace neo::convolution {
+
+/// fdl_index.hpp:12-41 — insert(write_pos), then for segment s: multiply(s, (write_pos + P - s) % P)
+template<typename IndexType = std::size_t>
+struct fdl_index {
+    using value_type = IndexType;
+
+    fdl_index() noexcept = default;
+    explicit fdl_index(IndexType num_segments) : _num_segments{num_segments} {}
+
+    auto reset() -> void { _write_pos = 0; }
+
+    template<std::invocable<IndexType> CopyCallback, std::invocable<IndexType, IndexType> MultiplyCallback>
+    auto operator()(CopyCallback copy_callback, MultiplyCallback callback) -> void
+    {
+        copy_callback(_write_pos);
+        for (IndexType segment{0}; segment < _num_segments; ++segment) {
+            callback(segment, static_cast<IndexType>((_write_pos + _num_segments - segment) % _num_segments));
+        }
+        if (++_write_pos; _write_pos >= _num_segments) reset();
+    }
+
+private:
+    IndexType _num_segments{0};
+    IndexType _write_pos{0};
+};
+
+/// P = ceil(L / B) (stft.hpp:21-25, overlap 0)
+[[nodiscard]] inline auto num_partitions(std::size_t length, std::size_t block) -> std::size_t
+{
+    std::int64_t p = 0;
+    neo::hip::check(neo_hip_num_partitions(std::int64_t(length), int(block), &p));
+    return std::size_t(p);
+}
+
+/// uniform_partition.hpp:12-26: impulse [C][L] -> [C][P][B+1] (computed on the GPU)
+template<typename InMat>
+    requires neo::hip::detail::matrix_like<InMat>
+[[nodiscard]] auto uniform_partition(InMat impulse_response, std::size_t block_size)
+    -> neo::hip::array<std::complex<float>, 3>
+{
+    auto const C = std::size_t(impulse_response.extent(0)), L = std::size_t(impulse_response.extent(1));
+    std::vector<float> ir(C * L);
+    for (std::size_t c = 0; c < C; ++c)
+        for (std::size_t i = 0; i < L; ++i) ir[c * L + i] = float(neo::hip::detail::at(impulse_response, c, i));
+    auto const P = num_partitions(L, block_size);
+    neo::hip::array<std::complex<float>, 3> out;
+    out.buf.resize(C * P * (block_size + 1));
+    out.ext[0] = C;
+    out.ext[1] = P;
+    out.ext[2] = block_size + 1;
+    neo::hip::check(neo_hip_uniform_partition(ir.data(), int(C), std::int64_t(L), int(block_size), out.data(), 0,
+                                              neo::hip::detail::default_device()));
+    return out;
+}
+
+/// normalize_impulse.hpp:11-33 (rank 1: unit energy; rank 2: min factor over channels)
+template<typename Obj>
+auto normalize_impulse(Obj obj) noexcept -> void
+{
+    std::size_t C = 1, L = 0;
+    if constexpr (neo::hip::detail::matrix_like<Obj>) {
+        C = std::size_t(obj.extent(0));
+        L = std::size_t(obj.extent(1));
+    } else {
+        L = std::size_t(obj.extent(0));
+    }
+    if (C == 0 || L == 0) return;
+    std::vector<float> buf(C * L);
+    for (std::size_t c = 0; c < C; ++c)
+        for (std::size_t i = 0; i < L; ++i) {
+            if constexpr (neo::hip::detail::matrix_like<Obj>) buf[c * L + i] = neo::hip::detail::at(obj, c, i);
+            else buf[i] = neo::hip::detail::at(obj, i);
+        }
+    neo::hip::check_or_abort(neo_hip_normalize_impulse(buf.data(), int(C), std::int64_t(L), 0,
+                                                       neo::hip::detail::default_device()));
+    for (std::size_t c = 0; c < C; ++c)
+        for (std::size_t i = 0; i < L; ++i) {
+            if constexpr (neo::hip::detail::matrix_like<Obj>) neo::hip::detail::at(obj, c, i) = buf[c * L + i];
+            else neo::hip::detail::at(obj, i) = buf[i];
+        }
+}
+
+namespace detail {
+struct upols_deleter {
+    void operator()(neo_hip_upols* h) const noexcept { neo_hip_upols_destroy(h); }
+};
+using upols_ptr = std::unique_ptr<neo_hip_upols, upols_deleter>;
+}  // namespace detail
+
+/// C independent UPOLS convolvers on one GPU, stepped together.
+struct upols_multichannel {
+    upols_multichannel(std::size_t channels, std::size_t block_size, std::size_t partitions,
+                       int device = neo::hip::detail::default_device())
+        : _C{channels}, _B{block_size}, _P{partitions}
+    {
+        neo_hip_upols* h = nullptr;
+        neo::hip::check(neo_hip_upols_create(int(channels), int(block_size), int(partitions), device, &h));
+        _h.reset(h);
+    }
+
+    /// filter [C][P][B+1] complex<float>, contiguous host memory; resets state
+    auto filter(std::complex<float> const* partitions) -> void
+    {
+        neo::hip::check(neo_hip_upols_set_filter(_h.get(), partitions, 0));
+    }
+    /// normalize_impulse (optional) + uniform_partition of ir [C][length] on the GPU
+    auto impulse(float const* ir, std::size_t length, bool normalize = true) -> void
+    {
+        neo::hip::check(neo_hip_upols_set_impulse(_h.get(), ir, std::int64_t(length), normalize ? 1 : 0, 0));
+    }
+    /// one block for every channel, in place, io [C][B] host memory (synchronous)
+    auto operator()(float* io) noexcept -> void { neo::hip::check_or_abort(neo_hip_upols_process(_h.get(), io, 0, nullptr)); }
+    /// one block, device pointers, channel c at in + c*ld_in (asynchronous on stream)
+    auto process_device(float const* in, std::size_t ld_in, float* out, std::size_t ld_out, void* stream = nullptr) -> void
+    {
+        neo::hip::check(neo_hip_upols_process_device(_h.get(), in, std::int64_t(ld_in), out, std::int64_t(ld_out), stream));
+    }
+    auto reset() -> void { neo::hip::check(neo_hip_upols_reset(_h.get())); }
+
+    [[nodiscard]] auto channels() const noexcept { return _C; }
+    [[nodiscard]] auto block_size() const noexcept { return _B; }
+    [[nodiscard]] auto partitions() const noexcept { return _P; }
+
+private:
+    std::size_t _C, _B, _P;
+    detail::upols_ptr _h;
+};
+
+/// Single-channel drop-in for upols_convolver<complex<float>> (uniform_partitioned_convolver.hpp:13-65):
+/// default-constructible; filter([P][B+1]) (re)initializes everything; operator()(block[B]) in place.
+template<typename Complex>
+struct hip_upols_convolver {
+    static_assert(std::same_as<Complex, std::complex<float>>);
+    using value_type = Complex;
+    using accumulator_type = neo::hip::array<Complex, 1>;
+
+    hip_upols_convolver() = default;
+
+    template<typename InMat>
+        requires neo::hip::detail::matrix_like<InMat>
+    auto filter(InMat filter) -> void
+    {
+        auto const P = std::size_t(filter.extent(0)), bins = std::size_t(filter.extent(1));
+        std::vector<Complex> h(P * bins);
+        for (std::size_t p = 0; p < P; ++p)
+            for (std::size_t k = 0; k < bins; ++k) h[p * bins + k] = Complex(neo::hip::detail::at(filter, p, k));
+        if (!_impl || _impl->partitions() != P || _impl->block_size() != bins - 1)
+            _impl = std::make_unique<upols_multichannel>(1, bins - 1, P);
+        _impl->filter(h.data());
+        _block.resize(bins - 1);
+    }
+
+    template<typename Vec>
+        requires neo::hip::detail::vector_like<Vec>
+    auto operator()(Vec block) -> void
+    {
+        if (neo::hip::detail::contiguous(block)) {
+            (*_impl)(block.data_handle());
+            return;
+        }
+        neo::hip::detail::gather(block, _block.data());
+        (*_impl)(_block.data());
+        neo::hip::detail::scatter(_block.data(), block);
+    }
+
+private:
+    std::unique_ptr<upols_multichannel> _impl;
+    std::vector<float> _block;
+};
+
+template<typename Complex>
+using upols_convolver = hip_upols_convolver<Complex>;
+
+template<typename Complex>
+using split_upols_convolver = hip_upols_convolver<Complex>;
+
+/// dense_convolve<upols_convolver> (DenseConvolution.hpp:39-70) over plain arrays:
+/// signal [C][N], ir [C][L] -> out [C][N]; normalizes + partitions the IR, tail block zero-padded.
+inline auto dense_convolve(float const* signal, std::size_t channels, std::size_t num_samples, float const* ir,
+                           std::size_t ir_length, std::size_t block_size, float* out) -> void
+{
+    upols_multichannel conv{channels, block_size, num_partitions(ir_length, block_size)};
+    conv.impulse(ir, ir_length, true);
+    std::vector<float> block(channels * block_size);
+    for (std::size_t i = 0; i < num_samples; i += block_size) {
+        auto const n = std::min(block_size, num_samples - i);
+        std::fill(block.begin(), block.end(), 0.0F);
+        for (std::size_t c = 0; c < channels; ++c)
+            std::copy(signal + c * num_samples + i, signal + c * num_samples + i + n, block.data() + c * block_size);
+        conv(block.data());
+        for (std::size_t c = 0; c < channels; ++c)
+            std::copy(block.data() + c * block_size, block.data() + c * block_size + n, out + c * num_samples + i);
+    }
+}
+
+}  // namespace neo::convolution

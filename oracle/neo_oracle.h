@@ -1,0 +1,21 @@
+/* neo_oracle.h — declarations of the CPU restatement (TEST INFRASTRUCTURE ONLY). */
+#ifndef NEO_ORACLE_H
+#define NEO_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+int oracle_fft_c2c(int order, int dir, float* x);
+int oracle_rfft(int order, const float* in, float* out);
+int oracle_irfft(int order, const float* in, float* out);
+void oracle_normalize_impulse(float* ir, size_t channels, size_t length);
+size_t oracle_num_partitions(size_t length, size_t block);
+int oracle_uniform_partition(const float* ir, size_t channels, size_t length, size_t block, float* out);
+int oracle_dense_convolve(const float* signal, float* out, const float* parts, size_t C, size_t N, size_t P, size_t B,
+                          int threads);
+void oracle_noise(uint64_t seed, float* out, size_t n);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,209 @@
+// test_api.cpp — the reference's own hot-path tests re-expressed against the
+// MI355X neo::fft / neo::convolution headers (include/neo/*.hpp -> libneo_hip.so),
+// checked against the CPU restatement (oracle/, test infrastructure).
+// Mirrors: src/neo/fft/fft_test.cpp:53-130, rfft_test.cpp:40-126,
+// src/neo/convolution/uniform_partitioned_convolver_test.cpp:35-75,
+// fdl_index_test.cpp:7-68, uniform_partition_test.cpp:8-37.
+#include <neo/convolution.hpp>
+#include <neo/fft.hpp>
+
+#include "../../oracle/neo_oracle.h"
+
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <vector>
+
+static int failures = 0;
+#define REQUIRE(cond)                                                          \
+    do {                                                                       \
+        if (!(cond)) {                                                         \
+            std::printf("FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond);        \
+            ++failures;                                                        \
+        }                                                                      \
+    } while (0)
+
+using cf = std::complex<float>;
+
+static std::vector<cf> cnoise(std::uint64_t seed, std::size_t n)
+{
+    std::vector<cf> v(n);
+    oracle_noise(seed, reinterpret_cast<float*>(v.data()), 2 * n);
+    return v;
+}
+
+static std::vector<float> rnoise(std::uint64_t seed, std::size_t n)
+{
+    std::vector<float> v(n);
+    oracle_noise(seed, v.data(), n);
+    return v;
+}
+
+template<typename A, typename B>
+static double max_abs_diff(A const& a, B const& b)
+{
+    double m = 0;
+    for (std::size_t i = 0; i < a.size(); ++i) m = std::max(m, double(std::abs(a[i] - b[i])));
+    return m;
+}
+
+static void test_fft_plan()
+{
+    bool threw = false;
+    try {
+        neo::fft::fft_plan<cf> p{neo::fft::from_order, neo::fft::next_order(neo::fft::fft_plan<cf>::max_size() + 1U)};
+    } catch (std::runtime_error const&) {
+        threw = true;
+    }
+    REQUIRE(threw);  // fft_test.cpp:62-67
+    for (std::size_t order = 2; order <= 14; ++order) {
+        auto plan = neo::fft::fft_plan<cf>{neo::fft::from_order, order};
+        REQUIRE(plan.order() == order);
+        REQUIRE(plan.size() == neo::fft::size(order));
+        REQUIRE(neo::fft::next_order(plan.size()) == plan.order());
+        auto const noise = cnoise(order, plan.size());
+        // inplace (fft_test.cpp:79-91)
+        auto io = noise;
+        auto v = neo::hip::make_view(io.data(), io.size());
+        neo::fft::fft(plan, v);
+        auto ref = noise;
+        oracle_fft_c2c(int(order), -1, reinterpret_cast<float*>(ref.data()));
+        double peak = 0;
+        for (auto const& r : ref) peak = std::max(peak, double(std::abs(r)));
+        REQUIRE(max_abs_diff(io, ref) / peak <= 1e-5);
+        neo::fft::ifft(plan, v);
+        for (auto& x : io) x *= 1.0F / float(plan.size());
+        REQUIRE(max_abs_diff(io, noise) <= 1e-5);
+        // copy (fft_test.cpp:93-110)
+        std::vector<cf> tmp(plan.size()), out(plan.size());
+        neo::fft::fft(plan, neo::hip::make_view(noise.data(), noise.size()), neo::hip::make_view(tmp.data(), tmp.size()));
+        neo::fft::ifft(plan, neo::hip::make_view(tmp.data(), tmp.size()), neo::hip::make_view(out.data(), out.size()));
+        for (auto& x : out) x *= 1.0F / float(plan.size());
+        REQUIRE(max_abs_diff(out, noise) <= 1e-5);
+        // inplace strided (fft_test.cpp:114-128): column 0 of a [2][N] layout_left buffer
+        std::vector<cf> buf(2 * plan.size());
+        auto col = neo::hip::make_strided_view(buf.data(), plan.size(), 2);
+        for (std::size_t i = 0; i < plan.size(); ++i) col(i) = noise[i];
+        neo::fft::fft(plan, col);
+        neo::fft::ifft(plan, col);
+        double m = 0;
+        for (std::size_t i = 0; i < plan.size(); ++i) m = std::max(m, double(std::abs(col(i) / float(plan.size()) - noise[i])));
+        REQUIRE(m <= 1e-5);
+    }
+}
+
+static void test_rfft_plan()
+{
+    for (std::size_t order = 2; order <= 14; ++order) {
+        auto rfft = neo::fft::rfft_plan<float>{neo::fft::from_order, order};
+        REQUIRE(rfft.size() == neo::fft::size(order));
+        auto signal = rnoise(100 + order, rfft.size());
+        auto const original = signal;
+        std::vector<cf> spectrum(rfft.size() / 2 + 1);
+        neo::fft::rfft(rfft, neo::hip::make_view(signal.data(), signal.size()),
+                       neo::hip::make_view(spectrum.data(), spectrum.size()));
+        std::vector<cf> ref(rfft.size() / 2 + 1);
+        oracle_rfft(int(order), original.data(), reinterpret_cast<float*>(ref.data()));
+        double peak = 0;
+        for (auto const& r : ref) peak = std::max(peak, double(std::abs(r)));
+        REQUIRE(max_abs_diff(spectrum, ref) / peak <= 1e-5);
+        neo::fft::irfft(rfft, neo::hip::make_view(spectrum.data(), spectrum.size()),
+                        neo::hip::make_view(signal.data(), signal.size()));
+        for (auto& x : signal) x *= 1.0F / float(rfft.size());
+        REQUIRE(max_abs_diff(signal, original) <= 1e-5);  // rfft_test.cpp:40-71
+    }
+}
+
+static void test_convolver_identity()
+{
+    for (std::size_t B : {128, 256, 512, 1024}) {
+        std::vector<cf> filt(3 * (B + 1), cf{0, 0});
+        for (std::size_t k = 0; k <= B; ++k) filt[k] = cf{1, 0};  // generate_identity_impulse
+        auto const signal = rnoise(B, B * 20);
+        auto output = signal;
+        neo::convolution::upols_convolver<cf> conv;
+        conv.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
+        for (std::size_t i = 0; i < output.size(); i += B) conv(neo::hip::make_view(output.data() + i, B));
+        REQUIRE(max_abs_diff(output, signal) <= 1e-5);
+        neo::convolution::split_upols_convolver<cf> split;
+        output = signal;
+        split.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
+        for (std::size_t i = 0; i < output.size(); i += B) split(neo::hip::make_view(output.data() + i, B));
+        REQUIRE(max_abs_diff(output, signal) <= 1e-5);
+    }
+}
+
+static void test_dense_convolve_vs_oracle()
+{
+    std::size_t const C = 3, B = 256, L = 3000, N = B * 12 + 77;
+    std::vector<float> ir(C * L), sig(C * N), out(C * N), ref(C * N);
+    for (std::size_t c = 0; c < C; ++c) {
+        auto a = rnoise(10 + c, L), b = rnoise(20 + c, N);
+        std::copy(a.begin(), a.end(), ir.begin() + c * L);
+        std::copy(b.begin(), b.end(), sig.begin() + c * N);
+    }
+    neo::convolution::dense_convolve(sig.data(), C, N, ir.data(), L, B, out.data());
+    auto irn = ir;
+    oracle_normalize_impulse(irn.data(), C, L);
+    auto const P = oracle_num_partitions(L, B);
+    REQUIRE(P == neo::convolution::num_partitions(L, B));
+    std::vector<float> parts(C * P * (B + 1) * 2);
+    oracle_uniform_partition(irn.data(), C, L, B, parts.data());
+    oracle_dense_convolve(sig.data(), ref.data(), parts.data(), C, N, P, B, 1);
+    double peak = 0;
+    for (float r : ref) peak = std::max(peak, double(std::abs(r)));
+    REQUIRE(max_abs_diff(out, ref) / peak <= 1e-5);
+    // normalize_impulse (rank 2, bit-exact) and uniform_partition through the header API
+    auto irh = ir;
+    neo::convolution::normalize_impulse(neo::hip::make_matrix_view(irh.data(), C, L));
+    REQUIRE(irh == irn);
+    auto H = neo::convolution::uniform_partition(neo::hip::make_matrix_view(irn.data(), C, L), B);
+    REQUIRE(H.extent(0) == C && H.extent(1) == P && H.extent(2) == B + 1);
+    double hp = 0, hd = 0;
+    for (std::size_t i = 0; i < H.size(); ++i) {
+        cf const r{parts[2 * i], parts[2 * i + 1]};
+        hp = std::max(hp, double(std::abs(r)));
+        hd = std::max(hd, double(std::abs(H.buf[i] - r)));
+    }
+    REQUIRE(hd / hp <= 1e-5);
+}
+
+static void test_fdl_index()
+{
+    // fdl_index_test.cpp:7-68
+    auto indexer = neo::convolution::fdl_index<int>{3};
+    std::vector<std::pair<int, int>> seen;
+    indexer([](int i) { REQUIRE(i == 0); }, [&](int f, int g) { seen.emplace_back(f, g); });
+    REQUIRE((seen == std::vector<std::pair<int, int>>{{0, 0}, {1, 2}, {2, 1}}));
+    seen.clear();
+    indexer([](int i) { REQUIRE(i == 1); }, [&](int f, int g) { seen.emplace_back(f, g); });
+    REQUIRE((seen == std::vector<std::pair<int, int>>{{0, 1}, {1, 0}, {2, 2}}));
+    indexer([](int i) { REQUIRE(i == 2); }, [](int, int) {});
+    indexer([](int i) { REQUIRE(i == 0); }, [](int, int) {});
+}
+
+static void test_uniform_partition_shapes()
+{
+    for (auto [C, L] : std::vector<std::pair<std::size_t, std::size_t>>{{1, 4096}, {2, 4096}, {2, 4095}}) {
+        std::vector<float> ir(C * L, 0.0F);
+        auto H = neo::convolution::uniform_partition(neo::hip::make_matrix_view(ir.data(), C, L), 128);
+        REQUIRE(H.extent(0) == C && H.extent(1) == 32 && H.extent(2) == 129);
+    }
+}
+
+int main()
+{
+    test_fdl_index();
+    int n = 0;
+    if (neo_hip_device_count(&n) != NEO_HIP_OK || n < 1) {
+        std::printf("no GPU: only host-side checks ran\n");
+        return failures ? 1 : 0;
+    }
+    test_fft_plan();
+    test_rfft_plan();
+    test_convolver_identity();
+    test_dense_convolve_vs_oracle();
+    test_uniform_partition_shapes();
+    std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);
+    return failures ? 1 : 0;
+}
