@@ -59,6 +59,11 @@ def dist_setup(args):
     return world, rank, local
 
 
+def shard(total: int, world: int, rank: int):
+    """Contiguous channel range [lo, hi) owned by `rank` (sizes differ by at most one)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
 def barrier(world):
     if world > 1:
         import torch.distributed as dist

@@ -1,0 +1,89 @@
+"""world_size-2 gloo tests (CPU) of the multi-GPU path: bench.py's distributed
+helpers (barrier, max over ranks) and the claim the sharding relies on — UPOLS
+channels are independent, so a channel-sharded run equals the unsharded one
+exactly (checked with the oracle's dense_convolve on each rank's shard)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
+    import bench
+    import oracle as O
+    import torch.distributed as dist
+
+    try:
+        w, r, _ = bench.dist_setup(None)
+        assert (w, r) == (world, rank)
+        bench.barrier(w)
+        m = bench.max_over_ranks(float(rank + 1) * 0.5, w)
+        # shard 6 channels over the ranks, B=128, 1500-tap IR, 9 blocks
+        C, B, L, nb = 6, 128, 1500, 9
+        lo, hi = bench.shard(C, w, r)
+        ir = np.stack([O.noise(40 + c, L) for c in range(C)])
+        parts = O.uniform_partition(O.normalize_impulse(ir), B)  # global normalization, then shard
+        sig = np.stack([O.noise(50 + c, B * nb) for c in range(C)])
+        out = O.dense_convolve(sig[lo:hi], parts[lo:hi])
+        q.put((rank, m, lo, hi, out))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((rank, "error", repr(e), None, None))
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_shard_equals_unsharded():
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
+    import oracle as O
+
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r
+    assert all(r[1] == 1.0 for r in res)  # max over ranks of {0.5, 1.0}
+    res.sort()
+    spans = [(r[2], r[3]) for r in res]
+    assert spans[0][0] == 0 and spans[-1][1] == 6 and spans[0][1] == spans[1][0]
+    C, B, L, nb = 6, 128, 1500, 9
+    ir = np.stack([O.noise(40 + c, L) for c in range(C)])
+    parts = O.uniform_partition(O.normalize_impulse(ir), B)
+    sig = np.stack([O.noise(50 + c, B * nb) for c in range(C)])
+    full = O.dense_convolve(sig, parts)
+    sharded = np.concatenate([r[4] for r in res])
+    assert np.array_equal(full, sharded)
+
+
+def test_shard_ranges():
+    sys.path.insert(0, REPO)
+    import bench
+
+    for total in (1, 7, 256, 2048):
+        for world in (1, 2, 4, 8):
+            spans = [bench.shard(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
