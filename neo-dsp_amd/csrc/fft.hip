@@ -40,14 +40,14 @@ __global__ __launch_bounds__(256) void k_c2c_lds(const cf* __restrict__ in, cf* 
     if (active) {
         const cf* src = in + g * N;
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = src[t + m * T];
+        for (int m = 0; m < E; ++m) v[m] = ld_nt(src + t + m * T);
     }
     __syncthreads();
     stockham<N, E, DIR>(v, smem + f * LL, tw, t, active);
     if (active) {
         cf* dst = out + g * N;
 #pragma unroll
-        for (int m = 0; m < E; ++m) dst[t + m * T] = v[m];
+        for (int m = 0; m < E; ++m) st_nt(dst + t + m * T, v[m]);
     }
 }
 
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void k_r2c_lds(const float* __restrict__ in, c
     if (active) {
         const cf* src = reinterpret_cast<const cf*>(in + g * 2 * M);  // z[n] = x[2n] + i x[2n+1]
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = src[t + m * T];
+        for (int m = 0; m < E; ++m) v[m] = ld_nt(src + t + m * T);
     }
     __syncthreads();
     stockham<M, E, -1>(v, lds, tw1, t, active);
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_c2r_lds(const cf* __restrict__ in, floa
     if (active) {
         cf* dst = reinterpret_cast<cf*>(out + g * 2 * M);
 #pragma unroll
-        for (int m = 0; m < E; ++m) dst[t + m * T] = v[m];
+        for (int m = 0; m < E; ++m) st_nt(dst + t + m * T, v[m]);
     }
 }
 

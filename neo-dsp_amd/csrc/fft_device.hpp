@@ -26,6 +26,44 @@ struct alignas(8) cf {  // complex float, interleaved {re, im} = std::complex<fl
     float x, y;
 };
 
+// Streaming (nontemporal) global accesses: HBM-streamed data that no later
+// kernel re-reads from cache (measured: 4096-pt batched FFT 0.856 -> 0.739 ms).
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ cf ld_nt(const cf* p)
+{
+    const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p));
+    return {v.x, v.y};
+}
+__device__ __forceinline__ void st_nt(cf* p, cf a)
+{
+    f2v v;
+    v.x = a.x;
+    v.y = a.y;
+    __builtin_nontemporal_store(v, reinterpret_cast<f2v*>(p));
+}
+__device__ __forceinline__ float4 ld4_nt(const float4* p)
+{
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4_nt(float4* p, float4 a)
+{
+    f4v v;
+    v.x = a.x;
+    v.y = a.y;
+    v.z = a.z;
+    v.w = a.w;
+    __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+}
+template<bool NT>
+__device__ __forceinline__ float4 ld4(const float4* p)
+{
+    if constexpr (NT) return ld4_nt(p);
+    else return *p;
+}
+
 __device__ __forceinline__ cf cadd(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ cf csub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }

@@ -27,6 +27,7 @@
 #include "fft_device_real.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 namespace neo_hip {
@@ -73,32 +74,35 @@ __device__ __forceinline__ cf finish(const acc4& a, bool bin0)
 // Load the overlap-save window [prev | in] of channel c as the packed complex
 // sequence z[n] = w[2n] + i w[2n+1] (lane t owns n = t + m*T), forward FFT, and
 // leave the natural-order spectrum Z in `fft` (lpad'ed).
-template<int B>
+// E = 8 elements per lane keeps this fused r2c from raising the MAC kernel's
+// register count (the MAC loop itself needs ~60 VGPRs; occupancy is what streams HBM).
+template<int B, int E = (B / 8 <= 256 ? 8 : B / 256)>  // T = B / E <= 256 lanes
 __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, const cf* tw1, int tid)
 {
-    using K = upols_cfg<B>;
-    const bool active = tid < K::T;
-    cf v[K::E];
+    constexpr int T = B / E;
+    static_assert(T <= 256 && B % E == 0, "window FFT must fit one 256-lane workgroup");
+    const bool active = tid < T;
+    cf v[E];
     if (active) {
         const cf* pz = reinterpret_cast<const cf*>(prev_c);
         const cf* iz = reinterpret_cast<const cf*>(in_c);
 #pragma unroll
-        for (int m = 0; m < K::E; ++m) {
-            const int n = tid + m * K::T;
+        for (int m = 0; m < E; ++m) {
+            const int n = tid + m * T;
             v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
         }
     }
     __syncthreads();  // twiddles staged by the caller
-    stockham<B, K::E, -1>(v, fft, tw1, tid, active);
+    stockham<B, E, -1>(v, fft, tw1, tid, active);
     if (active) {
 #pragma unroll
-        for (int m = 0; m < K::E; ++m) fft[lpad(tid + m * K::T)] = v[m];
+        for (int m = 0; m < E; ++m) fft[lpad(tid + m * T)] = v[m];
     }
     __syncthreads();
 }
 
-template<int B>
-__global__ __launch_bounds__(256) void k_upols_mac(const float* __restrict__ in, int64_t ld_in,
+template<int B, bool NT, int UNROLL = upols_cfg<B>::U>
+__global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_mac(const float* __restrict__ in, int64_t ld_in,
                                                    float* __restrict__ prev, const cf* __restrict__ H,
                                                    cf* __restrict__ fdl, cf* __restrict__ part,
                                                    const int* __restrict__ wp_dev, const cf* __restrict__ twg, int P,
@@ -154,21 +158,21 @@ __global__ __launch_bounds__(256) void k_upols_mac(const float* __restrict__ in,
     }
     // main loop: U row-groups in flight, no bounds checks inside
     int p = pstart + rs;
-    for (; p + (K::U - 1) * K::RPI < p1; p += K::U * K::RPI) {
-        float4 hv[K::U][K::VPT], xv[K::U][K::VPT];
+    for (; p + (UNROLL - 1) * K::RPI < p1; p += UNROLL * K::RPI) {
+        float4 hv[UNROLL][K::VPT], xv[UNROLL][K::VPT];
 #pragma unroll
-        for (int u = 0; u < K::U; ++u) {
+        for (int u = 0; u < UNROLL; ++u) {
             const int pp = p + u * K::RPI;
             const int fr = w >= pp ? w - pp : w - pp + P;
 #pragma unroll
             for (int v = 0; v < K::VPT; ++v) {
                 const int q = q0 + v * K::QT;
-                hv[u][v] = H4[int64_t(pp) * K::Q + q];
-                xv[u][v] = F4[int64_t(fr) * K::Q + q];
+                hv[u][v] = ld4<NT>(H4 + int64_t(pp) * K::Q + q);
+                xv[u][v] = ld4<NT>(F4 + int64_t(fr) * K::Q + q);
             }
         }
 #pragma unroll
-        for (int u = 0; u < K::U; ++u)
+        for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
             for (int v = 0; v < K::VPT; ++v) mac2(a[2 * v], a[2 * v + 1], hv[u][v], xv[u][v]);
     }
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(256) void k_upols_mac(const float* __restrict__ in,
 #pragma unroll
         for (int v = 0; v < K::VPT; ++v) {
             const int q = q0 + v * K::QT;
-            mac2(a[2 * v], a[2 * v + 1], H4[int64_t(p) * K::Q + q], F4[int64_t(fr) * K::Q + q]);
+            mac2(a[2 * v], a[2 * v + 1], ld4<NT>(H4 + int64_t(p) * K::Q + q), ld4<NT>(F4 + int64_t(fr) * K::Q + q));
         }
     }
 
@@ -365,6 +369,7 @@ struct neo_hip_upols {
     float* io = nullptr;       // device staging for host-pointer process()
     float* io_host = nullptr;  // pinned staging
     bool timing = false;
+    bool nt = true;  // streaming (nontemporal) filter/FDL loads; NEO_HIP_NT=0 selects plain loads (A/B)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double mac_ms = 0.0;
     int64_t launches = 0;
@@ -476,8 +481,13 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
         NEO_HIP_CHECK(hipEventRecord(ev.first, s));
     }
     const unsigned grid = unsigned(h->C) * unsigned(h->S);
-    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_mac<BB>), dim3(grid), dim3(256), 0, s, in, ld_in, h->prev,
-                                                h->H, h->fdl, h->part, h->wp, h->tw, h->P, h->S, h->rows))
+    if (h->nt) {
+        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_mac<BB, true>), dim3(grid), dim3(256), 0, s, in, ld_in,
+                                                    h->prev, h->H, h->fdl, h->part, h->wp, h->tw, h->P, h->S, h->rows))
+    } else {
+        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_mac<BB, false>), dim3(grid), dim3(256), 0, s, in, ld_in,
+                                                    h->prev, h->H, h->fdl, h->part, h->wp, h->tw, h->P, h->S, h->rows))
+    }
     NEO_HIP_LAUNCH_CHECK();
     if (h->timing) {
         NEO_HIP_CHECK(hipEventRecord(ev.second, s));
@@ -514,8 +524,11 @@ NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, in
     h->C = channels;
     h->B = block;
     h->P = partitions;
-    // splits per channel: aim for ~2048 workgroups (8 per CU), <= 64 partial slabs
-    const int target = 2048;
+    if (const char* e = std::getenv("NEO_HIP_NT")) h->nt = std::atoi(e) != 0;
+    // splits per channel: aim for ~1024 workgroups (4 per CU, all resident at 8 waves/SIMD;
+    // A/B on MI355X: 1024 beat 512/768/2048/4096 at C4 and C5), <= 64 partial slabs
+    int target = 1024;
+    if (const char* e = std::getenv("NEO_HIP_SPLIT_WGS")) target = std::max(1, std::atoi(e));
     int S = std::max(1, std::min({(target + channels - 1) / channels, partitions, 64}));
     h->rows = (partitions + S - 1) / S;
     h->S = (partitions + h->rows - 1) / h->rows;

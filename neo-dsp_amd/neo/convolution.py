@@ -152,6 +152,13 @@ class UpolsConvolver:
                                                                   nb, ctypes.c_void_p(s)))
         return out
 
+    def process_blocks_ptr(self, in_ptr: int, out_ptr: int, ld: int, nblocks: int, stream: int = 0) -> None:
+        """nblocks consecutive blocks through the C-ABI loop: channel c of block t at
+        in_ptr + 4*(c*ld + t*B) (device pointers)."""
+        _native.check(_native.load().neo_hip_upols_process_blocks(self._h, ctypes.c_void_p(in_ptr),
+                                                                  ctypes.c_void_p(out_ptr), int(ld), int(nblocks),
+                                                                  ctypes.c_void_p(stream)))
+
     # -- instrumentation ------------------------------------------------------
     def set_timing(self, enable: bool) -> None:
         _native.check(_native.load().neo_hip_upols_set_timing(self._h, int(enable)))

@@ -189,3 +189,29 @@ def test_full_size_properties(neo_gpu, oracle, C, B, L):
         parts = oracle.uniform_partition(irh[c:c + 1], B)
         ref = oracle.dense_convolve(xh[c:c + 1], parts)
         assert peak_err(ox[c].cpu().numpy(), ref[0]) <= TOL
+
+
+def test_multirow_splits_with_wraparound(neo_gpu, oracle):
+    """More blocks than partitions and several partitions per split (every split carries
+    nonzero FDL rows, ring wraps), forced via NEO_HIP_SPLIT_WGS read at create time."""
+    import os
+
+    B, L, C, nb = 128, 50 * 128, 2, 130  # P = 50
+    ir = np.stack([oracle.noise(700 + c, L) for c in range(C)])
+    sig = np.stack([oracle.noise(710 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, oracle.uniform_partition(oracle.normalize_impulse(ir), B))
+    for target in ("6", "1", "64"):
+        os.environ["NEO_HIP_SPLIT_WGS"] = target
+        try:
+            P = neo_gpu.num_partitions(L, B)
+            conv = neo_gpu.UpolsConvolver(C, B, P)
+            conv.set_impulse(ir)
+            out = np.empty_like(sig)
+            for t in range(nb):
+                blk = np.ascontiguousarray(sig[:, t * B:(t + 1) * B])
+                conv(blk)
+                out[:, t * B:(t + 1) * B] = blk
+        finally:
+            del os.environ["NEO_HIP_SPLIT_WGS"]
+        assert conv.splits == {"6": 3, "1": 1, "64": 25}[target]  # S = ceil(P / ceil(P / min(ceil(t/C), P, 64)))
+        assert peak_err(out, ref) <= TOL, (target, conv.splits)
