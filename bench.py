@@ -138,11 +138,20 @@ def cpu_baseline_fft(threads):
                       f"{dt:.2f} s; scales linearly with batch"}
 
 
+def device_for(local: int) -> int:
+    """One process per GPU: LOCAL_RANK -> device (modulo the visible devices, so a
+    multi-rank rehearsal on a smaller box shares GPUs)."""
+    import torch
+
+    return local % max(1, torch.cuda.device_count())
+
+
 def run_upols(args, world, rank, local):
     import torch
     import neo
 
     C, B, L = WORKLOADS[args.workload]
+    local = device_for(local)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     P = neo.num_partitions(L, B)
@@ -217,6 +226,7 @@ def run_fft(args, world, rank, local):
     import torch
     import neo
 
+    local = device_for(local)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     N, batch = 4096, 65536

@@ -3,26 +3,25 @@
 // Replaces C instances of neo's upols_convolver<complex<float>>
 // (src/neo/convolution/dense_convolver.hpp:19-20) stepped by dense_convolve /
 // DenseConvolution (extra/plugin/src/dsp/DenseConvolution.hpp:39-70). One block
-// step for all channels is two kernels:
+// step for all channels is ONE kernel, k_upols_step, grid C x S:
 //
-//   k_upols_mac  grid C x S. Workgroup (c, s) accumulates filter partitions
-//                p in [p0, p1) of channel c:  acc[k] += H[c][p][k] * FDL[c][(w-p) mod P][k]
-//                (fdl_index.hpp:23-36 ring order; dense_filter.hpp:30-35 MAC).
-//                The s == 0 workgroup first runs the overlap-save r2c of
-//                [previous block | new block] (overlap_save.hpp:90-103) as a packed
-//                B-point complex FFT in LDS, inserts it as FDL row w
-//                (dense_fdl.hpp:27-30) and uses it for p = 0 straight from LDS.
-//                Streams 16 B per bin per partition from HBM: the roofline kernel.
-//   k_upols_out  grid C. Sums the S partial spectra (fixed order), runs the c2r
-//                (fallback_rfft_plan.hpp:38-55) as a packed inverse FFT in LDS,
-//                scales by 1/2B and writes the last B samples (overlap_save.hpp:104-111).
+//   - workgroup (c, s) accumulates filter partitions p in [p0, p1) of channel c:
+//       acc[k] += H[c][p][k] * FDL[c][(w - p) mod P][k]
+//     (fdl_index.hpp:23-36 ring order; dense_filter.hpp:30-35 / multiply_add MAC),
+//     streaming 16 B per bin per partition from HBM — the roofline part;
+//   - split s == 0 first runs the overlap-save r2c of [previous block | new block]
+//     (overlap_save.hpp:90-103) as a packed B-point complex FFT in LDS, inserts it as
+//     FDL row w (dense_fdl.hpp:27-30) and uses it for p = 0 straight from LDS;
+//   - the last split of a channel to finish sums the S partial spectra in fixed order,
+//     runs the c2r (fallback_rfft_plan.hpp:38-55) as a packed inverse FFT in LDS,
+//     scales by 1/2B and writes the last B samples (overlap_save.hpp:104-111).
 //
 // Device layout (HBM), all packed rows of B complex with bin 0 = {DC, Nyquist}
 // (both purely real for real signals, so the fold is exact):
 //   H    [C][P][B]   filter partitions (uniform_partition.hpp layout, packed)
 //   FDL  [C][P][B]   frequency-domain delay line (ring, write position w)
 //   prev [C][B]      previous input block (first half of the overlap-save window)
-//   part [C][S][B]   per-split partial spectra
+//   part [C][S][B]   per-split partial spectra; arrivals [C] split counters
 #include "common.hpp"
 #include "fft_device_real.hpp"
 
@@ -101,31 +100,69 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
     __syncthreads();
 }
 
-template<int B, bool NT, int UNROLL = upols_cfg<B>::U>
-__global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_mac(const float* __restrict__ in, int64_t ld_in,
-                                                   float* __restrict__ prev, const cf* __restrict__ H,
-                                                   cf* __restrict__ fdl, cf* __restrict__ part,
-                                                   const int* __restrict__ wp_dev, const cf* __restrict__ twg, int P,
-                                                   int S, int rows)
+// c2r of the packed spectrum X (LDS) -> samples [B, 2B) of the overlap-save window,
+// scaled by 1/2B, written to out_c (fallback_rfft_plan.hpp:38-55, overlap_save.hpp:104-111).
+// E = 4 keeps the fused kernel inside its 64-VGPR budget (T = B/E <= 256 lanes).
+template<int B, int E = (B / 4 <= 256 ? 4 : B / 256)>
+__device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, int tid)
 {
     using K = upols_cfg<B>;
-    __shared__ __attribute__((aligned(16))) cf xnew[B];
+    constexpr int T = B / E;
+    static_assert(T <= 256 && B % E == 0, "c2r must fit one 256-lane workgroup");
+    const bool active = tid < T;
+    cf v[E];
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int k = tid + m * T;
+            const cf x0 = X[0];
+            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
+                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
+        }
+    }
+    stockham<B, E, +1>(v, fft, tw, tid, active);
+    if (active) {
+        const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108
+        cf* o = reinterpret_cast<cf*>(out_c);
+#pragma unroll
+        for (int m = E / 2; m < E; ++m) {  // window samples [B, 2B): z[n], n >= B/2
+            const int n = tid + m * T;
+            o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+        }
+    }
+}
+
+// One whole block step for every channel (grid C x S, 256 lanes). Workgroup (c, s)
+// accumulates partitions [p0, p1) into a partial spectrum; split 0 first runs the
+// window r2c and inserts FDL row w. Each workgroup publishes its slab, and the last
+// of a channel's S workgroups to arrive (agent-scope release -> counter -> acquire,
+// cdna_hip_programming.md §6 G16 / split-K seam) sums the slabs in the fixed order
+// s = 0..S-1 and runs the c2r: one launch per block, deterministic results.
+template<int B, bool NT, bool FUSED, int UNROLL = upols_cfg<B>::U>
+__global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
+    const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
+    const cf* __restrict__ H, cf* __restrict__ fdl, cf* __restrict__ part, int* __restrict__ arrivals,
+    const cf* __restrict__ twg, int P, int S, int rows, int w, int64_t cstride, int64_t pstride)
+{
+    using K = upols_cfg<B>;
+    __shared__ __attribute__((aligned(16))) cf xnew[B];  // new spectrum; later the summed spectrum
     __shared__ cf fft[K::LL];
     __shared__ cf tw[K::TW1 + K::TW2];
     __shared__ __attribute__((aligned(16))) float4 red[K::RPI > 1 ? 256 * 2 * K::VPT : 1];
+    __shared__ int last;
 
     const int tid = threadIdx.x;
     const int c = blockIdx.x / S, s = blockIdx.x - c * S;
     const int p0 = s * rows, p1 = min(P, p0 + rows);
-    const int w = *wp_dev;
-    const int64_t crow = int64_t(c) * P * B;  // channel base in H / FDL (complex units)
+    const int64_t crow = int64_t(c) * cstride;  // channel base in H / FDL (complex units); row p at + p * pstride
+    const int64_t ps4 = pstride / 2;            // row stride in float4 units
 
     if (s == 0) {
         for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
         const float* in_c = in + int64_t(c) * ld_in;
         float* prev_c = prev + int64_t(c) * B;
         window_fft<B>(prev_c, in_c, fft, tw, tid);
-        cf* row = fdl + crow + int64_t(w) * B;
+        cf* row = fdl + crow + int64_t(w) * pstride;
         for (int k = tid; k < B; k += 256) {
             const cf x = r2c_split<B>(fft, tw + K::TW1, k);
             xnew[k] = x;
@@ -156,19 +193,19 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_mac(const fl
         }
         pstart = 1;
     }
-    // main loop: U row-groups in flight, no bounds checks inside
+    // main loop: UNROLL row-groups in flight, no bounds checks inside
     int p = pstart + rs;
     for (; p + (UNROLL - 1) * K::RPI < p1; p += UNROLL * K::RPI) {
         float4 hv[UNROLL][K::VPT], xv[UNROLL][K::VPT];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             const int pp = p + u * K::RPI;
-            const int fr = w >= pp ? w - pp : w - pp + P;
+            const int fr = w >= pp ? w - pp : w - pp + P;  // fdl_index.hpp:28-31 ring
 #pragma unroll
             for (int v = 0; v < K::VPT; ++v) {
                 const int q = q0 + v * K::QT;
-                hv[u][v] = ld4<NT>(H4 + int64_t(pp) * K::Q + q);
-                xv[u][v] = ld4<NT>(F4 + int64_t(fr) * K::Q + q);
+                hv[u][v] = ld4<NT>(H4 + int64_t(pp) * ps4 + q);
+                xv[u][v] = ld4<NT>(F4 + int64_t(fr) * ps4 + q);
             }
         }
 #pragma unroll
@@ -181,12 +218,12 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_mac(const fl
 #pragma unroll
         for (int v = 0; v < K::VPT; ++v) {
             const int q = q0 + v * K::QT;
-            mac2(a[2 * v], a[2 * v + 1], ld4<NT>(H4 + int64_t(p) * K::Q + q), ld4<NT>(F4 + int64_t(fr) * K::Q + q));
+            mac2(a[2 * v], a[2 * v + 1], ld4<NT>(H4 + int64_t(p) * ps4 + q), ld4<NT>(F4 + int64_t(fr) * ps4 + q));
         }
     }
 
     if constexpr (K::RPI > 1) {
-        // fold the row groups (fixed order -> deterministic)
+        // fold the row groups into group 0 (fixed order -> deterministic)
 #pragma unroll
         for (int v = 0; v < K::VPT; ++v) {
             red[(tid * K::VPT + v) * 2 + 0] = make_float4(a[2 * v].rr, a[2 * v].ii, a[2 * v].ri, a[2 * v].ir);
@@ -194,29 +231,93 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_mac(const fl
                 make_float4(a[2 * v + 1].rr, a[2 * v + 1].ii, a[2 * v + 1].ri, a[2 * v + 1].ir);
         }
         __syncthreads();
-        if (rs != 0) return;
-        for (int g = 1; g < K::RPI; ++g) {
+        if (rs == 0) {
+            for (int g = 1; g < K::RPI; ++g) {
 #pragma unroll
-            for (int v = 0; v < K::VPT; ++v) {
-                const int idx = ((g * K::QT + q0) * K::VPT + v) * 2;
-                const float4 r0 = red[idx], r1 = red[idx + 1];
-                a[2 * v].rr += r0.x; a[2 * v].ii += r0.y; a[2 * v].ri += r0.z; a[2 * v].ir += r0.w;
-                a[2 * v + 1].rr += r1.x; a[2 * v + 1].ii += r1.y; a[2 * v + 1].ri += r1.z; a[2 * v + 1].ir += r1.w;
+                for (int v = 0; v < K::VPT; ++v) {
+                    const int idx = ((g * K::QT + q0) * K::VPT + v) * 2;
+                    const float4 r0 = red[idx], r1 = red[idx + 1];
+                    a[2 * v].rr += r0.x; a[2 * v].ii += r0.y; a[2 * v].ri += r0.z; a[2 * v].ir += r0.w;
+                    a[2 * v + 1].rr += r1.x; a[2 * v + 1].ii += r1.y; a[2 * v + 1].ri += r1.z; a[2 * v + 1].ir += r1.w;
+                }
             }
         }
     }
-    float4* out = reinterpret_cast<float4*>(part + (int64_t(c) * S + s) * B);
+    float* out_c = out + int64_t(c) * ld_out;
+
+    if (FUSED && S == 1) {  // whole channel in this workgroup: finish straight from registers
+        __syncthreads();  // xnew reads (p = 0) done before it is overwritten
+        if (rs == 0) {
 #pragma unroll
-    for (int v = 0; v < K::VPT; ++v) {
-        const int q = q0 + v * K::QT;
-        const cf b0 = finish(a[2 * v], q == 0), b1 = finish(a[2 * v + 1], false);
-        out[q] = make_float4(b0.x, b0.y, b1.x, b1.y);
+            for (int v = 0; v < K::VPT; ++v) {
+                const int q = q0 + v * K::QT;
+                const cf b0 = finish(a[2 * v], q == 0), b1 = finish(a[2 * v + 1], false);
+                reinterpret_cast<float4*>(xnew)[q] = make_float4(b0.x, b0.y, b1.x, b1.y);
+            }
+        }
+        __syncthreads();
+        c2r_tail<B>(xnew, fft, tw, out_c, tid);
+        return;
     }
+
+    // publish this split's slab
+    float4* slab = reinterpret_cast<float4*>(part + (int64_t(c) * S + s) * B);
+    if (rs == 0) {
+#pragma unroll
+        for (int v = 0; v < K::VPT; ++v) {
+            const int q = q0 + v * K::QT;
+            const cf b0 = finish(a[2 * v], q == 0), b1 = finish(a[2 * v + 1], false);
+            slab[q] = make_float4(b0.x, b0.y, b1.x, b1.y);
+        }
+    }
+    if constexpr (!FUSED) return;  // k_upols_finish sums the slabs in the next launch
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the release's wait (G16 pitfall)
+        const int before = __hip_atomic_fetch_add(arrivals + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = before == S - 1;
+    }
+    __syncthreads();
+    if (!last) return;  // uniform per workgroup
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(arrivals + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next step
+    }
+    if (s != 0)
+        for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+    __syncthreads();
+
+    // sum the S slabs in order s = 0..S-1, 8 loads in flight
+    const float4* p4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * B);
+    for (int q = tid; q < K::Q; q += 256) {
+        float4 sum = p4[q];
+        int t = 1;
+        for (; t + 7 < S; t += 8) {
+            float4 r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) r[u] = p4[int64_t(t + u) * K::Q + q];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                sum.x += r[u].x; sum.y += r[u].y; sum.z += r[u].z; sum.w += r[u].w;
+            }
+        }
+        for (; t < S; ++t) {
+            const float4 r = p4[int64_t(t) * K::Q + q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        reinterpret_cast<float4*>(xnew)[q] = sum;
+    }
+    __syncthreads();
+    c2r_tail<B>(xnew, fft, tw, out_c, tid);
 }
 
+// Unfused tail (one workgroup per channel): sum the S slabs in order, c2r, write.
 template<int B>
-__global__ __launch_bounds__(256) void k_upols_out(const cf* __restrict__ part, float* __restrict__ out, int64_t ld_out,
-                                                   int* __restrict__ wp_dev, const cf* __restrict__ twg, int P, int S)
+__global__ __launch_bounds__(256) void k_upols_finish(const cf* __restrict__ part, float* __restrict__ out,
+                                                      int64_t ld_out, const cf* __restrict__ twg, int S)
 {
     using K = upols_cfg<B>;
     __shared__ __attribute__((aligned(16))) cf X[B];
@@ -227,38 +328,24 @@ __global__ __launch_bounds__(256) void k_upols_out(const cf* __restrict__ part, 
     const float4* p4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * B);
     for (int q = tid; q < K::Q; q += 256) {
         float4 sum = p4[q];
-        for (int s = 1; s < S; ++s) {
-            const float4 t = p4[int64_t(s) * K::Q + q];
-            sum.x += t.x; sum.y += t.y; sum.z += t.z; sum.w += t.w;
+        int t = 1;
+        for (; t + 7 < S; t += 8) {
+            float4 r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) r[u] = p4[int64_t(t + u) * K::Q + q];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                sum.x += r[u].x; sum.y += r[u].y; sum.z += r[u].z; sum.w += r[u].w;
+            }
+        }
+        for (; t < S; ++t) {
+            const float4 r = p4[int64_t(t) * K::Q + q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         reinterpret_cast<float4*>(X)[q] = sum;
     }
     __syncthreads();
-    const bool active = tid < K::T;
-    cf v[K::E];
-    if (active) {
-#pragma unroll
-        for (int m = 0; m < K::E; ++m) {
-            const int k = tid + m * K::T;
-            const cf x0 = X[0];
-            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
-                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
-        }
-    }
-    stockham<B, K::E, +1>(v, fft, tw, tid, active);
-    if (active) {
-        const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108
-        cf* o = reinterpret_cast<cf*>(out + int64_t(c) * ld_out);
-#pragma unroll
-        for (int m = K::E / 2; m < K::E; ++m) {  // samples [B, 2B) of the window
-            const int n = tid + m * K::T;
-            o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
-        }
-    }
-    if (c == 0 && tid == 0) {
-        const int w = *wp_dev + 1;  // fdl_index.hpp:35-37
-        *wp_dev = w >= P ? 0 : w;
-    }
+    c2r_tail<B, (B / 16 <= 256 ? (B >= 16 ? 16 : B) : B / 256)>(X, fft, tw, out + int64_t(c) * ld_out, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -269,7 +356,8 @@ __global__ __launch_bounds__(256) void k_upols_out(const cf* __restrict__ part, 
 // [C][P][B] (UPOLS layout) or unpacked [C][P][B+1] (reference layout).
 template<int B, bool PACKED>
 __global__ __launch_bounds__(256) void k_partition(const float* __restrict__ ir, int64_t L, int P,
-                                                   cf* __restrict__ out, const cf* __restrict__ twg)
+                                                   cf* __restrict__ out, const cf* __restrict__ twg, int64_t cstride,
+                                                   int64_t pstride)
 {
     using K = upols_cfg<B>;
     __shared__ cf fft[K::LL];
@@ -299,7 +387,7 @@ __global__ __launch_bounds__(256) void k_partition(const float* __restrict__ ir,
     }
     __syncthreads();
     if constexpr (PACKED) {
-        cf* row = out + cp * B;
+        cf* row = out + c * cstride + p * pstride;  // device layout (see neo_hip_upols)
         for (int k = tid; k < B; k += 256) row[k] = r2c_split<B>(fft, tw + K::TW1, k);
     } else {
         cf* row = out + cp * (B + 1);
@@ -316,13 +404,15 @@ __global__ __launch_bounds__(256) void k_partition(const float* __restrict__ ir,
 }
 
 // filter [C][P][B+1] (reference layout) -> packed [C][P][B]
-__global__ void k_pack_filter(const cf* __restrict__ in, cf* __restrict__ out, int B, int64_t rows)
+__global__ void k_pack_filter(const cf* __restrict__ in, cf* __restrict__ out, int B, int64_t rows, int P,
+                              int64_t cstride, int64_t pstride)
 {
     const int64_t gid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (gid >= rows * B) return;
     const int64_t r = gid / B, k = gid - r * B;
+    const int64_t c = r / P, p = r - c * P;
     const cf* src = in + r * (B + 1);
-    out[gid] = k == 0 ? cf{src[0].x, src[B].x} : src[k];
+    out[c * cstride + p * pstride + k] = k == 0 ? cf{src[0].x, src[B].x} : src[k];
 }
 
 // normalize_energy_factor (normalize_energy.hpp:17-44) with the reference's exact
@@ -364,13 +454,19 @@ struct neo_hip_upols {
     cf* fdl = nullptr;
     cf* part = nullptr;
     float* prev = nullptr;
-    int* wp = nullptr;
+    int* arrivals = nullptr;  // per-channel split arrival counters (zero between steps)
+    int wpos = 0;             // FDL write position (fdl_index.hpp:35-37), host-side
     cf* tw = nullptr;
     float* io = nullptr;       // device staging for host-pointer process()
     float* io_host = nullptr;  // pinned staging
     bool timing = false;
     bool nt = true;  // streaming (nontemporal) filter/FDL loads; NEO_HIP_NT=0 selects plain loads (A/B)
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    bool fused = false;  // NEO_HIP_FUSED=1: one launch per block (last-arriver tail); A/B: slower at C4/C5
+    // H / FDL layout: row p of channel c at c * cstride + p * pstride (complex units).
+    // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
+    int64_t cstride = 0, pstride = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool, reused across timing windows
+    size_t events_used = 0;
     double mac_ms = 0.0;
     int64_t launches = 0;
 };
@@ -417,7 +513,8 @@ int reset_state(upols_t* h, hipStream_t s)
 {
     NEO_HIP_CHECK(hipMemsetAsync(h->fdl, 0, size_t(h->C) * h->P * h->B * sizeof(cf), s));
     NEO_HIP_CHECK(hipMemsetAsync(h->prev, 0, size_t(h->C) * h->B * sizeof(float), s));
-    NEO_HIP_CHECK(hipMemsetAsync(h->wp, 0, sizeof(int), s));
+    NEO_HIP_CHECK(hipMemsetAsync(h->arrivals, 0, size_t(h->C) * sizeof(int), s));
+    h->wpos = 0;
     return NEO_HIP_OK;
 }
 
@@ -432,7 +529,7 @@ void destroy(upols_t* h)
     (void)hipFree(h->fdl);
     (void)hipFree(h->part);
     (void)hipFree(h->prev);
-    (void)hipFree(h->wp);
+    (void)hipFree(h->arrivals);
     (void)hipFree(h->tw);
     (void)hipFree(h->io);
     if (h->io_host) (void)hipHostFree(h->io_host);
@@ -441,17 +538,18 @@ void destroy(upols_t* h)
 }
 
 // normalize (optional) + partition ir [C][L] (device) into packed or unpacked rows.
-int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s)
+int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s,
+                     int64_t cstride = 0, int64_t pstride = 0)
 {
     const int64_t P = partitions_for(L, B);
     const int64_t blocks = int64_t(C) * P;
     if (blocks > 0x7fffffff) return fail(NEO_HIP_EINVAL, "too many partitions");
     if (packed) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_partition<BB, true>), dim3(unsigned(blocks)), dim3(256), 0, s,
-                                                 d_ir, L, int(P), out, tw))
+                                                 d_ir, L, int(P), out, tw, cstride, pstride))
     } else {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_partition<BB, false>), dim3(unsigned(blocks)), dim3(256), 0, s,
-                                                 d_ir, L, int(P), out, tw))
+                                                 d_ir, L, int(P), out, tw, cstride, pstride))
     }
     NEO_HIP_LAUNCH_CHECK();
     return NEO_HIP_OK;
@@ -476,26 +574,36 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
 {
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (h->timing) {
-        NEO_HIP_CHECK(hipEventCreate(&ev.first));
-        NEO_HIP_CHECK(hipEventCreate(&ev.second));
+        if (h->events_used == h->events.size()) {
+            NEO_HIP_CHECK(hipEventCreate(&ev.first));
+            NEO_HIP_CHECK(hipEventCreate(&ev.second));
+            h->events.push_back(ev);
+        }
+        ev = h->events[h->events_used];
         NEO_HIP_CHECK(hipEventRecord(ev.first, s));
     }
     const unsigned grid = unsigned(h->C) * unsigned(h->S);
-    if (h->nt) {
-        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_mac<BB, true>), dim3(grid), dim3(256), 0, s, in, ld_in,
-                                                    h->prev, h->H, h->fdl, h->part, h->wp, h->tw, h->P, h->S, h->rows))
+#define NEO_STEP(NTV, FU)                                                                                     \
+    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, NTV, FU>), dim3(grid), dim3(256), 0, s, in, ld_in, \
+                                                out, ld_out, h->prev, h->H, h->fdl, h->part, h->arrivals, h->tw,   \
+                                                h->P, h->S, h->rows, h->wpos, h->cstride, h->pstride))
+    if (h->fused) {
+        if (h->nt) NEO_STEP(true, true) else NEO_STEP(false, true)
     } else {
-        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_mac<BB, false>), dim3(grid), dim3(256), 0, s, in, ld_in,
-                                                    h->prev, h->H, h->fdl, h->part, h->wp, h->tw, h->P, h->S, h->rows))
+        if (h->nt) NEO_STEP(true, false) else NEO_STEP(false, false)
     }
+#undef NEO_STEP
     NEO_HIP_LAUNCH_CHECK();
     if (h->timing) {
         NEO_HIP_CHECK(hipEventRecord(ev.second, s));
-        h->events.push_back(ev);
+        ++h->events_used;
     }
-    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_out<BB>), dim3(unsigned(h->C)), dim3(256), 0, s, h->part,
-                                                out, ld_out, h->wp, h->tw, h->P, h->S))
-    NEO_HIP_LAUNCH_CHECK();
+    if (!h->fused) {
+        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_finish<BB>), dim3(unsigned(h->C)), dim3(256), 0, s,
+                                                    h->part, out, ld_out, h->tw, h->S))
+        NEO_HIP_LAUNCH_CHECK();
+    }
+    h->wpos = h->wpos + 1 >= h->P ? 0 : h->wpos + 1;  // fdl_index.hpp:35-37
     return NEO_HIP_OK;
 }
 
@@ -525,11 +633,19 @@ NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, in
     h->B = block;
     h->P = partitions;
     if (const char* e = std::getenv("NEO_HIP_NT")) h->nt = std::atoi(e) != 0;
+    if (const char* e = std::getenv("NEO_HIP_FUSED")) h->fused = std::atoi(e) != 0;
+    h->cstride = int64_t(partitions) * block;
+    h->pstride = block;
+    if (const char* e = std::getenv("NEO_HIP_LAYOUT"); e && std::string(e) == "pcb") {
+        h->cstride = block;
+        h->pstride = int64_t(channels) * block;
+    }
     // splits per channel: aim for ~1024 workgroups (4 per CU, all resident at 8 waves/SIMD;
     // A/B on MI355X: 1024 beat 512/768/2048/4096 at C4 and C5), <= 64 partial slabs
     int target = 1024;
     if (const char* e = std::getenv("NEO_HIP_SPLIT_WGS")) target = std::max(1, std::atoi(e));
-    int S = std::max(1, std::min({(target + channels - 1) / channels, partitions, 64}));
+    // >= 8 rows per split keeps the out kernel's slab sum short at small C (C3: 24 splits)
+    int S = std::max(1, std::min({(target + channels - 1) / channels, (partitions + 7) / 8, 64}));
     h->rows = (partitions + S - 1) / S;
     h->S = (partitions + h->rows - 1) / h->rows;
     const size_t rowbytes = size_t(block) * sizeof(cf);
@@ -544,7 +660,7 @@ NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, in
         hipMalloc(reinterpret_cast<void**>(&h->fdl), nrows * rowbytes) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->part), size_t(channels) * h->S * rowbytes) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->prev), size_t(channels) * block * sizeof(float)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&h->wp), sizeof(int)) != hipSuccess)
+        hipMalloc(reinterpret_cast<void**>(&h->arrivals), size_t(channels) * sizeof(int)) != hipSuccess)
         return bail(fail(NEO_HIP_ENOMEM, "device allocation of %zu bytes failed", 2 * nrows * rowbytes));
     int rc = upload_tw(&h->tw, block);
     if (rc) return bail(rc);
@@ -602,7 +718,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
     }
     const int64_t total = rows * h->B;
     hipLaunchKernelGGL(k_pack_filter, dim3(unsigned((total + 255) / 256)), dim3(256), 0, h->stream, src, h->H, h->B,
-                       rows);
+                       rows, h->P, h->cstride, h->pstride);
     int rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "pack kernel launch failed");
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
@@ -628,7 +744,7 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
         hipSuccess)
         rc = fail(NEO_HIP_ERUNTIME, "impulse copy failed");
     if (!rc && normalize) rc = normalize_device(d, h->C, length, h->stream);
-    if (!rc) rc = partition_device(d, h->C, length, h->B, true, h->H, h->tw, h->stream);
+    if (!rc) rc = partition_device(d, h->C, length, h->B, true, h->H, h->tw, h->stream, h->cstride, h->pstride);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     (void)hipFree(d);
@@ -692,16 +808,15 @@ NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* 
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     device_guard g(h->device);
-    for (auto& e : h->events) {
+    for (size_t i = 0; i < h->events_used; ++i) {
+        auto& e = h->events[i];
         NEO_HIP_CHECK(hipEventSynchronize(e.second));
         float ms = 0.f;
         NEO_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
         h->mac_ms += ms;
         ++h->launches;
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
     }
-    h->events.clear();
+    h->events_used = 0;
     if (mac_ms) *mac_ms = h->mac_ms;
     if (launches) *launches = h->launches;
     h->mac_ms = 0.0;
