@@ -59,7 +59,17 @@ def dist_setup(args):
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo prints connection chatter on fd 1; keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(devnull)
     return world, rank, local
 
 
@@ -213,7 +223,7 @@ def run_upols(args, world, rank, local):
                    "splits": conv.splits, "parallelism": f"channel-shard x{world} (no collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": load_pmc_traffic(args.workload),
-                     "kernel": f"k_upols_mac<{B}>", "kernel_avg_ms": mac_avg_ms,
+                     "kernel": f"k_upols_step<{B}>", "kernel_avg_ms": mac_avg_ms,
                      "algorithmic_bytes_per_launch": bytes_mac},
         "effective_hbm_gbs_step": bytes_mac * world / (elapsed / args.steps) / 1e9 / world,
     }

@@ -20,9 +20,22 @@
 #include <concepts>
 #include <cstddef>
 #include <memory>
+#include <stdexcept>
 #include <vector>
 
 namespace neo::convolution {
+
+/// method.hpp:8-17
+enum struct method
+{
+    automatic,
+    direct,
+    fft,
+    ola,
+    ols,
+    upola,
+    upols,
+};
 
 /// fdl_index.hpp:12-41 — insert(write_pos), then for segment s: multiply(s, (write_pos + P - s) % P)
 template<typename IndexType = std::size_t>
@@ -112,14 +125,18 @@ struct upols_deleter {
 using upols_ptr = std::unique_ptr<neo_hip_upols, upols_deleter>;
 }  // namespace detail
 
-/// C independent UPOLS convolvers on one GPU, stepped together.
+/// C independent uniformly-partitioned convolvers (UPOLS, or UPOLA with method::upola)
+/// on one GPU, stepped together.
 struct upols_multichannel {
     upols_multichannel(std::size_t channels, std::size_t block_size, std::size_t partitions,
-                       int device = neo::hip::detail::default_device())
+                       int device = neo::hip::detail::default_device(), method m = method::upols)
         : _C{channels}, _B{block_size}, _P{partitions}
     {
+        if (m != method::upols && m != method::upola)
+            throw std::invalid_argument{"neo_hip: multichannel convolver supports method::upols and method::upola"};
         neo_hip_upols* h = nullptr;
-        neo::hip::check(neo_hip_upols_create(int(channels), int(block_size), int(partitions), device, &h));
+        auto create = m == method::upols ? neo_hip_upols_create : neo_hip_upola_create;
+        neo::hip::check(create(int(channels), int(block_size), int(partitions), device, &h));
         _h.reset(h);
     }
 
@@ -151,9 +168,10 @@ private:
     detail::upols_ptr _h;
 };
 
-/// Single-channel drop-in for upols_convolver<complex<float>> (uniform_partitioned_convolver.hpp:13-65):
-/// default-constructible; filter([P][B+1]) (re)initializes everything; operator()(block[B]) in place.
-template<typename Complex>
+/// Single-channel drop-in for upols_convolver<complex<float>> (uniform_partitioned_convolver.hpp:13-65)
+/// and, with M = method::upola, upola_convolver: default-constructible; filter([P][B+1])
+/// (re)initializes everything; operator()(block[B]) in place.
+template<typename Complex, method M = method::upols>
 struct hip_upols_convolver {
     static_assert(std::same_as<Complex, std::complex<float>>);
     using value_type = Complex;
@@ -170,7 +188,7 @@ struct hip_upols_convolver {
         for (std::size_t p = 0; p < P; ++p)
             for (std::size_t k = 0; k < bins; ++k) h[p * bins + k] = Complex(neo::hip::detail::at(filter, p, k));
         if (!_impl || _impl->partitions() != P || _impl->block_size() != bins - 1)
-            _impl = std::make_unique<upols_multichannel>(1, bins - 1, P);
+            _impl = std::make_unique<upols_multichannel>(1, bins - 1, P, neo::hip::detail::default_device(), M);
         _impl->filter(h.data());
         _block.resize(bins - 1);
     }
@@ -199,12 +217,20 @@ using upols_convolver = hip_upols_convolver<Complex>;
 template<typename Complex>
 using split_upols_convolver = hip_upols_convolver<Complex>;
 
+/// dense_convolver.hpp:23-24, 32-35 (overlap-add stage, same FDL MAC)
+template<typename Complex>
+using upola_convolver = hip_upols_convolver<Complex, method::upola>;
+
+template<typename Complex>
+using split_upola_convolver = hip_upols_convolver<Complex, method::upola>;
+
 /// dense_convolve<upols_convolver> (DenseConvolution.hpp:39-70) over plain arrays:
 /// signal [C][N], ir [C][L] -> out [C][N]; normalizes + partitions the IR, tail block zero-padded.
 inline auto dense_convolve(float const* signal, std::size_t channels, std::size_t num_samples, float const* ir,
-                           std::size_t ir_length, std::size_t block_size, float* out) -> void
+                           std::size_t ir_length, std::size_t block_size, float* out, method m = method::upols) -> void
 {
-    upols_multichannel conv{channels, block_size, num_partitions(ir_length, block_size)};
+    upols_multichannel conv{channels, block_size, num_partitions(ir_length, block_size),
+                            neo::hip::detail::default_device(), m};
     conv.impulse(ir, ir_length, true);
     std::vector<float> block(channels * block_size);
     for (std::size_t i = 0; i < num_samples; i += block_size) {
@@ -216,6 +242,26 @@ inline auto dense_convolve(float const* signal, std::size_t channels, std::size_
         for (std::size_t c = 0; c < channels; ++c)
             std::copy(block.data() + c * block_size, block.data() + c * block_size + n, out + c * num_samples + i);
     }
+}
+
+/// fft_convolve (fft_convolver.hpp:72-93): full linear convolution on the GPU, host arrays
+inline auto fft_convolve(float const* signal, std::size_t n, float const* patch, std::size_t m) -> std::vector<float>
+{
+    if (n == 0 || m == 0) return {};
+    std::vector<float> out(n + m - 1);
+    neo::hip::check(neo_hip_fft_convolve(signal, std::int64_t(n), patch, std::int64_t(m), out.data(), 0,
+                                         neo::hip::detail::default_device()));
+    return out;
+}
+
+/// direct_convolve (direct_convolve.hpp:58-68): same loop order and float rounding as the reference
+inline auto direct_convolve(float const* signal, std::size_t n, float const* patch, std::size_t m) -> std::vector<float>
+{
+    if (n == 0 || m == 0) return {};
+    std::vector<float> out(n + m - 1);
+    neo::hip::check(neo_hip_direct_convolve(signal, std::int64_t(n), patch, std::int64_t(m), out.data(), 0,
+                                            neo::hip::detail::default_device()));
+    return out;
 }
 
 }  // namespace neo::convolution

@@ -80,6 +80,10 @@ NEO_HIP_API int neo_hip_fft_execute_host(neo_hip_fft_plan* plan, const void* in,
  * power of two in [16, 4096]; output block t corresponds to input block t
  * (zero latency). Channels are independent. */
 NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, int device, neo_hip_upols** h);
+/* Same engine with the overlap-add stage: C instances of upola_convolver<complex<float>>
+ * (dense_convolver.hpp:23-24; overlap_add.hpp:76-106). All other neo_hip_upols_*
+ * entry points apply to it unchanged. */
+NEO_HIP_API int neo_hip_upola_create(int channels, int block, int partitions, int device, neo_hip_upols** h);
 NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h);
 /* filter [C][P][B+1] complex (uniform_partition layout), host or device memory;
  * like uniform_partitioned_convolver::filter() it also resets all state. */
@@ -112,6 +116,16 @@ NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t
                                           int is_device, int device);
 /* in place on ir [C][L]: scale all channels by min_c 1/sqrt(sum ir[c]^2). */
 NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t length, int is_device, int device);
+
+/* -- one-shot full convolution (extra/python/src/neo/__init__.py:43-48) ----
+ * out has n + m - 1 samples; n == 0 or m == 0 is a no-op (empty result).
+ * fft_convolve: fft_convolver.hpp:19-93 (one r2c/c2r pair of size
+ * 2^next_order(n+m-1) <= 2^27). direct_convolve: direct_convolve.hpp:14-56,
+ * bit-identical to the reference's float loop. Host or device pointers. */
+NEO_HIP_API int neo_hip_fft_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
+                                     int is_device, int device);
+NEO_HIP_API int neo_hip_direct_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
+                                        int is_device, int device);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,192 @@
+// convolve.hip — one-shot full linear convolution on MI355X: fft_convolve and
+// direct_convolve, the reference's Python `neo.convolve` methods
+// (extra/python/src/neo/__init__.py:43-48 -> main.cpp:169-198).
+//
+//   fft_convolve    (src/neo/convolution/fft_convolver.hpp:19-93): zero-pad both inputs
+//                   to N = 2^next_order(n+m-1), r2c both (one batched plan), complex
+//                   product, c2r, 1/N, keep n+m-1 samples.
+//   direct_convolve (src/neo/convolution/direct_convolve.hpp:14-56): one lane per output
+//                   sample, the reference's loop order and float accumulation (no FMA),
+//                   so results are bit-identical to the reference's scalar loop.
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace neo_hip {
+
+// rows [2][N]: row 0 = signal zero-padded, row 1 = patch zero-padded
+__global__ void k_pad2(const float* __restrict__ a, int64_t n, const float* __restrict__ b, int64_t m,
+                       float* __restrict__ rows, int64_t N)
+{
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < 2 * N; i += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t r = i / N, k = i - r * N;
+        rows[i] = r == 0 ? (k < n ? a[k] : 0.f) : (k < m ? b[k] : 0.f);
+    }
+}
+
+// spectra [2][bins]: row 0 *= row 1 (algorithm/multiply.hpp: out = x * y)
+__global__ void k_spectral_multiply(cf* __restrict__ spec, int64_t bins)
+{
+    for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < bins; k += int64_t(gridDim.x) * blockDim.x)
+        spec[k] = cmul(spec[k], spec[bins + k]);
+}
+
+__global__ void k_scale_copy(const float* __restrict__ in, float* __restrict__ out, int64_t len, float scale)
+{
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < len; i += int64_t(gridDim.x) * blockDim.x)
+        out[i] = in[i] * scale;
+}
+
+// direct_convolve.hpp:14-56: with (a, na) the longer input and (b, nb) the shorter,
+// out[k] = sum_{m} a[m] * b[k - m], m ascending, accumulated in float.
+__global__ void k_direct_convolve(const float* __restrict__ a, int64_t na, const float* __restrict__ b, int64_t nb,
+                                  float* __restrict__ out)
+{
+#pragma clang fp contract(off)  // product then sum, two roundings, like the reference (no FMA)
+    const int64_t mm = na + nb - 1;
+    for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < mm; k += int64_t(gridDim.x) * blockDim.x) {
+        int64_t lo, hi;  // m range
+        if (k < nb) {
+            lo = 0;
+            hi = k + 1;
+        } else {
+            lo = k - nb + 1;  // i in the reference
+            hi = std::min(nb + lo, na);
+        }
+        float acc = 0.0f;
+        for (int64_t mi = lo; mi < hi; ++mi) {
+            const float prod = a[mi] * b[k - mi];  // contract(off): not fused with the add
+            acc = acc + prod;
+        }
+        out[k] = acc;
+    }
+}
+
+unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192))); }
+
+struct device_buffers {
+    const float* a = nullptr;
+    const float* b = nullptr;
+    float* out = nullptr;
+    float* tmp_a = nullptr;
+    float* tmp_b = nullptr;
+    float* tmp_out = nullptr;
+    ~device_buffers()
+    {
+        (void)hipFree(tmp_a);
+        (void)hipFree(tmp_b);
+        (void)hipFree(tmp_out);
+    }
+    int stage(const float* ha, int64_t n, const float* hb, int64_t m, float* hout, int is_device, hipStream_t s)
+    {
+        if (is_device) {
+            a = ha;
+            b = hb;
+            out = hout;
+            return NEO_HIP_OK;
+        }
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_a), size_t(n) * sizeof(float)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_b), size_t(m) * sizeof(float)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_out), size_t(n + m - 1) * sizeof(float)));
+        NEO_HIP_CHECK(hipMemcpyAsync(tmp_a, ha, size_t(n) * sizeof(float), hipMemcpyHostToDevice, s));
+        NEO_HIP_CHECK(hipMemcpyAsync(tmp_b, hb, size_t(m) * sizeof(float), hipMemcpyHostToDevice, s));
+        a = tmp_a;
+        b = tmp_b;
+        out = tmp_out;
+        return NEO_HIP_OK;
+    }
+};
+
+}  // namespace neo_hip
+
+using namespace neo_hip;
+
+extern "C" {
+
+NEO_HIP_API int neo_hip_fft_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
+                                     int is_device, int device)
+{
+    if (n < 0 || m < 0) return fail(NEO_HIP_EINVAL, "negative length");
+    if (n == 0 || m == 0) return NEO_HIP_OK;  // fft_convolver.hpp:80-82: empty result
+    if (!signal || !patch || !out) return fail(NEO_HIP_EINVAL, "null buffer");
+    const int64_t len = n + m - 1;
+    int order = 0;
+    while ((int64_t(1) << order) < len) ++order;
+    if (order > 27) return fail(NEO_HIP_EINVAL, "convolution of %lld samples exceeds the max FFT order 27", (long long)len);
+    device_guard g(device);
+    if (g.rc) return g.rc;
+    const int64_t N = int64_t(1) << order, bins = N / 2 + 1;
+    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
+    hipStream_t s = nullptr;
+    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    int rc = NEO_HIP_OK;
+    neo_hip_fft_plan *r2c = nullptr, *c2r = nullptr;
+    float* rows = nullptr;
+    cf* spec = nullptr;
+    {
+        device_buffers io;
+        rc = io.stage(signal, n, patch, m, out, is_device, s);
+        if (!rc) rc = neo_hip_fft_plan_create(order, 2, NEO_HIP_R2C, device, &r2c);
+        if (!rc) rc = neo_hip_fft_plan_create(order, 1, NEO_HIP_C2R, device, &c2r);
+        if (!rc && (hipMalloc(reinterpret_cast<void**>(&rows), size_t(2 * N) * sizeof(float)) != hipSuccess ||
+                    hipMalloc(reinterpret_cast<void**>(&spec), size_t(2 * bins) * sizeof(cf)) != hipSuccess))
+            rc = fail(NEO_HIP_ENOMEM, "convolution buffers");
+        if (!rc) {
+            hipLaunchKernelGGL(k_pad2, dim3(grid_for(2 * N)), dim3(256), 0, s, io.a, n, io.b, m, rows, N);
+            rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "pad launch failed");
+        }
+        if (!rc) rc = neo_hip_fft_execute(r2c, rows, spec, -1, s);
+        if (!rc) {
+            hipLaunchKernelGGL(k_spectral_multiply, dim3(grid_for(bins)), dim3(256), 0, s, spec, bins);
+            rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "multiply launch failed");
+        }
+        if (!rc) rc = neo_hip_fft_execute(c2r, spec, rows, +1, s);
+        if (!rc) {
+            hipLaunchKernelGGL(k_scale_copy, dim3(grid_for(len)), dim3(256), 0, s, rows, io.out, len,
+                               1.0f / float(N));  // fft_convolver.hpp:66-70
+            rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "scale launch failed");
+        }
+        if (!rc && !is_device &&
+            hipMemcpyAsync(out, io.out, size_t(len) * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess)
+            rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
+        if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
+    }
+    neo_hip_fft_plan_destroy(r2c);
+    neo_hip_fft_plan_destroy(c2r);
+    (void)hipFree(rows);
+    (void)hipFree(spec);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+NEO_HIP_API int neo_hip_direct_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
+                                        int is_device, int device)
+{
+    if (n < 0 || m < 0) return fail(NEO_HIP_EINVAL, "negative length");
+    if (n == 0 || m == 0) return NEO_HIP_OK;
+    if (!signal || !patch || !out) return fail(NEO_HIP_EINVAL, "null buffer");
+    device_guard g(device);
+    if (g.rc) return g.rc;
+    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());
+    hipStream_t s = nullptr;
+    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    int rc = NEO_HIP_OK;
+    {
+        device_buffers io;
+        rc = io.stage(signal, n, patch, m, out, is_device, s);
+        if (!rc) {
+            const bool sig_long = n >= m;  // direct_convolve.hpp:22 vs :35
+            hipLaunchKernelGGL(k_direct_convolve, dim3(grid_for(n + m - 1)), dim3(256), 0, s, sig_long ? io.a : io.b,
+                               sig_long ? n : m, sig_long ? io.b : io.a, sig_long ? m : n, io.out);
+            rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "direct launch failed");
+        }
+        if (!rc && !is_device &&
+            hipMemcpyAsync(out, io.out, size_t(n + m - 1) * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess)
+            rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
+        if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
+    }
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+}  // extern "C"

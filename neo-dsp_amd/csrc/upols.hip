@@ -73,9 +73,11 @@ __device__ __forceinline__ cf finish(const acc4& a, bool bin0)
 // Load the overlap-save window [prev | in] of channel c as the packed complex
 // sequence z[n] = w[2n] + i w[2n+1] (lane t owns n = t + m*T), forward FFT, and
 // leave the natural-order spectrum Z in `fft` (lpad'ed).
-// E = 8 elements per lane keeps this fused r2c from raising the MAC kernel's
-// register count (the MAC loop itself needs ~60 VGPRs; occupancy is what streams HBM).
-template<int B, int E = (B / 8 <= 256 ? 8 : B / 256)>  // T = B / E <= 256 lanes
+// E = 8 elements per lane keeps this fused r2c from raising the kernel's register
+// count (the MAC loop itself needs ~60 VGPRs; occupancy is what streams HBM).
+// OLS window = [previous block | new block] (overlap_save.hpp:90-95);
+// OLA window = [new block | zeros]          (overlap_add.hpp:84-86).
+template<int B, bool OLA, int E = (B / 8 <= 256 ? 8 : B / 256)>
 __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, const cf* tw1, int tid)
 {
     constexpr int T = B / E;
@@ -88,7 +90,8 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int n = tid + m * T;
-            v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+            if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
+            else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
         }
     }
     __syncthreads();  // twiddles staged by the caller
@@ -100,11 +103,12 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
     __syncthreads();
 }
 
-// c2r of the packed spectrum X (LDS) -> samples [B, 2B) of the overlap-save window,
-// scaled by 1/2B, written to out_c (fallback_rfft_plan.hpp:38-55, overlap_save.hpp:104-111).
+// c2r of the packed spectrum X (LDS), scaled by 1/2B (fallback_rfft_plan.hpp:38-55):
+//   OLS: out = window samples [B, 2B)                       (overlap_save.hpp:104-111)
+//   OLA: out = samples [0, B) + overlap; overlap = [B, 2B)  (overlap_add.hpp:92-106)
 // E = 4 keeps the fused kernel inside its 64-VGPR budget (T = B/E <= 256 lanes).
-template<int B, int E = (B / 4 <= 256 ? 4 : B / 256)>
-__device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, int tid)
+template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256)>
+__device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, float* ovl_c, int tid)
 {
     using K = upols_cfg<B>;
     constexpr int T = B / E;
@@ -122,12 +126,28 @@ __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, flo
     }
     stockham<B, E, +1>(v, fft, tw, tid, active);
     if (active) {
-        const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108
+        const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108 / overlap_add.hpp:98
         cf* o = reinterpret_cast<cf*>(out_c);
+        if constexpr (OLA) {
+            cf* ov = reinterpret_cast<cf*>(ovl_c);
+            // the same lane reads overlap[n] (m < E/2) before writing it (m >= E/2: n - B/2)
 #pragma unroll
-        for (int m = E / 2; m < E; ++m) {  // window samples [B, 2B): z[n], n >= B/2
-            const int n = tid + m * T;
-            o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+            for (int m = 0; m < E / 2; ++m) {
+                const int n = tid + m * T;
+                const cf old = ov[n];
+                o[n] = {v[m].x * scale + old.x, v[m].y * scale + old.y};
+            }
+#pragma unroll
+            for (int m = E / 2; m < E; ++m) {
+                const int n = tid + m * T;
+                ov[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+            }
+        } else {
+#pragma unroll
+            for (int m = E / 2; m < E; ++m) {  // window samples [B, 2B): z[n], n >= B/2
+                const int n = tid + m * T;
+                o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+            }
         }
     }
 }
@@ -138,7 +158,7 @@ __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, flo
 // of a channel's S workgroups to arrive (agent-scope release -> counter -> acquire,
 // cdna_hip_programming.md §6 G16 / split-K seam) sums the slabs in the fixed order
 // s = 0..S-1 and runs the c2r: one launch per block, deterministic results.
-template<int B, bool NT, bool FUSED, int UNROLL = upols_cfg<B>::U>
+template<int B, bool FUSED, bool OLA, int UNROLL = upols_cfg<B>::U>
 __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, cf* __restrict__ part, int* __restrict__ arrivals,
@@ -161,16 +181,17 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
         for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
         const float* in_c = in + int64_t(c) * ld_in;
         float* prev_c = prev + int64_t(c) * B;
-        window_fft<B>(prev_c, in_c, fft, tw, tid);
+        window_fft<B, OLA>(prev_c, in_c, fft, tw, tid);
         cf* row = fdl + crow + int64_t(w) * pstride;
         for (int k = tid; k < B; k += 256) {
             const cf x = r2c_split<B>(fft, tw + K::TW1, k);
             xnew[k] = x;
             row[k] = x;
         }
-        // the window's second half becomes the next call's first half
-        for (int i = tid; i < B / 4; i += 256)
-            reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
+        if constexpr (!OLA) {  // the window's second half becomes the next call's first half
+            for (int i = tid; i < B / 4; i += 256)
+                reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
+        }
         __syncthreads();
     }
 
@@ -204,8 +225,8 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
 #pragma unroll
             for (int v = 0; v < K::VPT; ++v) {
                 const int q = q0 + v * K::QT;
-                hv[u][v] = ld4<NT>(H4 + int64_t(pp) * ps4 + q);
-                xv[u][v] = ld4<NT>(F4 + int64_t(fr) * ps4 + q);
+                hv[u][v] = ld4_nt(H4 + int64_t(pp) * ps4 + q);
+                xv[u][v] = ld4_nt(F4 + int64_t(fr) * ps4 + q);
             }
         }
 #pragma unroll
@@ -218,7 +239,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
 #pragma unroll
         for (int v = 0; v < K::VPT; ++v) {
             const int q = q0 + v * K::QT;
-            mac2(a[2 * v], a[2 * v + 1], ld4<NT>(H4 + int64_t(p) * ps4 + q), ld4<NT>(F4 + int64_t(fr) * ps4 + q));
+            mac2(a[2 * v], a[2 * v + 1], ld4_nt(H4 + int64_t(p) * ps4 + q), ld4_nt(F4 + int64_t(fr) * ps4 + q));
         }
     }
 
@@ -256,7 +277,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
             }
         }
         __syncthreads();
-        c2r_tail<B>(xnew, fft, tw, out_c, tid);
+        c2r_tail<B, OLA>(xnew, fft, tw, out_c, prev + int64_t(c) * B, tid);
         return;
     }
 
@@ -311,13 +332,14 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
         reinterpret_cast<float4*>(xnew)[q] = sum;
     }
     __syncthreads();
-    c2r_tail<B>(xnew, fft, tw, out_c, tid);
+    c2r_tail<B, OLA>(xnew, fft, tw, out_c, prev + int64_t(c) * B, tid);
 }
 
 // Unfused tail (one workgroup per channel): sum the S slabs in order, c2r, write.
-template<int B>
+template<int B, bool OLA>
 __global__ __launch_bounds__(256) void k_upols_finish(const cf* __restrict__ part, float* __restrict__ out,
-                                                      int64_t ld_out, const cf* __restrict__ twg, int S)
+                                                      int64_t ld_out, float* __restrict__ ovl,
+                                                      const cf* __restrict__ twg, int S)
 {
     using K = upols_cfg<B>;
     __shared__ __attribute__((aligned(16))) cf X[B];
@@ -345,7 +367,8 @@ __global__ __launch_bounds__(256) void k_upols_finish(const cf* __restrict__ par
         reinterpret_cast<float4*>(X)[q] = sum;
     }
     __syncthreads();
-    c2r_tail<B, (B / 16 <= 256 ? (B >= 16 ? 16 : B) : B / 256)>(X, fft, tw, out + int64_t(c) * ld_out, tid);
+    c2r_tail<B, OLA, (B / 16 <= 256 ? (B >= 16 ? 16 : B) : B / 256)>(X, fft, tw, out + int64_t(c) * ld_out,
+                                                                     ovl + int64_t(c) * B, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -420,11 +443,15 @@ __global__ void k_pack_filter(const cf* __restrict__ in, cf* __restrict__ out, i
 // 1/sqrt. One lane per channel.
 __global__ void k_energy_factor(const float* __restrict__ ir, int64_t L, int C, float* __restrict__ factor)
 {
+#pragma clang fp contract(off)  // x*x then +, two roundings, like the reference (no FMA)
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     const float* x = ir + int64_t(c) * L;
     float e = 0.0f;
-    for (int64_t i = 0; i < L; ++i) e = __fadd_rn(e, __fmul_rn(x[i], x[i]));
+    for (int64_t i = 0; i < L; ++i) {
+        const float sq = x[i] * x[i];  // contract(off): not fused with the add
+        e = e + sq;
+    }
     factor[c] = e == 0.0f ? 1.0f : __fdiv_rn(1.0f, __fsqrt_rn(e));
 }
 
@@ -460,7 +487,7 @@ struct neo_hip_upols {
     float* io = nullptr;       // device staging for host-pointer process()
     float* io_host = nullptr;  // pinned staging
     bool timing = false;
-    bool nt = true;  // streaming (nontemporal) filter/FDL loads; NEO_HIP_NT=0 selects plain loads (A/B)
+    bool ola = false;  // upola_convolver (overlap-add stage) instead of upols (overlap-save)
     bool fused = false;  // NEO_HIP_FUSED=1: one launch per block (last-arriver tail); A/B: slower at C4/C5
     // H / FDL layout: row p of channel c at c * cstride + p * pstride (complex units).
     // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
@@ -583,14 +610,14 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
         NEO_HIP_CHECK(hipEventRecord(ev.first, s));
     }
     const unsigned grid = unsigned(h->C) * unsigned(h->S);
-#define NEO_STEP(NTV, FU)                                                                                     \
-    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, NTV, FU>), dim3(grid), dim3(256), 0, s, in, ld_in, \
+#define NEO_STEP(FU, OL)                                                                                      \
+    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, FU, OL>), dim3(grid), dim3(256), 0, s, in, ld_in, \
                                                 out, ld_out, h->prev, h->H, h->fdl, h->part, h->arrivals, h->tw,   \
                                                 h->P, h->S, h->rows, h->wpos, h->cstride, h->pstride))
     if (h->fused) {
-        if (h->nt) NEO_STEP(true, true) else NEO_STEP(false, true)
+        if (h->ola) NEO_STEP(true, true) else NEO_STEP(true, false)
     } else {
-        if (h->nt) NEO_STEP(true, false) else NEO_STEP(false, false)
+        if (h->ola) NEO_STEP(false, true) else NEO_STEP(false, false)
     }
 #undef NEO_STEP
     NEO_HIP_LAUNCH_CHECK();
@@ -599,8 +626,13 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
         ++h->events_used;
     }
     if (!h->fused) {
-        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_finish<BB>), dim3(unsigned(h->C)), dim3(256), 0, s,
-                                                    h->part, out, ld_out, h->tw, h->S))
+        if (h->ola) {
+            NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_finish<BB, true>), dim3(unsigned(h->C)), dim3(256), 0,
+                                                        s, h->part, out, ld_out, h->prev, h->tw, h->S))
+        } else {
+            NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_finish<BB, false>), dim3(unsigned(h->C)), dim3(256),
+                                                        0, s, h->part, out, ld_out, h->prev, h->tw, h->S))
+        }
         NEO_HIP_LAUNCH_CHECK();
     }
     h->wpos = h->wpos + 1 >= h->P ? 0 : h->wpos + 1;  // fdl_index.hpp:35-37
@@ -618,7 +650,10 @@ NEO_HIP_API int neo_hip_num_partitions(int64_t length, int block, int64_t* parti
     return NEO_HIP_OK;
 }
 
-NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
+}  // extern "C"
+
+namespace {
+int create_convolver(int channels, int block, int partitions, int device, bool ola, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
     *out = nullptr;
@@ -632,7 +667,7 @@ NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, in
     h->C = channels;
     h->B = block;
     h->P = partitions;
-    if (const char* e = std::getenv("NEO_HIP_NT")) h->nt = std::atoi(e) != 0;
+    h->ola = ola;
     if (const char* e = std::getenv("NEO_HIP_FUSED")) h->fused = std::atoi(e) != 0;
     h->cstride = int64_t(partitions) * block;
     h->pstride = block;
@@ -669,6 +704,19 @@ NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, in
     if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(NEO_HIP_ERUNTIME, "sync failed"));
     *out = h;
     return NEO_HIP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
+{
+    return create_convolver(channels, block, partitions, device, false, out);
+}
+
+NEO_HIP_API int neo_hip_upola_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
+{
+    return create_convolver(channels, block, partitions, device, true, out);
 }
 
 NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h)

@@ -7,8 +7,9 @@ is libneo_hip.so (include/neo_hip.h). Put `<repo>/neo-dsp_amd` on sys.path.
 from . import _native
 from . import convolution
 from . import fft
-from .convolution import (UpolsConvolver, dense_convolve, normalize_impulse, num_partitions,
-                          split_upols_convolver, uniform_partition, upols_convolver)
+from .convolution import (UpolsConvolver, convolve, dense_convolve, direct_convolve, fft_convolve, normalize_impulse,
+                          num_partitions, split_upola_convolver, split_upols_convolver, uniform_partition,
+                          upola_convolver, upols_convolver)
 
 __version__ = "0.1.0"
 
@@ -18,8 +19,13 @@ __all__ = [
     "UpolsConvolver",
     "upols_convolver",
     "split_upols_convolver",
+    "upola_convolver",
+    "split_upola_convolver",
     "uniform_partition",
     "normalize_impulse",
     "num_partitions",
     "dense_convolve",
+    "convolve",
+    "fft_convolve",
+    "direct_convolve",
 ]

@@ -33,6 +33,7 @@ SIGNATURES = {
     "neo_hip_fft_execute": (_i, [_vp, _vp, _vp, _i, _vp]),
     "neo_hip_fft_execute_host": (_i, [_vp, _vp, _vp, _i]),
     "neo_hip_upols_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "neo_hip_upola_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
     "neo_hip_upols_destroy": (_i, [_vp]),
     "neo_hip_upols_set_filter": (_i, [_vp, _vp, _i]),
     "neo_hip_upols_set_impulse": (_i, [_vp, _vp, _i64, _i, _i]),
@@ -46,6 +47,8 @@ SIGNATURES = {
     "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
     "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),
     "neo_hip_normalize_impulse": (_i, [_vp, _i, _i64, _i, _i]),
+    "neo_hip_fft_convolve": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
+    "neo_hip_direct_convolve": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
 }
 
 _lib = None

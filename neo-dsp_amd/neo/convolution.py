@@ -8,6 +8,7 @@ Python; extra/python/src/main.cpp:227-234 only lists the `upols` method enum):
                            uniform_partitioned_convolver.hpp:13-65
   - split_upols_convolver  dense_convolver.hpp:38-42 (same math, SoA on the CPU;
                            one device layout here)
+  - upola_convolver        dense_convolver.hpp:23-24 (overlap_add.hpp:76-106 stage)
   - dense_convolve         extra/plugin/src/dsp/DenseConvolution.hpp:39-70
 Everything runs on the GPU through libneo_hip.so; there is no CPU fallback.
 """
@@ -26,7 +27,12 @@ __all__ = [
     "UpolsConvolver",
     "upols_convolver",
     "split_upols_convolver",
+    "upola_convolver",
+    "split_upola_convolver",
     "dense_convolve",
+    "fft_convolve",
+    "direct_convolve",
+    "convolve",
 ]
 
 
@@ -80,13 +86,16 @@ class UpolsConvolver:
     (output block t corresponds to input block t, overlap_save.hpp:84-112).
     """
 
-    def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0):
+    def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols"):
         lib = _native.load()
         h = ctypes.c_void_p()
-        _native.check(lib.neo_hip_upols_create(int(channels), int(block_size), int(partitions), int(device),
-                                               ctypes.byref(h)))
+        if method not in ("upols", "upola"):
+            raise ValueError(f"method must be 'upols' or 'upola', got {method!r}")
+        create = lib.neo_hip_upols_create if method == "upols" else lib.neo_hip_upola_create
+        _native.check(create(int(channels), int(block_size), int(partitions), int(device), ctypes.byref(h)))
         self._h = h
         self.channels, self.block_size, self.partitions, self.device = channels, block_size, partitions, device
+        self.method = method
 
     # -- setup ------------------------------------------------------------
     def filter(self, partitions) -> None:
@@ -191,6 +200,8 @@ class upols_convolver:
     """Single-channel drop-in for upols_convolver<complex<float>>: default-constructible,
     filter([P][B+1]) then __call__(block[B]) in place."""
 
+    _method = "upols"
+
     def __init__(self, device: int = 0):
         self._impl = None
         self._device = device
@@ -202,7 +213,7 @@ class upols_convolver:
         P, bins = H.shape
         impl = self._impl
         if impl is None or (impl.partitions, impl.block_size) != (P, bins - 1):
-            impl = UpolsConvolver(1, bins - 1, P, self._device)
+            impl = UpolsConvolver(1, bins - 1, P, self._device, method=self._method)
         impl.filter(H[None])
         self._impl = impl
 
@@ -215,16 +226,25 @@ class upols_convolver:
 split_upols_convolver = upols_convolver
 
 
-def dense_convolve(signal, impulse_response, block_size: int, device: int = 0) -> np.ndarray:
-    """dense_convolve<upols_convolver> (DenseConvolution.hpp:39-70): normalize the IR matrix,
-    partition it, run every block (tail zero-padded) and return the output truncated to N."""
+class upola_convolver(upols_convolver):
+    """Single-channel drop-in for upola_convolver<complex<float>> (overlap-add stage)."""
+
+    _method = "upola"
+
+
+split_upola_convolver = upola_convolver
+
+
+def dense_convolve(signal, impulse_response, block_size: int, device: int = 0, method: str = "upols") -> np.ndarray:
+    """dense_convolve<upols_convolver | upola_convolver> (DenseConvolution.hpp:39-70): normalize
+    the IR matrix, partition it, run every block (tail zero-padded), output truncated to N."""
     sig = np.ascontiguousarray(np.atleast_2d(np.asarray(signal, dtype=np.float32)))
     ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
     C, N = sig.shape
     if ir.shape[0] != C:
         raise ValueError("signal and impulse response channel counts differ")
     P = num_partitions(ir.shape[1], block_size)
-    conv = UpolsConvolver(C, block_size, P, device)
+    conv = UpolsConvolver(C, block_size, P, device, method=method)
     conv.set_impulse(ir, normalize=True)
     nb = -(-N // block_size)
     out = np.empty_like(sig)
@@ -237,3 +257,39 @@ def dense_convolve(signal, impulse_response, block_size: int, device: int = 0) -
         out[:, lo:hi] = block[:, : hi - lo]
     conv.close()
     return out
+
+
+def _one_shot(fn, signal, patch, device):
+    a = np.ascontiguousarray(np.asarray(signal), dtype=None)
+    b = np.ascontiguousarray(np.asarray(patch), dtype=None)
+    if a.ndim != 1 or b.ndim != 1:
+        raise RuntimeError("unsupported dimension: in1 and in2 must be 1-D")  # main.cpp:173-175
+    if a.dtype != np.float32 or b.dtype != np.float32:
+        raise TypeError("neo_hip convolves float32 data (the GPU path computes in float32)")
+    if a.size == 0 or b.size == 0:
+        return np.zeros(0, np.float32)
+    out = np.empty(a.size + b.size - 1, np.float32)
+    _native.check(fn(_ptr(a), a.size, _ptr(b), b.size, _ptr(out), 0, int(device)))
+    return out
+
+
+def fft_convolve(signal, patch, device: int = 0) -> np.ndarray:
+    """Full linear convolution through one r2c/c2r pair (fft_convolver.hpp:19-93)."""
+    return _one_shot(_native.load().neo_hip_fft_convolve, signal, patch, device)
+
+
+def direct_convolve(signal, patch, device: int = 0) -> np.ndarray:
+    """Full linear convolution, direct sum (direct_convolve.hpp:14-56), bit-identical loop order."""
+    return _one_shot(_native.load().neo_hip_direct_convolve, signal, patch, device)
+
+
+def convolve(in1, in2, mode: str = "full", method: str = "auto", device: int = 0) -> np.ndarray:
+    """neo.convolve (extra/python/src/neo/__init__.py:43-48): method "fft" -> fft_convolve,
+    anything else -> direct_convolve; only mode "full" (others raise RuntimeError, main.cpp:197)."""
+    if mode not in ("full", "valid", "same"):
+        raise KeyError(mode)
+    if mode != "full":
+        raise RuntimeError("unsupported convolution mode")
+    if method == "fft":
+        return fft_convolve(in1, in2, device)
+    return direct_convolve(in1, in2, device)

@@ -275,6 +275,8 @@ typedef struct oracle_upols {
     float* cbuf;    /* [n] complex: the overlap stage's complex buffer */
     float* rbuf;    /* [n] real */
     int split;      /* 1: split_upols_convolver (dense_split_fdl/filter) */
+    int ola;        /* 1: upola_convolver (overlap_add stage, overlap_add.hpp:76-106) */
+    float* overlap; /* [B] overlap-add tail */
     float* Hs;      /* split filter [2][P][bins] */
     float* fdls;    /* split fdl [2][P][bins] */
     float* accs;    /* split accumulator [2][bins] */
@@ -312,7 +314,7 @@ void oracle_upols_destroy(oracle_upols* u)
 {
     if (!u) return;
     free(u->H); free(u->fdl); free(u->acc); free(u->window); free(u->cbuf); free(u->rbuf);
-    free(u->Hs); free(u->fdls); free(u->accs);
+    free(u->Hs); free(u->fdls); free(u->accs); free(u->overlap);
     free(u);
 }
 
@@ -347,9 +349,40 @@ static void upols_callback(oracle_upols* u, float* coeffs /* bins complex, in pl
     if (++u->write_pos >= P) u->write_pos = 0;
 }
 
+/* overlap_add::operator() (overlap_add.hpp:76-106): window = [block | 0], rfft,
+ * callback, irfft, 1/N, block = window[0:B] + overlap, overlap = window[B:2B]. */
+static int upola_process(oracle_upols* u, float* block)
+{
+    const size_t B = u->B, n = u->n;
+    memcpy(u->window, block, sizeof(float) * B);
+    memset(u->window + B, 0, sizeof(float) * (n - B));
+    int rc = oracle_rfft(u->order, u->window, u->cbuf);
+    if (rc) return rc;
+    upols_callback(u, u->cbuf);
+    rc = oracle_irfft(u->order, u->cbuf, u->window);
+    if (rc) return rc;
+    const float scale = 1.0f / (float)n;
+    for (size_t i = 0; i < n; ++i) u->window[i] *= scale;
+    for (size_t i = 0; i < B; ++i) block[i] = u->window[i] + u->overlap[i];
+    memcpy(u->overlap, u->window + B, sizeof(float) * B);
+    return 0;
+}
+
+/* uniform_partitioned_convolver<overlap_add, ...> = upola_convolver (dense_convolver.hpp:23-24) */
+oracle_upols* oracle_upola_create(size_t P, size_t bins, const float* H, int split)
+{
+    oracle_upols* u = oracle_upols_create(P, bins, H, split);
+    if (!u) return NULL;
+    u->ola = 1;
+    u->overlap = (float*)calloc(u->B, sizeof(float));
+    /* overlap_add.hpp:43-46: next_order(output_size<full>(B, F)) = next_order(2B - 1) */
+    return u;
+}
+
 /* one block of B samples, in place (overlap_save::operator(), :84-112) */
 int oracle_upols_process(oracle_upols* u, float* block)
 {
+    if (u->ola) return upola_process(u, block);
     const size_t B = u->B, n = u->n;
     /* slide_window_left + copy block -> window[n-B, n) */
     memmove(u->window, u->window + B, sizeof(float) * (n - B));
@@ -411,7 +444,7 @@ int oracle_overlap_save_identity(size_t block, float* signal, size_t num_blocks)
 
 typedef struct {
     const float* signal; float* out; const float* parts;
-    size_t C, N, P, B, c0, c1; int rc;
+    size_t C, N, P, B, c0, c1; int rc; int ola;
 } dc_job;
 
 static void* dc_worker(void* arg)
@@ -420,7 +453,8 @@ static void* dc_worker(void* arg)
     const size_t bins = j->B + 1;
     float* block = (float*)malloc(sizeof(float) * j->B);
     for (size_t c = j->c0; c < j->c1 && j->rc == 0; ++c) {
-        oracle_upols* u = oracle_upols_create(j->P, bins, j->parts + 2 * bins * j->P * c, 0);
+        oracle_upols* u = j->ola ? oracle_upola_create(j->P, bins, j->parts + 2 * bins * j->P * c, 0)
+                                 : oracle_upols_create(j->P, bins, j->parts + 2 * bins * j->P * c, 0);
         if (!u) { j->rc = -2; break; }
         for (size_t i = 0; i < j->N; i += j->B) {
             const size_t cnt = (j->N - i) < j->B ? (j->N - i) : j->B;
@@ -435,8 +469,8 @@ static void* dc_worker(void* arg)
     return NULL;
 }
 
-int oracle_dense_convolve(const float* signal, float* out, const float* parts,
-                          size_t C, size_t N, size_t P, size_t B, int threads)
+int oracle_dense_convolve_method(const float* signal, float* out, const float* parts,
+                                 size_t C, size_t N, size_t P, size_t B, int threads, int ola)
 {
     if (threads < 1) threads = 1;
     if ((size_t)threads > C) threads = (int)C;
@@ -444,7 +478,7 @@ int oracle_dense_convolve(const float* signal, float* out, const float* parts,
     dc_job jobs[256];
     if (threads > 256) threads = 256;
     for (int t = 0; t < threads; ++t) {
-        jobs[t] = (dc_job){signal, out, parts, C, N, P, B, C * t / threads, C * (t + 1) / threads, 0};
+        jobs[t] = (dc_job){signal, out, parts, C, N, P, B, C * t / threads, C * (t + 1) / threads, 0, ola};
         if (threads == 1) dc_worker(&jobs[t]);
         else pthread_create(&tid[t], NULL, dc_worker, &jobs[t]);
     }
@@ -454,6 +488,81 @@ int oracle_dense_convolve(const float* signal, float* out, const float* parts,
         if (jobs[t].rc) rc = jobs[t].rc;
     }
     return rc;
+}
+
+int oracle_dense_convolve(const float* signal, float* out, const float* parts,
+                          size_t C, size_t N, size_t P, size_t B, int threads)
+{
+    return oracle_dense_convolve_method(signal, out, parts, C, N, P, B, threads, 0);
+}
+
+/* no-op-callback overlap_add stage (overlap_test.cpp:21-64 with overlap_add) */
+int oracle_overlap_add_identity(size_t block, float* signal, size_t num_blocks)
+{
+    const size_t bins = block + 1;
+    float* h = (float*)calloc(2 * bins, sizeof(float));
+    for (size_t k = 0; k < bins; ++k) h[2 * k] = 1.0f; /* identity: all-ones spectrum, one partition */
+    oracle_upols* u = oracle_upola_create(1, bins, h, 0);
+    free(h);
+    if (!u) return -2;
+    int rc = oracle_upols_run(u, signal, num_blocks);
+    oracle_upols_destroy(u);
+    return rc;
+}
+
+/* fft_convolve (fft_convolver.hpp:19-93): full linear convolution through one
+ * next_order(N+M-1) rfft pair; out has N+M-1 samples. */
+int oracle_fft_convolve(const float* signal, size_t n, const float* patch, size_t m, float* out)
+{
+    if (n == 0 || m == 0) return 0;
+    const size_t len = n + m - 1;
+    int order = 0;
+    while (((size_t)1 << order) < len) ++order;
+    const size_t N = (size_t)1 << order, bins = N / 2 + 1;
+    float* tmp = (float*)calloc(N, sizeof(float));
+    float* a = (float*)malloc(sizeof(float) * 2 * bins);
+    float* b = (float*)malloc(sizeof(float) * 2 * bins);
+    memcpy(tmp, signal, sizeof(float) * n);
+    int rc = oracle_rfft(order, tmp, a);
+    memset(tmp, 0, sizeof(float) * N);
+    memcpy(tmp, patch, sizeof(float) * m);
+    if (!rc) rc = oracle_rfft(order, tmp, b);
+    if (!rc) {
+        /* multiply (algorithm/multiply.hpp): complex product */
+        for (size_t k = 0; k < bins; ++k) {
+            const float xr = a[2 * k], xi = a[2 * k + 1], yr = b[2 * k], yi = b[2 * k + 1];
+            a[2 * k] = xr * yr - xi * yi;
+            a[2 * k + 1] = xr * yi + xi * yr;
+        }
+        rc = oracle_irfft(order, a, tmp);
+    }
+    if (!rc) {
+        const float scale = 1.0f / (float)N;
+        for (size_t i = 0; i < len; ++i) out[i] = tmp[i] * scale;
+    }
+    free(tmp); free(a); free(b);
+    return rc;
+}
+
+/* direct_convolve (direct_convolve.hpp:14-56), same loop order and float accumulation */
+void oracle_direct_convolve(const float* signal, size_t n, const float* patch, size_t l, float* out)
+{
+    const size_t mm = n + l - 1;
+    const float* a = signal;  /* n >= l: sum signal[m] * patch[k - m] */
+    const float* b = patch;
+    size_t na = n, nb = l;
+    if (n < l) { a = patch; b = signal; na = l; nb = n; }  /* :35-50 swaps the roles */
+    size_t i = 0;
+    for (size_t k = 0; k < nb; ++k) {
+        out[k] = 0.0f;
+        for (size_t m = 0; m <= k; ++m) out[k] += a[m] * b[k - m];
+    }
+    for (size_t k = nb; k < mm; ++k) {
+        out[k] = 0.0f;
+        ++i;
+        const size_t t1 = nb + i, tmin = t1 < na ? t1 : na;
+        for (size_t m = i; m < tmin; ++m) out[k] += a[m] * b[k - m];
+    }
 }
 
 /* ------------------------------------------------------------------------ */

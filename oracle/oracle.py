@@ -58,6 +58,12 @@ def lib():
         L.oracle_overlap_save_identity.argtypes = [_sz, _f32p, _sz]
         L.oracle_dense_convolve.argtypes = [_f32p, _f32p, _f32p, _sz, _sz, _sz, _sz, ctypes.c_int]
         L.oracle_noise.argtypes = [ctypes.c_uint64, _f32p, _sz]
+        L.oracle_upola_create.argtypes = [_sz, _sz, _f32p, ctypes.c_int]
+        L.oracle_upola_create.restype = ctypes.c_void_p
+        L.oracle_dense_convolve_method.argtypes = [_f32p, _f32p, _f32p, _sz, _sz, _sz, _sz, ctypes.c_int, ctypes.c_int]
+        L.oracle_overlap_add_identity.argtypes = [_sz, _f32p, _sz]
+        L.oracle_fft_convolve.argtypes = [_f32p, _sz, _f32p, _sz, _f32p]
+        L.oracle_direct_convolve.argtypes = [_f32p, _sz, _f32p, _sz, _f32p]
         _lib = L
     return _lib
 
@@ -185,13 +191,15 @@ def uniform_partition(ir: np.ndarray, block: int) -> np.ndarray:
 
 
 class Upols:
-    """upols_convolver<complex<float>> (or split_upols_convolver with split=True), one channel."""
+    """upols_convolver<complex<float>> (split_upols_convolver with split=True; upola_convolver
+    with ola=True), one channel."""
 
-    def __init__(self, filt: np.ndarray, split: bool = False):
+    def __init__(self, filt: np.ndarray, split: bool = False, ola: bool = False):
         filt = np.ascontiguousarray(filt, dtype=np.complex64)
         self.P, self.bins = filt.shape
         self.B = self.bins - 1
-        self._h = lib().oracle_upols_create(self.P, self.bins, _cf(filt).reshape(-1), int(split))
+        create = lib().oracle_upola_create if ola else lib().oracle_upols_create
+        self._h = create(self.P, self.bins, _cf(filt).reshape(-1), int(split))
 
     def __call__(self, block: np.ndarray) -> np.ndarray:
         b = np.array(block, dtype=np.float32, copy=True)
@@ -216,13 +224,41 @@ def overlap_save_identity(signal: np.ndarray, block: int) -> np.ndarray:
     return s
 
 
-def dense_convolve(signal: np.ndarray, partitions: np.ndarray, threads: int = 1) -> np.ndarray:
-    """dense_convolve<upols_convolver> on already-partitioned filters [C][P][B+1]."""
+def dense_convolve(signal: np.ndarray, partitions: np.ndarray, threads: int = 1, method: str = "upols") -> np.ndarray:
+    """dense_convolve<upols_convolver | upola_convolver> on already-partitioned filters [C][P][B+1]."""
     signal = np.ascontiguousarray(signal, dtype=np.float32)
     C, N = signal.shape
     _, P, bins = partitions.shape
     out = np.empty_like(signal)
-    rc = lib().oracle_dense_convolve(signal, out, _cf(partitions).reshape(-1), C, N, P, bins - 1, threads)
+    rc = lib().oracle_dense_convolve_method(signal, out, _cf(partitions).reshape(-1), C, N, P, bins - 1, threads,
+                                            int(method == "upola"))
     if rc:
         raise RuntimeError("oracle dense_convolve failed")
+    return out
+
+
+def overlap_add_identity(signal: np.ndarray, block: int) -> np.ndarray:
+    s = np.array(signal, dtype=np.float32, copy=True)
+    lib().oracle_overlap_add_identity(block, s, s.shape[0] // block)
+    return s
+
+
+def fft_convolve(signal: np.ndarray, patch: np.ndarray) -> np.ndarray:
+    """fft_convolve (fft_convolver.hpp:19-93), full mode."""
+    a = np.ascontiguousarray(signal, dtype=np.float32)
+    b = np.ascontiguousarray(patch, dtype=np.float32)
+    if a.size == 0 or b.size == 0:
+        return np.zeros(0, np.float32)
+    out = np.empty(a.size + b.size - 1, np.float32)
+    if lib().oracle_fft_convolve(a, a.size, b, b.size, out):
+        raise RuntimeError("oracle fft_convolve failed")
+    return out
+
+
+def direct_convolve(signal: np.ndarray, patch: np.ndarray) -> np.ndarray:
+    """direct_convolve (direct_convolve.hpp:14-56), full mode."""
+    a = np.ascontiguousarray(signal, dtype=np.float32)
+    b = np.ascontiguousarray(patch, dtype=np.float32)
+    out = np.empty(a.size + b.size - 1, np.float32)
+    lib().oracle_direct_convolve(a, a.size, b, b.size, out)
     return out

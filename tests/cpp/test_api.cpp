@@ -125,6 +125,11 @@ static void test_convolver_identity()
         conv.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
         for (std::size_t i = 0; i < output.size(); i += B) conv(neo::hip::make_view(output.data() + i, B));
         REQUIRE(max_abs_diff(output, signal) <= 1e-5);
+        output = signal;
+        neo::convolution::upola_convolver<cf> upola;
+        upola.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
+        for (std::size_t i = 0; i < output.size(); i += B) upola(neo::hip::make_view(output.data() + i, B));
+        REQUIRE(max_abs_diff(output, signal) <= 1e-5);
         neo::convolution::split_upols_convolver<cf> split;
         output = signal;
         split.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
@@ -168,6 +173,18 @@ static void test_dense_convolve_vs_oracle()
     REQUIRE(hd / hp <= 1e-5);
 }
 
+static void test_one_shot_convolve()
+{
+    auto const x = rnoise(55, 1000), p = rnoise(56, 333);
+    auto const f = neo::convolution::fft_convolve(x.data(), x.size(), p.data(), p.size());
+    auto const d = neo::convolution::direct_convolve(x.data(), x.size(), p.data(), p.size());
+    REQUIRE(f.size() == 1332 && d.size() == 1332);
+    double peak = 0;
+    for (float v : d) peak = std::max(peak, double(std::abs(v)));
+    REQUIRE(max_abs_diff(f, d) / peak <= 1e-5);
+    REQUIRE(neo::convolution::fft_convolve(x.data(), 0, p.data(), p.size()).empty());
+}
+
 static void test_fdl_index()
 {
     // fdl_index_test.cpp:7-68
@@ -204,6 +221,7 @@ int main()
     test_convolver_identity();
     test_dense_convolve_vs_oracle();
     test_uniform_partition_shapes();
+    test_one_shot_convolve();
     std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);
     return failures ? 1 : 0;
 }

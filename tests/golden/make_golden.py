@@ -79,6 +79,24 @@ def main():
                           "P": int(parts.shape[1])}
         np.savez_compressed(os.path.join(HERE, name + ".npz"), ir=ir, signal=sig, out=out)
 
+    # (5b) UPOLA (upola_convolver) output, 2 ch, B=256, L=2560, 40 blocks
+    B, L, C, nb, seed = 256, 2560, 2, 40, 8
+    ir = np.stack([O.noise(seed * 100 + c, L) for c in range(C)])
+    irn = O.normalize_impulse(ir)
+    parts = O.uniform_partition(irn, B)
+    sig = np.stack([O.noise(seed * 1000 + c, B * nb) for c in range(C)])
+    out = O.dense_convolve(sig, parts, method="upola")
+    errs = [peak(out[c], np.convolve(sig[c].astype(np.float64), irn[c].astype(np.float64))[: B * nb]) for c in range(C)]
+    manifest["upola_b256_l2560_2ch_seed8"] = {"B": B, "L": L, "C": C, "blocks": nb, "vs_f64_direct": max(errs)}
+    np.savez_compressed(os.path.join(HERE, "upola_b256_l2560_2ch_seed8.npz"), ir=ir, signal=sig, out=out)
+
+    # (5c) fft_convolve / direct_convolve, signal 5000, patch 777, seed 9
+    x, p = O.noise(90, 5000), O.noise(91, 777)
+    fc, dc = O.fft_convolve(x, p), O.direct_convolve(x, p)
+    t = np.convolve(x.astype(np.float64), p.astype(np.float64))
+    manifest["convolve_5000x777_seed9"] = {"fft_vs_f64": peak(fc, t), "direct_vs_f64": peak(dc, t)}
+    np.savez(os.path.join(HERE, "convolve_5000x777_seed9.npz"), signal=x, patch=p, fft=fc, direct=dc)
+
     # (6) multiply_add KAT (multiply_add_test.cpp:52-95)
     for n in (2, 33, 128):
         y = O.multiply_add(np.full(n, 1 + 2j, np.complex64), np.full(n, 3 + 4j, np.complex64),

@@ -199,3 +199,48 @@ def test_noise_generator(oracle):
     assert np.array_equal(oracle.noise(123, 5000), oracle.noise_np(123, 5000))
     x = oracle.noise(1, 100000)
     assert x.min() >= -1 and x.max() < 1 and abs(x.mean()) < 0.01
+
+
+@pytest.mark.parametrize("B", [128, 512])
+def test_overlap_add_identity(oracle, B):
+    """overlap_test.cpp:21-64 with overlap_add: a pass-through spectrum gives output == input."""
+    sig = oracle.noise(B + 1, B * 8)
+    out = oracle.overlap_add_identity(sig, B)
+    assert np.abs(out - sig).max() <= 1e-5
+
+
+@pytest.mark.parametrize("B", [128, 256, 512, 1024])
+@pytest.mark.parametrize("split", [False, True])
+def test_upola_identity(oracle, B, split):
+    """uniform_partitioned_convolver_test.cpp:35-75 (upola_convolver, split_upola_convolver)."""
+    h = np.zeros((3, B + 1), np.complex64)
+    h[0] = 1
+    sig = oracle.noise(B + 7, B * 20)
+    out = oracle.Upols(h, split=split, ola=True).run(sig)
+    assert np.abs(out - sig).max() <= 1e-5
+
+
+def test_upola_matches_direct_convolution(oracle):
+    B, L = 256, 3000
+    ir = oracle.normalize_impulse(oracle.noise(11, L))
+    sig = oracle.noise(12, B * 30)
+    out = oracle.Upols(oracle.uniform_partition(ir, B)[0], ola=True).run(sig)
+    truth = np.convolve(sig.astype(np.float64), ir.astype(np.float64))[: len(sig)]
+    assert peak_err(out, truth) < 1e-6
+
+
+@pytest.mark.parametrize("n,m", [(2, 2), (3, 9), (10, 4), (128, 7), (555, 10), (1000, 333)])
+def test_fft_and_direct_convolve(oracle, n, m):
+    """fft_convolver_test.cpp:15-38, direct_convolve_test.cpp:15-32, python test.py:21-39:
+    a delta patch reproduces the signal; both methods equal float64 np.convolve."""
+    x = oracle.noise(n, n)
+    p = oracle.noise(m, m)
+    truth = np.convolve(x.astype(np.float64), p.astype(np.float64))
+    for f in (oracle.fft_convolve, oracle.direct_convolve):
+        y = f(x, p)
+        assert y.shape == (n + m - 1,)
+        assert peak_err(y, truth) < 2e-6
+    delta = np.zeros(m, np.float32)
+    delta[0] = 1
+    for f in (oracle.fft_convolve, oracle.direct_convolve):
+        assert np.abs(f(x, delta)[:n] - x).max() <= 1e-5

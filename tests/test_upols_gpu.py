@@ -75,11 +75,12 @@ def test_uniform_partition_vs_oracle(neo_gpu, oracle):
 
 def test_normalize_impulse_bit_exact(neo_gpu, oracle):
     """Sequential float energy (normalize_energy.hpp:21-33): the GPU rounds identically."""
-    ir = np.stack([oracle.noise(50 + c, 48000) * (c + 1) for c in range(4)]).astype(np.float32)
-    ref = oracle.normalize_impulse(ir)
-    got = ir.copy()
-    neo_gpu.normalize_impulse(got)
-    assert np.array_equal(got, ref)
+    for C, L in [(4, 48000), (2, 480000)]:  # up to 10 s @ 48 kHz, where rounding order matters most
+        ir = np.stack([oracle.noise(50 + c, L) * (c + 1) for c in range(C)]).astype(np.float32)
+        ref = oracle.normalize_impulse(ir)
+        got = ir.copy()
+        neo_gpu.normalize_impulse(got)
+        assert np.array_equal(got, ref), (C, L)
     # normalize_impulse_test.cpp:13-56 known answers
     v = np.zeros(33, np.float32)
     v[0] = 2
@@ -216,3 +217,69 @@ def test_multirow_splits_with_wraparound(neo_gpu, oracle):
         # S = ceil(P / ceil(P / min(ceil(t/C), ceil(P/8), 64)))
         assert conv.splits == {"6": 3, "1": 1, "64": 7}[target]
         assert peak_err(out, ref) <= TOL, (target, conv.splits)
+
+
+# ---------------------------------------------------------------- UPOLA (overlap-add stage)
+@pytest.mark.parametrize("B", [128, 256, 512, 1024])
+def test_upola_identity_ir(neo_gpu, oracle, B):
+    """uniform_partitioned_convolver_test.cpp:35-75 with upola_convolver / split_upola_convolver."""
+    for cls in (neo_gpu.upola_convolver, neo_gpu.split_upola_convolver):
+        sig = oracle.noise(B + 3, B * 20)
+        conv = cls()
+        conv.filter(identity_impulse(B, 3))
+        out = sig.copy()
+        for i in range(0, len(out), B):
+            blk = out[i:i + B].copy()
+            conv(blk)
+            out[i:i + B] = blk
+        assert np.abs(out - sig).max() <= 1e-5
+
+
+@pytest.mark.parametrize("B,L,C,nb", [(512, 4096, 1, 40), (256, 2560, 2, 40), (128, 1000, 3, 30), (16, 100, 2, 20),
+                                      (2048, 9000, 1, 6), (4096, 12000, 1, 5), (64, 64 * 50, 2, 120)])
+def test_upola_random_ir_vs_oracle(neo_gpu, oracle, B, L, C, nb):
+    ir = np.stack([oracle.noise(120 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    sig = np.stack([oracle.noise(130 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts, method="upola")
+    got = neo_gpu.dense_convolve(sig, ir, B, method="upola")
+    assert peak_err(got, ref) <= TOL
+    assert np.abs(got - ref).max() <= 1e-5
+
+
+def test_golden_upola(neo_gpu):
+    g = np.load(os.path.join(GOLD, "upola_b256_l2560_2ch_seed8.npz"))
+    got = neo_gpu.dense_convolve(g["signal"], g["ir"], 256, method="upola")
+    assert peak_err(got, g["out"]) <= TOL
+
+
+def test_upola_equals_upols(neo_gpu, oracle):
+    """Both stages compute the same linear convolution of the stream."""
+    B, L, C, nb = 256, 4000, 2, 30
+    ir = np.stack([oracle.noise(140 + c, L) for c in range(C)])
+    sig = np.stack([oracle.noise(150 + c, B * nb) for c in range(C)])
+    a = neo_gpu.dense_convolve(sig, ir, B, method="upols")
+    b = neo_gpu.dense_convolve(sig, ir, B, method="upola")
+    assert peak_err(b, a) <= TOL
+
+
+def test_fused_step_matches_two_launch(neo_gpu, oracle):
+    """NEO_HIP_FUSED=1 (last-arriver tail in one launch) equals the default two-launch step."""
+    import os as _os
+
+    B, L, C, nb = 256, 60 * 256, 3, 70
+    ir = np.stack([oracle.noise(160 + c, L) for c in range(C)])
+    sig = np.stack([oracle.noise(170 + c, B * nb) for c in range(C)])
+    outs = []
+    for fused in ("0", "1"):
+        for method in ("upols", "upola"):
+            _os.environ["NEO_HIP_FUSED"] = fused
+            _os.environ["NEO_HIP_SPLIT_WGS"] = "12"  # 4 splits per channel
+            try:
+                outs.append((fused, method, neo_gpu.dense_convolve(sig, ir, B, method=method)))
+            finally:
+                del _os.environ["NEO_HIP_FUSED"], _os.environ["NEO_HIP_SPLIT_WGS"]
+    ref = {m: oracle.dense_convolve(sig, oracle.uniform_partition(oracle.normalize_impulse(ir), B), method=m)
+           for m in ("upols", "upola")}
+    for fused, method, out in outs:
+        assert peak_err(out, ref[method]) <= TOL, (fused, method)
