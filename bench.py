@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS) + ["c2"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--host-io", action="store_true",
+                    help="time the host-buffer boundary (neo_hip_upols_process on pinned-staged host memory): "
+                         "PCIe-inclusive, reported for DESIGN.md, never the headline value")
     return ap.parse_args()
 
 
@@ -232,6 +235,36 @@ def run_upols(args, world, rank, local):
     return res
 
 
+def run_upols_host_io(args, world, rank, local):
+    """Host-buffer boundary: every block is copied host->device, processed and copied back
+    (the plugin's processFrame pattern, DenseConvolution.cpp:62-74)."""
+    import numpy as np
+    import torch
+    import neo
+
+    C, B, L = WORKLOADS[args.workload]
+    local = device_for(local)
+    torch.cuda.set_device(local)
+    P = neo.num_partitions(L, B)
+    conv = neo.UpolsConvolver(C, B, P, device=local)
+    g = torch.Generator(device="cuda").manual_seed(8 + rank)
+    conv.set_impulse(torch.rand((C, L), generator=g, device="cuda").mul_(2).sub_(1), normalize=True)
+    block = (np.random.default_rng(rank).random((C, B), dtype=np.float32) * 2 - 1)
+    t_warm = time.perf_counter()
+    while time.perf_counter() - t_warm < WARM_SECONDS:
+        conv(block)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        conv(block)
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    return {"metric": "Msamples/sec UPOLS convolver, host buffers (PCIe-inclusive, not the headline)",
+            "value": world * C * B * args.steps / elapsed / 1e6, "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "ms_per_step": elapsed * 1e3 / args.steps,
+            "config": {"workload": f"UPOLS {args.workload} host io", "bytes_per_step_pcie": 2 * 4 * C * B}}
+
+
 def run_fft(args, world, rank, local):
     import torch
     import neo
@@ -289,6 +322,9 @@ def main():
     world, rank, local = dist_setup(args)
     if args.workload == "c2":
         res = run_fft(args, world, rank, local)
+    elif args.host_io:
+        res = run_upols_host_io(args, world, rank, local)
+        args.no_cpu_baseline = True
     else:
         res = run_upols(args, world, rank, local)
     if rank == 0:

@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 TAG=${1:-r1}
 cd /tmp && export TMPDIR=/tmp
-for W in c5 c2; do
+for W in c5 c4 c2; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${W}_${C}_$TAG -o run -- \
       python3 $R/bench.py --workload $W --steps 5 --warmup 1 --no-cpu-baseline > $O/pmc_${W}_${C}_$TAG.log 2>&1 || exit $?
