@@ -440,19 +440,59 @@ __global__ void k_pack_filter(const cf* __restrict__ in, cf* __restrict__ out, i
 
 // normalize_energy_factor (normalize_energy.hpp:17-44) with the reference's exact
 // rounding: sequential float sum of x*x (multiply, then add; no FMA), then
-// 1/sqrt. One lane per channel.
-__global__ void k_energy_factor(const float* __restrict__ ir, int64_t L, int C, float* __restrict__ factor)
+// 1/sqrt.
+// One workgroup per kEnergyGroup channels: all 256 lanes stream a [G][256] tile of the
+// impulse with coalesced loads into LDS (double-buffered), then lane g < G folds row g
+// into its channel's energy in sample order. Zero padding past L adds +0.0f, which
+// leaves the running sum unchanged, so the rounding equals the reference's loop.
+constexpr int kEnergyGroup = 16;
+constexpr int kEnergyTile = 256;
+
+__global__ __launch_bounds__(256) void k_energy_factor(const float* __restrict__ ir, int64_t L, int C,
+                                                       float* __restrict__ factor)
 {
 #pragma clang fp contract(off)  // x*x then +, two roundings, like the reference (no FMA)
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const float* x = ir + int64_t(c) * L;
+    constexpr int G = kEnergyGroup, T = kEnergyTile, LD = T + 4;  // +4: conflict-free b128 row reads
+    __shared__ float tile[2][G * LD];
+    const int c0 = int(blockIdx.x) * G, t = int(threadIdx.x);
+    const int64_t chunks = (L + T - 1) / T;
+    float r[G];
+    bool valid = true;
+    auto load = [&](int64_t chunk) {
+        const int64_t i = chunk * T + t;
+        valid = i < L;
+        const int64_t ic = valid ? i : L - 1;  // clamped address, no branch around the loads
+#pragma unroll
+        for (int g = 0; g < G; ++g)  // rows past C repeat channel C-1; their sums are discarded
+            r[g] = ir[int64_t(min(c0 + g, C - 1)) * L + ic];
+    };
+    auto store = [&](int buf) {  // the zero select sits here so the loads stay in flight
+#pragma unroll
+        for (int g = 0; g < G; ++g) tile[buf][g * LD + t] = valid ? r[g] : 0.0f;
+    };
     float e = 0.0f;
-    for (int64_t i = 0; i < L; ++i) {
-        const float sq = x[i] * x[i];  // contract(off): not fused with the add
-        e = e + sq;
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int64_t chunk = 0; chunk < chunks; ++chunk) {
+        const int buf = int(chunk & 1);
+        if (chunk + 1 < chunks) load(chunk + 1);  // in flight while row t is summed
+        if (t < G) {
+            const float* row = &tile[buf][t * LD];
+#pragma unroll 8
+            for (int j = 0; j < T; j += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(row + j);
+                const float s0 = v.x * v.x, s1 = v.y * v.y, s2 = v.z * v.z, s3 = v.w * v.w;
+                e = e + s0;
+                e = e + s1;
+                e = e + s2;
+                e = e + s3;
+            }
+        }
+        if (chunk + 1 < chunks) store(buf ^ 1);
+        __syncthreads();
     }
-    factor[c] = e == 0.0f ? 1.0f : __fdiv_rn(1.0f, __fsqrt_rn(e));
+    if (t < G && c0 + t < C) factor[c0 + t] = e == 0.0f ? 1.0f : __fdiv_rn(1.0f, __fsqrt_rn(e));
 }
 
 // normalize_impulse.hpp:21-30: min factor over channels, then scale everything
@@ -587,7 +627,8 @@ int normalize_device(float* d_ir, int C, int64_t L, hipStream_t s)
     if (C < 1) return NEO_HIP_OK;
     float* factor = nullptr;
     NEO_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&factor), size_t(C) * sizeof(float), s));
-    hipLaunchKernelGGL(k_energy_factor, dim3(unsigned((C + 63) / 64)), dim3(64), 0, s, d_ir, L, C, factor);
+    hipLaunchKernelGGL(k_energy_factor, dim3(unsigned((C + kEnergyGroup - 1) / kEnergyGroup)), dim3(256), 0, s, d_ir, L,
+                       C, factor);
     NEO_HIP_LAUNCH_CHECK();
     const int64_t n = int64_t(C) * L;
     const unsigned blocks = unsigned(std::min<int64_t>((n + 255) / 256, 4096));

@@ -75,7 +75,9 @@ def test_uniform_partition_vs_oracle(neo_gpu, oracle):
 
 def test_normalize_impulse_bit_exact(neo_gpu, oracle):
     """Sequential float energy (normalize_energy.hpp:21-33): the GPU rounds identically."""
-    for C, L in [(4, 48000), (2, 480000)]:  # up to 10 s @ 48 kHz, where rounding order matters most
+    # up to 10 s @ 48 kHz, where rounding order matters most; ragged C (not a multiple of
+    # the 16-channel group) and L (not a multiple of the 256-sample tile)
+    for C, L in [(4, 48000), (2, 480000), (17, 48001), (3, 255), (1, 1), (20, 256)]:
         ir = np.stack([oracle.noise(50 + c, L) * (c + 1) for c in range(C)]).astype(np.float32)
         ref = oracle.normalize_impulse(ir)
         got = ir.copy()
