@@ -7,6 +7,7 @@
 //   normalize_impulse         normalize_impulse.hpp:11-33  (bit-exact rounding on the GPU)
 //   upols_convolver           dense_convolver.hpp:19-20 + uniform_partitioned_convolver.hpp:13-65
 //   split_upols_convolver     dense_convolver.hpp:38-42 (same math; one device layout)
+//   upola_convolver(_v2)      dense_convolver.hpp:23-28 (overlap_add / overlap_add_convolver)
 // plus the GPU-shaped entry the plugin and CLI loops map onto: upols_multichannel,
 // C channels stepped by one launch pair per block ([C][B] in, [C][P][B+1] filter),
 // and dense_convolve (extra/plugin/src/dsp/DenseConvolution.hpp:39-70).
@@ -118,6 +119,10 @@ auto normalize_impulse(Obj obj) noexcept -> void
         }
 }
 
+/// selects upola_convolver_v2 (overlap_add_convolver.hpp:20-136) in upols_multichannel
+struct upola_v2_tag {};
+inline constexpr upola_v2_tag upola_v2{};
+
 namespace detail {
 struct upols_deleter {
     void operator()(neo_hip_upols* h) const noexcept { neo_hip_upols_destroy(h); }
@@ -140,6 +145,16 @@ struct upols_multichannel {
         _h.reset(h);
     }
 
+    /// C instances of upola_convolver_v2 (sub-block input through process())
+    upols_multichannel(upola_v2_tag, std::size_t channels, std::size_t block_size, std::size_t partitions,
+                       int device = neo::hip::detail::default_device())
+        : _C{channels}, _B{block_size}, _P{partitions}
+    {
+        neo_hip_upols* h = nullptr;
+        neo::hip::check(neo_hip_upola2_create(int(channels), int(block_size), int(partitions), device, &h));
+        _h.reset(h);
+    }
+
     /// filter [C][P][B+1] complex<float>, contiguous host memory; resets state
     auto filter(std::complex<float> const* partitions) -> void
     {
@@ -156,6 +171,13 @@ struct upols_multichannel {
     auto process_device(float const* in, std::size_t ld_in, float* out, std::size_t ld_out, void* stream = nullptr) -> void
     {
         neo::hip::check(neo_hip_upols_process_device(_h.get(), in, std::int64_t(ld_in), out, std::int64_t(ld_out), stream));
+    }
+    /// num_samples per channel, in place, io [C][num_samples] host memory (synchronous);
+    /// any count for upola_v2, whole blocks otherwise (overlap_add_convolver.hpp:80-134)
+    auto process(float* io, std::size_t num_samples) noexcept -> void
+    {
+        auto const n = std::int64_t(num_samples);
+        neo::hip::check_or_abort(neo_hip_upols_process_samples(_h.get(), io, n, io, n, n, 0, nullptr));
     }
     auto reset() -> void { neo::hip::check(neo_hip_upols_reset(_h.get())); }
 
@@ -211,6 +233,49 @@ private:
     std::vector<float> _block;
 };
 
+/// Single-channel drop-in for upola_convolver_v2<complex<float>> (dense_convolver.hpp:28,
+/// overlap_add_convolver.hpp:20-136): operator()(samples) takes any number of samples.
+template<typename Complex>
+struct hip_upola2_convolver {
+    static_assert(std::same_as<Complex, std::complex<float>>);
+    using value_type = Complex;
+    using accumulator_type = neo::hip::array<Complex, 1>;
+
+    hip_upola2_convolver() = default;
+
+    template<typename InMat>
+        requires neo::hip::detail::matrix_like<InMat>
+    auto filter(InMat filter) -> void
+    {
+        auto const P = std::size_t(filter.extent(0)), bins = std::size_t(filter.extent(1));
+        std::vector<Complex> h(P * bins);
+        for (std::size_t p = 0; p < P; ++p)
+            for (std::size_t k = 0; k < bins; ++k) h[p * bins + k] = Complex(neo::hip::detail::at(filter, p, k));
+        if (!_impl || _impl->partitions() != P || _impl->block_size() != bins - 1)
+            _impl = std::make_unique<upols_multichannel>(upola_v2, 1, bins - 1, P);
+        _impl->filter(h.data());
+    }
+
+    template<typename Vec>
+        requires neo::hip::detail::vector_like<Vec>
+    auto operator()(Vec inout) -> void
+    {
+        auto const n = std::size_t(inout.extent(0));
+        if (neo::hip::detail::contiguous(inout)) {
+            _impl->process(inout.data_handle(), n);
+            return;
+        }
+        _buf.resize(n);
+        neo::hip::detail::gather(inout, _buf.data());
+        _impl->process(_buf.data(), n);
+        neo::hip::detail::scatter(_buf.data(), inout);
+    }
+
+private:
+    std::unique_ptr<upols_multichannel> _impl;
+    std::vector<float> _buf;
+};
+
 template<typename Complex>
 using upols_convolver = hip_upols_convolver<Complex>;
 
@@ -223,6 +288,10 @@ using upola_convolver = hip_upols_convolver<Complex, method::upola>;
 
 template<typename Complex>
 using split_upola_convolver = hip_upols_convolver<Complex, method::upola>;
+
+/// dense_convolver.hpp:28
+template<typename Complex>
+using upola_convolver_v2 = hip_upola2_convolver<Complex>;
 
 /// dense_convolve<upols_convolver> (DenseConvolution.hpp:39-70) over plain arrays:
 /// signal [C][N], ir [C][L] -> out [C][N]; normalizes + partitions the IR, tail block zero-padded.

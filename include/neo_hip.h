@@ -84,6 +84,12 @@ NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, in
  * (dense_convolver.hpp:23-24; overlap_add.hpp:76-106). All other neo_hip_upols_*
  * entry points apply to it unchanged. */
 NEO_HIP_API int neo_hip_upola_create(int channels, int block, int partitions, int device, neo_hip_upols** h);
+/* C instances of upola_convolver_v2<complex<float>> = overlap_add_convolver
+ * (dense_convolver.hpp:28; overlap_add_convolver.hpp:20-136): overlap-add that also
+ * takes sub-block input through neo_hip_upols_process_samples, with the reference's
+ * window state (the irfft result is written back into the real window, :114). Whole
+ * blocks through the other process calls behave like neo_hip_upola_create. */
+NEO_HIP_API int neo_hip_upola2_create(int channels, int block, int partitions, int device, neo_hip_upols** h);
 NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h);
 /* filter [C][P][B+1] complex (uniform_partition layout), host or device memory;
  * like uniform_partitioned_convolver::filter() it also resets all state. */
@@ -102,6 +108,13 @@ NEO_HIP_API int neo_hip_upols_process_device(neo_hip_upols* h, const float* in, 
 /* nblocks consecutive blocks: channel c samples at in + c*ld + t*B. */
 NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, float* out, int64_t ld,
                                              int64_t nblocks, void* stream);
+/* num_samples samples for every channel: channel c at in + c*ld_in / out + c*ld_out
+ * (in == out allowed), host (synchronous) or device (asynchronous on `stream`) memory.
+ * upola_convolver_v2 handles accept any count, split at block boundaries like
+ * overlap_add_convolver::operator() (:80-134); upols / upola handles need a multiple
+ * of the block (the reference's operator() takes exactly one block). */
+NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
+                                              int64_t ld_out, int64_t num_samples, int is_device, void* stream);
 NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
 /* MAC-kernel timing with HIP events recorded on the launch stream (for the
  * roofline in bench.py): enable, then read the accumulated ms / launch count. */

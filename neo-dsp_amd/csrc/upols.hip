@@ -158,13 +158,16 @@ __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, flo
 // of a channel's S workgroups to arrive (agent-scope release -> counter -> acquire,
 // cdna_hip_programming.md §6 G16 / split-K seam) sums the slabs in the fixed order
 // s = 0..S-1 and runs the c2r: one launch per block, deterministic results.
-template<int B, bool FUSED, bool OLA, int UNROLL = upols_cfg<B>::U>
+// TAIL (upola_convolver_v2 sub-block pieces): no window / insert, partitions p >= 1 only
+// (overlap_add_convolver.hpp:96-108), slabs summed by k_upola2_piece.
+template<int B, bool FUSED, bool OLA, bool TAIL = false, int UNROLL = upols_cfg<B>::U>
 __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, cf* __restrict__ part, int* __restrict__ arrivals,
     const cf* __restrict__ twg, int P, int S, int rows, int w, int64_t cstride, int64_t pstride)
 {
     using K = upols_cfg<B>;
+    static_assert(!(TAIL && FUSED), "the v2 tail is summed by k_upola2_piece");
     __shared__ __attribute__((aligned(16))) cf xnew[B];  // new spectrum; later the summed spectrum
     __shared__ cf fft[K::LL];
     __shared__ cf tw[K::TW1 + K::TW2];
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
     const int64_t crow = int64_t(c) * cstride;  // channel base in H / FDL (complex units); row p at + p * pstride
     const int64_t ps4 = pstride / 2;            // row stride in float4 units
 
-    if (s == 0) {
+    if (!TAIL && s == 0) {
         for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
         const float* in_c = in + int64_t(c) * ld_in;
         float* prev_c = prev + int64_t(c) * B;
@@ -203,7 +206,8 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
     const float4* H4 = reinterpret_cast<const float4*>(H + crow);
     const float4* F4 = reinterpret_cast<const float4*>(fdl + crow);
     int pstart = p0;
-    if (p0 == 0) {
+    if (TAIL && p0 == 0) pstart = 1;
+    if (!TAIL && p0 == 0) {
         if (rs == 0) {
             const float4* Xn = reinterpret_cast<const float4*>(xnew);
 #pragma unroll
@@ -371,6 +375,103 @@ __global__ __launch_bounds__(256) void k_upols_finish(const cf* __restrict__ par
                                                                      ovl + int64_t(c) * B, tid);
 }
 
+// upola_convolver_v2 piece (overlap_add_convolver.hpp:71-136), one workgroup per channel,
+// for n samples at block position pos. The real window [C][2B] is state, exactly as in
+// the reference: the irfft result is written back into it (:114), so a later piece of
+// the same block transforms [earlier output | new samples | earlier output]. Steps:
+//   sum_first (pos == 0): tmp = sum of the TAIL slabs (partitions p >= 1, :96-108)
+//   window[pos, pos+n) = input; X = rfft(window); FDL row w = X          (:90-94)
+//   acc = tmp + X * H[0]                                                 (:110-112)
+//   window = irfft(acc) / 2B; out = window[pos, pos+n) + overlap[...]    (:114-118)
+//   complete (pos + n == B): overlap = window[B, 2B); window = 0         (:122-131)
+// Whole blocks at pos 0 take the UPOLA launch pair instead: with a zero window and
+// full input the two are the same computation.
+template<int B>
+__global__ __launch_bounds__(256) void k_upola2_piece(
+    const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, int n, int pos,
+    float* __restrict__ window, float* __restrict__ ovl, cf* __restrict__ tmp, const cf* __restrict__ part, int S,
+    int sum_first, const cf* __restrict__ H, cf* __restrict__ fdl, int w, const cf* __restrict__ twg, int64_t cstride,
+    int64_t pstride)
+{
+    using K = upols_cfg<B>;
+    constexpr int E = K::E, T = K::T;
+    __shared__ __attribute__((aligned(16))) float wl[2 * B];  // real window, then the irfft output
+    __shared__ __attribute__((aligned(16))) cf acc[B];
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    const int tid = threadIdx.x, c = blockIdx.x;
+    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+
+    cf* tmp_c = tmp + int64_t(c) * B;
+    if (sum_first) {  // fixed order s = 0..S-1, like k_upols_finish
+        const cf* pc = part + int64_t(c) * S * B;
+        for (int k = tid; k < B; k += 256) {
+            cf sum = pc[k];
+            for (int t = 1; t < S; ++t) {
+                const cf r = pc[int64_t(t) * B + k];
+                sum.x += r.x;
+                sum.y += r.y;
+            }
+            acc[k] = sum;
+            tmp_c[k] = sum;
+        }
+    } else {
+        for (int k = tid; k < B; k += 256) acc[k] = tmp_c[k];
+    }
+    float* win_c = window + int64_t(c) * 2 * B;
+    const float* in_c = in + int64_t(c) * ld_in;
+    for (int i = tid; i < 2 * B; i += 256) wl[i] = (i >= pos && i < pos + n) ? in_c[i - pos] : win_c[i];
+    __syncthreads();
+
+    const bool active = tid < T;
+    cf v[E];
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = reinterpret_cast<const cf*>(wl)[tid + m * T];
+    }
+    stockham<B, E, -1>(v, fft, tw, tid, active);
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) fft[lpad(tid + m * T)] = v[m];
+    }
+    __syncthreads();
+    cf* row = fdl + int64_t(c) * cstride + int64_t(w) * pstride;
+    const cf* h0 = H + int64_t(c) * cstride;  // partition 0
+    for (int k = tid; k < B; k += 256) {
+        const cf x = r2c_split<B>(fft, tw + K::TW1, k), h = h0[k], a = acc[k];
+        row[k] = x;
+        acc[k] = k == 0 ? cf{x.x * h.x + a.x, x.y * h.y + a.y}  // packed {DC, Nyquist}: real products
+                        : cf{(x.x * h.x - x.y * h.y) + a.x, (x.x * h.y + x.y * h.x) + a.y};
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int k = tid + m * T;
+            const cf a0 = acc[0];
+            v[m] = k == 0 ? c2r_join<B>(cf{a0.x, 0.f}, cf{a0.y, 0.f}, tw + K::TW1, 0)
+                          : c2r_join<B>(acc[k], acc[B - k], tw + K::TW1, k);
+        }
+    }
+    stockham<B, E, +1>(v, fft, tw, tid, active);
+    if (active) {
+        const float scale = 1.0f / float(2 * B);  // :115
+#pragma unroll
+        for (int m = 0; m < E; ++m) reinterpret_cast<cf*>(wl)[tid + m * T] = {v[m].x * scale, v[m].y * scale};
+    }
+    __syncthreads();
+    float* out_c = out + int64_t(c) * ld_out;
+    float* ovl_c = ovl + int64_t(c) * B;
+    for (int j = tid; j < n; j += 256) out_c[j] = wl[pos + j] + ovl_c[pos + j];
+    if (pos + n == B) {
+        __syncthreads();  // overlap reads above are done before it is replaced
+        for (int i = tid; i < B; i += 256) ovl_c[i] = wl[B + i];
+        for (int i = tid; i < 2 * B; i += 256) win_c[i] = 0.0f;
+    } else {
+        for (int i = tid; i < 2 * B; i += 256) win_c[i] = wl[i];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // setup path
 // ---------------------------------------------------------------------------
@@ -526,8 +627,15 @@ struct neo_hip_upols {
     cf* tw = nullptr;
     float* io = nullptr;       // device staging for host-pointer process()
     float* io_host = nullptr;  // pinned staging
+    float* samples_dev = nullptr;   // process_samples host staging (device side)
+    float* samples_host = nullptr;  // process_samples host staging (pinned)
+    size_t samples_cap = 0;
     bool timing = false;
     bool ola = false;  // upola_convolver (overlap-add stage) instead of upols (overlap-save)
+    bool v2 = false;   // upola_convolver_v2: sub-block input (implies ola)
+    int in_pos = 0;    // v2: samples of the current block already consumed (_input_pos)
+    float* window = nullptr;  // v2: real window [C][2B]
+    cf* tmp = nullptr;        // v2: tail accumulator [C][B] packed (_tmp_accumulator)
     bool fused = false;  // NEO_HIP_FUSED=1: one launch per block (last-arriver tail); A/B: slower at C4/C5
     // H / FDL layout: row p of channel c at c * cstride + p * pstride (complex units).
     // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
@@ -581,7 +689,12 @@ int reset_state(upols_t* h, hipStream_t s)
     NEO_HIP_CHECK(hipMemsetAsync(h->fdl, 0, size_t(h->C) * h->P * h->B * sizeof(cf), s));
     NEO_HIP_CHECK(hipMemsetAsync(h->prev, 0, size_t(h->C) * h->B * sizeof(float), s));
     NEO_HIP_CHECK(hipMemsetAsync(h->arrivals, 0, size_t(h->C) * sizeof(int), s));
+    if (h->v2) {
+        NEO_HIP_CHECK(hipMemsetAsync(h->window, 0, size_t(h->C) * 2 * h->B * sizeof(float), s));
+        NEO_HIP_CHECK(hipMemsetAsync(h->tmp, 0, size_t(h->C) * h->B * sizeof(cf), s));
+    }
     h->wpos = 0;
+    h->in_pos = 0;
     return NEO_HIP_OK;
 }
 
@@ -597,9 +710,13 @@ void destroy(upols_t* h)
     (void)hipFree(h->part);
     (void)hipFree(h->prev);
     (void)hipFree(h->arrivals);
+    (void)hipFree(h->window);
+    (void)hipFree(h->tmp);
     (void)hipFree(h->tw);
     (void)hipFree(h->io);
     if (h->io_host) (void)hipHostFree(h->io_host);
+    (void)hipFree(h->samples_dev);
+    if (h->samples_host) (void)hipHostFree(h->samples_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -680,6 +797,64 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
     return NEO_HIP_OK;
 }
 
+// One v2 piece of n samples at block position h->in_pos (n <= B - in_pos).
+int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int n, hipStream_t s)
+{
+    const int sum_first = h->in_pos == 0;
+    if (sum_first) {  // tail MAC over partitions p >= 1 into the split slabs
+        const unsigned grid = unsigned(h->C) * unsigned(h->S);
+        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, false, true, true>), dim3(grid), dim3(256), 0, s,
+                                                    in, ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part,
+                                                    h->arrivals, h->tw, h->P, h->S, h->rows, h->wpos, h->cstride,
+                                                    h->pstride))
+        NEO_HIP_LAUNCH_CHECK();
+    }
+    NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upola2_piece<BB>), dim3(unsigned(h->C)), dim3(256), 0, s, in, ld_in,
+                                                out, ld_out, n, h->in_pos, h->window, h->prev, h->tmp, h->part, h->S,
+                                                sum_first, h->H, h->fdl, h->wpos, h->tw, h->cstride, h->pstride))
+    NEO_HIP_LAUNCH_CHECK();
+    h->in_pos += n;
+    if (h->in_pos == h->B) {  // block complete: next FDL row (overlap_add_convolver.hpp:131)
+        h->in_pos = 0;
+        h->wpos = h->wpos + 1 >= h->P ? 0 : h->wpos + 1;
+    }
+    return NEO_HIP_OK;
+}
+
+// Any number of samples for every channel (channel c at in + c * ld_in). upols / upola
+// handles take whole blocks only; v2 handles split the samples at block boundaries
+// (overlap_add_convolver.hpp:80-134) and run whole aligned blocks through launch_step.
+int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t n, hipStream_t s)
+{
+    const int B = h->B;
+    if (!h->v2) {
+        if (n % B) return fail(NEO_HIP_EINVAL, "upols/upola convolvers take whole blocks (%lld samples, block %d)",
+                               (long long)n, B);
+        const bool aligned = !((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) &&
+                             !((ld_in | ld_out) & 3);
+        if (!aligned) return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
+        for (int64_t t = 0; t < n / B; ++t) {
+            int rc = launch_step(h, in + t * B, ld_in, out + t * B, ld_out, s);
+            if (rc) return rc;
+        }
+        return NEO_HIP_OK;
+    }
+    int64_t done = 0;
+    while (done < n) {
+        const int k = int(std::min<int64_t>(n - done, B - h->in_pos));
+        const float* ip = in + done;
+        float* op = out + done;
+        // whole block on an 8-byte grid: the UPOLA pair computes the same thing
+        const bool pair = h->in_pos == 0 && k == B &&
+                          !((reinterpret_cast<uintptr_t>(ip) | reinterpret_cast<uintptr_t>(op)) & 7) &&
+                          !((ld_in | ld_out) & 1);
+        int rc = pair ? launch_step(h, ip, ld_in, op, ld_out, s) : launch_piece(h, ip, ld_in, op, ld_out, k, s);
+        if (rc) return rc;
+        done += k;
+    }
+    return NEO_HIP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -694,7 +869,7 @@ NEO_HIP_API int neo_hip_num_partitions(int64_t length, int block, int64_t* parti
 }  // extern "C"
 
 namespace {
-int create_convolver(int channels, int block, int partitions, int device, bool ola, neo_hip_upols** out)
+int create_convolver(int channels, int block, int partitions, int device, bool ola, bool v2, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
     *out = nullptr;
@@ -708,7 +883,8 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->C = channels;
     h->B = block;
     h->P = partitions;
-    h->ola = ola;
+    h->ola = ola || v2;
+    h->v2 = v2;
     if (const char* e = std::getenv("NEO_HIP_FUSED")) h->fused = std::atoi(e) != 0;
     h->cstride = int64_t(partitions) * block;
     h->pstride = block;
@@ -736,7 +912,10 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
         hipMalloc(reinterpret_cast<void**>(&h->fdl), nrows * rowbytes) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->part), size_t(channels) * h->S * rowbytes) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->prev), size_t(channels) * block * sizeof(float)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&h->arrivals), size_t(channels) * sizeof(int)) != hipSuccess)
+        hipMalloc(reinterpret_cast<void**>(&h->arrivals), size_t(channels) * sizeof(int)) != hipSuccess ||
+        (v2 && (hipMalloc(reinterpret_cast<void**>(&h->window), size_t(channels) * 2 * block * sizeof(float)) !=
+                    hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&h->tmp), size_t(channels) * rowbytes) != hipSuccess)))
         return bail(fail(NEO_HIP_ENOMEM, "device allocation of %zu bytes failed", 2 * nrows * rowbytes));
     int rc = upload_tw(&h->tw, block);
     if (rc) return bail(rc);
@@ -752,12 +931,17 @@ extern "C" {
 
 NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
 {
-    return create_convolver(channels, block, partitions, device, false, out);
+    return create_convolver(channels, block, partitions, device, false, false, out);
 }
 
 NEO_HIP_API int neo_hip_upola_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
 {
-    return create_convolver(channels, block, partitions, device, true, out);
+    return create_convolver(channels, block, partitions, device, true, false, out);
+}
+
+NEO_HIP_API int neo_hip_upola2_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
+{
+    return create_convolver(channels, block, partitions, device, true, true, out);
 }
 
 NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h)
@@ -849,6 +1033,7 @@ NEO_HIP_API int neo_hip_upols_process_device(neo_hip_upols* h, const float* in, 
         return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
     device_guard g(h->device);
     if (g.rc) return g.rc;
+    if (h->v2) return process_samples(h, in, ld_in, out, ld_out, h->B, as_stream(stream));  // may be mid-block
     return launch_step(h, in, ld_in, out, ld_out, as_stream(stream));  // NULL = HIP null stream
 }
 
@@ -878,11 +1063,48 @@ NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_dev
     }
     std::copy(io, io + size_t(h->C) * h->B, h->io_host);
     NEO_HIP_CHECK(hipMemcpyAsync(h->io, h->io_host, bytes, hipMemcpyHostToDevice, s));
-    int rc = launch_step(h, h->io, h->B, h->io, h->B, s);
+    int rc = h->v2 ? process_samples(h, h->io, h->B, h->io, h->B, h->B, s) : launch_step(h, h->io, h->B, h->io, h->B, s);
     if (rc) return rc;
     NEO_HIP_CHECK(hipMemcpyAsync(h->io_host, h->io, bytes, hipMemcpyDeviceToHost, s));
     NEO_HIP_CHECK(hipStreamSynchronize(s));
     std::copy(h->io_host, h->io_host + size_t(h->C) * h->B, io);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
+                                              int64_t ld_out, int64_t num_samples, int is_device, void* stream)
+{
+    if (!h || !in || !out) return fail(NEO_HIP_EINVAL, "null handle or buffer");
+    if (num_samples < 0 || ld_in < num_samples || ld_out < num_samples)
+        return fail(NEO_HIP_EINVAL, "num_samples must be in [0, ld]");
+    if (num_samples == 0) return NEO_HIP_OK;
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    if (is_device) return process_samples(h, in, ld_in, out, ld_out, num_samples, as_stream(stream));
+    hipStream_t s = stream ? as_stream(stream) : h->stream;
+    // host I/O: pinned staging (grown on demand), 1-D copies, synchronous like process()
+    const size_t count = size_t(h->C) * size_t(num_samples);
+    if (count > h->samples_cap) {
+        (void)hipFree(h->samples_dev);
+        if (h->samples_host) (void)hipHostFree(h->samples_host);
+        h->samples_dev = nullptr;
+        h->samples_host = nullptr;
+        h->samples_cap = 0;
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->samples_dev), count * sizeof(float)));
+        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->samples_host), count * sizeof(float),
+                                    hipHostMallocDefault));
+        h->samples_cap = count;
+    }
+    for (int c = 0; c < h->C; ++c)
+        std::copy(in + c * ld_in, in + c * ld_in + num_samples, h->samples_host + size_t(c) * num_samples);
+    NEO_HIP_CHECK(hipMemcpyAsync(h->samples_dev, h->samples_host, count * sizeof(float), hipMemcpyHostToDevice, s));
+    int rc = process_samples(h, h->samples_dev, num_samples, h->samples_dev, num_samples, num_samples, s);
+    if (rc) return rc;
+    NEO_HIP_CHECK(hipMemcpyAsync(h->samples_host, h->samples_dev, count * sizeof(float), hipMemcpyDeviceToHost, s));
+    NEO_HIP_CHECK(hipStreamSynchronize(s));
+    for (int c = 0; c < h->C; ++c)
+        std::copy(h->samples_host + size_t(c) * num_samples, h->samples_host + size_t(c + 1) * num_samples,
+                  out + c * ld_out);
     return NEO_HIP_OK;
 }
 

@@ -9,7 +9,7 @@ from . import convolution
 from . import fft
 from .convolution import (UpolsConvolver, convolve, dense_convolve, direct_convolve, fft_convolve, normalize_impulse,
                           num_partitions, split_upola_convolver, split_upols_convolver, uniform_partition,
-                          upola_convolver, upols_convolver)
+                          upola_convolver, upola_convolver_v2, upols_convolver)
 
 __version__ = "0.1.0"
 
@@ -21,6 +21,7 @@ __all__ = [
     "split_upols_convolver",
     "upola_convolver",
     "split_upola_convolver",
+    "upola_convolver_v2",
     "uniform_partition",
     "normalize_impulse",
     "num_partitions",

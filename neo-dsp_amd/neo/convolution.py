@@ -9,6 +9,8 @@ Python; extra/python/src/main.cpp:227-234 only lists the `upols` method enum):
   - split_upols_convolver  dense_convolver.hpp:38-42 (same math, SoA on the CPU;
                            one device layout here)
   - upola_convolver        dense_convolver.hpp:23-24 (overlap_add.hpp:76-106 stage)
+  - upola_convolver_v2     dense_convolver.hpp:28 (overlap_add_convolver.hpp:20-136,
+                           sub-block input)
   - dense_convolve         extra/plugin/src/dsp/DenseConvolution.hpp:39-70
 Everything runs on the GPU through libneo_hip.so; there is no CPU fallback.
 """
@@ -29,6 +31,7 @@ __all__ = [
     "split_upols_convolver",
     "upola_convolver",
     "split_upola_convolver",
+    "upola_convolver_v2",
     "dense_convolve",
     "fft_convolve",
     "direct_convolve",
@@ -89,9 +92,11 @@ class UpolsConvolver:
     def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols"):
         lib = _native.load()
         h = ctypes.c_void_p()
-        if method not in ("upols", "upola"):
-            raise ValueError(f"method must be 'upols' or 'upola', got {method!r}")
-        create = lib.neo_hip_upols_create if method == "upols" else lib.neo_hip_upola_create
+        creators = {"upols": lib.neo_hip_upols_create, "upola": lib.neo_hip_upola_create,
+                    "upola_v2": lib.neo_hip_upola2_create}
+        if method not in creators:
+            raise ValueError(f"method must be 'upols', 'upola' or 'upola_v2', got {method!r}")
+        create = creators[method]
         _native.check(create(int(channels), int(block_size), int(partitions), int(device), ctypes.byref(h)))
         self._h = h
         self.channels, self.block_size, self.partitions, self.device = channels, block_size, partitions, device
@@ -143,6 +148,28 @@ class UpolsConvolver:
             raise ValueError("block must hold channels * block_size samples")
         _native.check(_native.load().neo_hip_upols_process(self._h, _ptr(block), 0, None))
         return block
+
+    def process(self, samples, stream: int = 0):
+        """Any number of samples per channel, in place: [C][n] float32 ndarray or CUDA
+        tensor. upola_v2 splits at block boundaries like overlap_add_convolver::operator()
+        (overlap_add_convolver.hpp:80-134); upols/upola need n % block_size == 0."""
+        lib = _native.load()
+        if _is_torch(samples):
+            import torch
+
+            assert samples.dtype == torch.float32 and samples.is_contiguous()
+            n = samples.shape[-1]
+            s = stream or torch.cuda.current_stream(samples.device).cuda_stream
+            p = ctypes.c_void_p(samples.data_ptr())
+            _native.check(lib.neo_hip_upols_process_samples(self._h, p, n, p, n, n, 1, ctypes.c_void_p(s)))
+            return samples
+        if not (isinstance(samples, np.ndarray) and samples.dtype == np.float32 and samples.flags.c_contiguous):
+            raise TypeError("samples must be a C-contiguous float32 array")
+        n = samples.shape[-1] if samples.ndim else 0
+        if samples.size != self.channels * n:
+            raise ValueError("samples must be [channels][n]")
+        _native.check(lib.neo_hip_upols_process_samples(self._h, _ptr(samples), n, _ptr(samples), n, n, 0, None))
+        return samples
 
     def process_device(self, in_ptr: int, ld_in: int, out_ptr: int, ld_out: int, stream: int = 0) -> None:
         _native.check(_native.load().neo_hip_upols_process_device(self._h, ctypes.c_void_p(in_ptr), int(ld_in),
@@ -233,6 +260,23 @@ class upola_convolver(upols_convolver):
 
 
 split_upola_convolver = upola_convolver
+
+
+class upola_convolver_v2(upols_convolver):
+    """Single-channel drop-in for upola_convolver_v2<complex<float>> (overlap_add_convolver.hpp:
+    20-136): __call__ takes any number of samples, in place."""
+
+    _method = "upola_v2"
+
+    def __call__(self, samples):
+        if self._impl is None:
+            raise RuntimeError("filter() must be called first")
+        if _is_torch(samples):
+            return self._impl.process(samples.view(1, -1))
+        if not (isinstance(samples, np.ndarray) and samples.dtype == np.float32 and samples.flags.c_contiguous):
+            raise TypeError("samples must be a C-contiguous float32 array")
+        self._impl.process(samples.reshape(1, -1))  # a view: processed in place
+        return samples
 
 
 def dense_convolve(signal, impulse_response, block_size: int, device: int = 0, method: str = "upols") -> np.ndarray:

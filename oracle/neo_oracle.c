@@ -510,6 +510,95 @@ int oracle_overlap_add_identity(size_t block, float* signal, size_t num_blocks)
     return rc;
 }
 
+/* ------------------------------------------------------------------------ */
+/* upola_convolver_v2 = overlap_add_convolver<complex, dense_fdl, dense_filter> */
+/* (dense_convolver.hpp:28; overlap_add_convolver.hpp:20-136): overlap-add with */
+/* sub-block input. Restated step by step, including that the irfft writes   */
+/* back into the real window (:114), so a later piece of the same block       */
+/* transforms [earlier output | new samples | earlier output].                */
+/* ------------------------------------------------------------------------ */
+typedef struct oracle_upola2 {
+    size_t B, P, bins, n;
+    int order;
+    size_t input_pos, cur;  /* _input_pos, _current_segment */
+    float* H;               /* [P][bins] complex */
+    float* fdl;             /* [P][bins] complex */
+    float* acc;             /* [bins] complex: _accumulator */
+    float* tmp;             /* [bins] complex: _tmp_accumulator */
+    float* window;          /* [n] real: _real_window */
+    float* overlap;         /* [n] real: _overlap */
+    float* cwin;            /* [bins] complex: _complex_window */
+} oracle_upola2;
+
+/* filter() (:54-69): block = bins - 1, plan order next_order(2B), all state zero */
+oracle_upola2* oracle_upola2_create(size_t P, size_t bins, const float* H)
+{
+    oracle_upola2* u = (oracle_upola2*)calloc(1, sizeof(oracle_upola2));
+    if (!u) return NULL;
+    u->B = bins - 1; u->P = P; u->bins = bins;
+    int order = 0;
+    while (((size_t)1 << order) < 2 * u->B) ++order;
+    u->order = order; u->n = (size_t)1 << order;
+    u->H = (float*)malloc(sizeof(float) * 2 * P * bins);
+    memcpy(u->H, H, sizeof(float) * 2 * P * bins);
+    u->fdl = (float*)calloc(2 * P * bins, sizeof(float));
+    u->acc = (float*)calloc(2 * bins, sizeof(float));
+    u->tmp = (float*)calloc(2 * bins, sizeof(float));
+    u->window = (float*)calloc(u->n, sizeof(float));
+    u->overlap = (float*)calloc(u->n, sizeof(float));
+    u->cwin = (float*)calloc(2 * (u->n / 2 + 1), sizeof(float));
+    return u;
+}
+
+void oracle_upola2_destroy(oracle_upola2* u)
+{
+    if (!u) return;
+    free(u->H); free(u->fdl); free(u->acc); free(u->tmp); free(u->window); free(u->overlap); free(u->cwin);
+    free(u);
+}
+
+/* operator()(inout) (:71-136): any number of samples, in place */
+int oracle_upola2_process(oracle_upola2* u, float* inout, size_t num_samples)
+{
+    const size_t B = u->B, P = u->P, bins = u->bins, n = u->n;
+    size_t done = 0;
+    while (done < num_samples) {
+        const int was_empty = u->input_pos == 0;
+        size_t k = num_samples - done;
+        if (k > B - u->input_pos) k = B - u->input_pos;
+        memcpy(u->window + u->input_pos, inout + done, sizeof(float) * k);   /* :90-91 */
+        int rc = oracle_rfft(u->order, u->window, u->cwin);                  /* :92 */
+        if (rc) return rc;
+        memcpy(u->fdl + 2 * bins * u->cur, u->cwin, sizeof(float) * 2 * bins); /* :94 */
+        if (was_empty) {                                                      /* :96-108 */
+            memset(u->tmp, 0, sizeof(float) * 2 * bins);
+            size_t f = u->cur;
+            for (size_t p = 1; p < P; ++p) {
+                if (++f >= P) f -= P;
+                oracle_multiply_add(u->fdl + 2 * bins * f, u->H + 2 * bins * p, u->tmp, u->tmp, bins);
+            }
+        }
+        memcpy(u->acc, u->tmp, sizeof(float) * 2 * bins);                    /* :110 */
+        oracle_multiply_add(u->fdl + 2 * bins * u->cur, u->H, u->acc, u->acc, bins); /* :111 */
+        memcpy(u->cwin, u->acc, sizeof(float) * 2 * bins);                   /* :112 */
+        rc = oracle_irfft(u->order, u->cwin, u->window);                     /* :114 */
+        if (rc) return rc;
+        const float scale = 1.0f / (float)n;                                 /* :115 */
+        for (size_t i = 0; i < n; ++i) u->window[i] *= scale;
+        for (size_t i = 0; i < k; ++i)                                       /* :117-118 */
+            inout[done + i] = u->window[u->input_pos + i] + u->overlap[u->input_pos + i];
+        u->input_pos += k;
+        if (u->input_pos == B) {                                             /* :120-132 */
+            u->input_pos = 0;
+            memcpy(u->overlap, u->window + B, sizeof(float) * B);
+            memset(u->window, 0, sizeof(float) * n);
+            u->cur = u->cur > 0 ? u->cur - 1 : P - 1;
+        }
+        done += k;
+    }
+    return 0;
+}
+
 /* fft_convolve (fft_convolver.hpp:19-93): full linear convolution through one
  * next_order(N+M-1) rfft pair; out has N+M-1 samples. */
 int oracle_fft_convolve(const float* signal, size_t n, const float* patch, size_t m, float* out)

@@ -15,6 +15,10 @@ int oracle_uniform_partition(const float* ir, size_t channels, size_t length, si
 int oracle_dense_convolve(const float* signal, float* out, const float* parts, size_t C, size_t N, size_t P, size_t B,
                           int threads);
 void oracle_noise(uint64_t seed, float* out, size_t n);
+typedef struct oracle_upola2 oracle_upola2;
+oracle_upola2* oracle_upola2_create(size_t P, size_t bins, const float* H);
+void oracle_upola2_destroy(oracle_upola2* u);
+int oracle_upola2_process(oracle_upola2* u, float* inout, size_t num_samples);
 #ifdef __cplusplus
 }
 #endif

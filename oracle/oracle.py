@@ -58,6 +58,10 @@ def lib():
         L.oracle_overlap_save_identity.argtypes = [_sz, _f32p, _sz]
         L.oracle_dense_convolve.argtypes = [_f32p, _f32p, _f32p, _sz, _sz, _sz, _sz, ctypes.c_int]
         L.oracle_noise.argtypes = [ctypes.c_uint64, _f32p, _sz]
+        L.oracle_upola2_create.argtypes = [_sz, _sz, _f32p]
+        L.oracle_upola2_create.restype = ctypes.c_void_p
+        L.oracle_upola2_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_upola2_process.argtypes = [ctypes.c_void_p, _f32p, _sz]
         L.oracle_upola_create.argtypes = [_sz, _sz, _f32p, ctypes.c_int]
         L.oracle_upola_create.restype = ctypes.c_void_p
         L.oracle_dense_convolve_method.argtypes = [_f32p, _f32p, _f32p, _sz, _sz, _sz, _sz, ctypes.c_int, ctypes.c_int]
@@ -215,6 +219,28 @@ class Upols:
     def __del__(self):
         if getattr(self, "_h", None):
             lib().oracle_upols_destroy(self._h)
+            self._h = None
+
+
+class Upola2:
+    """upola_convolver_v2<complex<float>> (overlap_add_convolver.hpp:20-136), one channel:
+    __call__ takes any number of samples (sub-block input), in place on a copy."""
+
+    def __init__(self, filt: np.ndarray):
+        filt = np.ascontiguousarray(filt, dtype=np.complex64)
+        self.P, self.bins = filt.shape
+        self.B = self.bins - 1
+        self._h = lib().oracle_upola2_create(self.P, self.bins, _cf(filt).reshape(-1))
+
+    def __call__(self, samples: np.ndarray) -> np.ndarray:
+        b = np.array(samples, dtype=np.float32, copy=True)
+        if lib().oracle_upola2_process(self._h, b, b.shape[0]):
+            raise RuntimeError("oracle upola_convolver_v2 failed")
+        return b
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oracle_upola2_destroy(self._h)
             self._h = None
 
 

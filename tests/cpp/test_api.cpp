@@ -11,7 +11,9 @@
 
 #include <cmath>
 #include <complex>
+#include <algorithm>
 #include <cstdio>
+#include <iterator>
 #include <vector>
 
 static int failures = 0;
@@ -130,6 +132,16 @@ static void test_convolver_identity()
         upola.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
         for (std::size_t i = 0; i < output.size(); i += B) upola(neo::hip::make_view(output.data() + i, B));
         REQUIRE(max_abs_diff(output, signal) <= 1e-5);
+        neo::convolution::upola_convolver_v2<cf> v2;  // whole blocks, then uneven pieces
+        output = signal;
+        v2.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
+        for (std::size_t i = 0; i < output.size(); i += B) v2(neo::hip::make_view(output.data() + i, B));
+        REQUIRE(max_abs_diff(output, signal) <= 1e-5);
+        output = signal;
+        v2.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
+        for (std::size_t i = 0, step = B / 3; i < output.size(); i += step, step = step * 2 % (3 * B) + 1)
+            v2(neo::hip::make_view(output.data() + i, std::min(step, output.size() - i)));
+        REQUIRE(max_abs_diff(output, signal) <= 1e-5);
         neo::convolution::split_upols_convolver<cf> split;
         output = signal;
         split.filter(neo::hip::make_matrix_view(filt.data(), 3, B + 1));
@@ -171,6 +183,31 @@ static void test_dense_convolve_vs_oracle()
         hd = std::max(hd, double(std::abs(H.buf[i] - r)));
     }
     REQUIRE(hd / hp <= 1e-5);
+}
+
+static void test_upola_v2_pieces_vs_oracle()
+{
+    // overlap_add_convolver::operator() with sub-block calls, against the restatement
+    std::size_t const B = 256, L = 2000, N = B * 10;
+    auto ir = rnoise(61, L);
+    oracle_normalize_impulse(ir.data(), 1, L);
+    auto const P = oracle_num_partitions(L, B);
+    std::vector<float> parts(P * (B + 1) * 2);
+    oracle_uniform_partition(ir.data(), 1, L, B, parts.data());
+    auto const sig = rnoise(62, N);
+    auto got = sig, ref = sig;
+    neo::convolution::upola_convolver_v2<cf> conv;
+    conv.filter(neo::hip::make_matrix_view(reinterpret_cast<cf*>(parts.data()), P, B + 1));
+    auto* o = oracle_upola2_create(P, B + 1, parts.data());
+    std::size_t const cuts[] = {0, 100, 100 + B, 3 * B + 7, 3 * B + 8, 6 * B, 7 * B + B / 2, N};
+    for (std::size_t i = 0; i + 1 < std::size(cuts); ++i) {
+        conv(neo::hip::make_view(got.data() + cuts[i], cuts[i + 1] - cuts[i]));
+        oracle_upola2_process(o, ref.data() + cuts[i], cuts[i + 1] - cuts[i]);
+    }
+    oracle_upola2_destroy(o);
+    double peak = 0;
+    for (float r : ref) peak = std::max(peak, double(std::abs(r)));
+    REQUIRE(max_abs_diff(got, ref) / peak <= 1e-5);
 }
 
 static void test_one_shot_convolve()
@@ -222,6 +259,7 @@ int main()
     test_dense_convolve_vs_oracle();
     test_uniform_partition_shapes();
     test_one_shot_convolve();
+    test_upola_v2_pieces_vs_oracle();
     std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);
     return failures ? 1 : 0;
 }

@@ -244,3 +244,84 @@ def test_fft_and_direct_convolve(oracle, n, m):
     delta[0] = 1
     for f in (oracle.fft_convolve, oracle.direct_convolve):
         assert np.abs(f(x, delta)[:n] - x).max() <= 1e-5
+
+
+def _upola2_f64(filt, pieces):
+    """Independent float64 numpy statement of overlap_add_convolver::operator()
+    (overlap_add_convolver.hpp:71-136), used to check the C restatement's state machine."""
+    P, bins = filt.shape
+    B, n = bins - 1, 2 * (bins - 1)
+    H = filt.astype(np.complex128)
+    fdl = np.zeros((P, bins), np.complex128)
+    tmp = np.zeros(bins, np.complex128)
+    window, overlap = np.zeros(n), np.zeros(n)
+    pos = cur = 0
+    outs = []
+    for x in pieces:
+        x = x.astype(np.float64)
+        y_all, done = np.empty(len(x)), 0
+        while done < len(x):
+            empty = pos == 0
+            k = min(len(x) - done, B - pos)
+            window[pos:pos + k] = x[done:done + k]
+            fdl[cur] = np.fft.rfft(window)
+            if empty:
+                idx = [(cur + p) % P for p in range(1, P)]
+                tmp = (fdl[idx] * H[1:]).sum(axis=0) if P > 1 else np.zeros(bins, np.complex128)
+            acc = tmp + fdl[cur] * H[0]
+            window = np.fft.irfft(acc, n)  # numpy's 1/n = the reference's unnormalized c2r * 1/n
+            y_all[done:done + k] = window[pos:pos + k] + overlap[pos:pos + k]
+            pos += k
+            if pos == B:
+                pos = 0
+                overlap[:B] = window[B:]
+                window = np.zeros(n)
+                cur = cur - 1 if cur > 0 else P - 1
+            done += k
+        outs.append(y_all)
+    return outs
+
+
+@pytest.mark.parametrize("B", [128, 256, 512, 1024])
+def test_upola_v2_identity(oracle, B):
+    """uniform_partitioned_convolver_test.cpp:35-75 with upola_convolver_v2 (full blocks),
+    plus sub-block calls: the identity filter passes any piece pattern through."""
+    h = np.zeros((3, B + 1), np.complex64)
+    h[0] = 1
+    sig = oracle.noise(B + 9, B * 20)
+    conv = oracle.Upola2(h)
+    out = np.concatenate([conv(sig[i:i + B]) for i in range(0, len(sig), B)])
+    assert np.abs(out - sig).max() <= 1e-5
+    conv = oracle.Upola2(h)
+    cuts = [0, B // 3, B + 5, 3 * B, 3 * B + 1, 7 * B - 2, len(sig)]
+    out = np.concatenate([conv(sig[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert np.abs(out - sig).max() <= 1e-5
+
+
+def test_upola_v2_full_blocks_equal_upola(oracle):
+    """With whole blocks v2 is the UPOLA math (same ring pairing, tmp + H0*X order)."""
+    B, L = 256, 3000
+    ir = oracle.normalize_impulse(oracle.noise(21, L))
+    H = oracle.uniform_partition(ir, B)[0]
+    sig = oracle.noise(22, B * 30)
+    conv = oracle.Upola2(H)
+    v2 = np.concatenate([conv(sig[i:i + B]) for i in range(0, len(sig), B)])
+    v1 = oracle.Upols(H, ola=True).run(sig)
+    truth = np.convolve(sig.astype(np.float64), ir.astype(np.float64))[: len(sig)]
+    assert peak_err(v2, truth) < 1e-6
+    assert peak_err(v2, v1) < 1e-6
+
+
+def test_upola_v2_sub_block_pieces(oracle):
+    """Sub-block calls follow the reference's state machine step by step (window reuse after
+    the irfft included); pinned against an independent float64 statement."""
+    B, L = 128, 1000
+    ir = oracle.normalize_impulse(oracle.noise(23, L))
+    H = oracle.uniform_partition(ir, B)[0]
+    sig = oracle.noise(24, B * 12)
+    cuts = [0, 50, 50 + B, 2 * B + 77, 2 * B + 78, 5 * B, 5 * B + 3 * B // 2, 9 * B + 1, len(sig)]
+    pieces = [sig[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    conv = oracle.Upola2(H)
+    got = np.concatenate([conv(p) for p in pieces])
+    ref = np.concatenate(_upola2_f64(H, pieces))
+    assert peak_err(got, ref) < 1e-5

@@ -285,3 +285,90 @@ def test_fused_step_matches_two_launch(neo_gpu, oracle):
            for m in ("upols", "upola")}
     for fused, method, out in outs:
         assert peak_err(out, ref[method]) <= TOL, (fused, method)
+
+
+# ------------------------------------------- UPOLA v2 (overlap_add_convolver, sub-block input)
+def _v2_reference(oracle, parts, sig, cuts):
+    """oracle.Upola2 per channel over the same piece boundaries."""
+    out = np.empty_like(sig)
+    for c in range(sig.shape[0]):
+        o = oracle.Upola2(parts[c])
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            out[c, a:b] = o(sig[c, a:b])
+    return out
+
+
+@pytest.mark.parametrize("B", [128, 256, 512, 1024])
+def test_upola_v2_identity_ir(neo_gpu, oracle, B):
+    """uniform_partitioned_convolver_test.cpp:35-75 with upola_convolver_v2 (whole blocks),
+    then uneven pieces (the identity filter passes any piece pattern through)."""
+    sig = oracle.noise(B + 5, B * 20)
+    conv = neo_gpu.upola_convolver_v2()
+    conv.filter(identity_impulse(B, 3))
+    out = sig.copy()
+    for i in range(0, len(out), B):
+        blk = out[i:i + B].copy()
+        conv(blk)
+        out[i:i + B] = blk
+    assert np.abs(out - sig).max() <= 1e-5
+    conv.filter(identity_impulse(B, 3))
+    cuts = [0, B // 3, B + 5, 3 * B, 3 * B + 1, 7 * B - 2, len(sig)]
+    out = np.concatenate([conv(sig[a:b].copy()) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert np.abs(out - sig).max() <= 1e-5
+
+
+@pytest.mark.parametrize("B,L,C", [(128, 1000, 3), (256, 2560, 2), (512, 4096, 1), (16, 100, 2), (64, 64, 2),
+                                   (4096, 12000, 1)])
+def test_upola_v2_pieces_vs_oracle(neo_gpu, oracle, B, L, C):
+    """Sub-block calls (host I/O) against the restatement of overlap_add_convolver::operator(),
+    window reuse after the irfft included; whole aligned blocks take the UPOLA launch pair."""
+    ir = np.stack([oracle.noise(180 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    N = B * 9
+    sig = np.stack([oracle.noise(190 + c, N) for c in range(C)])
+    cuts = sorted({0, 1, B // 2 + 1, B + B // 2 + 1, 3 * B + 1, 4 * B + 1, 4 * B + 2, 6 * B, 8 * B, N})
+    ref = _v2_reference(oracle, parts, sig, cuts)
+    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method="upola_v2")
+    conv.filter(parts)
+    got = np.concatenate([conv.process(np.ascontiguousarray(sig[:, a:b])) for a, b in zip(cuts[:-1], cuts[1:])],
+                         axis=1)
+    assert peak_err(got, ref) <= TOL
+
+
+def test_upola_v2_device_pieces_and_blocks(neo_gpu, oracle):
+    """CUDA-tensor pieces (device path) equal host pieces; whole blocks equal upola."""
+    torch = pytest.importorskip("torch")
+    B, L, C = 256, 5000, 4
+    ir = np.stack([oracle.noise(200 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    N = B * 12
+    sig = np.stack([oracle.noise(210 + c, N) for c in range(C)])
+    cuts = [0, 3, B + 3, 2 * B + 3, 5 * B, 5 * B + 77, 9 * B, N]
+    ref = _v2_reference(oracle, parts, sig, cuts)
+    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method="upola_v2")
+    conv.filter(parts)
+    outs = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        t = torch.from_numpy(np.ascontiguousarray(sig[:, a:b])).cuda()
+        conv.process(t)
+        outs.append(t.cpu().numpy())
+    got = np.concatenate(outs, axis=1)
+    assert peak_err(got, ref) <= TOL
+    # whole blocks: v2 == upola (same math; the launch pair does the work)
+    v2 = neo_gpu.dense_convolve(sig, ir, B, method="upola_v2")
+    v1 = neo_gpu.dense_convolve(sig, ir, B, method="upola")
+    assert peak_err(v2, v1) <= TOL
+    # reset returns to the initial state
+    conv.reset()
+    t = torch.from_numpy(np.ascontiguousarray(sig[:, :cuts[1]])).cuda()
+    conv.process(t)
+    assert peak_err(t.cpu().numpy(), ref[:, :cuts[1]]) <= TOL
+
+
+def test_process_samples_errors(neo_gpu):
+    c = neo_gpu.UpolsConvolver(2, 128, 3)  # upols: whole blocks only
+    with pytest.raises(RuntimeError):
+        c.process(np.zeros((2, 100), np.float32))
+    c.process(np.zeros((2, 256), np.float32))  # two whole blocks are fine
+    with pytest.raises(ValueError):
+        neo_gpu.UpolsConvolver(1, 128, 3, method="upola_v3")
