@@ -105,9 +105,18 @@ NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_dev
  * (in == out allowed); asynchronous on `stream` (NULL = HIP null stream). */
 NEO_HIP_API int neo_hip_upols_process_device(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
                                              int64_t ld_out, void* stream);
-/* nblocks consecutive blocks: channel c samples at in + c*ld + t*B. */
+/* nblocks consecutive blocks: channel c samples at in + c*ld + t*B (16-byte aligned, ld
+ * a multiple of 4; in == out allowed). With batching on (the default) whole groups of T
+ * blocks (32 for B <= 512, fewer for larger blocks; neo_hip_upols_batch_info) share one
+ * pass over the filter and the FDL, so HBM traffic per block drops ~T-fold; results equal the one-block-per-pass path within
+ * float rounding (another summation order). The rest run one block per pass. */
 NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, float* out, int64_t ld,
                                              int64_t nblocks, void* stream);
+/* process_blocks batching on (default) or off (one block per pass, as a real-time
+ * caller stepping process_device block by block). */
+NEO_HIP_API int neo_hip_upols_set_batch(neo_hip_upols* h, int enable);
+/* blocks one process_blocks pass consumes (1 with batching off) and its splits per channel */
+NEO_HIP_API int neo_hip_upols_batch_info(neo_hip_upols* h, int* blocks_per_pass, int* splits);
 /* num_samples samples for every channel: channel c at in + c*ld_in / out + c*ld_out
  * (in == out allowed), host (synchronous) or device (asynchronous on `stream`) memory.
  * upola_convolver_v2 handles accept any count, split at block boundaries like

@@ -6,7 +6,7 @@
 // step for all channels is ONE kernel, k_upols_step, grid C x S:
 //
 //   - workgroup (c, s) accumulates filter partitions p in [p0, p1) of channel c:
-//       acc[k] += H[c][p][k] * FDL[c][(w - p) mod P][k]
+//       acc[k] += H[c][p][k] * FDL[c][(w - p) mod R][k]
 //     (fdl_index.hpp:23-36 ring order; dense_filter.hpp:30-35 / multiply_add MAC),
 //     streaming 16 B per bin per partition from HBM — the roofline part;
 //   - split s == 0 first runs the overlap-save r2c of [previous block | new block]
@@ -18,8 +18,10 @@
 //
 // Device layout (HBM), all packed rows of B complex with bin 0 = {DC, Nyquist}
 // (both purely real for real signals, so the fold is exact):
-//   H    [C][P][B]   filter partitions (uniform_partition.hpp layout, packed)
-//   FDL  [C][P][B]   frequency-domain delay line (ring, write position w)
+//   H    [C][R][B]   filter partitions (uniform_partition.hpp layout, packed; rows >= P unused)
+//   FDL  [C][R][B]   frequency-domain delay line, a ring of R = P + kMaxBatch - 1 rows
+//                    (write position w; the extra rows let a batch of T <= kMaxBatch
+//                    new blocks be inserted before any of them is consumed)
 //   prev [C][B]      previous input block (first half of the overlap-save window)
 //   part [C][S][B]   per-split partial spectra; arrivals [C] split counters
 #include "common.hpp"
@@ -27,6 +29,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace neo_hip {
@@ -164,7 +168,7 @@ template<int B, bool FUSED, bool OLA, bool TAIL = false, int UNROLL = upols_cfg<
 __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, cf* __restrict__ part, int* __restrict__ arrivals,
-    const cf* __restrict__ twg, int P, int S, int rows, int w, int64_t cstride, int64_t pstride)
+    const cf* __restrict__ twg, int P, int ring, int S, int rows, int w, int64_t cstride, int64_t pstride)
 {
     using K = upols_cfg<B>;
     static_assert(!(TAIL && FUSED), "the v2 tail is summed by k_upola2_piece");
@@ -225,7 +229,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             const int pp = p + u * K::RPI;
-            const int fr = w >= pp ? w - pp : w - pp + P;  // fdl_index.hpp:28-31 ring
+            const int fr = w >= pp ? w - pp : w - pp + ring;  // fdl_index.hpp:28-31 ring
 #pragma unroll
             for (int v = 0; v < K::VPT; ++v) {
                 const int q = q0 + v * K::QT;
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
             for (int v = 0; v < K::VPT; ++v) mac2(a[2 * v], a[2 * v + 1], hv[u][v], xv[u][v]);
     }
     for (; p < p1; p += K::RPI) {
-        const int fr = w >= p ? w - p : w - p + P;
+        const int fr = w >= p ? w - p : w - p + ring;
 #pragma unroll
         for (int v = 0; v < K::VPT; ++v) {
             const int q = q0 + v * K::QT;
@@ -473,6 +477,250 @@ __global__ __launch_bounds__(256) void k_upola2_piece(
 }
 
 // ---------------------------------------------------------------------------
+// Batched blocks (process_blocks): T consecutive blocks per pass over H and the FDL.
+// ---------------------------------------------------------------------------
+// Block j of a batch (write position w) is inserted as FDL row (w + j) mod R and uses
+// rows (w + j - p) mod R, so partition p of all T blocks reads one H row and T rows of
+// the FDL of which T - 1 were already read for p - 1: a workgroup that walks p in order
+// keeps a sliding window of T FDL rows in registers and streams one H row and one new
+// FDL row per partition. HBM bytes per pass stay ~16·P·B per channel (the single-block
+// figure) while the pass produces T blocks: T× the work per byte.
+template<int B, int NB>
+struct batch_cfg {
+    static constexpr int Q = B / NB;               // vectors (NB bins each) per row
+    static constexpr int L = Q < 512 ? Q : 512;    // lanes per MAC workgroup
+    static constexpr int VPT = Q / L;              // vectors per lane
+};
+template<int NB>
+using bvec = std::conditional_t<NB == 2, f4v, f2v>;  // NB interleaved complex bins
+
+// Window r2c of block j (grid C x T): [x_{j-1} | x_j] (OLS, x_{-1} = prev) or [x_j | 0]
+// (OLA), inserted as FDL row (w + j) mod R.
+template<int B, bool OLA>
+__global__ __launch_bounds__(256) void k_batch_window(const float* __restrict__ in, int64_t ld_in,
+                                                      const float* __restrict__ prev, cf* __restrict__ fdl,
+                                                      const cf* __restrict__ twg, int T, int ring, int w,
+                                                      int64_t cstride, int64_t pstride)
+{
+    using K = upols_cfg<B>;
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    const int tid = threadIdx.x, c = blockIdx.x / T, j = blockIdx.x - c * T;
+    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+    const float* in_c = in + int64_t(c) * ld_in + int64_t(j) * B;
+    const float* prev_c = j == 0 ? prev + int64_t(c) * B : in_c - B;
+    window_fft<B, OLA>(prev_c, in_c, fft, tw, tid);
+    const int r = w + j < ring ? w + j : w + j - ring;
+    cf* row = fdl + int64_t(c) * cstride + int64_t(r) * pstride;
+    for (int k = tid; k < B; k += 256) row[k] = r2c_split<B>(fft, tw + K::TW1, k);
+}
+
+// Per bin two packed pairs d = (sum hr*xr, sum hi*xi) and x = (sum hr*xi, sum hi*xr): each
+// is one v_pk_fma_f32 per partition (x with the operand halves swapped), and the packed
+// bin 0 stays exact: bin 0 -> d (DC, Nyquist), other bins -> {d.x - d.y, x.x + x.y}.
+struct acc3 {
+    f2v d, x;
+};
+
+// Step U of a T-step chunk (p = pb + U; U is a template argument so every slot index
+// is static and the arrays stay in registers): take H row p and FDL row (w - p) from
+// prefetch slot U mod D (loaded D steps earlier) into window slot (T - U) mod T, issue
+// the loads for p + D, then MAC all T blocks; block j reads window slot (j - U) mod T.
+// D bounds the loads in flight per lane (and so the registers they hold).
+template<int T, int NB, int VPT, int L, int D, int U>
+__device__ __forceinline__ void batch_step(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)[T][VPT], bvec<NB> (&ph)[D][VPT],
+                                           bvec<NB> (&pf)[D][VPT], const bvec<NB>* Hv, const bvec<NB>* Fv,
+                                           int64_t psv, int tid, int ring, int w, int p, int p1)
+{
+    constexpr int slot = U % D;
+    bvec<NB> hv[VPT];
+    const bool valid = p < p1;  // the last chunk of a split may run past p1: zero filter row
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        f[(T - U) % T][v] = pf[slot][v];
+        hv[v] = valid ? ph[slot][v] : bvec<NB>(0.0f);
+    }
+    const int pn = p + D < p1 ? p + D : p1 - 1;  // past the end: a harmless re-read, no branch
+    {
+        int r = w - pn;
+        r = r < 0 ? r + ring : r;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            pf[slot][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
+            ph[slot][v] = __builtin_nontemporal_load(Hv + int64_t(pn) * psv + tid + v * L);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            const bvec<NB> x = f[(j - U + T) % T][v], h = hv[v];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                acc3& A = a[j][v * NB + b];
+                const f2v hb = {h[2 * b], h[2 * b + 1]}, xb = {x[2 * b], x[2 * b + 1]};
+                A.d = __builtin_elementwise_fma(hb, xb, A.d);
+                A.x = __builtin_elementwise_fma(hb, xb.yx, A.x);
+            }
+        }
+    __builtin_amdgcn_sched_barrier(0);  // keep each step's loads D steps ahead, not all hoisted
+}
+
+template<int T, int NB, int VPT, int L, int D, int... U>
+__device__ __forceinline__ void batch_chunk(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)[T][VPT], bvec<NB> (&ph)[D][VPT],
+                                            bvec<NB> (&pf)[D][VPT], const bvec<NB>* Hv, const bvec<NB>* Fv,
+                                            int64_t psv, int tid, int ring, int w, int pb, int p1,
+                                            std::integer_sequence<int, U...>)
+{
+    (batch_step<T, NB, VPT, L, D, U>(a, f, ph, pf, Hv, Fv, psv, tid, ring, w, pb + U, p1), ...);
+}
+
+// MAC pass for T blocks (grid C x S, batch_cfg<B, NB>::L lanes, NB bins per lane-vector):
+// workgroup (c, s) walks partitions [p0, p1) and writes T partial spectra to
+// part[c][s][j][B].
+template<int B, int T, int NB, int D = 4>
+__global__ __launch_bounds__((batch_cfg<B, NB>::L)) void k_batch_mac(const cf* __restrict__ H,
+                                                                   const cf* __restrict__ fdl, cf* __restrict__ part,
+                                                                   int P, int ring, int S, int rows, int w,
+                                                                   int64_t cstride, int64_t pstride)
+{
+    using K = batch_cfg<B, NB>;
+    using V = bvec<NB>;
+    constexpr int VPT = K::VPT, L = K::L;
+    const int tid = threadIdx.x;
+    const int c = blockIdx.x / S, s = blockIdx.x - c * S;
+    const int p0 = s * rows, p1 = min(P, p0 + rows);
+    const int64_t psv = pstride / NB;  // row stride in vectors
+    const V* Hv = reinterpret_cast<const V*>(H + int64_t(c) * cstride);
+    const V* Fv = reinterpret_cast<const V*>(fdl + int64_t(c) * cstride);
+
+    acc3 a[T][NB * VPT];
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+        for (int v = 0; v < NB * VPT; ++v) a[j][v] = {f2v(0.0f), f2v(0.0f)};
+    V f[T][VPT];
+#pragma unroll
+    for (int sl = 1; sl < T; ++sl) {  // rows block sl needs at p0
+        int r = w + sl - p0;
+        r = r < 0 ? r + ring : (r >= ring ? r - ring : r);
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) f[sl][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
+    }
+    V ph[D][VPT], pf[D][VPT];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {  // prefetch partitions p0 .. p0 + D - 1
+        const int p = p0 + d < p1 ? p0 + d : p0;
+        int r = w - p;
+        r = r < 0 ? r + ring : r;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            pf[d][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
+            ph[d][v] = __builtin_nontemporal_load(Hv + int64_t(p) * psv + tid + v * L);
+        }
+    }
+    for (int pb = p0; pb < p1; pb += T)
+        batch_chunk<T, NB, VPT, L, D>(a, f, ph, pf, Hv, Fv, psv, tid, ring, w, pb, p1,
+                                      std::make_integer_sequence<int, T>{});
+
+    cf* slab = part + (int64_t(c) * S + s) * T * B;
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            V o;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const acc3& A = a[j][v * NB + b];
+                const bool bin0 = tid + v * L == 0 && b == 0;
+                o[2 * b] = bin0 ? A.d.x : A.d.x - A.d.y;
+                o[2 * b + 1] = bin0 ? A.d.y : A.x.x + A.x.y;
+            }
+            *reinterpret_cast<V*>(slab + int64_t(j) * B + (tid + v * L) * NB) = o;
+        }
+}
+
+// Sum the S slabs of block j in order, c2r, 1/2B (grid C x T, 256 lanes).
+//   OLS: out_j = window samples [B, 2B); workgroup j = T-1 first saves x_{T-1} as the
+//        next batch's previous block (before out_j, which may alias it, is written).
+//   OLA: out_j = samples [0, B) (overlap added by k_batch_ola), tail_j = [B, 2B).
+template<int B, bool OLA>
+__global__ __launch_bounds__(256) void k_batch_finish(const cf* __restrict__ part, int S, int T,
+                                                      const float* __restrict__ in, int64_t ld_in,
+                                                      float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
+                                                      float* __restrict__ tail, const cf* __restrict__ twg)
+{
+    using K = upols_cfg<B>;
+    constexpr int E = K::E, TT = K::T;
+    __shared__ __attribute__((aligned(16))) cf X[B];
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    const int tid = threadIdx.x, c = blockIdx.x / T, j = blockIdx.x - c * T;
+    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+    if (!OLA && j == T - 1) {
+        const float4* x4 = reinterpret_cast<const float4*>(in + int64_t(c) * ld_in + int64_t(j) * B);
+        float4* p4 = reinterpret_cast<float4*>(prev + int64_t(c) * B);
+        for (int i = tid; i < B / 4; i += 256) p4[i] = x4[i];
+    }
+    const float4* s4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * T * B + int64_t(j) * B);
+    const int64_t sstride = int64_t(T) * K::Q;  // float4 between consecutive slabs of one block
+    for (int q = tid; q < K::Q; q += 256) {
+        float4 sum = s4[q];
+        for (int t = 1; t < S; ++t) {
+            const float4 r = s4[t * sstride + q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        reinterpret_cast<float4*>(X)[q] = sum;
+    }
+    __syncthreads();
+    const bool active = tid < TT;
+    cf v[E];
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int k = tid + m * TT;
+            const cf x0 = X[0];
+            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
+                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
+        }
+    }
+    stockham<B, E, +1>(v, fft, tw, tid, active);
+    if (active) {
+        const float scale = 1.0f / float(2 * B);
+        cf* o = reinterpret_cast<cf*>(out + int64_t(c) * ld_out + int64_t(j) * B);
+        if constexpr (OLA) {
+            cf* tl = reinterpret_cast<cf*>(tail + (int64_t(c) * T + j) * B);
+#pragma unroll
+            for (int m = 0; m < E / 2; ++m) o[tid + m * TT] = {v[m].x * scale, v[m].y * scale};
+#pragma unroll
+            for (int m = E / 2; m < E; ++m) tl[tid + m * TT - B / 2] = {v[m].x * scale, v[m].y * scale};
+        } else {
+#pragma unroll
+            for (int m = E / 2; m < E; ++m) o[tid + m * TT - B / 2] = {v[m].x * scale, v[m].y * scale};
+        }
+    }
+}
+
+// OLA overlap for a batch (grid C): out_j += tail_{j-1} (out_0 += overlap), overlap = tail_{T-1}
+template<int B>
+__global__ __launch_bounds__(256) void k_batch_ola(float* __restrict__ out, int64_t ld_out,
+                                                   const float* __restrict__ tail, float* __restrict__ ovl, int T)
+{
+    const int c = blockIdx.x;
+    float* o = out + int64_t(c) * ld_out;
+    const float* tl = tail + int64_t(c) * T * B;
+    float* ov = ovl + int64_t(c) * B;
+    for (int i = threadIdx.x; i < B; i += 256) {
+        float carry = ov[i];
+        for (int j = 0; j < T; ++j) {
+            o[int64_t(j) * B + i] += carry;
+            carry = tl[int64_t(j) * B + i];
+        }
+        ov[i] = carry;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // setup path
 // ---------------------------------------------------------------------------
 // uniform_partition (uniform_partition.hpp:12-26 -> stft.hpp:56-99): partition p
@@ -615,8 +863,13 @@ __global__ void k_scale_min(float* __restrict__ ir, int64_t n, const float* __re
 
 using namespace neo_hip;
 
+namespace neo_hip {
+constexpr int kMaxBatch = 32;  // most blocks one batched MAC pass consumes (process_blocks)
+}
+
 struct neo_hip_upols {
     int device = 0, C = 0, B = 0, P = 0, S = 1, rows = 1;
+    int ring = 0;  // FDL ring rows R = P + kMaxBatch - 1
     hipStream_t stream = nullptr;
     cf* H = nullptr;
     cf* fdl = nullptr;
@@ -627,6 +880,11 @@ struct neo_hip_upols {
     cf* tw = nullptr;
     float* io = nullptr;       // device staging for host-pointer process()
     float* io_host = nullptr;  // pinned staging
+    bool batch = true;      // process_blocks runs T blocks per MAC pass (neo_hip_upols_set_batch)
+    int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
+    int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
+    cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
+    float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
     size_t samples_cap = 0;
@@ -686,7 +944,7 @@ int upload_tw(cf** d, int B)
 
 int reset_state(upols_t* h, hipStream_t s)
 {
-    NEO_HIP_CHECK(hipMemsetAsync(h->fdl, 0, size_t(h->C) * h->P * h->B * sizeof(cf), s));
+    NEO_HIP_CHECK(hipMemsetAsync(h->fdl, 0, size_t(h->C) * h->ring * h->B * sizeof(cf), s));
     NEO_HIP_CHECK(hipMemsetAsync(h->prev, 0, size_t(h->C) * h->B * sizeof(float), s));
     NEO_HIP_CHECK(hipMemsetAsync(h->arrivals, 0, size_t(h->C) * sizeof(int), s));
     if (h->v2) {
@@ -716,6 +974,8 @@ void destroy(upols_t* h)
     (void)hipFree(h->io);
     if (h->io_host) (void)hipHostFree(h->io_host);
     (void)hipFree(h->samples_dev);
+    (void)hipFree(h->part_b);
+    (void)hipFree(h->tail);
     if (h->samples_host) (void)hipHostFree(h->samples_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -771,7 +1031,7 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
 #define NEO_STEP(FU, OL)                                                                                      \
     NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, FU, OL>), dim3(grid), dim3(256), 0, s, in, ld_in, \
                                                 out, ld_out, h->prev, h->H, h->fdl, h->part, h->arrivals, h->tw,   \
-                                                h->P, h->S, h->rows, h->wpos, h->cstride, h->pstride))
+                                                h->P, h->ring, h->S, h->rows, h->wpos, h->cstride, h->pstride))
     if (h->fused) {
         if (h->ola) NEO_STEP(true, true) else NEO_STEP(true, false)
     } else {
@@ -793,7 +1053,102 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
         }
         NEO_HIP_LAUNCH_CHECK();
     }
-    h->wpos = h->wpos + 1 >= h->P ? 0 : h->wpos + 1;  // fdl_index.hpp:35-37
+    h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;  // fdl_index.hpp:35-37
+    return NEO_HIP_OK;
+}
+
+// blocks per batched pass for block B and NB bins per lane-vector: the requested T,
+// capped so one lane's accumulators (T * NB * VPT * 4 floats) stay <= 128 registers
+constexpr int batch_t(int B, int NB, int want)
+{
+    const int Q = B / NB, L = Q < 512 ? Q : 512, VPT = Q / L;
+    int t = want;
+    while (t > 2 && t * NB * VPT > 32) t /= 2;
+    return t;
+}
+
+int batch_blocks(const upols_t* h) { return batch_t(h->B, h->bNB, h->bT); }
+
+// dispatch k_batch_mac over (B, NB, T) for the valid combinations
+template<int BB, int NB>
+int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
+{
+    constexpr int L = batch_cfg<BB, NB>::L;
+    const unsigned grid = unsigned(h->C) * unsigned(h->Sb);
+#define NEO_BATCH_T(TT)                                                                                          \
+    case TT:                                                                                                     \
+        if constexpr (batch_t(BB, NB, TT) == TT) {                                                               \
+            hipLaunchKernelGGL((k_batch_mac<BB, TT, NB>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, \
+                               h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride);                      \
+            break;                                                                                               \
+        }                                                                                                        \
+        return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);
+    switch (T) {
+        NEO_BATCH_T(2)
+        NEO_BATCH_T(4)
+        NEO_BATCH_T(8)
+        NEO_BATCH_T(16)
+        NEO_BATCH_T(32)
+        default: return fail(NEO_HIP_EINVAL, "batch of %d blocks not available", T);
+    }
+#undef NEO_BATCH_T
+    NEO_HIP_LAUNCH_CHECK();
+    return NEO_HIP_OK;
+}
+
+// T consecutive blocks: window r2c + insert (C x T), one MAC pass (C x Sb), per-block
+// finish (C x T), OLA overlap chain (C).
+int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
+{
+    const int B = h->B, T = batch_blocks(h);
+    if (!h->part_b) {
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
+                                size_t(h->C) * h->Sb * kMaxBatch * B * sizeof(cf)));
+        if (h->ola)
+            NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * B * sizeof(float)));
+    }
+    const unsigned gCT = unsigned(h->C) * unsigned(T);
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, true>), dim3(gCT), dim3(256), 0, s, in, ld_in,
+                                                 h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))
+    } else {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, false>), dim3(gCT), dim3(256), 0, s, in, ld_in,
+                                                 h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (h->timing) {
+        if (h->events_used == h->events.size()) {
+            NEO_HIP_CHECK(hipEventCreate(&ev.first));
+            NEO_HIP_CHECK(hipEventCreate(&ev.second));
+            h->events.push_back(ev);
+        }
+        ev = h->events[h->events_used];
+        NEO_HIP_CHECK(hipEventRecord(ev.first, s));
+    }
+    int rc = NEO_HIP_OK;
+    if (h->bNB == 2) {
+        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s)))
+    } else {
+        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s)))
+    }
+    if (rc) return rc;
+    if (h->timing) {
+        NEO_HIP_CHECK(hipEventRecord(ev.second, s));
+        ++h->events_used;
+    }
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_finish<BB, true>), dim3(gCT), dim3(256), 0, s, h->part_b,
+                                                 h->Sb, T, in, ld_in, out, ld_out, h->prev, h->tail, h->tw))
+        NEO_HIP_LAUNCH_CHECK();
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_ola<BB>), dim3(unsigned(h->C)), dim3(256), 0, s, out, ld_out,
+                                                 h->tail, h->prev, T))
+    } else {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_finish<BB, false>), dim3(gCT), dim3(256), 0, s, h->part_b,
+                                                 h->Sb, T, in, ld_in, out, ld_out, h->prev, h->tail, h->tw))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    h->wpos = (h->wpos + T) % h->ring;
     return NEO_HIP_OK;
 }
 
@@ -805,7 +1160,8 @@ int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         const unsigned grid = unsigned(h->C) * unsigned(h->S);
         NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, false, true, true>), dim3(grid), dim3(256), 0, s,
                                                     in, ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part,
-                                                    h->arrivals, h->tw, h->P, h->S, h->rows, h->wpos, h->cstride,
+                                                    h->arrivals, h->tw, h->P, h->ring, h->S, h->rows, h->wpos,
+                                                    h->cstride,
                                                     h->pstride))
         NEO_HIP_LAUNCH_CHECK();
     }
@@ -816,7 +1172,7 @@ int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     h->in_pos += n;
     if (h->in_pos == h->B) {  // block complete: next FDL row (overlap_add_convolver.hpp:131)
         h->in_pos = 0;
-        h->wpos = h->wpos + 1 >= h->P ? 0 : h->wpos + 1;
+        h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
     }
     return NEO_HIP_OK;
 }
@@ -883,10 +1239,11 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->C = channels;
     h->B = block;
     h->P = partitions;
+    h->ring = partitions + kMaxBatch - 1;
     h->ola = ola || v2;
     h->v2 = v2;
     if (const char* e = std::getenv("NEO_HIP_FUSED")) h->fused = std::atoi(e) != 0;
-    h->cstride = int64_t(partitions) * block;
+    h->cstride = int64_t(h->ring) * block;
     h->pstride = block;
     if (const char* e = std::getenv("NEO_HIP_LAYOUT"); e && std::string(e) == "pcb") {
         h->cstride = block;
@@ -900,8 +1257,18 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     int S = std::max(1, std::min({(target + channels - 1) / channels, (partitions + 7) / 8, 64}));
     h->rows = (partitions + S - 1) / S;
     h->S = (partitions + h->rows - 1) / h->rows;
+    // batched passes: same workgroup target, >= 2T partitions per split so the sliding FDL
+    // window's warm-up (T - 1 extra rows per split) stays under half the split's rows
+    if (const char* e = std::getenv("NEO_HIP_BATCH_T")) h->bT = std::max(2, std::min(kMaxBatch, std::atoi(e)));
+    if (const char* e = std::getenv("NEO_HIP_BATCH_NB")) h->bNB = std::atoi(e) == 1 ? 1 : 2;
+    int btarget = target;
+    if (const char* e = std::getenv("NEO_HIP_BATCH_WGS")) btarget = std::max(1, std::atoi(e));
+    const int bt = batch_t(block, h->bNB, h->bT);
+    int Sb = std::max(1, std::min({(btarget + channels - 1) / channels, partitions / (2 * bt), 64}));
+    h->rows_b = (partitions + Sb - 1) / Sb;
+    h->Sb = (partitions + h->rows_b - 1) / h->rows_b;
     const size_t rowbytes = size_t(block) * sizeof(cf);
-    const size_t nrows = size_t(channels) * size_t(partitions);
+    const size_t nrows = size_t(channels) * size_t(h->ring);  // H uses the first P rows of each channel
     auto bail = [&](int code) {
         destroy(h);
         return code;
@@ -1041,9 +1408,23 @@ NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, 
                                              void* stream)
 {
     if (!h || !in || !out) return fail(NEO_HIP_EINVAL, "null handle or buffer");
-    if (ld < nblocks * h->B) return fail(NEO_HIP_EINVAL, "ld < nblocks * block");
-    for (int64_t t = 0; t < nblocks; ++t) {
-        int rc = neo_hip_upols_process_device(h, in + t * h->B, ld, out + t * h->B, ld, stream);
+    if (nblocks < 0 || ld < nblocks * h->B) return fail(NEO_HIP_EINVAL, "ld < nblocks * block");
+    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15 || ld & 3)
+        return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    hipStream_t s = as_stream(stream);
+    const int B = h->B, T = batch_blocks(h);
+    int64_t t = 0;
+    // whole batches of T blocks per MAC pass (v2 only from a block boundary)
+    if (h->batch && !(h->v2 && h->in_pos != 0)) {
+        for (; t + T <= nblocks; t += T) {
+            int rc = launch_batch(h, in + t * B, ld, out + t * B, ld, s);
+            if (rc) return rc;
+        }
+    }
+    for (; t < nblocks; ++t) {  // the rest one block per pass
+        int rc = neo_hip_upols_process_device(h, in + t * B, ld, out + t * B, ld, stream);
         if (rc) return rc;
     }
     return NEO_HIP_OK;
@@ -1086,6 +1467,8 @@ NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in,
     const size_t count = size_t(h->C) * size_t(num_samples);
     if (count > h->samples_cap) {
         (void)hipFree(h->samples_dev);
+    (void)hipFree(h->part_b);
+    (void)hipFree(h->tail);
         if (h->samples_host) (void)hipHostFree(h->samples_host);
         h->samples_dev = nullptr;
         h->samples_host = nullptr;
@@ -1105,6 +1488,21 @@ NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in,
     for (int c = 0; c < h->C; ++c)
         std::copy(h->samples_host + size_t(c) * num_samples, h->samples_host + size_t(c + 1) * num_samples,
                   out + c * ld_out);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_batch_info(neo_hip_upols* h, int* blocks_per_pass, int* splits)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    if (blocks_per_pass) *blocks_per_pass = h->batch ? batch_blocks(h) : 1;
+    if (splits) *splits = h->batch ? h->Sb : h->S;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_set_batch(neo_hip_upols* h, int enable)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    h->batch = enable != 0;
     return NEO_HIP_OK;
 }
 

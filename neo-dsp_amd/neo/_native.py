@@ -36,6 +36,8 @@ SIGNATURES = {
     "neo_hip_upola_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
     "neo_hip_upola2_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
     "neo_hip_upols_process_samples": (_i, [_vp, _vp, _i64, _vp, _i64, _i64, _i, _vp]),
+    "neo_hip_upols_set_batch": (_i, [_vp, _i]),
+    "neo_hip_upols_batch_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "neo_hip_upols_destroy": (_i, [_vp]),
     "neo_hip_upols_set_filter": (_i, [_vp, _vp, _i]),
     "neo_hip_upols_set_impulse": (_i, [_vp, _vp, _i64, _i, _i]),

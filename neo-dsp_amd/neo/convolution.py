@@ -195,6 +195,16 @@ class UpolsConvolver:
                                                                   ctypes.c_void_p(out_ptr), int(ld), int(nblocks),
                                                                   ctypes.c_void_p(stream)))
 
+    def set_batch(self, enable: bool) -> None:
+        """process_blocks: T blocks per MAC pass (default) or one block per pass."""
+        _native.check(_native.load().neo_hip_upols_set_batch(self._h, int(enable)))
+
+    def batch_info(self):
+        """(blocks per process_blocks pass, splits per channel of that pass)."""
+        t, s = ctypes.c_int(), ctypes.c_int()
+        _native.check(_native.load().neo_hip_upols_batch_info(self._h, ctypes.byref(t), ctypes.byref(s)))
+        return t.value, s.value
+
     # -- instrumentation ------------------------------------------------------
     def set_timing(self, enable: bool) -> None:
         _native.check(_native.load().neo_hip_upols_set_timing(self._h, int(enable)))
