@@ -301,15 +301,21 @@ inline auto dense_convolve(float const* signal, std::size_t channels, std::size_
     upols_multichannel conv{channels, block_size, num_partitions(ir_length, block_size),
                             neo::hip::detail::default_device(), m};
     conv.impulse(ir, ir_length, true);
-    std::vector<float> block(channels * block_size);
-    for (std::size_t i = 0; i < num_samples; i += block_size) {
-        auto const n = std::min(block_size, num_samples - i);
-        std::fill(block.begin(), block.end(), 0.0F);
+    // whole signal in chunks of <= 2^26 samples: one upload, batched passes over the
+    // filter and FDL, one download per chunk; the tail block is zero-padded
+    std::size_t const nb = (num_samples + block_size - 1) / block_size;
+    std::size_t chunk = std::max<std::size_t>(1, (std::size_t(1) << 26) / (channels * block_size));
+    if (chunk >= 32) chunk = chunk / 32 * 32;
+    std::vector<float> buf;
+    for (std::size_t t0 = 0; t0 < nb; t0 += chunk) {
+        std::size_t const t1 = std::min(nb, t0 + chunk), lo = t0 * block_size,
+                          hi = std::min(num_samples, t1 * block_size), n = (t1 - t0) * block_size;
+        buf.assign(channels * n, 0.0F);
         for (std::size_t c = 0; c < channels; ++c)
-            std::copy(signal + c * num_samples + i, signal + c * num_samples + i + n, block.data() + c * block_size);
-        conv(block.data());
+            std::copy(signal + c * num_samples + lo, signal + c * num_samples + hi, buf.data() + c * n);
+        conv.process(buf.data(), n);
         for (std::size_t c = 0; c < channels; ++c)
-            std::copy(block.data() + c * block_size, block.data() + c * block_size + n, out + c * num_samples + i);
+            std::copy(buf.data() + c * n, buf.data() + c * n + (hi - lo), out + c * num_samples + lo);
     }
 }
 

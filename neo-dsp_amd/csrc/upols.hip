@@ -1183,30 +1183,35 @@ int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
 int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t n, hipStream_t s)
 {
     const int B = h->B;
+    const int T = h->batch ? batch_blocks(h) : 1;
+    const bool a16 = !((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) &&
+                     !((ld_in | ld_out) & 3);
     if (!h->v2) {
         if (n % B) return fail(NEO_HIP_EINVAL, "upols/upola convolvers take whole blocks (%lld samples, block %d)",
                                (long long)n, B);
-        const bool aligned = !((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) &&
-                             !((ld_in | ld_out) & 3);
-        if (!aligned) return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
-        for (int64_t t = 0; t < n / B; ++t) {
-            int rc = launch_step(h, in + t * B, ld_in, out + t * B, ld_out, s);
-            if (rc) return rc;
-        }
-        return NEO_HIP_OK;
+        if (!a16) return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
     }
     int64_t done = 0;
     while (done < n) {
-        const int k = int(std::min<int64_t>(n - done, B - h->in_pos));
         const float* ip = in + done;
         float* op = out + done;
-        // whole block on an 8-byte grid: the UPOLA pair computes the same thing
-        const bool pair = h->in_pos == 0 && k == B &&
-                          !((reinterpret_cast<uintptr_t>(ip) | reinterpret_cast<uintptr_t>(op)) & 7) &&
-                          !((ld_in | ld_out) & 1);
-        int rc = pair ? launch_step(h, ip, ld_in, op, ld_out, s) : launch_piece(h, ip, ld_in, op, ld_out, k, s);
+        int rc;
+        if (h->in_pos == 0 && T > 1 && n - done >= int64_t(T) * B && a16 && done % 4 == 0) {
+            rc = launch_batch(h, ip, ld_in, op, ld_out, s);  // T whole blocks, one pass
+            done += int64_t(T) * B;
+        } else if (!h->v2) {
+            rc = launch_step(h, ip, ld_in, op, ld_out, s);
+            done += B;
+        } else {
+            const int k = int(std::min<int64_t>(n - done, B - h->in_pos));
+            // whole block on an 8-byte grid: the UPOLA pair computes the same thing
+            const bool pair = h->in_pos == 0 && k == B &&
+                              !((reinterpret_cast<uintptr_t>(ip) | reinterpret_cast<uintptr_t>(op)) & 7) &&
+                              !((ld_in | ld_out) & 1);
+            rc = pair ? launch_step(h, ip, ld_in, op, ld_out, s) : launch_piece(h, ip, ld_in, op, ld_out, k, s);
+            done += k;
+        }
         if (rc) return rc;
-        done += k;
     }
     return NEO_HIP_OK;
 }
@@ -1413,21 +1418,8 @@ NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, 
         return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
     device_guard g(h->device);
     if (g.rc) return g.rc;
-    hipStream_t s = as_stream(stream);
-    const int B = h->B, T = batch_blocks(h);
-    int64_t t = 0;
-    // whole batches of T blocks per MAC pass (v2 only from a block boundary)
-    if (h->batch && !(h->v2 && h->in_pos != 0)) {
-        for (; t + T <= nblocks; t += T) {
-            int rc = launch_batch(h, in + t * B, ld, out + t * B, ld, s);
-            if (rc) return rc;
-        }
-    }
-    for (; t < nblocks; ++t) {  // the rest one block per pass
-        int rc = neo_hip_upols_process_device(h, in + t * B, ld, out + t * B, ld, stream);
-        if (rc) return rc;
-    }
-    return NEO_HIP_OK;
+    // whole groups of T blocks per pass (batching on), the rest one block per pass
+    return process_samples(h, in, ld, out, ld, nblocks * h->B, as_stream(stream));
 }
 
 NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_device, void* stream)

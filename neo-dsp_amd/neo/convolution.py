@@ -301,14 +301,18 @@ def dense_convolve(signal, impulse_response, block_size: int, device: int = 0, m
     conv = UpolsConvolver(C, block_size, P, device, method=method)
     conv.set_impulse(ir, normalize=True)
     nb = -(-N // block_size)
+    # whole signal in chunks of <= 2^26 samples: one upload, batched passes (T blocks per
+    # pass over filter + FDL), one download per chunk; the tail block is zero-padded
+    chunk = max(1, (1 << 26) // (C * block_size))
+    chunk = chunk // 32 * 32 or chunk
     out = np.empty_like(sig)
-    block = np.zeros((C, block_size), dtype=np.float32)
-    for t in range(nb):
-        lo, hi = t * block_size, min(N, (t + 1) * block_size)
-        block[:] = 0.0
-        block[:, : hi - lo] = sig[:, lo:hi]
-        conv(block)
-        out[:, lo:hi] = block[:, : hi - lo]
+    for t0 in range(0, nb, chunk):
+        t1 = min(nb, t0 + chunk)
+        lo, hi = t0 * block_size, min(N, t1 * block_size)
+        buf = np.zeros((C, (t1 - t0) * block_size), dtype=np.float32)
+        buf[:, : hi - lo] = sig[:, lo:hi]
+        conv.process(buf)
+        out[:, lo:hi] = buf[:, : hi - lo]
     conv.close()
     return out
 

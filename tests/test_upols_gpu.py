@@ -147,11 +147,19 @@ def test_errors(neo_gpu):
 
 def test_device_blocks_match_host_blocks(neo_gpu, oracle):
     torch = pytest.importorskip("torch")
-    B, L, C, nb = 512, 20000, 4, 24
+    B, L, C, nb = 512, 20000, 4, 72
     ir = np.stack([oracle.noise(90 + c, L) for c in range(C)])
     sig = np.stack([oracle.noise(95 + c, B * nb) for c in range(C)])
-    ref = neo_gpu.dense_convolve(sig, ir, B)
     P = neo_gpu.num_partitions(L, B)
+    # host blocks one at a time: the streaming step
+    host = neo_gpu.UpolsConvolver(C, B, P)
+    host.set_impulse(ir)
+    ref = sig.copy()
+    for i in range(nb):
+        blk = np.ascontiguousarray(ref[:, i * B:(i + 1) * B])
+        host(blk)
+        ref[:, i * B:(i + 1) * B] = blk
+    assert peak_err(neo_gpu.dense_convolve(sig, ir, B), ref) <= TOL  # batched passes
     conv = neo_gpu.UpolsConvolver(C, B, P)
     conv.set_impulse(torch.from_numpy(ir).cuda(), normalize=True)
     t = torch.from_numpy(sig).cuda()
