@@ -864,7 +864,8 @@ __global__ void k_scale_min(float* __restrict__ ir, int64_t n, const float* __re
 using namespace neo_hip;
 
 namespace neo_hip {
-constexpr int kMaxBatch = 32;  // most blocks one batched MAC pass consumes (process_blocks)
+constexpr int kMaxBatch = 32;
+constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch  // most blocks one batched MAC pass consumes (process_blocks)
 }
 
 struct neo_hip_upols {
@@ -894,7 +895,10 @@ struct neo_hip_upols {
     int in_pos = 0;    // v2: samples of the current block already consumed (_input_pos)
     float* window = nullptr;  // v2: real window [C][2B]
     cf* tmp = nullptr;        // v2: tail accumulator [C][B] packed (_tmp_accumulator)
-    bool fused = false;  // NEO_HIP_FUSED=1: one launch per block (last-arriver tail); A/B: slower at C4/C5
+    // one launch per block (last-arriver tail) instead of MAC + finish: on for small filter
+    // + FDL working sets, where the step is launch-bound (C3: 10.6 vs 12.4 us per block),
+    // off for HBM-bound ones (C5: 0.342 vs 0.303 ms); NEO_HIP_FUSED=0/1 overrides
+    bool fused = false;
     // H / FDL layout: row p of channel c at c * cstride + p * pstride (complex units).
     // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
     int64_t cstride = 0, pstride = 0;
@@ -1247,6 +1251,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->ring = partitions + kMaxBatch - 1;
     h->ola = ola || v2;
     h->v2 = v2;
+    h->fused = 2.0 * 8.0 * double(channels) * double(partitions) * double(block) < double(kFusedMaxBytes);
     if (const char* e = std::getenv("NEO_HIP_FUSED")) h->fused = std::atoi(e) != 0;
     h->cstride = int64_t(h->ring) * block;
     h->pstride = block;

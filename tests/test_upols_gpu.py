@@ -40,7 +40,11 @@ def test_identity_ir(neo_gpu, oracle, B):
 @pytest.mark.parametrize("B,L,C,nb", [(512, 4096, 1, 40), (256, 2560, 2, 40), (128, 1000, 3, 30),
                                       (16, 100, 2, 20), (64, 64, 1, 10), (1024, 5000, 2, 12),
                                       (2048, 9000, 1, 6), (4096, 12000, 1, 5), (32, 7, 1, 8)])
-def test_random_ir_vs_oracle(neo_gpu, oracle, B, L, C, nb):
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_random_ir_vs_oracle(neo_gpu, oracle, monkeypatch, B, L, C, nb, fused):
+    """Both step forms: MAC + finish launches, and one launch with the last-arriver tail
+    (the default below 64 MiB of filter + FDL)."""
+    monkeypatch.setenv("NEO_HIP_FUSED", fused)
     ir = np.stack([oracle.noise(20 + c, L) for c in range(C)])
     irn = oracle.normalize_impulse(ir)
     parts = oracle.uniform_partition(irn, B)
