@@ -277,7 +277,9 @@ def run_upols_offline(args, conv, C, B, P, xp, yp, ld, stream, world):
     mac_avg_ms = max_over_ranks(mac_ms / max(launches, 1), world)
     bytes_pass = C * 16 * P * B  # filter + FDL streamed once per pass of T blocks
     gbs = bytes_pass / (mac_avg_ms * 1e-3) / 1e9
+    traffic = load_pmc_traffic(args.workload + "_offline")
     return {"value": world * C * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": T,
+            "traffic": traffic, "traffic_over_algorithmic": traffic / bytes_pass if traffic else None,
             "ms_per_block": elapsed * 1e3 / nb, "splits": splits, "kernel": f"k_batch_mac<{B},{T},1>",
             "kernel_avg_ms": mac_avg_ms,
             "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS}

@@ -18,5 +18,6 @@ cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$TAG -o run -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline > $O/prof_c5_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2_$TAG -o run -- python3 $R/bench.py --workload c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_c2_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- python3 $R/bench.py --workload c4 --steps 50 --no-cpu-baseline > $O/prof_c4_$TAG.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$TAG -o run -- python3 $R/bench.py --workload c3 --steps 200 --no-cpu-baseline > $O/prof_c3_$TAG.log 2>&1 && \
 cd $R && bash tools/gpu_pmc.sh $TAG
 echo "round exit=$?"
