@@ -585,7 +585,7 @@ __device__ __forceinline__ void batch_chunk(acc3 (&a)[T][NB * VPT], bvec<NB> (&f
 // MAC pass for T blocks (grid C x S, batch_cfg<B, NB>::L lanes, NB bins per lane-vector):
 // workgroup (c, s) walks partitions [p0, p1) and writes T partial spectra to
 // part[c][s][j][B].
-template<int B, int T, int NB, int D = 4>
+template<int B, int T, int NB, int D = (T < 4 ? T : 4)>  // D divides T: prefetch slots line up across chunks
 __global__ __launch_bounds__((batch_cfg<B, NB>::L)) void k_batch_mac(const cf* __restrict__ H,
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
@@ -1109,9 +1109,9 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
 
 // T consecutive blocks: window r2c + insert (C x T), one MAC pass (C x Sb), per-block
 // finish (C x T), OLA overlap chain (C).
-int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
+int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s)
 {
-    const int B = h->B, T = batch_blocks(h);
+    const int B = h->B;
     if (!h->part_b) {
         NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
                                 size_t(h->C) * h->Sb * kMaxBatch * B * sizeof(cf)));
@@ -1207,9 +1207,12 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
         const float* ip = in + done;
         float* op = out + done;
         int rc;
-        if (h->in_pos == 0 && T > 1 && n - done >= int64_t(T) * B && a16 && done % 4 == 0) {
-            rc = launch_batch(h, ip, ld_in, op, ld_out, s);  // T whole blocks, one pass
-            done += int64_t(T) * B;
+        // the largest power-of-two batch (<= T) of whole blocks left, one pass over H + FDL
+        int tb = 1;
+        while (tb * 2 <= T && n - done >= int64_t(tb) * 2 * B) tb *= 2;
+        if (h->in_pos == 0 && tb > 1 && a16 && done % 4 == 0) {
+            rc = launch_batch(h, ip, ld_in, op, ld_out, tb, s);
+            done += int64_t(tb) * B;
         } else if (!h->v2) {
             rc = launch_step(h, ip, ld_in, op, ld_out, s);
             done += B;

@@ -449,3 +449,27 @@ def test_batched_mixed_with_single_blocks(neo_gpu, oracle):
             pos += n
         torch.cuda.synchronize()
         assert peak_err(t.cpu().numpy(), ref) <= TOL, method
+
+
+@pytest.mark.parametrize("T", [2, 4, 8, 16, 32])
+@pytest.mark.parametrize("nbins", ["1", "2"])
+def test_every_batch_size(neo_gpu, oracle, monkeypatch, T, nbins):
+    """Each compiled batch size (and the smaller ones used for leftovers) against the oracle,
+    with 1 or 2 bins per lane-vector."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("NEO_HIP_BATCH_T", str(T))
+    monkeypatch.setenv("NEO_HIP_BATCH_NB", nbins)
+    B, L, C = 256, 9000, 2
+    nb = 2 * T + 3
+    ir = np.stack([oracle.noise(270 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    sig = np.stack([oracle.noise(280 + c, B * nb) for c in range(C)])
+    for method in ("upols", "upola"):
+        ref = oracle.dense_convolve(sig, parts, method=method)
+        conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
+        conv.filter(parts)
+        assert conv.batch_info()[0] == T
+        t = torch.from_numpy(sig).cuda()
+        conv.process_blocks(t)
+        torch.cuda.synchronize()
+        assert peak_err(t.cpu().numpy(), ref) <= TOL, method
