@@ -468,7 +468,7 @@ def test_every_batch_size(neo_gpu, oracle, monkeypatch, T, nbins):
         ref = oracle.dense_convolve(sig, parts, method=method)
         conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
         conv.filter(parts)
-        assert conv.batch_info()[0] == T
+        assert conv.batch_info()[0] == min(T, 32 // int(nbins))  # accumulator cap at B = 256
         t = torch.from_numpy(sig).cuda()
         conv.process_blocks(t)
         torch.cuda.synchronize()
