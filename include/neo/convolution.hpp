@@ -320,22 +320,34 @@ inline auto dense_convolve(float const* signal, std::size_t channels, std::size_
 }
 
 /// fft_convolve (fft_convolver.hpp:72-93): full linear convolution on the GPU, host arrays
-inline auto fft_convolve(float const* signal, std::size_t n, float const* patch, std::size_t m) -> std::vector<float>
+/// (float or double, like the reference's Python overloads, main.cpp:255-258)
+template<typename Float>
+    requires(std::same_as<Float, float> || std::same_as<Float, double>)
+inline auto fft_convolve(Float const* signal, std::size_t n, Float const* patch, std::size_t m) -> std::vector<Float>
 {
     if (n == 0 || m == 0) return {};
-    std::vector<float> out(n + m - 1);
-    neo::hip::check(neo_hip_fft_convolve(signal, std::int64_t(n), patch, std::int64_t(m), out.data(), 0,
-                                         neo::hip::detail::default_device()));
+    std::vector<Float> out(n + m - 1);
+    auto const f = [] {
+        if constexpr (std::same_as<Float, double>) return neo_hip_fft_convolve_f64;
+        else return neo_hip_fft_convolve;
+    }();
+    neo::hip::check(f(signal, std::int64_t(n), patch, std::int64_t(m), out.data(), 0, neo::hip::detail::default_device()));
     return out;
 }
 
-/// direct_convolve (direct_convolve.hpp:58-68): same loop order and float rounding as the reference
-inline auto direct_convolve(float const* signal, std::size_t n, float const* patch, std::size_t m) -> std::vector<float>
+/// direct_convolve (direct_convolve.hpp:58-68): same loop order and rounding as the reference
+template<typename Float>
+    requires(std::same_as<Float, float> || std::same_as<Float, double>)
+inline auto direct_convolve(Float const* signal, std::size_t n, Float const* patch, std::size_t m)
+    -> std::vector<Float>
 {
     if (n == 0 || m == 0) return {};
-    std::vector<float> out(n + m - 1);
-    neo::hip::check(neo_hip_direct_convolve(signal, std::int64_t(n), patch, std::int64_t(m), out.data(), 0,
-                                            neo::hip::detail::default_device()));
+    std::vector<Float> out(n + m - 1);
+    auto const f = [] {
+        if constexpr (std::same_as<Float, double>) return neo_hip_direct_convolve_f64;
+        else return neo_hip_direct_convolve;
+    }();
+    neo::hip::check(f(signal, std::int64_t(n), patch, std::int64_t(m), out.data(), 0, neo::hip::detail::default_device()));
     return out;
 }
 

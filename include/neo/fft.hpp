@@ -71,12 +71,14 @@ inline plan_ptr make_plan(int order, std::int64_t batch, int kind, int device)
 /// Batched complex-to-complex plan on one GPU (replaces c2c_dit2_plan).
 template<typename Complex>
 struct hip_fft_plan {
-    static_assert(std::same_as<Complex, std::complex<float>>, "the MI355X path transforms complex<float>");
+    static_assert(std::same_as<Complex, std::complex<float>> || std::same_as<Complex, std::complex<double>>,
+                  "the MI355X path transforms complex<float> or complex<double>");
     using value_type = Complex;
     using size_type = std::size_t;
+    static constexpr int kind = NEO_HIP_C2C | (std::same_as<Complex, std::complex<double>> ? NEO_HIP_F64 : 0);
 
     hip_fft_plan(from_order_tag /*tag*/, size_type order, int device = neo::hip::detail::default_device())
-        : _order{check_order(order)}, _device{device}, _plan{detail::make_plan(int(order), 1, NEO_HIP_C2C, device)}
+        : _order{check_order(order)}, _device{device}, _plan{detail::make_plan(int(order), 1, kind, device)}
     {}
 
     [[nodiscard]] static constexpr auto max_order() noexcept -> size_type { return 27; }
@@ -119,7 +121,7 @@ struct hip_fft_plan {
     auto execute_device(Complex const* in, Complex* out, std::size_t batch, direction dir, void* stream = nullptr) -> void
     {
         if (batch != _batch) {
-            _batched = detail::make_plan(int(_order), std::int64_t(batch), NEO_HIP_C2C, _device);
+            _batched = detail::make_plan(int(_order), std::int64_t(batch), kind, _device);
             _batch = batch;
         }
         neo::hip::check(neo_hip_fft_execute(_batched.get(), in, out, int(dir), stream));
@@ -173,15 +175,17 @@ constexpr auto ifft(Plan& plan, InVec input, OutVec output) -> void
 /// c2r reads N/2+1 bins (Im of DC/Nyquist ignored), unnormalized.
 template<typename Float, typename Complex = std::complex<Float>>
 struct hip_rfft_plan {
-    static_assert(std::same_as<Float, float> && std::same_as<Complex, std::complex<float>>);
+    static_assert((std::same_as<Float, float> || std::same_as<Float, double>) &&
+                  std::same_as<Complex, std::complex<Float>>);
     using real_type = Float;
     using complex_type = Complex;
     using size_type = std::size_t;
+    static constexpr int f64 = std::same_as<Float, double> ? NEO_HIP_F64 : 0;
 
     hip_rfft_plan(from_order_tag /*tag*/, size_type order, int device = neo::hip::detail::default_device())
         : _order{order},
-          _r2c{detail::make_plan(int(order), 1, NEO_HIP_R2C, device)},
-          _c2r{detail::make_plan(int(order), 1, NEO_HIP_C2R, device)}
+          _r2c{detail::make_plan(int(order), 1, NEO_HIP_R2C | f64, device)},
+          _c2r{detail::make_plan(int(order), 1, NEO_HIP_C2R | f64, device)}
     {}
 
     [[nodiscard]] auto order() const noexcept -> size_type { return _order; }

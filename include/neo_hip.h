@@ -44,7 +44,10 @@ enum neo_hip_status {
     NEO_HIP_ENODEV = 4    /* no such GPU */
 };
 
-enum neo_hip_fft_kind { NEO_HIP_C2C = 0, NEO_HIP_R2C = 1, NEO_HIP_C2R = 2 };
+/* fft kinds; OR NEO_HIP_F64 for std::complex<double> / double plans (the reference's
+ * fft_plan<complex<double>>, rfft_plan<double>; Python _neo.fft complex128 overloads,
+ * extra/python/src/main.cpp:248-252). */
+enum neo_hip_fft_kind { NEO_HIP_C2C = 0, NEO_HIP_R2C = 1, NEO_HIP_C2R = 2, NEO_HIP_F64 = 16 };
 
 typedef struct neo_hip_fft_plan neo_hip_fft_plan;
 typedef struct neo_hip_upols neo_hip_upols;
@@ -148,6 +151,11 @@ NEO_HIP_API int neo_hip_fft_convolve(const float* signal, int64_t n, const float
                                      int is_device, int device);
 NEO_HIP_API int neo_hip_direct_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
                                         int is_device, int device);
+/* double overloads (main.cpp:257-258 bind both float and double) */
+NEO_HIP_API int neo_hip_fft_convolve_f64(const double* signal, int64_t n, const double* patch, int64_t m, double* out,
+                                         int is_device, int device);
+NEO_HIP_API int neo_hip_direct_convolve_f64(const double* signal, int64_t n, const double* patch, int64_t m,
+                                            double* out, int is_device, int device);
 
 #ifdef __cplusplus
 }

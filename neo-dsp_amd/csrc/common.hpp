@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace neo_hip {
@@ -58,34 +59,42 @@ struct device_guard {
 
 // Two-level forward twiddle table for an FFT of size n (see twiddle<> in
 // fft_device.hpp): [0,64) = W^e, [64, 64+n/64) = W^(64h), W = exp(-2*pi*i/n),
-// computed in double and rounded once to float.
-inline std::vector<cf> make_twiddle_table(int64_t n)
+// computed in double (long double for the f64 tables) and rounded once.
+template<class C = cf>
+inline std::vector<C> make_twiddle_table(int64_t n)
 {
+    using R = real_of<C>;
+    using W = std::conditional_t<sizeof(R) == 8, long double, double>;
+    const W pi2 = W(2) * W(3.14159265358979323846264338327950288L);
     const int64_t lo = 64, hi = n <= 64 ? 0 : n / 64;
-    std::vector<cf> t(static_cast<size_t>(lo + hi));
+    std::vector<C> t(static_cast<size_t>(lo + hi));
     for (int64_t e = 0; e < lo; ++e) {
-        const double a = -2.0 * M_PI * double(e % (n > 0 ? n : 1)) / double(n > 0 ? n : 1);
-        t[size_t(e)] = {float(std::cos(a)), float(std::sin(a))};
+        const W a = -pi2 * W(e % (n > 0 ? n : 1)) / W(n > 0 ? n : 1);
+        t[size_t(e)] = {R(std::cos(a)), R(std::sin(a))};
     }
     for (int64_t h = 0; h < hi; ++h) {
-        const double a = -2.0 * M_PI * double(64 * h) / double(n);
-        t[size_t(lo + h)] = {float(std::cos(a)), float(std::sin(a))};
+        const W a = -pi2 * W(64 * h) / W(n);
+        t[size_t(lo + h)] = {R(std::cos(a)), R(std::sin(a))};
     }
     return t;
 }
 
 // Split table for the global-memory passes of large transforms: e = hi*2^lo_bits + lo.
-inline std::vector<cf> make_split_table(int order, int lo_bits)
+template<class C = cf>
+inline std::vector<C> make_split_table(int order, int lo_bits)
 {
+    using R = real_of<C>;
+    using W = std::conditional_t<sizeof(R) == 8, long double, double>;
+    const W pi2 = W(2) * W(3.14159265358979323846264338327950288L);
     const int64_t n = int64_t(1) << order, nlo = int64_t(1) << lo_bits, nhi = n >> lo_bits;
-    std::vector<cf> t(static_cast<size_t>(nlo + nhi));
+    std::vector<C> t(static_cast<size_t>(nlo + nhi));
     for (int64_t e = 0; e < nlo; ++e) {
-        const double a = -2.0 * M_PI * double(e) / double(n);
-        t[size_t(e)] = {float(std::cos(a)), float(std::sin(a))};
+        const W a = -pi2 * W(e) / W(n);
+        t[size_t(e)] = {R(std::cos(a)), R(std::sin(a))};
     }
     for (int64_t h = 0; h < nhi; ++h) {
-        const double a = -2.0 * M_PI * double(h * nlo) / double(n);
-        t[size_t(nlo + h)] = {float(std::cos(a)), float(std::sin(a))};
+        const W a = -pi2 * W(h * nlo) / W(n);
+        t[size_t(nlo + h)] = {R(std::cos(a)), R(std::sin(a))};
     }
     return t;
 }

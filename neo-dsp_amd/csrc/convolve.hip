@@ -11,36 +11,41 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace neo_hip {
 
 // rows [2][N]: row 0 = signal zero-padded, row 1 = patch zero-padded
-__global__ void k_pad2(const float* __restrict__ a, int64_t n, const float* __restrict__ b, int64_t m,
-                       float* __restrict__ rows, int64_t N)
+template<class R>
+__global__ void k_pad2(const R* __restrict__ a, int64_t n, const R* __restrict__ b, int64_t m, R* __restrict__ rows,
+                       int64_t N)
 {
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < 2 * N; i += int64_t(gridDim.x) * blockDim.x) {
         const int64_t r = i / N, k = i - r * N;
-        rows[i] = r == 0 ? (k < n ? a[k] : 0.f) : (k < m ? b[k] : 0.f);
+        rows[i] = r == 0 ? (k < n ? a[k] : R(0)) : (k < m ? b[k] : R(0));
     }
 }
 
 // spectra [2][bins]: row 0 *= row 1 (algorithm/multiply.hpp: out = x * y)
-__global__ void k_spectral_multiply(cf* __restrict__ spec, int64_t bins)
+template<class C>
+__global__ void k_spectral_multiply(C* __restrict__ spec, int64_t bins)
 {
     for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < bins; k += int64_t(gridDim.x) * blockDim.x)
         spec[k] = cmul(spec[k], spec[bins + k]);
 }
 
-__global__ void k_scale_copy(const float* __restrict__ in, float* __restrict__ out, int64_t len, float scale)
+template<class R>
+__global__ void k_scale_copy(const R* __restrict__ in, R* __restrict__ out, int64_t len, R scale)
 {
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < len; i += int64_t(gridDim.x) * blockDim.x)
         out[i] = in[i] * scale;
 }
 
 // direct_convolve.hpp:14-56: with (a, na) the longer input and (b, nb) the shorter,
-// out[k] = sum_{m} a[m] * b[k - m], m ascending, accumulated in float.
-__global__ void k_direct_convolve(const float* __restrict__ a, int64_t na, const float* __restrict__ b, int64_t nb,
-                                  float* __restrict__ out)
+// out[k] = sum_{m} a[m] * b[k - m], m ascending, accumulated in R (float or double).
+template<class R>
+__global__ void k_direct_convolve(const R* __restrict__ a, int64_t na, const R* __restrict__ b, int64_t nb,
+                                  R* __restrict__ out)
 {
 #pragma clang fp contract(off)  // product then sum, two roundings, like the reference (no FMA)
     const int64_t mm = na + nb - 1;
@@ -53,9 +58,9 @@ __global__ void k_direct_convolve(const float* __restrict__ a, int64_t na, const
             lo = k - nb + 1;  // i in the reference
             hi = std::min(nb + lo, na);
         }
-        float acc = 0.0f;
+        R acc = R(0);
         for (int64_t mi = lo; mi < hi; ++mi) {
-            const float prod = a[mi] * b[k - mi];  // contract(off): not fused with the add
+            const R prod = a[mi] * b[k - mi];  // contract(off): not fused with the add
             acc = acc + prod;
         }
         out[k] = acc;
@@ -64,20 +69,21 @@ __global__ void k_direct_convolve(const float* __restrict__ a, int64_t na, const
 
 unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192))); }
 
+template<class R>
 struct device_buffers {
-    const float* a = nullptr;
-    const float* b = nullptr;
-    float* out = nullptr;
-    float* tmp_a = nullptr;
-    float* tmp_b = nullptr;
-    float* tmp_out = nullptr;
+    const R* a = nullptr;
+    const R* b = nullptr;
+    R* out = nullptr;
+    R* tmp_a = nullptr;
+    R* tmp_b = nullptr;
+    R* tmp_out = nullptr;
     ~device_buffers()
     {
         (void)hipFree(tmp_a);
         (void)hipFree(tmp_b);
         (void)hipFree(tmp_out);
     }
-    int stage(const float* ha, int64_t n, const float* hb, int64_t m, float* hout, int is_device, hipStream_t s)
+    int stage(const R* ha, int64_t n, const R* hb, int64_t m, R* hout, int is_device, hipStream_t s)
     {
         if (is_device) {
             a = ha;
@@ -85,11 +91,11 @@ struct device_buffers {
             out = hout;
             return NEO_HIP_OK;
         }
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_a), size_t(n) * sizeof(float)));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_b), size_t(m) * sizeof(float)));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_out), size_t(n + m - 1) * sizeof(float)));
-        NEO_HIP_CHECK(hipMemcpyAsync(tmp_a, ha, size_t(n) * sizeof(float), hipMemcpyHostToDevice, s));
-        NEO_HIP_CHECK(hipMemcpyAsync(tmp_b, hb, size_t(m) * sizeof(float), hipMemcpyHostToDevice, s));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_a), size_t(n) * sizeof(R)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_b), size_t(m) * sizeof(R)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_out), size_t(n + m - 1) * sizeof(R)));
+        NEO_HIP_CHECK(hipMemcpyAsync(tmp_a, ha, size_t(n) * sizeof(R), hipMemcpyHostToDevice, s));
+        NEO_HIP_CHECK(hipMemcpyAsync(tmp_b, hb, size_t(m) * sizeof(R), hipMemcpyHostToDevice, s));
         a = tmp_a;
         b = tmp_b;
         out = tmp_out;
@@ -97,15 +103,11 @@ struct device_buffers {
     }
 };
 
-}  // namespace neo_hip
-
-using namespace neo_hip;
-
-extern "C" {
-
-NEO_HIP_API int neo_hip_fft_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
-                                     int is_device, int device)
+template<class R>
+int fft_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, R* out, int is_device, int device)
 {
+    using C = std::conditional_t<sizeof(R) == 8, cd, cf>;
+    const int f64 = sizeof(R) == 8 ? NEO_HIP_F64 : 0;
     if (n < 0 || m < 0) return fail(NEO_HIP_EINVAL, "negative length");
     if (n == 0 || m == 0) return NEO_HIP_OK;  // fft_convolver.hpp:80-82: empty result
     if (!signal || !patch || !out) return fail(NEO_HIP_EINVAL, "null buffer");
@@ -121,33 +123,33 @@ NEO_HIP_API int neo_hip_fft_convolve(const float* signal, int64_t n, const float
     NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
     int rc = NEO_HIP_OK;
     neo_hip_fft_plan *r2c = nullptr, *c2r = nullptr;
-    float* rows = nullptr;
-    cf* spec = nullptr;
+    R* rows = nullptr;
+    C* spec = nullptr;
     {
-        device_buffers io;
+        device_buffers<R> io;
         rc = io.stage(signal, n, patch, m, out, is_device, s);
-        if (!rc) rc = neo_hip_fft_plan_create(order, 2, NEO_HIP_R2C, device, &r2c);
-        if (!rc) rc = neo_hip_fft_plan_create(order, 1, NEO_HIP_C2R, device, &c2r);
-        if (!rc && (hipMalloc(reinterpret_cast<void**>(&rows), size_t(2 * N) * sizeof(float)) != hipSuccess ||
-                    hipMalloc(reinterpret_cast<void**>(&spec), size_t(2 * bins) * sizeof(cf)) != hipSuccess))
+        if (!rc) rc = neo_hip_fft_plan_create(order, 2, NEO_HIP_R2C | f64, device, &r2c);
+        if (!rc) rc = neo_hip_fft_plan_create(order, 1, NEO_HIP_C2R | f64, device, &c2r);
+        if (!rc && (hipMalloc(reinterpret_cast<void**>(&rows), size_t(2 * N) * sizeof(R)) != hipSuccess ||
+                    hipMalloc(reinterpret_cast<void**>(&spec), size_t(2 * bins) * sizeof(C)) != hipSuccess))
             rc = fail(NEO_HIP_ENOMEM, "convolution buffers");
         if (!rc) {
-            hipLaunchKernelGGL(k_pad2, dim3(grid_for(2 * N)), dim3(256), 0, s, io.a, n, io.b, m, rows, N);
+            hipLaunchKernelGGL((k_pad2<R>), dim3(grid_for(2 * N)), dim3(256), 0, s, io.a, n, io.b, m, rows, N);
             rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "pad launch failed");
         }
         if (!rc) rc = neo_hip_fft_execute(r2c, rows, spec, -1, s);
         if (!rc) {
-            hipLaunchKernelGGL(k_spectral_multiply, dim3(grid_for(bins)), dim3(256), 0, s, spec, bins);
+            hipLaunchKernelGGL((k_spectral_multiply<C>), dim3(grid_for(bins)), dim3(256), 0, s, spec, bins);
             rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "multiply launch failed");
         }
         if (!rc) rc = neo_hip_fft_execute(c2r, spec, rows, +1, s);
         if (!rc) {
-            hipLaunchKernelGGL(k_scale_copy, dim3(grid_for(len)), dim3(256), 0, s, rows, io.out, len,
-                               1.0f / float(N));  // fft_convolver.hpp:66-70
+            hipLaunchKernelGGL((k_scale_copy<R>), dim3(grid_for(len)), dim3(256), 0, s, rows, io.out, len,
+                               R(1) / R(N));  // fft_convolver.hpp:66-70
             rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "scale launch failed");
         }
         if (!rc && !is_device &&
-            hipMemcpyAsync(out, io.out, size_t(len) * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess)
+            hipMemcpyAsync(out, io.out, size_t(len) * sizeof(R), hipMemcpyDeviceToHost, s) != hipSuccess)
             rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
         if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     }
@@ -159,8 +161,8 @@ NEO_HIP_API int neo_hip_fft_convolve(const float* signal, int64_t n, const float
     return rc;
 }
 
-NEO_HIP_API int neo_hip_direct_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
-                                        int is_device, int device)
+template<class R>
+int direct_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, R* out, int is_device, int device)
 {
     if (n < 0 || m < 0) return fail(NEO_HIP_EINVAL, "negative length");
     if (n == 0 || m == 0) return NEO_HIP_OK;
@@ -172,21 +174,52 @@ NEO_HIP_API int neo_hip_direct_convolve(const float* signal, int64_t n, const fl
     NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
     int rc = NEO_HIP_OK;
     {
-        device_buffers io;
+        device_buffers<R> io;
         rc = io.stage(signal, n, patch, m, out, is_device, s);
         if (!rc) {
             const bool sig_long = n >= m;  // direct_convolve.hpp:22 vs :35
-            hipLaunchKernelGGL(k_direct_convolve, dim3(grid_for(n + m - 1)), dim3(256), 0, s, sig_long ? io.a : io.b,
-                               sig_long ? n : m, sig_long ? io.b : io.a, sig_long ? m : n, io.out);
+            hipLaunchKernelGGL((k_direct_convolve<R>), dim3(grid_for(n + m - 1)), dim3(256), 0, s,
+                               sig_long ? io.a : io.b, sig_long ? n : m, sig_long ? io.b : io.a, sig_long ? m : n,
+                               io.out);
             rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "direct launch failed");
         }
         if (!rc && !is_device &&
-            hipMemcpyAsync(out, io.out, size_t(n + m - 1) * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess)
+            hipMemcpyAsync(out, io.out, size_t(n + m - 1) * sizeof(R), hipMemcpyDeviceToHost, s) != hipSuccess)
             rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
         if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     }
     (void)hipStreamDestroy(s);
     return rc;
+}
+
+}  // namespace neo_hip
+
+using namespace neo_hip;
+
+extern "C" {
+
+NEO_HIP_API int neo_hip_fft_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
+                                     int is_device, int device)
+{
+    return fft_convolve_impl(signal, n, patch, m, out, is_device, device);
+}
+
+NEO_HIP_API int neo_hip_fft_convolve_f64(const double* signal, int64_t n, const double* patch, int64_t m, double* out,
+                                         int is_device, int device)
+{
+    return fft_convolve_impl(signal, n, patch, m, out, is_device, device);
+}
+
+NEO_HIP_API int neo_hip_direct_convolve(const float* signal, int64_t n, const float* patch, int64_t m, float* out,
+                                        int is_device, int device)
+{
+    return direct_convolve_impl(signal, n, patch, m, out, is_device, device);
+}
+
+NEO_HIP_API int neo_hip_direct_convolve_f64(const double* signal, int64_t n, const double* patch, int64_t m,
+                                            double* out, int is_device, int device)
+{
+    return direct_convolve_impl(signal, n, patch, m, out, is_device, device);
 }
 
 }  // extern "C"

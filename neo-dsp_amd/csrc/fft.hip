@@ -24,28 +24,28 @@ __host__ __device__ constexpr int pick_e(int n) { return n >= 16 ? 16 : (n < 1 ?
 // ---------------------------------------------------------------------------
 // c2c, whole transforms in LDS. FPB transforms per 256-lane block for small N.
 // ---------------------------------------------------------------------------
-template<int N, int DIR>
-__global__ __launch_bounds__(256) void k_c2c_lds(const cf* __restrict__ in, cf* __restrict__ out,
-                                                 const cf* __restrict__ twg, int64_t batch)
+template<int N, int DIR, class C = cf>
+__global__ __launch_bounds__(256) void k_c2c_lds(const C* __restrict__ in, C* __restrict__ out,
+                                                 const C* __restrict__ twg, int64_t batch)
 {
     constexpr int E = pick_e(N), T = N / E, FPB = T >= 256 ? 1 : 256 / T;
     constexpr int TWL = twiddle_len<N>(), LL = lds_len(N);
-    __shared__ cf smem[FPB * LL + TWL];
-    cf* tw = smem + FPB * LL;
+    __shared__ C smem[FPB * LL + TWL];
+    C* tw = smem + FPB * LL;
     const int tid = threadIdx.x, f = tid / T, t = tid % T;
     for (int i = tid; i < TWL; i += FPB * T) tw[i] = twg[i];
     const int64_t g = int64_t(blockIdx.x) * FPB + f;
     const bool active = g < batch;
-    cf v[E];
+    C v[E];
     if (active) {
-        const cf* src = in + g * N;
+        const C* src = in + g * N;
 #pragma unroll
         for (int m = 0; m < E; ++m) v[m] = ld_nt(src + t + m * T);
     }
     __syncthreads();
     stockham<N, E, DIR>(v, smem + f * LL, tw, t, active);
     if (active) {
-        cf* dst = out + g * N;
+        C* dst = out + g * N;
 #pragma unroll
         for (int m = 0; m < E; ++m) st_nt(dst + t + m * T, v[m]);
     }
@@ -54,23 +54,24 @@ __global__ __launch_bounds__(256) void k_c2c_lds(const cf* __restrict__ in, cf* 
 // ---------------------------------------------------------------------------
 // r2c / c2r of N = 2M reals, whole transforms in LDS (unpacked N/2+1 bins).
 // ---------------------------------------------------------------------------
-template<int M>
-__global__ __launch_bounds__(256) void k_r2c_lds(const float* __restrict__ in, cf* __restrict__ out,
-                                                 const cf* __restrict__ twg, int64_t batch)
+template<int M, class C = cf>
+__global__ __launch_bounds__(256) void k_r2c_lds(const real_of<C>* __restrict__ in, C* __restrict__ out,
+                                                 const C* __restrict__ twg, int64_t batch)
 {
+    using R = real_of<C>;
     constexpr int E = pick_e(M), T = M / E, FPB = T >= 256 ? 1 : 256 / T;
     constexpr int TW1 = twiddle_len<M>(), TW2 = twiddle_len<2 * M>(), LL = lds_len(M);
-    __shared__ cf smem[FPB * LL + TW1 + TW2];
-    cf* tw1 = smem + FPB * LL;
-    cf* tw2 = tw1 + TW1;
+    __shared__ C smem[FPB * LL + TW1 + TW2];
+    C* tw1 = smem + FPB * LL;
+    C* tw2 = tw1 + TW1;
     const int tid = threadIdx.x, f = tid / T, t = tid % T;
     for (int i = tid; i < TW1 + TW2; i += FPB * T) tw1[i] = twg[i];
     const int64_t g = int64_t(blockIdx.x) * FPB + f;
     const bool active = g < batch;
-    cf* lds = smem + f * LL;
-    cf v[E];
+    C* lds = smem + f * LL;
+    C v[E];
     if (active) {
-        const cf* src = reinterpret_cast<const cf*>(in + g * 2 * M);  // z[n] = x[2n] + i x[2n+1]
+        const C* src = reinterpret_cast<const C*>(in + g * 2 * M);  // z[n] = x[2n] + i x[2n+1]
 #pragma unroll
         for (int m = 0; m < E; ++m) v[m] = ld_nt(src + t + m * T);
     }
@@ -82,14 +83,14 @@ __global__ __launch_bounds__(256) void k_r2c_lds(const float* __restrict__ in, c
     }
     __syncthreads();
     if (active) {
-        cf* dst = out + g * (M + 1);
+        C* dst = out + g * (M + 1);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int k = t + m * T;
-            const cf x = r2c_split<M>(lds, tw2, k);
+            const C x = r2c_split<M>(lds, tw2, k);
             if (k == 0) {
-                dst[0] = {x.x, 0.0f};
-                dst[M] = {x.y, 0.0f};
+                dst[0] = {x.x, R(0)};
+                dst[M] = {x.y, R(0)};
             } else {
                 dst[k] = x;
             }
@@ -97,26 +98,26 @@ __global__ __launch_bounds__(256) void k_r2c_lds(const float* __restrict__ in, c
     }
 }
 
-template<int M>
-__global__ __launch_bounds__(256) void k_c2r_lds(const cf* __restrict__ in, float* __restrict__ out,
-                                                 const cf* __restrict__ twg, int64_t batch)
+template<int M, class C = cf>
+__global__ __launch_bounds__(256) void k_c2r_lds(const C* __restrict__ in, real_of<C>* __restrict__ out,
+                                                 const C* __restrict__ twg, int64_t batch)
 {
     constexpr int E = pick_e(M), T = M / E, FPB = T >= 256 ? 1 : 256 / T;
     constexpr int TW1 = twiddle_len<M>(), TW2 = twiddle_len<2 * M>(), LL = lds_len(M + 1);
-    __shared__ cf smem[FPB * LL + TW1 + TW2];
-    cf* tw1 = smem + FPB * LL;
-    cf* tw2 = tw1 + TW1;
+    __shared__ C smem[FPB * LL + TW1 + TW2];
+    C* tw1 = smem + FPB * LL;
+    C* tw2 = tw1 + TW1;
     const int tid = threadIdx.x, f = tid / T, t = tid % T;
     for (int i = tid; i < TW1 + TW2; i += FPB * T) tw1[i] = twg[i];
     const int64_t g = int64_t(blockIdx.x) * FPB + f;
     const bool active = g < batch;
-    cf* lds = smem + f * LL;
+    C* lds = smem + f * LL;
     if (active) {
-        const cf* src = in + g * (M + 1);
+        const C* src = in + g * (M + 1);
         for (int k = t; k <= M; k += T) lds[lpad(k)] = src[k];
     }
     __syncthreads();
-    cf v[E];
+    C v[E];
     if (active) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
@@ -127,19 +128,21 @@ __global__ __launch_bounds__(256) void k_c2r_lds(const cf* __restrict__ in, floa
     __syncthreads();
     stockham<M, E, +1>(v, lds, tw1, t, active);
     if (active) {
-        cf* dst = reinterpret_cast<cf*>(out + g * 2 * M);
+        C* dst = reinterpret_cast<C*>(out + g * 2 * M);
 #pragma unroll
         for (int m = 0; m < E; ++m) st_nt(dst + t + m * T, v[m]);
     }
 }
 
 // order-0 real transforms (N = 1): X[0] = x[0]; x[0] = Re X[0]
-__global__ void k_r2c_order0(const float* in, cf* out, int64_t batch)
+template<class C>
+__global__ void k_r2c_order0(const real_of<C>* in, C* out, int64_t batch)
 {
     const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < batch) out[i] = {in[i], 0.0f};
+    if (i < batch) out[i] = {in[i], 0};
 }
-__global__ void k_c2r_order0(const cf* in, float* out, int64_t batch)
+template<class C>
+__global__ void k_c2r_order0(const C* in, real_of<C>* out, int64_t batch)
 {
     const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i < batch) out[i] = in[i].x;
@@ -148,15 +151,16 @@ __global__ void k_c2r_order0(const cf* in, float* out, int64_t batch)
 // ---------------------------------------------------------------------------
 // Large transforms: one global-memory Stockham pass of radix R.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ cf split_twiddle(const cf* tw, int lo_bits, int64_t e)
+template<class C>
+__device__ __forceinline__ C split_twiddle(const C* tw, int lo_bits, int64_t e)
 {
     const int64_t mask = (int64_t(1) << lo_bits) - 1;
     return cmul(tw[(int64_t(1) << lo_bits) + (e >> lo_bits)], tw[e & mask]);
 }
 
-template<int R, int DIR>
-__global__ __launch_bounds__(256) void k_pass(const cf* __restrict__ in, cf* __restrict__ out,
-                                              const cf* __restrict__ tw, int lo_bits, int64_t n, int64_t ns,
+template<int R, int DIR, class C = cf>
+__global__ __launch_bounds__(256) void k_pass(const C* __restrict__ in, C* __restrict__ out,
+                                              const C* __restrict__ tw, int lo_bits, int64_t n, int64_t ns,
                                               int64_t total)
 {
     const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(256) void k_pass(const cf* __restrict__ in, cf* __r
     const int64_t b = gid / nb, j = gid - b * nb;
     in += b * n;
     out += b * n;
-    cf v[R];
+    C v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
     const int64_t jm = j & (ns - 1);
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(256) void k_pass(const cf* __restrict__ in, cf* __r
         const int64_t step = jm * (n / (ns * R));
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-            cf w = split_twiddle(tw, lo_bits, step * r);
+            C w = split_twiddle(tw, lo_bits, step * r);
             if (DIR > 0) w.y = -w.y;
             v[r] = cmul(v[r], w);
         }
@@ -185,46 +189,49 @@ __global__ __launch_bounds__(256) void k_pass(const cf* __restrict__ in, cf* __r
 }
 
 // r2c split / c2r join for large sizes (global memory, one bin per lane).
-__global__ void k_r2c_split_global(const cf* __restrict__ z, cf* __restrict__ out, const cf* __restrict__ tw,
+template<class C>
+__global__ void k_r2c_split_global(const C* __restrict__ z, C* __restrict__ out, const C* __restrict__ tw,
                                    int lo_bits, int64_t m, int64_t batch)
 {
+    using Rl = real_of<C>;
     const int64_t gid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (gid >= batch * m) return;
     const int64_t b = gid / m, k = gid - b * m;
-    const cf* zr = z + b * m;
-    cf* dst = out + b * (m + 1);
-    const cf zk = zr[k];
+    const C* zr = z + b * m;
+    C* dst = out + b * (m + 1);
+    const C zk = zr[k];
     if (k == 0) {
-        dst[0] = {zk.x + zk.y, 0.0f};
-        dst[m] = {zk.x - zk.y, 0.0f};
+        dst[0] = {zk.x + zk.y, Rl(0)};
+        dst[m] = {zk.x - zk.y, Rl(0)};
         return;
     }
-    const cf zc = cconj(zr[m - k]);
-    const cf fe = cscale(cadd(zk, zc), 0.5f);
-    const cf d = csub(zk, zc);
-    const cf fo = {0.5f * d.y, -0.5f * d.x};
+    const C zc = cconj(zr[m - k]);
+    const C fe = cscale(cadd(zk, zc), Rl(0.5));
+    const C d = csub(zk, zc);
+    const C fo = {Rl(0.5) * d.y, Rl(-0.5) * d.x};
     dst[k] = cadd(fe, cmul(split_twiddle(tw, lo_bits, k), fo));
 }
 
-__global__ void k_c2r_join_global(const cf* __restrict__ x, cf* __restrict__ z, const cf* __restrict__ tw,
+template<class C>
+__global__ void k_c2r_join_global(const C* __restrict__ x, C* __restrict__ z, const C* __restrict__ tw,
                                   int lo_bits, int64_t m, int64_t batch)
 {
     const int64_t gid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (gid >= batch * m) return;
     const int64_t b = gid / m, k = gid - b * m;
-    const cf* xr = x + b * (m + 1);
-    cf a, c;
+    const C* xr = x + b * (m + 1);
+    C a, c;
     if (k == 0) {
-        a = {xr[0].x, 0.0f};
-        c = {xr[m].x, 0.0f};
+        a = {xr[0].x, 0};
+        c = {xr[m].x, 0};
     } else {
         a = xr[k];
         c = cconj(xr[m - k]);
     }
-    cf w = split_twiddle(tw, lo_bits, k);
+    C w = split_twiddle(tw, lo_bits, k);
     w.y = -w.y;
-    const cf fe = cadd(a, c);
-    const cf fo = cmul(csub(a, c), w);
+    const C fe = cadd(a, c);
+    const C fo = cmul(csub(a, c), w);
     z[b * m + k] = {fe.x - fo.y, fe.y + fo.x};
 }
 
@@ -234,14 +241,15 @@ using namespace neo_hip;
 
 struct neo_hip_fft_plan {
     int order = 0, kind = 0, device = 0;
+    bool f64 = false;        // complex<double> / double plans (NEO_HIP_F64)
     int64_t batch = 0, n = 0;
     hipStream_t stream = nullptr;
-    cf* d_tw = nullptr;      // LDS path: table(n) [c2c] or table(M) ++ table(2M) [real]
-    cf* d_split = nullptr;   // large path: split table of the inner c2c size
+    void* d_tw = nullptr;    // LDS path: table(n) [c2c] or table(M) ++ table(2M) [real]
+    void* d_split = nullptr; // large path: split table of the inner c2c size
     int lo_bits = 0;
-    cf* d_split2 = nullptr;  // large real path: split table of size 2M (join/split twiddles)
+    void* d_split2 = nullptr;  // large real path: split table of size 2M (join/split twiddles)
     int lo_bits2 = 0;
-    cf* d_scratch[3] = {nullptr, nullptr, nullptr};
+    void* d_scratch[3] = {nullptr, nullptr, nullptr};
     void* d_in = nullptr;    // staging for neo_hip_fft_execute_host
     void* d_out = nullptr;
     size_t in_bytes = 0, out_bytes = 0;
@@ -254,14 +262,14 @@ using plan_t = neo_hip_fft_plan;
 // inner complex FFT order of a plan (c2c: order, real: order-1)
 int inner_order(const plan_t* p) { return p->kind == NEO_HIP_C2C ? p->order : p->order - 1; }
 
-template<int DIR>
-int launch_c2c_lds(int order, const cf* in, cf* out, const cf* tw, int64_t batch, hipStream_t s)
+template<int DIR, class C>
+int launch_c2c_lds(int order, const C* in, C* out, const C* tw, int64_t batch, hipStream_t s)
 {
 #define NEO_C2C_CASE(ORD)                                                                            \
     case ORD: {                                                                                      \
         constexpr int N = 1 << ORD, E = pick_e(N), T = N / E, FPB = T >= 256 ? 1 : 256 / T;          \
         const int64_t blocks = (batch + FPB - 1) / FPB;                                              \
-        hipLaunchKernelGGL((k_c2c_lds<N, DIR>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s, in, out, tw, \
+        hipLaunchKernelGGL((k_c2c_lds<N, DIR, C>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s, in, out, tw, \
                            batch);                                                                   \
         break;                                                                                       \
     }
@@ -276,18 +284,20 @@ int launch_c2c_lds(int order, const cf* in, cf* out, const cf* tw, int64_t batch
     return NEO_HIP_OK;
 }
 
-int launch_real_lds(int kind, int m_order, const void* in, void* out, const cf* tw, int64_t batch, hipStream_t s)
+template<class C>
+int launch_real_lds(int kind, int m_order, const void* in, void* out, const C* tw, int64_t batch, hipStream_t s)
 {
+    using R = real_of<C>;
 #define NEO_REAL_CASE(ORD)                                                                            \
     case ORD: {                                                                                       \
         constexpr int M = 1 << ORD, E = pick_e(M), T = M / E, FPB = T >= 256 ? 1 : 256 / T;           \
         const int64_t blocks = (batch + FPB - 1) / FPB;                                               \
         if (kind == NEO_HIP_R2C)                                                                      \
-            hipLaunchKernelGGL((k_r2c_lds<M>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s,            \
-                               static_cast<const float*>(in), static_cast<cf*>(out), tw, batch);      \
+            hipLaunchKernelGGL((k_r2c_lds<M, C>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s,         \
+                               static_cast<const R*>(in), static_cast<C*>(out), tw, batch);           \
         else                                                                                          \
-            hipLaunchKernelGGL((k_c2r_lds<M>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s,            \
-                               static_cast<const cf*>(in), static_cast<float*>(out), tw, batch);      \
+            hipLaunchKernelGGL((k_c2r_lds<M, C>), dim3(unsigned(blocks)), dim3(FPB * T), 0, s,         \
+                               static_cast<const C*>(in), static_cast<R*>(out), tw, batch);           \
         break;                                                                                        \
     }
     switch (m_order) {
@@ -303,7 +313,8 @@ int launch_real_lds(int kind, int m_order, const void* in, void* out, const cf* 
 
 // Large c2c: radix-16 passes (remainder radix last), ping-pong through scratch
 // so that `in == out` is safe; the last pass writes `out`.
-int run_c2c_global(const plan_t* p, int order, const cf* in, cf* out, int dir, hipStream_t s)
+template<class C>
+int run_c2c_global(const plan_t* p, int order, const C* in, C* out, int dir, hipStream_t s)
 {
     const int64_t n = int64_t(1) << order;
     std::vector<int> radix;
@@ -313,20 +324,21 @@ int run_c2c_global(const plan_t* p, int order, const cf* in, cf* out, int dir, h
         rem -= r;
     }
     const int K = int(radix.size());
-    const cf* src = in;
+    const C* src = in;
+    const C* split = static_cast<const C*>(p->d_split);
     int64_t ns = 1;
     for (int i = 0; i < K; ++i) {
-        cf* dst = (i == K - 1) ? out : p->d_scratch[i & 1];
+        C* dst = (i == K - 1) ? out : static_cast<C*>(p->d_scratch[i & 1]);
         const int R = radix[size_t(i)];
         const int64_t total = p->batch * (n / R);
         const unsigned blocks = unsigned((total + 255) / 256);
 #define NEO_PASS(RR)                                                                                     \
     if (dir < 0)                                                                                         \
-        hipLaunchKernelGGL((k_pass<RR, -1>), dim3(blocks), dim3(256), 0, s, src, dst, p->d_split, p->lo_bits, \
-                           n, ns, total);                                                                \
+        hipLaunchKernelGGL((k_pass<RR, -1, C>), dim3(blocks), dim3(256), 0, s, src, dst, split, p->lo_bits, n, \
+                           ns, total);                                                                   \
     else                                                                                                 \
-        hipLaunchKernelGGL((k_pass<RR, +1>), dim3(blocks), dim3(256), 0, s, src, dst, p->d_split, p->lo_bits, \
-                           n, ns, total);
+        hipLaunchKernelGGL((k_pass<RR, +1, C>), dim3(blocks), dim3(256), 0, s, src, dst, split, p->lo_bits, n, \
+                           ns, total);
         switch (R) {
             case 16: NEO_PASS(16) break;
             case 8: NEO_PASS(8) break;
@@ -342,10 +354,11 @@ int run_c2c_global(const plan_t* p, int order, const cf* in, cf* out, int dir, h
     return NEO_HIP_OK;
 }
 
-int upload(cf** dst, const std::vector<cf>& v)
+template<class C>
+int upload(void** dst, const std::vector<C>& v)
 {
-    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dst), v.size() * sizeof(cf)));
-    NEO_HIP_CHECK(hipMemcpy(*dst, v.data(), v.size() * sizeof(cf), hipMemcpyHostToDevice));
+    NEO_HIP_CHECK(hipMalloc(dst, v.size() * sizeof(C)));
+    NEO_HIP_CHECK(hipMemcpy(*dst, v.data(), v.size() * sizeof(C), hipMemcpyHostToDevice));
     return NEO_HIP_OK;
 }
 
@@ -362,6 +375,78 @@ void free_plan(plan_t* p)
     delete p;
 }
 
+template<class C>
+int setup_tables(plan_t* p)
+{
+    const int io = inner_order(p);
+    int rc = NEO_HIP_OK;
+    if (io >= 0 && io <= kLdsMaxOrder) {
+        std::vector<C> t = make_twiddle_table<C>(int64_t(1) << io);
+        if (p->kind != NEO_HIP_C2C) {
+            std::vector<C> t2 = make_twiddle_table<C>(int64_t(2) << io);
+            t.insert(t.end(), t2.begin(), t2.end());
+        }
+        if ((rc = upload(&p->d_tw, t))) return rc;
+    } else if (io > kLdsMaxOrder) {
+        p->lo_bits = (io + 1) / 2;
+        if ((rc = upload(&p->d_split, make_split_table<C>(io, p->lo_bits)))) return rc;
+        const int64_t inner = int64_t(1) << io;
+        const int nscratch = p->kind == NEO_HIP_C2C ? 2 : 3;
+        for (int i = 0; i < nscratch; ++i)
+            if (hipMalloc(&p->d_scratch[i], size_t(inner * p->batch) * sizeof(C)) != hipSuccess)
+                return fail(NEO_HIP_ENOMEM, "scratch allocation failed");
+        if (p->kind != NEO_HIP_C2C) {
+            p->lo_bits2 = (io + 2) / 2;
+            if ((rc = upload(&p->d_split2, make_split_table<C>(io + 1, p->lo_bits2)))) return rc;
+        }
+    }
+    return NEO_HIP_OK;
+}
+
+template<class C>
+int execute(neo_hip_fft_plan* p, const void* in, void* out, int direction, hipStream_t s)
+{
+    using R = real_of<C>;
+    const int io = inner_order(p);
+    const C* tw = static_cast<const C*>(p->d_tw);
+    if (p->kind == NEO_HIP_C2C) {
+        const C* ci = static_cast<const C*>(in);
+        C* co = static_cast<C*>(out);
+        if (io <= kLdsMaxOrder)
+            return direction < 0 ? launch_c2c_lds<-1>(io, ci, co, tw, p->batch, s)
+                                 : launch_c2c_lds<+1>(io, ci, co, tw, p->batch, s);
+        return run_c2c_global(p, io, ci, co, direction, s);
+    }
+    if (io < 0) {  // order 0 real transform
+        const unsigned blocks = unsigned((p->batch + 255) / 256);
+        if (p->kind == NEO_HIP_R2C)
+            hipLaunchKernelGGL((k_r2c_order0<C>), dim3(blocks), dim3(256), 0, s, static_cast<const R*>(in),
+                               static_cast<C*>(out), p->batch);
+        else
+            hipLaunchKernelGGL((k_c2r_order0<C>), dim3(blocks), dim3(256), 0, s, static_cast<const C*>(in),
+                               static_cast<R*>(out), p->batch);
+        NEO_HIP_LAUNCH_CHECK();
+        return NEO_HIP_OK;
+    }
+    if (io <= kLdsMaxOrder) return launch_real_lds<C>(p->kind, io, in, out, tw, p->batch, s);
+    const int64_t m = int64_t(1) << io, total = m * p->batch;
+    const unsigned blocks = unsigned((total + 255) / 256);
+    C* z = static_cast<C*>(p->d_scratch[2]);
+    const C* split2 = static_cast<const C*>(p->d_split2);
+    if (p->kind == NEO_HIP_R2C) {
+        int rc = run_c2c_global(p, io, static_cast<const C*>(in), z, -1, s);
+        if (rc) return rc;
+        hipLaunchKernelGGL((k_r2c_split_global<C>), dim3(blocks), dim3(256), 0, s, z, static_cast<C*>(out), split2,
+                           p->lo_bits2, m, p->batch);
+        NEO_HIP_LAUNCH_CHECK();
+        return NEO_HIP_OK;
+    }
+    hipLaunchKernelGGL((k_c2r_join_global<C>), dim3(blocks), dim3(256), 0, s, static_cast<const C*>(in), z, split2,
+                       p->lo_bits2, m, p->batch);
+    NEO_HIP_LAUNCH_CHECK();
+    return run_c2c_global(p, io, static_cast<const C*>(z), static_cast<C*>(out), +1, s);
+}
+
 }  // namespace
 
 extern "C" {
@@ -372,6 +457,8 @@ NEO_HIP_API int neo_hip_fft_plan_create(int order, int64_t batch, int kind, int 
 {
     if (!out) return fail(NEO_HIP_EINVAL, "plan pointer is null");
     *out = nullptr;
+    const bool f64 = (kind & NEO_HIP_F64) != 0;
+    kind &= ~NEO_HIP_F64;
     if (order < 0 || order > kMaxOrder)
         return fail(NEO_HIP_EINVAL, "unsupported order '%d' (max_order %d)", order, kMaxOrder);
     if (batch < 1) return fail(NEO_HIP_EINVAL, "batch must be >= 1");
@@ -382,39 +469,20 @@ NEO_HIP_API int neo_hip_fft_plan_create(int order, int64_t batch, int kind, int 
     auto* p = new plan_t{};
     p->order = order;
     p->kind = kind;
+    p->f64 = f64;
     p->batch = batch;
     p->n = int64_t(1) << order;
     (void)hipGetDevice(&p->device);
-    int rc = NEO_HIP_OK;
     auto bail = [&](int code) {
         free_plan(p);
         return code;
     };
     if (hipStreamCreateWithFlags(&p->stream, hipStreamDefault) != hipSuccess)
         return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
-    const int io = inner_order(p);
-    if (io >= 0 && io <= kLdsMaxOrder) {
-        std::vector<cf> t = make_twiddle_table(int64_t(1) << io);
-        if (kind != NEO_HIP_C2C) {
-            std::vector<cf> t2 = make_twiddle_table(int64_t(2) << io);
-            t.insert(t.end(), t2.begin(), t2.end());
-        }
-        if ((rc = upload(&p->d_tw, t))) return bail(rc);
-    } else if (io > kLdsMaxOrder) {
-        p->lo_bits = (io + 1) / 2;
-        if ((rc = upload(&p->d_split, make_split_table(io, p->lo_bits)))) return bail(rc);
-        const int64_t inner = int64_t(1) << io;
-        const int nscratch = kind == NEO_HIP_C2C ? 2 : 3;
-        for (int i = 0; i < nscratch; ++i)
-            if (hipMalloc(reinterpret_cast<void**>(&p->d_scratch[i]), size_t(inner * batch) * sizeof(cf)) != hipSuccess)
-                return bail(fail(NEO_HIP_ENOMEM, "scratch allocation failed"));
-        if (kind != NEO_HIP_C2C) {
-            p->lo_bits2 = (io + 2) / 2;
-            if ((rc = upload(&p->d_split2, make_split_table(io + 1, p->lo_bits2)))) return bail(rc);
-        }
-    }
-    const size_t cbytes = size_t(p->n) * sizeof(cf), rbytes = size_t(p->n) * sizeof(float);
-    const size_t hbytes = size_t(p->n / 2 + 1) * sizeof(cf);
+    if (int rc = f64 ? setup_tables<cd>(p) : setup_tables<cf>(p)) return bail(rc);
+    const size_t rs = f64 ? sizeof(double) : sizeof(float), cs = 2 * rs;
+    const size_t cbytes = size_t(p->n) * cs, rbytes = size_t(p->n) * rs;
+    const size_t hbytes = size_t(p->n / 2 + 1) * cs;
     p->in_bytes = size_t(batch) * (kind == NEO_HIP_C2C ? cbytes : kind == NEO_HIP_R2C ? rbytes : hbytes);
     p->out_bytes = size_t(batch) * (kind == NEO_HIP_C2C ? cbytes : kind == NEO_HIP_R2C ? hbytes : rbytes);
     *out = p;
@@ -437,42 +505,7 @@ NEO_HIP_API int neo_hip_fft_execute(neo_hip_fft_plan* p, const void* in, void* o
     device_guard g(p->device);
     if (g.rc) return g.rc;
     hipStream_t s = as_stream(stream);  // NULL = the HIP null stream (torch's default stream)
-    const int io = inner_order(p);
-    if (p->kind == NEO_HIP_C2C) {
-        const cf* ci = static_cast<const cf*>(in);
-        cf* co = static_cast<cf*>(out);
-        if (io <= kLdsMaxOrder)
-            return direction < 0 ? launch_c2c_lds<-1>(io, ci, co, p->d_tw, p->batch, s)
-                                 : launch_c2c_lds<+1>(io, ci, co, p->d_tw, p->batch, s);
-        return run_c2c_global(p, io, ci, co, direction, s);
-    }
-    if (io < 0) {  // order 0 real transform
-        const unsigned blocks = unsigned((p->batch + 255) / 256);
-        if (p->kind == NEO_HIP_R2C)
-            hipLaunchKernelGGL(k_r2c_order0, dim3(blocks), dim3(256), 0, s, static_cast<const float*>(in),
-                               static_cast<cf*>(out), p->batch);
-        else
-            hipLaunchKernelGGL(k_c2r_order0, dim3(blocks), dim3(256), 0, s, static_cast<const cf*>(in),
-                               static_cast<float*>(out), p->batch);
-        NEO_HIP_LAUNCH_CHECK();
-        return NEO_HIP_OK;
-    }
-    if (io <= kLdsMaxOrder) return launch_real_lds(p->kind, io, in, out, p->d_tw, p->batch, s);
-    const int64_t m = int64_t(1) << io, total = m * p->batch;
-    const unsigned blocks = unsigned((total + 255) / 256);
-    cf* z = p->d_scratch[2];
-    if (p->kind == NEO_HIP_R2C) {
-        int rc = run_c2c_global(p, io, static_cast<const cf*>(in), z, -1, s);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_r2c_split_global, dim3(blocks), dim3(256), 0, s, z, static_cast<cf*>(out), p->d_split2,
-                           p->lo_bits2, m, p->batch);
-        NEO_HIP_LAUNCH_CHECK();
-        return NEO_HIP_OK;
-    }
-    hipLaunchKernelGGL(k_c2r_join_global, dim3(blocks), dim3(256), 0, s, static_cast<const cf*>(in), z, p->d_split2,
-                       p->lo_bits2, m, p->batch);
-    NEO_HIP_LAUNCH_CHECK();
-    return run_c2c_global(p, io, z, static_cast<cf*>(out), +1, s);
+    return p->f64 ? execute<cd>(p, in, out, direction, s) : execute<cf>(p, in, out, direction, s);
 }
 
 NEO_HIP_API int neo_hip_fft_execute_host(neo_hip_fft_plan* p, const void* in, void* out, int direction)

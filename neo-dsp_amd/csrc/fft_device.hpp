@@ -25,11 +25,18 @@ namespace neo_hip {
 struct alignas(8) cf {  // complex float, interleaved {re, im} = std::complex<float> layout
     float x, y;
 };
+struct alignas(16) cd {  // complex double, = std::complex<double> layout (the f64 plans)
+    double x, y;
+};
+template<class C>
+using real_of = decltype(C::x);
 
 // Streaming (nontemporal) global accesses: HBM-streamed data that no later
 // kernel re-reads from cache (measured: 4096-pt batched FFT 0.856 -> 0.739 ms).
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ cf ld_nt(const cf* p)
 {
@@ -42,6 +49,18 @@ __device__ __forceinline__ void st_nt(cf* p, cf a)
     v.x = a.x;
     v.y = a.y;
     __builtin_nontemporal_store(v, reinterpret_cast<f2v*>(p));
+}
+__device__ __forceinline__ cd ld_nt(const cd* p)
+{
+    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+    return {v.x, v.y};
+}
+__device__ __forceinline__ void st_nt(cd* p, cd a)
+{
+    d2v v;
+    v.x = a.x;
+    v.y = a.y;
+    __builtin_nontemporal_store(v, reinterpret_cast<d2v*>(p));
 }
 __device__ __forceinline__ float4 ld4_nt(const float4* p)
 {
@@ -64,11 +83,16 @@ __device__ __forceinline__ float4 ld4(const float4* p)
     else return *p;
 }
 
-__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
-__device__ __forceinline__ cf csub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
-__device__ __forceinline__ cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
-__device__ __forceinline__ cf cconj(cf a) { return {a.x, -a.y}; }
-__device__ __forceinline__ cf cscale(cf a, float s) { return {a.x * s, a.y * s}; }
+template<class C>
+__device__ __forceinline__ C cadd(C a, C b) { return {a.x + b.x, a.y + b.y}; }
+template<class C>
+__device__ __forceinline__ C csub(C a, C b) { return {a.x - b.x, a.y - b.y}; }
+template<class C>
+__device__ __forceinline__ C cmul(C a, C b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+template<class C>
+__device__ __forceinline__ C cconj(C a) { return {a.x, -a.y}; }
+template<class C>
+__device__ __forceinline__ C cscale(C a, real_of<C> s) { return {a.x * s, a.y * s}; }
 
 // cos/sin(2*pi*k/16), k = 0..15, rounded to float
 __device__ constexpr float kCos16[16] = {
@@ -82,18 +106,36 @@ __device__ constexpr float kSin16[16] = {
     0.0f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128674f,
     -1.0f, -0.92387953251128674f, -0.70710678118654752f, -0.38268343236508977f};
 
+__device__ constexpr double kCos16d[16] = {
+    1.0, 0.92387953251128674, 0.70710678118654752, 0.38268343236508977,
+    0.0, -0.38268343236508977, -0.70710678118654752, -0.92387953251128674,
+    -1.0, -0.92387953251128674, -0.70710678118654752, -0.38268343236508977,
+    0.0, 0.38268343236508977, 0.70710678118654752, 0.92387953251128674};
+__device__ constexpr double kSin16d[16] = {
+    0.0, 0.38268343236508977, 0.70710678118654752, 0.92387953251128674,
+    1.0, 0.92387953251128674, 0.70710678118654752, 0.38268343236508977,
+    0.0, -0.38268343236508977, -0.70710678118654752, -0.92387953251128674,
+    -1.0, -0.92387953251128674, -0.70710678118654752, -0.38268343236508977};
+
 // a * exp(DIR * 2*pi*i * k / 16); k is a compile-time constant after unrolling,
 // so the trivial rotations fold into swaps/negations.
-template<int DIR>
-__device__ __forceinline__ cf rot16(cf a, int k)
+template<int DIR, class C>
+__device__ __forceinline__ C rot16(C a, int k)
 {
     k &= 15;
     if (k == 0) return a;
     if (k == 8) return {-a.x, -a.y};
-    if (k == 4) return DIR < 0 ? cf{a.y, -a.x} : cf{-a.y, a.x};
-    if (k == 12) return DIR < 0 ? cf{-a.y, a.x} : cf{a.y, -a.x};
-    const float c = kCos16[k];
-    const float s = DIR < 0 ? -kSin16[k] : kSin16[k];
+    if (k == 4) return DIR < 0 ? C{a.y, -a.x} : C{-a.y, a.x};
+    if (k == 12) return DIR < 0 ? C{-a.y, a.x} : C{a.y, -a.x};
+    using R = real_of<C>;
+    R c, s;
+    if constexpr (sizeof(R) == 8) {
+        c = kCos16d[k];
+        s = DIR < 0 ? -kSin16d[k] : kSin16d[k];
+    } else {
+        c = kCos16[k];
+        s = DIR < 0 ? -kSin16[k] : kSin16[k];
+    }
     return {a.x * c - a.y * s, a.x * s + a.y * c};
 }
 
@@ -108,8 +150,8 @@ __host__ __device__ constexpr int bitrev_c(int v, int bits)
 
 // In-register R-point DFT (R | 16), natural order in and out.
 // Radix-2 DIF network, then a compile-time bit-reverse permutation.
-template<int R, int DIR>
-__device__ __forceinline__ void dft(cf (&v)[R])
+template<int R, int DIR, class C>
+__device__ __forceinline__ void dft(C (&v)[R])
 {
     if constexpr (R == 1) {
         return;
@@ -120,14 +162,14 @@ __device__ __forceinline__ void dft(cf (&v)[R])
             for (int blk = 0; blk < R; blk += 2 * half) {
 #pragma unroll
                 for (int j = 0; j < half; ++j) {
-                    const cf a = v[blk + j], b = v[blk + j + half];
+                    const C a = v[blk + j], b = v[blk + j + half];
                     v[blk + j] = cadd(a, b);
                     // twiddle W_{2half}^j = W_16^{j * 16 / (2 half)}
                     v[blk + j + half] = rot16<DIR>(csub(a, b), j * (16 / (2 * half)));
                 }
             }
         }
-        cf t[R];
+        C t[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) t[k] = v[bitrev_c(k, ilog2(R))];
 #pragma unroll
@@ -142,10 +184,10 @@ __host__ __device__ constexpr int lds_len(int n) { return n + n / 16 + 1; }
 
 // Two-level twiddle table for an FFT of size N: tw[0..63] = W^e (e < 64),
 // tw[64..64+N/64) = W^(64*h); W = exp(-2*pi*i/N) (forward). DIR=+1 conjugates.
-template<int N, int DIR>
-__device__ __forceinline__ cf twiddle(const cf* tw, int e)
+template<int N, int DIR, class C>
+__device__ __forceinline__ C twiddle(const C* tw, int e)
 {
-    cf w;
+    C w;
     if constexpr (N <= 64) {
         w = tw[e];
     } else {
@@ -171,8 +213,8 @@ __host__ __device__ constexpr int pass_radix()
 // Stockham passes from sub-length Ns upward. v[m] = element t + m*T on entry
 // (T = N/E); on exit v[m] = X[t + m*T]. `lds` holds lds_len(N) complex and is
 // reused by every pass; all threads of the block must call (barriers inside).
-template<int N, int E, int DIR, int Ns = 1>
-__device__ __forceinline__ void stockham(cf (&v)[E], cf* lds, const cf* tw, int t, bool active)
+template<int N, int E, int DIR, int Ns = 1, class C>
+__device__ __forceinline__ void stockham(C (&v)[E], C* lds, const C* tw, int t, bool active)
 {
     if constexpr (N == 1 || Ns >= N) {
         return;
@@ -185,7 +227,7 @@ __device__ __forceinline__ void stockham(cf (&v)[E], cf* lds, const cf* tw, int 
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 const int j = t + b * T;
-                cf w[R];
+                C w[R];
 #pragma unroll
                 for (int r = 0; r < R; ++r) w[r] = v[b + r * NB];
                 const int jm = j & (Ns - 1);

@@ -17,15 +17,16 @@ namespace neo_hip {
 
 // Forward split: Z = FFT_M(z) in `zl` (natural order, lpad'ed). Returns X[k]
 // for k in [0, M); X[0] is packed {DC, Nyquist}. tw2 = twiddle table of size 2M.
-template<int M>
-__device__ __forceinline__ cf r2c_split(const cf* zl, const cf* tw2, int k)
+template<int M, class C>
+__device__ __forceinline__ C r2c_split(const C* zl, const C* tw2, int k)
 {
-    const cf zk = zl[lpad(k)];
+    using R = real_of<C>;
+    const C zk = zl[lpad(k)];
     if (k == 0) return {zk.x + zk.y, zk.x - zk.y};
-    const cf zc = cconj(zl[lpad(M - k)]);
-    const cf fe = cscale(cadd(zk, zc), 0.5f);
-    const cf d = csub(zk, zc);
-    const cf fo = {0.5f * d.y, -0.5f * d.x};  // -i/2 * (zk - zc)
+    const C zc = cconj(zl[lpad(M - k)]);
+    const C fe = cscale(cadd(zk, zc), R(0.5));
+    const C d = csub(zk, zc);
+    const C fo = {R(0.5) * d.y, R(-0.5) * d.x};  // -i/2 * (zk - zc)
     return cadd(fe, cmul(twiddle<2 * M, -1>(tw2, k), fo));
 }
 
@@ -34,19 +35,19 @@ __device__ __forceinline__ cf r2c_split(const cf* zl, const cf* tw2, int k)
 // the unnormalized 2M-point inverse (fallback_rfft_plan.hpp:38-55: Hermitian
 // fill, backward c2c, real part; imaginary parts of DC/Nyquist ignored).
 // xk = X[k], xmk = X[M-k] for k > 0; for k == 0 pass dc/nyq in xk.x / xmk.x.
-template<int M>
-__device__ __forceinline__ cf c2r_join(cf xk, cf xmk, const cf* tw2, int k)
+template<int M, class C>
+__device__ __forceinline__ C c2r_join(C xk, C xmk, const C* tw2, int k)
 {
-    cf a, b;  // a = X[k], b = conj(X[M-k])
+    C a, b;  // a = X[k], b = conj(X[M-k])
     if (k == 0) {
-        a = {xk.x, 0.0f};
-        b = {xmk.x, 0.0f};
+        a = {xk.x, 0};
+        b = {xmk.x, 0};
     } else {
         a = xk;
         b = cconj(xmk);
     }
-    const cf fe = cadd(a, b);
-    const cf fo = cmul(csub(a, b), twiddle<2 * M, +1>(tw2, k));
+    const C fe = cadd(a, b);
+    const C fo = cmul(csub(a, b), twiddle<2 * M, +1>(tw2, k));
     return {fe.x - fo.y, fe.y + fo.x};  // fe + i*fo
 }
 

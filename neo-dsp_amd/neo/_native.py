@@ -20,6 +20,7 @@ NEO_HIP_ENOMEM = 3
 NEO_HIP_ENODEV = 4
 
 C2C, R2C, C2R = 0, 1, 2
+F64 = 16  # OR into the kind: complex128 / float64 plans
 
 # every symbol declared in include/neo_hip.h: (name, restype, argtypes)
 _vp, _i, _i64, _fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_float)
@@ -53,6 +54,8 @@ SIGNATURES = {
     "neo_hip_normalize_impulse": (_i, [_vp, _i, _i64, _i, _i]),
     "neo_hip_fft_convolve": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
     "neo_hip_direct_convolve": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
+    "neo_hip_fft_convolve_f64": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
+    "neo_hip_direct_convolve_f64": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
 }
 
 _lib = None

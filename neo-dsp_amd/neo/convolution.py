@@ -317,28 +317,33 @@ def dense_convolve(signal, impulse_response, block_size: int, device: int = 0, m
     return out
 
 
-def _one_shot(fn, signal, patch, device):
-    a = np.ascontiguousarray(np.asarray(signal), dtype=None)
-    b = np.ascontiguousarray(np.asarray(patch), dtype=None)
+def _one_shot(name, signal, patch, device):
+    """The reference binds float then double (main.cpp:255-258): a float64 pair picks the
+    double overload, anything else converts to float32 (pybind11's converting pass)."""
+    a = np.asarray(signal)
+    b = np.asarray(patch)
     if a.ndim != 1 or b.ndim != 1:
         raise RuntimeError("unsupported dimension: in1 and in2 must be 1-D")  # main.cpp:173-175
-    if a.dtype != np.float32 or b.dtype != np.float32:
-        raise TypeError("neo_hip convolves float32 data (the GPU path computes in float32)")
+    f64 = a.dtype == np.float64 and b.dtype == np.float64
+    dt = np.float64 if f64 else np.float32
+    a = np.ascontiguousarray(a, dtype=dt)
+    b = np.ascontiguousarray(b, dtype=dt)
     if a.size == 0 or b.size == 0:
-        return np.zeros(0, np.float32)
-    out = np.empty(a.size + b.size - 1, np.float32)
+        return np.zeros(0, dt)
+    out = np.empty(a.size + b.size - 1, dt)
+    fn = getattr(_native.load(), name + ("_f64" if f64 else ""))
     _native.check(fn(_ptr(a), a.size, _ptr(b), b.size, _ptr(out), 0, int(device)))
     return out
 
 
 def fft_convolve(signal, patch, device: int = 0) -> np.ndarray:
     """Full linear convolution through one r2c/c2r pair (fft_convolver.hpp:19-93)."""
-    return _one_shot(_native.load().neo_hip_fft_convolve, signal, patch, device)
+    return _one_shot("neo_hip_fft_convolve", signal, patch, device)
 
 
 def direct_convolve(signal, patch, device: int = 0) -> np.ndarray:
     """Full linear convolution, direct sum (direct_convolve.hpp:14-56), bit-identical loop order."""
-    return _one_shot(_native.load().neo_hip_direct_convolve, signal, patch, device)
+    return _one_shot("neo_hip_direct_convolve", signal, patch, device)
 
 
 def convolve(in1, in2, mode: str = "full", method: str = "auto", device: int = 0) -> np.ndarray:

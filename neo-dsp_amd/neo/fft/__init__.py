@@ -74,8 +74,8 @@ def _c2c(x, n, norm, direction):
     if _is_torch(x):
         import torch
 
-        if x.dtype != torch.complex64:
-            raise TypeError("neo_hip transforms complex64 (float32) data")
+        if x.dtype not in (torch.complex64, torch.complex128):
+            raise TypeError("device tensors: complex64 or complex128")
         if n is not None and n != x.shape[-1]:
             raise ValueError("device tensors: n must equal the last dimension")
         n = x.shape[-1]
@@ -83,28 +83,33 @@ def _c2c(x, n, norm, direction):
         xc = x.resolve_conj().contiguous()
         out = torch.empty_like(xc)
         batch = xc.numel() // n if n else 0
-        plan = get_plan(_native.C2C, order, batch, xc.device.index or 0)
+        kind = _native.C2C | (_native.F64 if x.dtype == torch.complex128 else 0)
+        plan = get_plan(kind, order, batch, xc.device.index or 0)
         plan.execute_device(xc.data_ptr(), out.data_ptr(), direction,
                             torch.cuda.current_stream(xc.device).cuda_stream)
         s = _scale(norm, n, inverse)
         return out if s == 1.0 else out.mul_(s)
     a = np.asarray(x)
-    if a.dtype != np.complex64:
-        if a.dtype == np.complex128 or not np.iscomplexobj(a) and a.dtype.kind not in "fiub":
-            raise TypeError("neo_hip transforms complex64 (float32) data; complex128 is not supported on the GPU path")
+    # the reference binds complex<float> then complex<double> (main.cpp:248-252): an exact
+    # complex64 / complex128 array picks its own overload, anything else is converted to
+    # the first one (pybind11's second, converting pass), i.e. complex64
+    if a.dtype != np.complex128 and a.dtype != np.complex64:
+        if a.dtype.kind not in "fciub":
+            raise TypeError(f"unsupported dtype {a.dtype}")
         a = a.astype(np.complex64)
     if a.ndim == 0:
         raise ValueError("input must have at least one dimension")
+    f64 = a.dtype == np.complex128
     n = a.shape[-1] if n is None else int(n)
     order = _check_size(n)
     a = np.ascontiguousarray(_fit(a, n))
     batch = a.size // n
     out = np.empty_like(a)
-    plan = get_plan(_native.C2C, order, batch, 0)
+    plan = get_plan(_native.C2C | (_native.F64 if f64 else 0), order, batch, 0)
     plan.execute_host(a, out, direction)
     s = _scale(norm, n, inverse)
     if s != 1.0:
-        out *= np.float32(s)
+        out *= (np.float64 if f64 else np.float32)(s)
     return out
 
 
@@ -119,31 +124,37 @@ def ifft(x, n=None, norm="backward"):
 
 
 def rfft(x, n=None, norm="backward"):
-    """Real-input forward DFT: N/2+1 bins (fallback_rfft_plan semantics, packed on the GPU)."""
-    a = np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+    """Real-input forward DFT: N/2+1 bins (fallback_rfft_plan semantics, packed on the GPU).
+    float64 input runs the double plan and returns complex128; anything else float32."""
+    a = np.asarray(x)
+    f64 = a.dtype == np.float64
+    a = np.ascontiguousarray(a, dtype=np.float64 if f64 else np.float32)
     n = a.shape[-1] if n is None else int(n)
     order = _check_size(n)
     a = np.ascontiguousarray(_fit(a, n))
     batch = a.size // n
-    out = np.empty(a.shape[:-1] + (n // 2 + 1,), dtype=np.complex64)
-    get_plan(_native.R2C, order, batch, 0).execute_host(a, out, -1)
+    out = np.empty(a.shape[:-1] + (n // 2 + 1,), dtype=np.complex128 if f64 else np.complex64)
+    get_plan(_native.R2C | (_native.F64 if f64 else 0), order, batch, 0).execute_host(a, out, -1)
     s = _scale(norm, n, False)
     if s != 1.0:
-        out *= np.float32(s)
+        out *= (np.float64 if f64 else np.float32)(s)
     return out
 
 
 def irfft(x, n=None, norm="backward"):
-    """Inverse of rfft: reads N/2+1 bins (Im of DC/Nyquist ignored), returns N reals."""
-    a = np.asarray(x, dtype=np.complex64)
+    """Inverse of rfft: reads N/2+1 bins (Im of DC/Nyquist ignored), returns N reals
+    (float64 for complex128 input)."""
+    a = np.asarray(x)
+    f64 = a.dtype == np.complex128
+    a = np.asarray(a, dtype=np.complex128 if f64 else np.complex64)
     n = 2 * (a.shape[-1] - 1) if n is None else int(n)
     order = _check_size(n)
     need = n // 2 + 1
     a = np.ascontiguousarray(_fit(a, need))
     batch = a.size // need
-    out = np.empty(a.shape[:-1] + (n,), dtype=np.float32)
-    get_plan(_native.C2R, order, batch, 0).execute_host(a, out, +1)
+    out = np.empty(a.shape[:-1] + (n,), dtype=np.float64 if f64 else np.float32)
+    get_plan(_native.C2R | (_native.F64 if f64 else 0), order, batch, 0).execute_host(a, out, +1)
     s = _scale(norm, n, True)
     if s != 1.0:
-        out *= np.float32(s)
+        out *= (np.float64 if f64 else np.float32)(s)
     return out

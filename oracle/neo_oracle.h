@@ -19,6 +19,11 @@ typedef struct oracle_upola2 oracle_upola2;
 oracle_upola2* oracle_upola2_create(size_t P, size_t bins, const float* H);
 void oracle_upola2_destroy(oracle_upola2* u);
 int oracle_upola2_process(oracle_upola2* u, float* inout, size_t num_samples);
+int oracle_fft_c2c_f64(int order, int dir, double* x);
+int oracle_rfft_f64(int order, const double* in, double* out);
+int oracle_irfft_f64(int order, const double* in, double* out);
+int oracle_fft_convolve_f64(const double* signal, size_t n, const double* patch, size_t m, double* out);
+void oracle_direct_convolve_f64(const double* signal, size_t n, const double* patch, size_t l, double* out);
 #ifdef __cplusplus
 }
 #endif

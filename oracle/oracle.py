@@ -20,12 +20,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
 
 _f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
 _sz = ctypes.c_size_t
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(_HERE, "neo_oracle.c")
-    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("neo_oracle.c", "neo_oracle_f64.c")]
+    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
     return _LIB
 
@@ -62,6 +63,11 @@ def lib():
         L.oracle_upola2_create.restype = ctypes.c_void_p
         L.oracle_upola2_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_upola2_process.argtypes = [ctypes.c_void_p, _f32p, _sz]
+        L.oracle_fft_c2c_f64.argtypes = [ctypes.c_int, ctypes.c_int, _f64p]
+        L.oracle_rfft_f64.argtypes = [ctypes.c_int, _f64p, _f64p]
+        L.oracle_irfft_f64.argtypes = [ctypes.c_int, _f64p, _f64p]
+        L.oracle_fft_convolve_f64.argtypes = [_f64p, _sz, _f64p, _sz, _f64p]
+        L.oracle_direct_convolve_f64.argtypes = [_f64p, _sz, _f64p, _sz, _f64p]
         L.oracle_upola_create.argtypes = [_sz, _sz, _f32p, ctypes.c_int]
         L.oracle_upola_create.restype = ctypes.c_void_p
         L.oracle_dense_convolve_method.argtypes = [_f32p, _f32p, _f32p, _sz, _sz, _sz, _sz, ctypes.c_int, ctypes.c_int]
@@ -287,4 +293,54 @@ def direct_convolve(signal: np.ndarray, patch: np.ndarray) -> np.ndarray:
     b = np.ascontiguousarray(patch, dtype=np.float32)
     out = np.empty(a.size + b.size - 1, np.float32)
     lib().oracle_direct_convolve(a, a.size, b, b.size, out)
+    return out
+
+
+# ---------------------------------------------------------------- double precision
+def fft_f64(x: np.ndarray, direction: int = -1) -> np.ndarray:
+    """fft_plan<complex<double>> over the last axis (unnormalized; direction -1 / +1)."""
+    a = np.array(x, dtype=np.complex128, copy=True)
+    n = a.shape[-1]
+    order = n.bit_length() - 1
+    flat = a.reshape(-1, n)
+    for i in range(flat.shape[0]):
+        row = np.ascontiguousarray(flat[i]).view(np.float64)
+        if lib().oracle_fft_c2c_f64(order, direction, row):
+            raise RuntimeError("oracle fft_f64 failed")
+        flat[i] = row.view(np.complex128)
+    return flat.reshape(a.shape)
+
+
+def rfft_f64(x: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(x, dtype=np.float64)
+    n = a.shape[-1]
+    out = np.empty(n // 2 + 1, np.complex128)
+    o = out.view(np.float64)
+    lib().oracle_rfft_f64(n.bit_length() - 1, a, o)
+    return out
+
+
+def irfft_f64(X: np.ndarray, n: int) -> np.ndarray:
+    a = np.ascontiguousarray(X, dtype=np.complex128).view(np.float64)
+    out = np.empty(n, np.float64)
+    lib().oracle_irfft_f64(n.bit_length() - 1, a, out)
+    return out
+
+
+def fft_convolve_f64(signal: np.ndarray, patch: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(signal, dtype=np.float64)
+    b = np.ascontiguousarray(patch, dtype=np.float64)
+    if a.size == 0 or b.size == 0:
+        return np.zeros(0, np.float64)
+    out = np.empty(a.size + b.size - 1, np.float64)
+    if lib().oracle_fft_convolve_f64(a, a.size, b, b.size, out):
+        raise RuntimeError("oracle fft_convolve_f64 failed")
+    return out
+
+
+def direct_convolve_f64(signal: np.ndarray, patch: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(signal, dtype=np.float64)
+    b = np.ascontiguousarray(patch, dtype=np.float64)
+    out = np.empty(a.size + b.size - 1, np.float64)
+    lib().oracle_direct_convolve_f64(a, a.size, b, b.size, out)
     return out

@@ -210,6 +210,57 @@ static void test_upola_v2_pieces_vs_oracle()
     REQUIRE(max_abs_diff(got, ref) / peak <= 1e-5);
 }
 
+static void test_double_precision()
+{
+    // fft_plan<complex<double>> (the reference's complex<double> instantiation) vs the
+    // double restatement; rfft_plan<double>; double one-shot convolutions
+    using cd = std::complex<double>;
+    for (int order : {0, 1, 5, 10, 12, 13, 16}) {
+        std::size_t const n = std::size_t(1) << order;
+        std::vector<cd> x(n);
+        auto const re = rnoise(300 + order, n), im = rnoise(400 + order, n);
+        for (std::size_t i = 0; i < n; ++i) x[i] = cd(re[i], im[i]);
+        auto ref = x;
+        oracle_fft_c2c_f64(order, -1, reinterpret_cast<double*>(ref.data()));
+        auto got = x;
+        neo::fft::fft_plan<cd> plan{neo::fft::from_order, std::size_t(order)};
+        neo::fft::fft(plan, neo::hip::make_view(got.data(), n));
+        double peak = 0;
+        for (auto v : ref) peak = std::max(peak, std::abs(v));
+        REQUIRE(max_abs_diff(got, ref) / peak <= 1e-12);
+        neo::fft::ifft(plan, neo::hip::make_view(got.data(), n));
+        for (auto& v : got) v /= double(n);
+        REQUIRE(max_abs_diff(got, x) <= 1e-12);
+    }
+    {
+        std::size_t const n = 1024;
+        std::vector<double> r(n);
+        auto const f = rnoise(500, n);
+        for (std::size_t i = 0; i < n; ++i) r[i] = f[i];
+        std::vector<cd> X(n / 2 + 1), ref(n / 2 + 1);
+        oracle_rfft_f64(10, r.data(), reinterpret_cast<double*>(ref.data()));
+        neo::fft::rfft_plan<double> rp{neo::fft::from_order, 10};
+        neo::fft::rfft(rp, neo::hip::make_view(r.data(), n), neo::hip::make_view(X.data(), n / 2 + 1));
+        REQUIRE(max_abs_diff(X, ref) <= 1e-11);
+        std::vector<double> back(n);
+        neo::fft::irfft(rp, neo::hip::make_view(X.data(), n / 2 + 1), neo::hip::make_view(back.data(), n));
+        for (auto& v : back) v /= double(n);
+        REQUIRE(max_abs_diff(back, r) <= 1e-13);
+    }
+    {
+        std::vector<double> a(1000), b(333);
+        auto const fa = rnoise(601, 1000), fb = rnoise(602, 333);
+        std::copy(fa.begin(), fa.end(), a.begin());
+        std::copy(fb.begin(), fb.end(), b.begin());
+        auto const d = neo::convolution::direct_convolve(a.data(), a.size(), b.data(), b.size());
+        auto const f = neo::convolution::fft_convolve(a.data(), a.size(), b.data(), b.size());
+        std::vector<double> ref(1332);
+        oracle_direct_convolve_f64(a.data(), a.size(), b.data(), b.size(), ref.data());
+        REQUIRE(d == ref);  // same loop order, double rounding, no FMA: bit-identical
+        REQUIRE(max_abs_diff(f, ref) <= 1e-12);
+    }
+}
+
 static void test_one_shot_convolve()
 {
     auto const x = rnoise(55, 1000), p = rnoise(56, 333);
@@ -260,6 +311,7 @@ int main()
     test_uniform_partition_shapes();
     test_one_shot_convolve();
     test_upola_v2_pieces_vs_oracle();
+    test_double_precision();
     std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);
     return failures ? 1 : 0;
 }

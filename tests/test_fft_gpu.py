@@ -158,3 +158,57 @@ def test_c2_full_shape_properties(neo_gpu, oracle):
     y2 = neo_gpu.fft.fft(xc * 2 + xc.conj())
     lin = y * 2 + neo_gpu.fft.fft(xc.conj())
     assert (torch.max(torch.abs(y2 - lin)) / torch.max(torch.abs(lin))).item() < 1e-5
+
+
+# ------------------------------------------------------------------ double precision
+TOL64 = 1e-12  # complex<double> / double plans: peak-normalized vs the double restatement
+
+
+@pytest.mark.parametrize("order", list(range(0, 15)) + [15, 17, 20])
+@pytest.mark.parametrize("direction", [-1, 1])
+def test_c2c_f64_vs_oracle(neo_gpu, oracle, order, direction):
+    """fft_plan<complex<double>> (the reference's double instantiation; Python complex128)."""
+    rng = np.random.default_rng(700 + order)
+    x = (rng.random((2, 1 << order)) * 2 - 1) + 1j * (rng.random((2, 1 << order)) * 2 - 1)
+    ref = oracle.fft_f64(x, direction)
+    y = neo_gpu.fft.fft(x) if direction < 0 else neo_gpu.fft.ifft(x, norm="forward")
+    assert y.dtype == np.complex128
+    assert peak_err(y, ref) <= TOL64
+
+
+def test_python_api_contract_complex128(neo_gpu):
+    """extra/python/test/test.py:10-18 with complex=np.complex128, and the pybind11 overload
+    rule: complex64 / complex128 keep their precision, other dtypes convert to complex64."""
+    for n in [4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096]:
+        z = neo_gpu.fft.fft(np.zeros(n, np.complex128))
+        assert z.shape == (n,) and z.dtype == np.complex128
+        imp = np.zeros(n, np.complex128)
+        imp[0] = 1
+        assert np.allclose(neo_gpu.fft.ifft(neo_gpu.fft.fft(imp.copy())), imp)
+    assert neo_gpu.fft.fft(np.zeros(8)).dtype == np.complex64        # float64 real: converted
+    assert neo_gpu.fft.fft(np.zeros(8, np.complex64)).dtype == np.complex64
+    x = np.arange(8).astype(np.complex128)
+    np.testing.assert_allclose(neo_gpu.fft.fft(x, norm="ortho"), np.fft.fft(x, norm="ortho"), atol=1e-13)
+
+
+@pytest.mark.parametrize("order", list(range(0, 15)) + [15, 17])
+def test_rfft_irfft_f64_vs_oracle(neo_gpu, oracle, order):
+    n = 1 << order
+    x = np.random.default_rng(800 + order).random(n) * 2 - 1
+    X = neo_gpu.fft.rfft(x)
+    assert X.dtype == np.complex128
+    assert peak_err(X, oracle.rfft_f64(x)) <= TOL64
+    back = neo_gpu.fft.irfft(X, n, norm="forward")  # unnormalized, like the plan
+    assert back.dtype == np.float64
+    assert peak_err(back, oracle.irfft_f64(X, n)) <= TOL64
+
+
+def test_c2c_f64_device_tensor(neo_gpu, oracle):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(900)
+    x = rng.random((4, 4096)) + 1j * rng.random((4, 4096))
+    t = torch.from_numpy(x).cuda()
+    y = neo_gpu.fft.fft(t)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.complex128
+    assert peak_err(y.cpu().numpy(), oracle.fft_f64(x, -1)) <= TOL64

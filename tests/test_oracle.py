@@ -325,3 +325,28 @@ def test_upola_v2_sub_block_pieces(oracle):
     got = np.concatenate([conv(p) for p in pieces])
     ref = np.concatenate(_upola2_f64(H, pieces))
     assert peak_err(got, ref) < 1e-5
+
+
+
+# ------------------------------------------------------------------ double precision
+@pytest.mark.parametrize("order", range(0, 15))
+def test_fft_f64_matches_numpy(oracle, order):
+    """The double restatement (c2c_dit2_plan<complex<double>>) against numpy's float64 FFT."""
+    rng = np.random.default_rng(order)
+    x = rng.random(1 << order) + 1j * rng.random(1 << order)
+    assert peak_err(oracle.fft_f64(x, -1), np.fft.fft(x)) < 1e-13
+    assert peak_err(oracle.fft_f64(x, +1), (1 << order) * np.fft.ifft(x)) < 1e-13
+    if order:
+        r = rng.random(1 << order)
+        X = oracle.rfft_f64(r)
+        assert peak_err(X, np.fft.rfft(r)) < 1e-13
+        assert peak_err(oracle.irfft_f64(X, 1 << order) / (1 << order), r) < 1e-13
+
+
+@pytest.mark.parametrize("n,m", [(2, 2), (3, 9), (10, 4), (555, 10), (1000, 333)])
+def test_convolve_f64_matches_numpy(oracle, n, m):
+    rng = np.random.default_rng(n + 17 * m)
+    x, p = rng.random(n), rng.random(m)
+    truth = np.convolve(x, p)
+    assert peak_err(oracle.direct_convolve_f64(x, p), truth) < 1e-13
+    assert peak_err(oracle.fft_convolve_f64(x, p), truth) < 1e-13
