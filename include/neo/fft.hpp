@@ -22,6 +22,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace neo::fft {
@@ -237,6 +238,30 @@ constexpr auto irfft(Plan& plan, InVec input, OutVec output)
 {
     return plan(input, output);
 }
+
+} // namespace neo::fft
+
+namespace neo {
+/// rfftfreq.hpp:12-30 (host index arithmetic): bin i of a size-n transform
+template<std::floating_point T>
+[[nodiscard]] constexpr auto rfftfreq(std::integral auto size, std::integral auto index, double inv_sample_rate) -> T
+{
+    auto const fs = T(1) / static_cast<T>(inv_sample_rate);
+    auto const inv_size = T(1) / static_cast<T>(size);
+    return static_cast<T>(index) * fs * inv_size;
+}
+
+template<typename Vec>
+constexpr auto rfftfreq(Vec vec, double inv_sample_rate) noexcept -> void
+{
+    auto const size = static_cast<int>(vec.extent(0));
+    for (int i = 0; i < size; ++i)
+        neo::hip::detail::at(vec, i) =
+            rfftfreq<std::remove_cvref_t<decltype(neo::hip::detail::at(vec, i))>>(size, i, inv_sample_rate);
+}
+}  // namespace neo
+
+namespace neo::fft {
 
 /// rfft.hpp:41-62: split the c2c spectrum of a + ib into rfft(a), rfft(b) (host utility)
 template<typename InVec, typename OutVecX, typename OutVecY>

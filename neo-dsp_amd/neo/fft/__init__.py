@@ -20,7 +20,7 @@ import numpy as np
 from .. import _native
 from ._plan import FFTPlan, get_plan
 
-__all__ = ["fft", "ifft", "rfft", "irfft", "FFTPlan", "get_plan", "next_order", "size", "max_order"]
+__all__ = ["fft", "ifft", "rfft", "irfft", "rfftfreq", "FFTPlan", "get_plan", "next_order", "size", "max_order"]
 
 _NORMS = ("backward", "ortho", "forward")
 
@@ -158,3 +158,13 @@ def irfft(x, n=None, norm="backward"):
     if s != 1.0:
         out *= (np.float64 if f64 else np.float32)(s)
     return out
+
+
+def rfftfreq(n: int, d: float = 1.0) -> np.ndarray:
+    """Bin frequencies, the reference's definition (src/neo/fft/rfftfreq.hpp:12-30,
+    main.cpp:211-222): n values i * (1/d) * (1/n), i < n. Index arithmetic on the host,
+    not a transform (nothing here runs on the GPU)."""
+    n = int(n)
+    fs = 1.0 / float(d)
+    inv = 1.0 / float(n) if n else 0.0
+    return np.arange(n, dtype=np.float64) * fs * inv

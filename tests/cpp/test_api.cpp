@@ -296,9 +296,19 @@ static void test_uniform_partition_shapes()
     }
 }
 
+static void test_rfftfreq()
+{
+    // extra/python/test/test.py:65-68 through the C++ header (host arithmetic)
+    std::vector<double> f(2);
+    neo::rfftfreq(neo::hip::make_view(f.data(), 2), 1.0 / 20.0);
+    REQUIRE(f[0] == 0.0 && std::abs(f[1] - 10.0) < 1e-12);
+    REQUIRE(std::abs(neo::rfftfreq<double>(2, 1, 1.0 / 44100.0) - 22050.0) < 1e-9);
+}
+
 int main()
 {
     test_fdl_index();
+    test_rfftfreq();
     int n = 0;
     if (neo_hip_device_count(&n) != NEO_HIP_OK || n < 1) {
         std::printf("no GPU: only host-side checks ran\n");

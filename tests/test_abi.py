@@ -81,3 +81,12 @@ def test_no_cpu_fallback_without_gpu():
         neo.fft.fft(np.zeros(8, np.complex64))
     with pytest.raises(RuntimeError):
         neo.UpolsConvolver(1, 128, 2)
+
+
+def test_rfftfreq_reference_values():
+    """extra/python/test/test.py:65-68 (host index arithmetic, no GPU)."""
+    import neo
+
+    assert neo.fft.rfftfreq(2) == pytest.approx([0.0, 0.5])
+    assert neo.fft.rfftfreq(2, 1.0 / 20.0) == pytest.approx([0.0, 10.0])
+    assert neo.fft.rfftfreq(2, 1.0 / 44100.0) == pytest.approx([0.0, 22050.0])
