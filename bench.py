@@ -151,6 +151,27 @@ def cpu_baseline_fft(threads):
                       f"{dt:.2f} s; scales linearly with batch"}
 
 
+def copy_ceiling_gbs(dev) -> float:
+    """Practical HBM ceiling measured in the same run: a 1 GiB device-to-device copy
+    (torch copy_ -> hipMemcpy D2D), read + write bytes over the best of 5."""
+    import torch
+
+    n = 1 << 28
+    a = torch.empty(n, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    best = None
+    for _ in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    return 2 * 4 * n / (best * 1e-3) / 1e9
+
+
 def device_for(local: int) -> int:
     """One process per GPU: LOCAL_RANK -> device (modulo the visible devices, so a
     multi-rank rehearsal on a smaller box shares GPUs)."""
@@ -234,7 +255,7 @@ def run_upols(args, world, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": load_pmc_traffic(args.workload),
                      "kernel": f"k_upols_step<{B}>", "kernel_avg_ms": mac_avg_ms,
-                     "algorithmic_bytes_per_launch": bytes_mac},
+                     "algorithmic_bytes_per_launch": bytes_mac, "d2d_copy_gbs": copy_ceiling_gbs(dev)},
         "effective_hbm_gbs_step": bytes_mac * world / (elapsed / args.steps) / 1e9 / world,
         "offline": offline,
     }
@@ -363,7 +384,8 @@ def run_fft(args, world, rank, local):
                    "parallelism": f"batch-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": load_pmc_traffic("c2"),
-                     "kernel": "k_c2c_lds<4096,-1>", "kernel_avg_ms": kms, "algorithmic_bytes_per_launch": bytes_launch},
+                     "kernel": "k_c2c_lds<4096,-1>", "kernel_avg_ms": kms, "algorithmic_bytes_per_launch": bytes_launch,
+                     "d2d_copy_gbs": copy_ceiling_gbs(dev)},
     }
 
 
@@ -387,6 +409,7 @@ def main():
 
                 model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")]
                 res["cpu_baseline"]["host_cpu"] = (model[0] if model else platform.processor())
+                res["cpu_baseline"]["host_cpus_visible"] = os.cpu_count()
             except OSError:
                 pass
         print(json.dumps(res), flush=True)
