@@ -495,8 +495,10 @@ __global__ __launch_bounds__(256) void k_upola2_piece(
 template<int B, int NB>
 struct batch_cfg {
     static constexpr int Q = B / NB;               // vectors (NB bins each) per row
-    static constexpr int L = Q < 512 ? Q : 512;    // lanes per MAC workgroup
-    static constexpr int VPT = Q / L;              // vectors per lane
+    static constexpr int L = Q < 256 ? Q : 256;    // lanes per MAC workgroup
+    static constexpr int VPT = 1;                  // vectors per lane
+    static constexpr int G = Q / L;                // workgroups per row (bin chunks): several
+                                                   // small workgroups per CU run out of phase
 };
 template<int NB>
 using bvec = std::conditional_t<NB == 2, f4v, f2v>;  // NB interleaved complex bins
@@ -585,8 +587,11 @@ __device__ __forceinline__ void batch_chunk(acc3 (&a)[T][NB * VPT], bvec<NB> (&f
 // MAC pass for T blocks (grid C x S, batch_cfg<B, NB>::L lanes, NB bins per lane-vector):
 // workgroup (c, s) walks partitions [p0, p1) and writes T partial spectra to
 // part[c][s][j][B].
-template<int B, int T, int NB, int D = (T < 4 ? T : 4)>  // D divides T: prefetch slots line up across chunks
-__global__ __launch_bounds__((batch_cfg<B, NB>::L)) void k_batch_mac(const cf* __restrict__ H,
+#ifndef NEO_BATCH_D
+#define NEO_BATCH_D 4
+#endif
+template<int B, int T, int NB, int D = (T < NEO_BATCH_D ? T : NEO_BATCH_D)>  // D divides T: slots line up across chunks
+__global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf* __restrict__ H,
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
                                                                    int64_t cstride, int64_t pstride)
@@ -594,8 +599,10 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L)) void k_batch_mac(const cf* _
     using K = batch_cfg<B, NB>;
     using V = bvec<NB>;
     constexpr int VPT = K::VPT, L = K::L;
-    const int tid = threadIdx.x;
-    const int c = blockIdx.x / S, s = blockIdx.x - c * S;
+    constexpr int G = K::G;
+    const int cs = blockIdx.x / G, gch = blockIdx.x - cs * G;
+    const int tid = gch * L + threadIdx.x;  // vector index within the row (bin chunk gch)
+    const int c = cs / S, s = cs - c * S;
     const int p0 = s * rows, p1 = min(P, p0 + rows);
     const int64_t psv = pstride / NB;  // row stride in vectors
     const V* Hv = reinterpret_cast<const V*>(H + int64_t(c) * cstride);
@@ -1072,7 +1079,8 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
 // capped so one lane's accumulators (T * NB * VPT * 4 floats) stay <= 128 registers
 constexpr int batch_t(int B, int NB, int want)
 {
-    const int Q = B / NB, L = Q < 512 ? Q : 512, VPT = Q / L;
+    (void)B;
+    const int VPT = 1;
     int t = want;
     while (t > 2 && t * NB * VPT > 32) t /= 2;
     return t;
@@ -1085,7 +1093,7 @@ template<int BB, int NB>
 int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
 {
     constexpr int L = batch_cfg<BB, NB>::L;
-    const unsigned grid = unsigned(h->C) * unsigned(h->Sb);
+    const unsigned grid = unsigned(h->C) * unsigned(h->Sb) * unsigned(batch_cfg<BB, NB>::G);
 #define NEO_BATCH_T(TT)                                                                                          \
     case TT:                                                                                                     \
         if constexpr (batch_t(BB, NB, TT) == TT) {                                                               \

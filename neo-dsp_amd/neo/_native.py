@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libneo_hip.so"))
+LIB_PATH = os.path.normpath(os.environ.get("NEO_HIP_LIBRARY") or os.path.join(_HERE, "..", "lib", "libneo_hip.so"))
 
 NEO_HIP_OK = 0
 NEO_HIP_EINVAL = 1
