@@ -212,3 +212,39 @@ def test_c2c_f64_device_tensor(neo_gpu, oracle):
     torch.cuda.synchronize()
     assert y.dtype == torch.complex128
     assert peak_err(y.cpu().numpy(), oracle.fft_f64(x, -1)) <= TOL64
+
+
+def test_max_order_round_trips(neo_gpu):
+    """The largest plan the reference allows (order 27 = max_order(), c2c_dit2_plan.hpp:58-61):
+    size-independent properties at full size — forward then backward gives N·x (c2c and
+    real), Parseval, and an impulse transforms to all ones."""
+    torch = pytest.importorskip("torch")
+    order, n = 27, 1 << 27
+    g = torch.Generator(device="cuda").manual_seed(27)
+    x = torch.complex(torch.rand(n, generator=g, device="cuda") * 2 - 1,
+                      torch.rand(n, generator=g, device="cuda") * 2 - 1)
+    plan = neo_gpu.fft.FFTPlan(0, order, 1)
+    X = torch.empty_like(x)
+    plan.execute_device(x.data_ptr(), X.data_ptr(), -1, torch.cuda.current_stream().cuda_stream)
+    y = torch.empty_like(x)
+    plan.execute_device(X.data_ptr(), y.data_ptr(), +1, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    err = ((y / n - x).abs().max() / x.abs().max()).item()
+    assert err <= 1e-5, err
+    ex = (x.abs() ** 2).double().sum().item()
+    eX = (X.abs() ** 2).double().sum().item() / n
+    assert abs(eX - ex) / ex <= 1e-5  # Parseval
+    d = torch.zeros_like(x)
+    d[0] = 1
+    plan.execute_device(d.data_ptr(), X.data_ptr(), -1, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert (X - 1).abs().max().item() <= 1e-6
+    del x, X, y, d
+    # real: r2c + c2r of 2^27 reals
+    r = torch.rand(n, generator=g, device="cuda") * 2 - 1
+    R = torch.empty(n // 2 + 1, dtype=torch.complex64, device="cuda")
+    back = torch.empty_like(r)
+    neo_gpu.fft.FFTPlan(1, order, 1).execute_device(r.data_ptr(), R.data_ptr(), -1, 0)
+    neo_gpu.fft.FFTPlan(2, order, 1).execute_device(R.data_ptr(), back.data_ptr(), +1, 0)
+    torch.cuda.synchronize()
+    assert ((back / n - r).abs().max() / r.abs().max()).item() <= 1e-5
