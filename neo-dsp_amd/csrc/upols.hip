@@ -24,144 +24,21 @@
 //                    new blocks be inserted before any of them is consumed)
 //   prev [C][B]      previous input block (first half of the overlap-save window)
 //   part [C][S][B]   per-split partial spectra; arrivals [C] split counters
-#include "common.hpp"
-#include "fft_device_real.hpp"
+//
+// This file: the single-block step (MAC + finish, or one launch with the last-arriver
+// tail), the upola_convolver_v2 piece kernel, the handle and the neo_hip_upols_* C-ABI.
+// upols_batch.hip: T blocks per pass (process_blocks). upols_setup.hip: partitioning
+// and normalization. upols_device.hpp / upols_handle.hpp: what they share.
+#include "upols_device.hpp"
+#include "upols_handle.hpp"
 
 #include <algorithm>
 #include <cstdlib>
-#include <type_traits>
+#include <string>
 #include <utility>
 #include <vector>
 
-// elements per lane of the per-channel tail transforms (c2r of k_upols_finish /
-// k_batch_finish): 4 per lane puts B/4 lanes to work (C5 finish 6.3 -> 4.9 us, batch 61 -> 29 us)
-#ifndef NEO_FINISH_E
-#define NEO_FINISH_E(B) ((B) / 4 <= 256 ? ((B) >= 4 ? 4 : (B)) : (B) / 256)
-#endif
-#define NEO_BATCH_FINISH_E(B) NEO_FINISH_E(B)
-
 namespace neo_hip {
-
-__host__ __device__ constexpr int upols_e(int b) { return b >= 16 ? 16 : b; }
-
-template<int B>
-struct upols_cfg {
-    static constexpr int E = upols_e(B);                 // FFT elements per lane
-    static constexpr int T = B / E;                      // FFT lanes
-    static constexpr int Q = B / 2;                      // float4 (2 bins) per row
-    static constexpr int QT = Q < 256 ? Q : 256;         // lanes per row group
-    static constexpr int RPI = 256 / QT;                 // rows in flight per iteration
-    static constexpr int VPT = Q / QT;                   // float4 per lane per row
-    static constexpr int U = VPT >= 4 ? 1 : 4 / VPT;     // row unroll
-    static constexpr int TW1 = twiddle_len<B>();
-    static constexpr int TW2 = twiddle_len<2 * B>();
-    static constexpr int LL = lds_len(B);
-};
-
-struct acc4 {  // 4 partial products per bin keep the packed bin 0 exact
-    float rr, ii, ri, ir;
-};
-
-__device__ __forceinline__ void mac2(acc4& a0, acc4& a1, float4 h, float4 x)
-{
-    a0.rr = fmaf(h.x, x.x, a0.rr);
-    a0.ii = fmaf(h.y, x.y, a0.ii);
-    a0.ri = fmaf(h.x, x.y, a0.ri);
-    a0.ir = fmaf(h.y, x.x, a0.ir);
-    a1.rr = fmaf(h.z, x.z, a1.rr);
-    a1.ii = fmaf(h.w, x.w, a1.ii);
-    a1.ri = fmaf(h.z, x.w, a1.ri);
-    a1.ir = fmaf(h.w, x.z, a1.ir);
-}
-
-// acc4 -> packed complex bin: bin 0 = {DC, Nyquist} (products of real values),
-// other bins = the complex product sum.
-__device__ __forceinline__ cf finish(const acc4& a, bool bin0)
-{
-    return bin0 ? cf{a.rr, a.ii} : cf{a.rr - a.ii, a.ri + a.ir};
-}
-
-// Load the overlap-save window [prev | in] of channel c as the packed complex
-// sequence z[n] = w[2n] + i w[2n+1] (lane t owns n = t + m*T), forward FFT, and
-// leave the natural-order spectrum Z in `fft` (lpad'ed).
-// E = 8 elements per lane keeps this fused r2c from raising the kernel's register
-// count (the MAC loop itself needs ~60 VGPRs; occupancy is what streams HBM).
-// OLS window = [previous block | new block] (overlap_save.hpp:90-95);
-// OLA window = [new block | zeros]          (overlap_add.hpp:84-86).
-template<int B, bool OLA, int E = (B / 8 <= 256 ? 8 : B / 256)>
-__device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, const cf* tw1, int tid)
-{
-    constexpr int T = B / E;
-    static_assert(T <= 256 && B % E == 0, "window FFT must fit one 256-lane workgroup");
-    const bool active = tid < T;
-    cf v[E];
-    if (active) {
-        const cf* pz = reinterpret_cast<const cf*>(prev_c);
-        const cf* iz = reinterpret_cast<const cf*>(in_c);
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int n = tid + m * T;
-            if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
-            else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
-        }
-    }
-    __syncthreads();  // twiddles staged by the caller
-    stockham<B, E, -1>(v, fft, tw1, tid, active);
-    if (active) {
-#pragma unroll
-        for (int m = 0; m < E; ++m) fft[lpad(tid + m * T)] = v[m];
-    }
-    __syncthreads();
-}
-
-// c2r of the packed spectrum X (LDS), scaled by 1/2B (fallback_rfft_plan.hpp:38-55):
-//   OLS: out = window samples [B, 2B)                       (overlap_save.hpp:104-111)
-//   OLA: out = samples [0, B) + overlap; overlap = [B, 2B)  (overlap_add.hpp:92-106)
-// E = 4 keeps the fused kernel inside its 64-VGPR budget (T = B/E <= 256 lanes).
-template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256)>
-__device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, float* ovl_c, int tid)
-{
-    using K = upols_cfg<B>;
-    constexpr int T = B / E;
-    static_assert(T <= 256 && B % E == 0, "c2r must fit one 256-lane workgroup");
-    const bool active = tid < T;
-    cf v[E];
-    if (active) {
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int k = tid + m * T;
-            const cf x0 = X[0];
-            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
-                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
-        }
-    }
-    stockham<B, E, +1>(v, fft, tw, tid, active);
-    if (active) {
-        const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108 / overlap_add.hpp:98
-        cf* o = reinterpret_cast<cf*>(out_c);
-        if constexpr (OLA) {
-            cf* ov = reinterpret_cast<cf*>(ovl_c);
-            // the same lane reads overlap[n] (m < E/2) before writing it (m >= E/2: n - B/2)
-#pragma unroll
-            for (int m = 0; m < E / 2; ++m) {
-                const int n = tid + m * T;
-                const cf old = ov[n];
-                o[n] = {v[m].x * scale + old.x, v[m].y * scale + old.y};
-            }
-#pragma unroll
-            for (int m = E / 2; m < E; ++m) {
-                const int n = tid + m * T;
-                ov[n - B / 2] = {v[m].x * scale, v[m].y * scale};
-            }
-        } else {
-#pragma unroll
-            for (int m = E / 2; m < E; ++m) {  // window samples [B, 2B): z[n], n >= B/2
-                const int n = tid + m * T;
-                o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
-            }
-        }
-    }
-}
 
 // One whole block step for every channel (grid C x S, 256 lanes). Workgroup (c, s)
 // accumulates partitions [p0, p1) into a partial spectrum; split 0 first runs the
@@ -483,482 +360,12 @@ __global__ __launch_bounds__(256) void k_upola2_piece(
     }
 }
 
-// ---------------------------------------------------------------------------
-// Batched blocks (process_blocks): T consecutive blocks per pass over H and the FDL.
-// ---------------------------------------------------------------------------
-// Block j of a batch (write position w) is inserted as FDL row (w + j) mod R and uses
-// rows (w + j - p) mod R, so partition p of all T blocks reads one H row and T rows of
-// the FDL of which T - 1 were already read for p - 1: a workgroup that walks p in order
-// keeps a sliding window of T FDL rows in registers and streams one H row and one new
-// FDL row per partition. HBM bytes per pass stay ~16·P·B per channel (the single-block
-// figure) while the pass produces T blocks: T× the work per byte.
-template<int B, int NB>
-struct batch_cfg {
-    static constexpr int Q = B / NB;               // vectors (NB bins each) per row
-    static constexpr int L = Q < 256 ? Q : 256;    // lanes per MAC workgroup
-    static constexpr int VPT = 1;                  // vectors per lane
-    static constexpr int G = Q / L;                // workgroups per row (bin chunks): several
-                                                   // small workgroups per CU run out of phase
-};
-template<int NB>
-using bvec = std::conditional_t<NB == 2, f4v, f2v>;  // NB interleaved complex bins
-
-// Window r2c of block j (grid C x T): [x_{j-1} | x_j] (OLS, x_{-1} = prev) or [x_j | 0]
-// (OLA), inserted as FDL row (w + j) mod R.
-template<int B, bool OLA>
-__global__ __launch_bounds__(256) void k_batch_window(const float* __restrict__ in, int64_t ld_in,
-                                                      const float* __restrict__ prev, cf* __restrict__ fdl,
-                                                      const cf* __restrict__ twg, int T, int ring, int w,
-                                                      int64_t cstride, int64_t pstride)
-{
-    using K = upols_cfg<B>;
-    __shared__ cf fft[K::LL];
-    __shared__ cf tw[K::TW1 + K::TW2];
-    const int tid = threadIdx.x, c = blockIdx.x / T, j = blockIdx.x - c * T;
-    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
-    const float* in_c = in + int64_t(c) * ld_in + int64_t(j) * B;
-    const float* prev_c = j == 0 ? prev + int64_t(c) * B : in_c - B;
-    window_fft<B, OLA>(prev_c, in_c, fft, tw, tid);
-    const int r = w + j < ring ? w + j : w + j - ring;
-    cf* row = fdl + int64_t(c) * cstride + int64_t(r) * pstride;
-    for (int k = tid; k < B; k += 256) row[k] = r2c_split<B>(fft, tw + K::TW1, k);
-}
-
-// Per bin two packed pairs d = (sum hr*xr, sum hi*xi) and x = (sum hr*xi, sum hi*xr): each
-// is one v_pk_fma_f32 per partition (x with the operand halves swapped), and the packed
-// bin 0 stays exact: bin 0 -> d (DC, Nyquist), other bins -> {d.x - d.y, x.x + x.y}.
-struct acc3 {
-    f2v d, x;
-};
-
-// Step U of a T-step chunk (p = pb + U; U is a template argument so every slot index
-// is static and the arrays stay in registers): take H row p and FDL row (w - p) from
-// prefetch slot U mod D (loaded D steps earlier) into window slot (T - U) mod T, issue
-// the loads for p + D, then MAC all T blocks; block j reads window slot (j - U) mod T.
-// D bounds the loads in flight per lane (and so the registers they hold).
-template<int T, int NB, int VPT, int L, int D, int U>
-__device__ __forceinline__ void batch_step(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)[T][VPT], bvec<NB> (&ph)[D][VPT],
-                                           bvec<NB> (&pf)[D][VPT], const bvec<NB>* Hv, const bvec<NB>* Fv,
-                                           int64_t psv, int tid, int ring, int w, int p, int p1)
-{
-    constexpr int slot = U % D;
-    bvec<NB> hv[VPT];
-    const bool valid = p < p1;  // the last chunk of a split may run past p1: zero filter row
-#pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        f[(T - U) % T][v] = pf[slot][v];
-        hv[v] = valid ? ph[slot][v] : bvec<NB>(0.0f);
-    }
-    const int pn = p + D < p1 ? p + D : p1 - 1;  // past the end: a harmless re-read, no branch
-    {
-        int r = w - pn;
-        r = r < 0 ? r + ring : r;
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            pf[slot][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
-            ph[slot][v] = __builtin_nontemporal_load(Hv + int64_t(pn) * psv + tid + v * L);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < T; ++j)
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            const bvec<NB> x = f[(j - U + T) % T][v], h = hv[v];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                acc3& A = a[j][v * NB + b];
-                const f2v hb = {h[2 * b], h[2 * b + 1]}, xb = {x[2 * b], x[2 * b + 1]};
-                A.d = __builtin_elementwise_fma(hb, xb, A.d);
-                A.x = __builtin_elementwise_fma(hb, xb.yx, A.x);
-            }
-        }
-    __builtin_amdgcn_sched_barrier(0);  // keep each step's loads D steps ahead, not all hoisted
-}
-
-template<int T, int NB, int VPT, int L, int D, int... U>
-__device__ __forceinline__ void batch_chunk(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)[T][VPT], bvec<NB> (&ph)[D][VPT],
-                                            bvec<NB> (&pf)[D][VPT], const bvec<NB>* Hv, const bvec<NB>* Fv,
-                                            int64_t psv, int tid, int ring, int w, int pb, int p1,
-                                            std::integer_sequence<int, U...>)
-{
-    (batch_step<T, NB, VPT, L, D, U>(a, f, ph, pf, Hv, Fv, psv, tid, ring, w, pb + U, p1), ...);
-}
-
-// MAC pass for T blocks (grid C x S, batch_cfg<B, NB>::L lanes, NB bins per lane-vector):
-// workgroup (c, s) walks partitions [p0, p1) and writes T partial spectra to
-// part[c][s][j][B].
-#ifndef NEO_BATCH_D
-#define NEO_BATCH_D 4
-#endif
-template<int B, int T, int NB, int D = (T < NEO_BATCH_D ? T : NEO_BATCH_D)>  // D divides T: slots line up across chunks
-__global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf* __restrict__ H,
-                                                                   const cf* __restrict__ fdl, cf* __restrict__ part,
-                                                                   int P, int ring, int S, int rows, int w,
-                                                                   int64_t cstride, int64_t pstride)
-{
-    using K = batch_cfg<B, NB>;
-    using V = bvec<NB>;
-    constexpr int VPT = K::VPT, L = K::L;
-    constexpr int G = K::G;
-    const int cs = blockIdx.x / G, gch = blockIdx.x - cs * G;
-    const int tid = gch * L + threadIdx.x;  // vector index within the row (bin chunk gch)
-    const int c = cs / S, s = cs - c * S;
-    const int p0 = s * rows, p1 = min(P, p0 + rows);
-    const int64_t psv = pstride / NB;  // row stride in vectors
-    const V* Hv = reinterpret_cast<const V*>(H + int64_t(c) * cstride);
-    const V* Fv = reinterpret_cast<const V*>(fdl + int64_t(c) * cstride);
-
-    acc3 a[T][NB * VPT];
-#pragma unroll
-    for (int j = 0; j < T; ++j)
-#pragma unroll
-        for (int v = 0; v < NB * VPT; ++v) a[j][v] = {f2v(0.0f), f2v(0.0f)};
-    V f[T][VPT];
-#pragma unroll
-    for (int sl = 1; sl < T; ++sl) {  // rows block sl needs at p0
-        int r = w + sl - p0;
-        r = r < 0 ? r + ring : (r >= ring ? r - ring : r);
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) f[sl][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
-    }
-    V ph[D][VPT], pf[D][VPT];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {  // prefetch partitions p0 .. p0 + D - 1
-        const int p = p0 + d < p1 ? p0 + d : p0;
-        int r = w - p;
-        r = r < 0 ? r + ring : r;
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            pf[d][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
-            ph[d][v] = __builtin_nontemporal_load(Hv + int64_t(p) * psv + tid + v * L);
-        }
-    }
-    for (int pb = p0; pb < p1; pb += T)
-        batch_chunk<T, NB, VPT, L, D>(a, f, ph, pf, Hv, Fv, psv, tid, ring, w, pb, p1,
-                                      std::make_integer_sequence<int, T>{});
-
-    cf* slab = part + (int64_t(c) * S + s) * T * B;
-#pragma unroll
-    for (int j = 0; j < T; ++j)
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            V o;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const acc3& A = a[j][v * NB + b];
-                const bool bin0 = tid + v * L == 0 && b == 0;
-                o[2 * b] = bin0 ? A.d.x : A.d.x - A.d.y;
-                o[2 * b + 1] = bin0 ? A.d.y : A.x.x + A.x.y;
-            }
-            *reinterpret_cast<V*>(slab + int64_t(j) * B + (tid + v * L) * NB) = o;
-        }
-}
-
-// Sum the S slabs of block j in order, c2r, 1/2B (grid C x T, 256 lanes).
-//   OLS: out_j = window samples [B, 2B); workgroup j = T-1 first saves x_{T-1} as the
-//        next batch's previous block (before out_j, which may alias it, is written).
-//   OLA: out_j = samples [0, B) (overlap added by k_batch_ola), tail_j = [B, 2B).
-template<int B, bool OLA>
-__global__ __launch_bounds__(256) void k_batch_finish(const cf* __restrict__ part, int S, int T,
-                                                      const float* __restrict__ in, int64_t ld_in,
-                                                      float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
-                                                      float* __restrict__ tail, const cf* __restrict__ twg)
-{
-    using K = upols_cfg<B>;
-    constexpr int E = NEO_BATCH_FINISH_E(B), TT = B / E;  // more lanes in the c2r than the 16-element form
-    __shared__ __attribute__((aligned(16))) cf X[B];
-    __shared__ cf fft[K::LL];
-    __shared__ cf tw[K::TW1 + K::TW2];
-    const int tid = threadIdx.x, c = blockIdx.x / T, j = blockIdx.x - c * T;
-    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
-    if (!OLA && j == T - 1) {
-        const float4* x4 = reinterpret_cast<const float4*>(in + int64_t(c) * ld_in + int64_t(j) * B);
-        float4* p4 = reinterpret_cast<float4*>(prev + int64_t(c) * B);
-        for (int i = tid; i < B / 4; i += 256) p4[i] = x4[i];
-    }
-    const float4* s4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * T * B + int64_t(j) * B);
-    const int64_t sstride = int64_t(T) * K::Q;  // float4 between consecutive slabs of one block
-    for (int q = tid; q < K::Q; q += 256) {
-        float4 sum = s4[q];
-        for (int t = 1; t < S; ++t) {
-            const float4 r = s4[t * sstride + q];
-            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
-        }
-        reinterpret_cast<float4*>(X)[q] = sum;
-    }
-    __syncthreads();
-    const bool active = tid < TT;
-    cf v[E];
-    if (active) {
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int k = tid + m * TT;
-            const cf x0 = X[0];
-            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
-                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
-        }
-    }
-    stockham<B, E, +1>(v, fft, tw, tid, active);
-    if (active) {
-        const float scale = 1.0f / float(2 * B);
-        cf* o = reinterpret_cast<cf*>(out + int64_t(c) * ld_out + int64_t(j) * B);
-        if constexpr (OLA) {
-            cf* tl = reinterpret_cast<cf*>(tail + (int64_t(c) * T + j) * B);
-#pragma unroll
-            for (int m = 0; m < E / 2; ++m) o[tid + m * TT] = {v[m].x * scale, v[m].y * scale};
-#pragma unroll
-            for (int m = E / 2; m < E; ++m) tl[tid + m * TT - B / 2] = {v[m].x * scale, v[m].y * scale};
-        } else {
-#pragma unroll
-            for (int m = E / 2; m < E; ++m) o[tid + m * TT - B / 2] = {v[m].x * scale, v[m].y * scale};
-        }
-    }
-}
-
-// OLA overlap for a batch (grid C): out_j += tail_{j-1} (out_0 += overlap), overlap = tail_{T-1}
-template<int B>
-__global__ __launch_bounds__(256) void k_batch_ola(float* __restrict__ out, int64_t ld_out,
-                                                   const float* __restrict__ tail, float* __restrict__ ovl, int T)
-{
-    const int c = blockIdx.x;
-    float* o = out + int64_t(c) * ld_out;
-    const float* tl = tail + int64_t(c) * T * B;
-    float* ov = ovl + int64_t(c) * B;
-    for (int i = threadIdx.x; i < B; i += 256) {
-        float carry = ov[i];
-        for (int j = 0; j < T; ++j) {
-            o[int64_t(j) * B + i] += carry;
-            carry = tl[int64_t(j) * B + i];
-        }
-        ov[i] = carry;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// setup path
-// ---------------------------------------------------------------------------
-// uniform_partition (uniform_partition.hpp:12-26 -> stft.hpp:56-99): partition p
-// of channel c = rfft_2B(ir[c][pB : pB+B] zero-padded to 2B). Packed output
-// [C][P][B] (UPOLS layout) or unpacked [C][P][B+1] (reference layout).
-template<int B, bool PACKED>
-__global__ __launch_bounds__(256) void k_partition(const float* __restrict__ ir, int64_t L, int P,
-                                                   cf* __restrict__ out, const cf* __restrict__ twg, int64_t cstride,
-                                                   int64_t pstride)
-{
-    using K = upols_cfg<B>;
-    __shared__ cf fft[K::LL];
-    __shared__ cf tw[K::TW1 + K::TW2];
-    const int tid = threadIdx.x;
-    const int64_t cp = blockIdx.x;
-    const int64_t c = cp / P, p = cp - c * P;
-    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
-    const bool active = tid < K::T;
-    const float* seg = ir + c * L + p * B;
-    const int64_t cnt = min(int64_t(B), L - p * B);
-    cf v[K::E];
-    if (active) {
-#pragma unroll
-        for (int m = 0; m < K::E; ++m) {
-            const int n = tid + m * K::T;  // z[n] = (w[2n], w[2n+1]); w = segment | zeros
-            const float a = 2 * n < cnt ? seg[2 * n] : 0.f;
-            const float b = 2 * n + 1 < cnt ? seg[2 * n + 1] : 0.f;
-            v[m] = {a, b};
-        }
-    }
-    __syncthreads();
-    stockham<B, K::E, -1>(v, fft, tw, tid, active);
-    if (active) {
-#pragma unroll
-        for (int m = 0; m < K::E; ++m) fft[lpad(tid + m * K::T)] = v[m];
-    }
-    __syncthreads();
-    if constexpr (PACKED) {
-        cf* row = out + c * cstride + p * pstride;  // device layout (see neo_hip_upols)
-        for (int k = tid; k < B; k += 256) row[k] = r2c_split<B>(fft, tw + K::TW1, k);
-    } else {
-        cf* row = out + cp * (B + 1);
-        for (int k = tid; k < B; k += 256) {
-            const cf x = r2c_split<B>(fft, tw + K::TW1, k);
-            if (k == 0) {
-                row[0] = {x.x, 0.f};
-                row[B] = {x.y, 0.f};
-            } else {
-                row[k] = x;
-            }
-        }
-    }
-}
-
-// filter [C][P][B+1] (reference layout) -> packed [C][P][B]
-__global__ void k_pack_filter(const cf* __restrict__ in, cf* __restrict__ out, int B, int64_t rows, int P,
-                              int64_t cstride, int64_t pstride)
-{
-    const int64_t gid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (gid >= rows * B) return;
-    const int64_t r = gid / B, k = gid - r * B;
-    const int64_t c = r / P, p = r - c * P;
-    const cf* src = in + r * (B + 1);
-    out[c * cstride + p * pstride + k] = k == 0 ? cf{src[0].x, src[B].x} : src[k];
-}
-
-// normalize_energy_factor (normalize_energy.hpp:17-44) with the reference's exact
-// rounding: sequential float sum of x*x (multiply, then add; no FMA), then
-// 1/sqrt.
-// One workgroup per kEnergyGroup channels: all 256 lanes stream a [G][256] tile of the
-// impulse with coalesced loads into LDS (double-buffered), then lane g < G folds row g
-// into its channel's energy in sample order. Zero padding past L adds +0.0f, which
-// leaves the running sum unchanged, so the rounding equals the reference's loop.
-constexpr int kEnergyGroup = 16;
-constexpr int kEnergyTile = 256;
-
-__global__ __launch_bounds__(256) void k_energy_factor(const float* __restrict__ ir, int64_t L, int C,
-                                                       float* __restrict__ factor)
-{
-#pragma clang fp contract(off)  // x*x then +, two roundings, like the reference (no FMA)
-    constexpr int G = kEnergyGroup, T = kEnergyTile, LD = T + 4;  // +4: conflict-free b128 row reads
-    __shared__ float tile[2][G * LD];
-    const int c0 = int(blockIdx.x) * G, t = int(threadIdx.x);
-    const int64_t chunks = (L + T - 1) / T;
-    float r[G];
-    bool valid = true;
-    auto load = [&](int64_t chunk) {
-        const int64_t i = chunk * T + t;
-        valid = i < L;
-        const int64_t ic = valid ? i : L - 1;  // clamped address, no branch around the loads
-#pragma unroll
-        for (int g = 0; g < G; ++g)  // rows past C repeat channel C-1; their sums are discarded
-            r[g] = ir[int64_t(min(c0 + g, C - 1)) * L + ic];
-    };
-    auto store = [&](int buf) {  // the zero select sits here so the loads stay in flight
-#pragma unroll
-        for (int g = 0; g < G; ++g) tile[buf][g * LD + t] = valid ? r[g] : 0.0f;
-    };
-    float e = 0.0f;
-    load(0);
-    store(0);
-    __syncthreads();
-    for (int64_t chunk = 0; chunk < chunks; ++chunk) {
-        const int buf = int(chunk & 1);
-        if (chunk + 1 < chunks) load(chunk + 1);  // in flight while row t is summed
-        if (t < G) {
-            const float* row = &tile[buf][t * LD];
-#pragma unroll 8
-            for (int j = 0; j < T; j += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(row + j);
-                const float s0 = v.x * v.x, s1 = v.y * v.y, s2 = v.z * v.z, s3 = v.w * v.w;
-                e = e + s0;
-                e = e + s1;
-                e = e + s2;
-                e = e + s3;
-            }
-        }
-        if (chunk + 1 < chunks) store(buf ^ 1);
-        __syncthreads();
-    }
-    if (t < G && c0 + t < C) factor[c0 + t] = e == 0.0f ? 1.0f : __fdiv_rn(1.0f, __fsqrt_rn(e));
-}
-
-// normalize_impulse.hpp:21-30: min factor over channels, then scale everything
-__global__ void k_scale_min(float* __restrict__ ir, int64_t n, const float* __restrict__ factor, int C)
-{
-    __shared__ float fmin_s;
-    if (threadIdx.x == 0) {
-        float f = factor[0];
-        for (int c = 1; c < C; ++c) f = fminf(f, factor[c]);
-        fmin_s = f;
-    }
-    __syncthreads();
-    const float f = fmin_s;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-        ir[i] = __fmul_rn(ir[i], f);
-}
-
 }  // namespace neo_hip
 
 using namespace neo_hip;
 
-namespace neo_hip {
-constexpr int kMaxBatch = 32;
-constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch  // most blocks one batched MAC pass consumes (process_blocks)
-}
-
-struct neo_hip_upols {
-    int device = 0, C = 0, B = 0, P = 0, S = 1, rows = 1;
-    int ring = 0;  // FDL ring rows R = P + kMaxBatch - 1
-    hipStream_t stream = nullptr;
-    cf* H = nullptr;
-    cf* fdl = nullptr;
-    cf* part = nullptr;
-    float* prev = nullptr;
-    int* arrivals = nullptr;  // per-channel split arrival counters (zero between steps)
-    int wpos = 0;             // FDL write position (fdl_index.hpp:35-37), host-side
-    cf* tw = nullptr;
-    float* io = nullptr;       // device staging for host-pointer process()
-    float* io_host = nullptr;  // pinned staging
-    bool batch = true;      // process_blocks runs T blocks per MAC pass (neo_hip_upols_set_batch)
-    int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
-    int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
-    cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
-    float* tail = nullptr;  // batched OLA tails [C][T][B]
-    float* samples_dev = nullptr;   // process_samples host staging (device side)
-    float* samples_host = nullptr;  // process_samples host staging (pinned)
-    size_t samples_cap = 0;
-    bool timing = false;
-    bool ola = false;  // upola_convolver (overlap-add stage) instead of upols (overlap-save)
-    bool v2 = false;   // upola_convolver_v2: sub-block input (implies ola)
-    int in_pos = 0;    // v2: samples of the current block already consumed (_input_pos)
-    float* window = nullptr;  // v2: real window [C][2B]
-    cf* tmp = nullptr;        // v2: tail accumulator [C][B] packed (_tmp_accumulator)
-    // one launch per block (last-arriver tail) instead of MAC + finish: on for small filter
-    // + FDL working sets, where the step is launch-bound (C3: 10.6 vs 12.4 us per block),
-    // off for HBM-bound ones (C5: 0.342 vs 0.303 ms); NEO_HIP_FUSED=0/1 overrides
-    bool fused = false;
-    // H / FDL layout: row p of channel c at c * cstride + p * pstride (complex units).
-    // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
-    int64_t cstride = 0, pstride = 0;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool, reused across timing windows
-    size_t events_used = 0;
-    double mac_ms = 0.0;
-    int64_t launches = 0;
-};
 
 namespace {
-
-using upols_t = neo_hip_upols;
-
-bool valid_block(int b) { return b >= 16 && b <= 4096 && (b & (b - 1)) == 0; }
-
-#define NEO_UPOLS_DISPATCH(B_, BODY) \
-    switch (B_) {                    \
-        case 16: { constexpr int BB = 16; BODY; break; }     \
-        case 32: { constexpr int BB = 32; BODY; break; }     \
-        case 64: { constexpr int BB = 64; BODY; break; }     \
-        case 128: { constexpr int BB = 128; BODY; break; }   \
-        case 256: { constexpr int BB = 256; BODY; break; }   \
-        case 512: { constexpr int BB = 512; BODY; break; }   \
-        case 1024: { constexpr int BB = 1024; BODY; break; } \
-        case 2048: { constexpr int BB = 2048; BODY; break; } \
-        case 4096: { constexpr int BB = 4096; BODY; break; } \
-        default: return fail(NEO_HIP_EINVAL, "unsupported block size %d", B_); \
-    }
-
-int64_t partitions_for(int64_t L, int B)
-{
-    // stft.hpp:21-25 with overlap 0: idiv(L - B, B) + 1 (= ceil(L/B) for L >= B);
-    // the reference underflows for L < B, we clamp to one partition.
-    if (L <= B) return 1;
-    return (L - B + B - 1) / B + 1;
-}
-
-int upload_tw(cf** d, int B)
-{
-    std::vector<cf> t = make_twiddle_table(B);
-    std::vector<cf> t2 = make_twiddle_table(2 * int64_t(B));
-    t.insert(t.end(), t2.begin(), t2.end());
-    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(d), t.size() * sizeof(cf)));
-    NEO_HIP_CHECK(hipMemcpy(*d, t.data(), t.size() * sizeof(cf), hipMemcpyHostToDevice));
-    return NEO_HIP_OK;
-}
 
 int reset_state(upols_t* h, hipStream_t s)
 {
@@ -997,40 +404,6 @@ void destroy(upols_t* h)
     if (h->samples_host) (void)hipHostFree(h->samples_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
-}
-
-// normalize (optional) + partition ir [C][L] (device) into packed or unpacked rows.
-int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s,
-                     int64_t cstride = 0, int64_t pstride = 0)
-{
-    const int64_t P = partitions_for(L, B);
-    const int64_t blocks = int64_t(C) * P;
-    if (blocks > 0x7fffffff) return fail(NEO_HIP_EINVAL, "too many partitions");
-    if (packed) {
-        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_partition<BB, true>), dim3(unsigned(blocks)), dim3(256), 0, s,
-                                                 d_ir, L, int(P), out, tw, cstride, pstride))
-    } else {
-        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_partition<BB, false>), dim3(unsigned(blocks)), dim3(256), 0, s,
-                                                 d_ir, L, int(P), out, tw, cstride, pstride))
-    }
-    NEO_HIP_LAUNCH_CHECK();
-    return NEO_HIP_OK;
-}
-
-int normalize_device(float* d_ir, int C, int64_t L, hipStream_t s)
-{
-    if (C < 1) return NEO_HIP_OK;
-    float* factor = nullptr;
-    NEO_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&factor), size_t(C) * sizeof(float), s));
-    hipLaunchKernelGGL(k_energy_factor, dim3(unsigned((C + kEnergyGroup - 1) / kEnergyGroup)), dim3(256), 0, s, d_ir, L,
-                       C, factor);
-    NEO_HIP_LAUNCH_CHECK();
-    const int64_t n = int64_t(C) * L;
-    const unsigned blocks = unsigned(std::min<int64_t>((n + 255) / 256, 4096));
-    hipLaunchKernelGGL(k_scale_min, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, d_ir, n, factor, C);
-    NEO_HIP_LAUNCH_CHECK();
-    NEO_HIP_CHECK(hipFreeAsync(factor, s));
-    return NEO_HIP_OK;
 }
 
 int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
@@ -1072,102 +445,6 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
         NEO_HIP_LAUNCH_CHECK();
     }
     h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;  // fdl_index.hpp:35-37
-    return NEO_HIP_OK;
-}
-
-// blocks per batched pass for block B and NB bins per lane-vector: the requested T,
-// capped so one lane's accumulators (T * NB * VPT * 4 floats) stay <= 128 registers
-constexpr int batch_t(int B, int NB, int want)
-{
-    (void)B;
-    const int VPT = 1;
-    int t = want;
-    while (t > 2 && t * NB * VPT > 32) t /= 2;
-    return t;
-}
-
-int batch_blocks(const upols_t* h) { return batch_t(h->B, h->bNB, h->bT); }
-
-// dispatch k_batch_mac over (B, NB, T) for the valid combinations
-template<int BB, int NB>
-int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
-{
-    constexpr int L = batch_cfg<BB, NB>::L;
-    const unsigned grid = unsigned(h->C) * unsigned(h->Sb) * unsigned(batch_cfg<BB, NB>::G);
-#define NEO_BATCH_T(TT)                                                                                          \
-    case TT:                                                                                                     \
-        if constexpr (batch_t(BB, NB, TT) == TT) {                                                               \
-            hipLaunchKernelGGL((k_batch_mac<BB, TT, NB>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, \
-                               h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride);                      \
-            break;                                                                                               \
-        }                                                                                                        \
-        return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);
-    switch (T) {
-        NEO_BATCH_T(2)
-        NEO_BATCH_T(4)
-        NEO_BATCH_T(8)
-        NEO_BATCH_T(16)
-        NEO_BATCH_T(32)
-        default: return fail(NEO_HIP_EINVAL, "batch of %d blocks not available", T);
-    }
-#undef NEO_BATCH_T
-    NEO_HIP_LAUNCH_CHECK();
-    return NEO_HIP_OK;
-}
-
-// T consecutive blocks: window r2c + insert (C x T), one MAC pass (C x Sb), per-block
-// finish (C x T), OLA overlap chain (C).
-int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s)
-{
-    const int B = h->B;
-    if (!h->part_b) {
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
-                                size_t(h->C) * h->Sb * kMaxBatch * B * sizeof(cf)));
-        if (h->ola)
-            NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * B * sizeof(float)));
-    }
-    const unsigned gCT = unsigned(h->C) * unsigned(T);
-    if (h->ola) {
-        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, true>), dim3(gCT), dim3(256), 0, s, in, ld_in,
-                                                 h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))
-    } else {
-        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, false>), dim3(gCT), dim3(256), 0, s, in, ld_in,
-                                                 h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))
-    }
-    NEO_HIP_LAUNCH_CHECK();
-    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (h->timing) {
-        if (h->events_used == h->events.size()) {
-            NEO_HIP_CHECK(hipEventCreate(&ev.first));
-            NEO_HIP_CHECK(hipEventCreate(&ev.second));
-            h->events.push_back(ev);
-        }
-        ev = h->events[h->events_used];
-        NEO_HIP_CHECK(hipEventRecord(ev.first, s));
-    }
-    int rc = NEO_HIP_OK;
-    if (h->bNB == 2) {
-        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s)))
-    } else {
-        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s)))
-    }
-    if (rc) return rc;
-    if (h->timing) {
-        NEO_HIP_CHECK(hipEventRecord(ev.second, s));
-        ++h->events_used;
-    }
-    if (h->ola) {
-        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_finish<BB, true>), dim3(gCT), dim3(256), 0, s, h->part_b,
-                                                 h->Sb, T, in, ld_in, out, ld_out, h->prev, h->tail, h->tw))
-        NEO_HIP_LAUNCH_CHECK();
-        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_ola<BB>), dim3(unsigned(h->C)), dim3(256), 0, s, out, ld_out,
-                                                 h->tail, h->prev, T))
-    } else {
-        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_finish<BB, false>), dim3(gCT), dim3(256), 0, s, h->part_b,
-                                                 h->Sb, T, in, ld_in, out, ld_out, h->prev, h->tail, h->tw))
-    }
-    NEO_HIP_LAUNCH_CHECK();
-    h->wpos = (h->wpos + T) % h->ring;
     return NEO_HIP_OK;
 }
 
@@ -1240,16 +517,6 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
 
 }  // namespace
 
-extern "C" {
-
-NEO_HIP_API int neo_hip_num_partitions(int64_t length, int block, int64_t* partitions)
-{
-    if (!partitions || block < 1 || length < 0) return fail(NEO_HIP_EINVAL, "bad arguments");
-    *partitions = partitions_for(length, block);
-    return NEO_HIP_OK;
-}
-
-}  // extern "C"
 
 namespace {
 int create_convolver(int channels, int block, int partitions, int device, bool ola, bool v2, neo_hip_upols** out)
@@ -1387,10 +654,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
         NEO_HIP_CHECK(hipMemcpyAsync(tmp, filter, bytes, hipMemcpyHostToDevice, h->stream));
         src = tmp;
     }
-    const int64_t total = rows * h->B;
-    hipLaunchKernelGGL(k_pack_filter, dim3(unsigned((total + 255) / 256)), dim3(256), 0, h->stream, src, h->H, h->B,
-                       rows, h->P, h->cstride, h->pstride);
-    int rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "pack kernel launch failed");
+    int rc = pack_filter(h, src, h->stream);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     if (tmp) (void)hipFree(tmp);
@@ -1549,71 +813,6 @@ NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* 
     h->mac_ms = 0.0;
     h->launches = 0;
     return NEO_HIP_OK;
-}
-
-NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t length, int block, void* out,
-                                          int is_device, int device)
-{
-    if (!ir || !out || channels < 1 || length < 1) return fail(NEO_HIP_EINVAL, "bad arguments");
-    if (!valid_block(block)) return fail(NEO_HIP_EINVAL, "block must be a power of two in [16, 4096], got %d", block);
-    device_guard g(device);
-    if (g.rc) return g.rc;
-    const int64_t P = partitions_for(length, block);
-    const size_t in_bytes = size_t(channels) * size_t(length) * sizeof(float);
-    const size_t out_bytes = size_t(channels) * size_t(P) * size_t(block + 1) * sizeof(cf);
-    hipStream_t s = nullptr;
-    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
-    cf* tw = nullptr;
-    const float* d_ir = ir;
-    float* tmp_in = nullptr;
-    cf* d_out = static_cast<cf*>(out);
-    int rc = upload_tw(&tw, block);
-    if (!rc && !is_device) {
-        if (hipMalloc(reinterpret_cast<void**>(&tmp_in), in_bytes) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&d_out), out_bytes) != hipSuccess)
-            rc = fail(NEO_HIP_ENOMEM, "allocation failed");
-        else if (hipMemcpyAsync(tmp_in, ir, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-            rc = fail(NEO_HIP_ERUNTIME, "copy failed");
-        d_ir = tmp_in;
-    }
-    if (!rc) rc = partition_device(d_ir, channels, length, block, false, d_out, tw, s);
-    if (!rc && !is_device && hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
-        rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
-    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
-    if (!is_device) {
-        (void)hipFree(tmp_in);
-        (void)hipFree(d_out);
-    }
-    (void)hipFree(tw);
-    (void)hipStreamDestroy(s);
-    return rc;
-}
-
-NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t length, int is_device, int device)
-{
-    if (!ir || channels < 0 || length < 0) return fail(NEO_HIP_EINVAL, "bad arguments");
-    if (channels == 0 || length == 0) return NEO_HIP_OK;
-    device_guard g(device);
-    if (g.rc) return g.rc;
-    hipStream_t s = nullptr;
-    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
-    const size_t bytes = size_t(channels) * size_t(length) * sizeof(float);
-    float* d = ir;
-    int rc = NEO_HIP_OK;
-    if (!is_device) {
-        if (hipMalloc(reinterpret_cast<void**>(&d), bytes) != hipSuccess) rc = fail(NEO_HIP_ENOMEM, "alloc failed");
-        else if (hipMemcpyAsync(d, ir, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-            rc = fail(NEO_HIP_ERUNTIME, "copy failed");
-    }
-    if (!rc) rc = normalize_device(d, channels, length, s);
-    if (!rc && !is_device && hipMemcpyAsync(ir, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
-        rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
-    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
-    if (!is_device && d) (void)hipFree(d);
-    (void)hipStreamDestroy(s);
-    return rc;
 }
 
 }  // extern "C"

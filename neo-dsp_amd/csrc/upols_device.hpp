@@ -1,0 +1,140 @@
+// upols_device.hpp — device building blocks shared by the UPOLS kernels
+// (upols.hip: single-block step / finish / v2 piece; upols_batch.hip: batched passes;
+// upols_setup.hip: partitioning): per-B geometry, the packed-bin MAC, the overlap
+// window r2c and the c2r tail (overlap_save.hpp:84-112, overlap_add.hpp:76-106).
+#pragma once
+
+#include "common.hpp"
+#include "fft_device_real.hpp"
+
+// elements per lane of the per-channel tail transforms (c2r of k_upols_finish /
+// k_batch_finish): 4 per lane puts B/4 lanes to work (C5 finish 6.3 -> 4.9 us, batch 61 -> 29 us)
+#ifndef NEO_FINISH_E
+#define NEO_FINISH_E(B) ((B) / 4 <= 256 ? ((B) >= 4 ? 4 : (B)) : (B) / 256)
+#endif
+#define NEO_BATCH_FINISH_E(B) NEO_FINISH_E(B)
+
+namespace neo_hip {
+
+__host__ __device__ constexpr int upols_e(int b) { return b >= 16 ? 16 : b; }
+
+template<int B>
+struct upols_cfg {
+    static constexpr int E = upols_e(B);                 // FFT elements per lane
+    static constexpr int T = B / E;                      // FFT lanes
+    static constexpr int Q = B / 2;                      // float4 (2 bins) per row
+    static constexpr int QT = Q < 256 ? Q : 256;         // lanes per row group
+    static constexpr int RPI = 256 / QT;                 // rows in flight per iteration
+    static constexpr int VPT = Q / QT;                   // float4 per lane per row
+    static constexpr int U = VPT >= 4 ? 1 : 4 / VPT;     // row unroll
+    static constexpr int TW1 = twiddle_len<B>();
+    static constexpr int TW2 = twiddle_len<2 * B>();
+    static constexpr int LL = lds_len(B);
+};
+
+struct acc4 {  // 4 partial products per bin keep the packed bin 0 exact
+    float rr, ii, ri, ir;
+};
+
+__device__ __forceinline__ void mac2(acc4& a0, acc4& a1, float4 h, float4 x)
+{
+    a0.rr = fmaf(h.x, x.x, a0.rr);
+    a0.ii = fmaf(h.y, x.y, a0.ii);
+    a0.ri = fmaf(h.x, x.y, a0.ri);
+    a0.ir = fmaf(h.y, x.x, a0.ir);
+    a1.rr = fmaf(h.z, x.z, a1.rr);
+    a1.ii = fmaf(h.w, x.w, a1.ii);
+    a1.ri = fmaf(h.z, x.w, a1.ri);
+    a1.ir = fmaf(h.w, x.z, a1.ir);
+}
+
+// acc4 -> packed complex bin: bin 0 = {DC, Nyquist} (products of real values),
+// other bins = the complex product sum.
+__device__ __forceinline__ cf finish(const acc4& a, bool bin0)
+{
+    return bin0 ? cf{a.rr, a.ii} : cf{a.rr - a.ii, a.ri + a.ir};
+}
+
+// Load the overlap-save window [prev | in] of channel c as the packed complex
+// sequence z[n] = w[2n] + i w[2n+1] (lane t owns n = t + m*T), forward FFT, and
+// leave the natural-order spectrum Z in `fft` (lpad'ed).
+// E = 8 elements per lane keeps this fused r2c from raising the kernel's register
+// count (the MAC loop itself needs ~60 VGPRs; occupancy is what streams HBM).
+// OLS window = [previous block | new block] (overlap_save.hpp:90-95);
+// OLA window = [new block | zeros]          (overlap_add.hpp:84-86).
+template<int B, bool OLA, int E = (B / 8 <= 256 ? 8 : B / 256)>
+__device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, const cf* tw1, int tid)
+{
+    constexpr int T = B / E;
+    static_assert(T <= 256 && B % E == 0, "window FFT must fit one 256-lane workgroup");
+    const bool active = tid < T;
+    cf v[E];
+    if (active) {
+        const cf* pz = reinterpret_cast<const cf*>(prev_c);
+        const cf* iz = reinterpret_cast<const cf*>(in_c);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int n = tid + m * T;
+            if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
+            else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+        }
+    }
+    __syncthreads();  // twiddles staged by the caller
+    stockham<B, E, -1>(v, fft, tw1, tid, active);
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) fft[lpad(tid + m * T)] = v[m];
+    }
+    __syncthreads();
+}
+
+// c2r of the packed spectrum X (LDS), scaled by 1/2B (fallback_rfft_plan.hpp:38-55):
+//   OLS: out = window samples [B, 2B)                       (overlap_save.hpp:104-111)
+//   OLA: out = samples [0, B) + overlap; overlap = [B, 2B)  (overlap_add.hpp:92-106)
+// E = 4 keeps the fused kernel inside its 64-VGPR budget (T = B/E <= 256 lanes).
+template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256)>
+__device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, float* ovl_c, int tid)
+{
+    using K = upols_cfg<B>;
+    constexpr int T = B / E;
+    static_assert(T <= 256 && B % E == 0, "c2r must fit one 256-lane workgroup");
+    const bool active = tid < T;
+    cf v[E];
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int k = tid + m * T;
+            const cf x0 = X[0];
+            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
+                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
+        }
+    }
+    stockham<B, E, +1>(v, fft, tw, tid, active);
+    if (active) {
+        const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108 / overlap_add.hpp:98
+        cf* o = reinterpret_cast<cf*>(out_c);
+        if constexpr (OLA) {
+            cf* ov = reinterpret_cast<cf*>(ovl_c);
+            // the same lane reads overlap[n] (m < E/2) before writing it (m >= E/2: n - B/2)
+#pragma unroll
+            for (int m = 0; m < E / 2; ++m) {
+                const int n = tid + m * T;
+                const cf old = ov[n];
+                o[n] = {v[m].x * scale + old.x, v[m].y * scale + old.y};
+            }
+#pragma unroll
+            for (int m = E / 2; m < E; ++m) {
+                const int n = tid + m * T;
+                ov[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+            }
+        } else {
+#pragma unroll
+            for (int m = E / 2; m < E; ++m) {  // window samples [B, 2B): z[n], n >= B/2
+                const int n = tid + m * T;
+                o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+            }
+        }
+    }
+}
+
+}  // namespace neo_hip

@@ -1,0 +1,109 @@
+// upols_handle.hpp — the UPOLS convolver handle (neo_hip_upols) and the host helpers
+// shared by the translation units that implement it (upols.hip, upols_batch.hip,
+// upols_setup.hip).
+#pragma once
+
+#include "common.hpp"
+
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+namespace neo_hip {
+constexpr int kMaxBatch = 32;                          // most blocks one batched MAC pass consumes
+constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch
+}  // namespace neo_hip
+
+struct neo_hip_upols {
+    int device = 0, C = 0, B = 0, P = 0, S = 1, rows = 1;
+    int ring = 0;  // FDL ring rows R = P + kMaxBatch - 1
+    hipStream_t stream = nullptr;
+    neo_hip::cf* H = nullptr;
+    neo_hip::cf* fdl = nullptr;
+    neo_hip::cf* part = nullptr;
+    float* prev = nullptr;
+    int* arrivals = nullptr;  // per-channel split arrival counters (zero between steps)
+    int wpos = 0;             // FDL write position (fdl_index.hpp:35-37), host-side
+    neo_hip::cf* tw = nullptr;
+    float* io = nullptr;       // device staging for host-pointer process()
+    float* io_host = nullptr;  // pinned staging
+    bool batch = true;      // process_blocks runs T blocks per MAC pass (neo_hip_upols_set_batch)
+    int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
+    int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
+    neo_hip::cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
+    float* tail = nullptr;  // batched OLA tails [C][T][B]
+    float* samples_dev = nullptr;   // process_samples host staging (device side)
+    float* samples_host = nullptr;  // process_samples host staging (pinned)
+    size_t samples_cap = 0;
+    bool timing = false;
+    bool ola = false;  // upola_convolver (overlap-add stage) instead of upols (overlap-save)
+    bool v2 = false;   // upola_convolver_v2: sub-block input (implies ola)
+    int in_pos = 0;    // v2: samples of the current block already consumed (_input_pos)
+    float* window = nullptr;  // v2: real window [C][2B]
+    neo_hip::cf* tmp = nullptr;        // v2: tail accumulator [C][B] packed (_tmp_accumulator)
+    // one launch per block (last-arriver tail) instead of MAC + finish: on for small filter
+    // + FDL working sets, where the step is launch-bound (C3: 10.6 vs 12.4 us per block),
+    // off for HBM-bound ones (C5: 0.342 vs 0.303 ms); NEO_HIP_FUSED=0/1 overrides
+    bool fused = false;
+    // H / FDL layout: row p of channel c at c * cstride + p * pstride (complex units).
+    // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
+    int64_t cstride = 0, pstride = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool, reused across timing windows
+    size_t events_used = 0;
+    double mac_ms = 0.0;
+    int64_t launches = 0;
+};
+
+
+namespace neo_hip {
+
+using upols_t = neo_hip_upols;
+
+inline bool valid_block(int b) { return b >= 16 && b <= 4096 && (b & (b - 1)) == 0; }
+
+#define NEO_UPOLS_DISPATCH(B_, BODY) \
+    switch (B_) {                    \
+        case 16: { constexpr int BB = 16; BODY; break; }     \
+        case 32: { constexpr int BB = 32; BODY; break; }     \
+        case 64: { constexpr int BB = 64; BODY; break; }     \
+        case 128: { constexpr int BB = 128; BODY; break; }   \
+        case 256: { constexpr int BB = 256; BODY; break; }   \
+        case 512: { constexpr int BB = 512; BODY; break; }   \
+        case 1024: { constexpr int BB = 1024; BODY; break; } \
+        case 2048: { constexpr int BB = 2048; BODY; break; } \
+        case 4096: { constexpr int BB = 4096; BODY; break; } \
+        default: return fail(NEO_HIP_EINVAL, "unsupported block size %d", B_); \
+    }
+
+inline int64_t partitions_for(int64_t L, int B)
+{
+    // stft.hpp:21-25 with overlap 0: idiv(L - B, B) + 1 (= ceil(L/B) for L >= B);
+    // the reference underflows for L < B, we clamp to one partition.
+    if (L <= B) return 1;
+    return (L - B + B - 1) / B + 1;
+}
+
+// blocks per batched pass for block B and NB bins per lane-vector: the requested T,
+// capped so one lane's accumulators (T * NB * VPT * 4 floats) stay <= 128 registers
+constexpr int batch_t(int B, int NB, int want)
+{
+    (void)B;
+    const int VPT = 1;
+    int t = want;
+    while (t > 2 && t * NB * VPT > 32) t /= 2;
+    return t;
+}
+
+inline int batch_blocks(const upols_t* h) { return batch_t(h->B, h->bNB, h->bT); }
+
+// upols_batch.hip: T whole blocks in one pass over the filter and the FDL
+int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s);
+// upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device
+int upload_tw(cf** d, int B);
+int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s,
+                     int64_t cstride = 0, int64_t pstride = 0);
+int normalize_device(float* d_ir, int C, int64_t L, hipStream_t s);
+// filter [C][P][B+1] (reference layout, device) -> packed H rows of the handle
+int pack_filter(upols_t* h, const cf* src, hipStream_t s);
+
+}  // namespace neo_hip
