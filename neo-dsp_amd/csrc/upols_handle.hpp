@@ -12,6 +12,7 @@
 namespace neo_hip {
 constexpr int kMaxBatch = 32;                          // most blocks one batched MAC pass consumes
 constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch
+constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read cacheable (256 MiB Infinity Cache)
 }  // namespace neo_hip
 
 struct neo_hip_upols {
@@ -48,6 +49,7 @@ struct neo_hip_upols {
     // H / FDL layout: row p of channel c at c * cstride + p * pstride (complex units).
     // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
     int64_t cstride = 0, pstride = 0;
+    int pc = 0;  // filter rows per channel read with the cacheable policy (kCacheBudgetBytes; NEO_HIP_CACHE_ROWS)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool, reused across timing windows
     size_t events_used = 0;
     double mac_ms = 0.0;

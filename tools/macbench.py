@@ -23,6 +23,7 @@ for spec in specs:
         k, v = kv.split("=")
         os.environ[k] = v
     c = neo.UpolsConvolver(C, B, P)
+    c.set_batch(False)  # the streaming step (one MAC pass per block)
     c.set_impulse(ir)
     variants[spec] = c
 x = torch.rand((C, steps * B), generator=g, device="cuda") * 2 - 1
