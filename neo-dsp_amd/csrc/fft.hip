@@ -8,7 +8,7 @@
 // runs the Stockham passes through LDS and stores the natural-order result.
 // Larger sizes: ceil(log2 N / 10) global Stockham passes of radix 64..1024 whose DFTs
 // run in LDS over groups of adjacent columns (ping-pong scratch); 2-2.4x faster than
-// the radix-16 register passes they replaced (k_pass, kept for reference/A-B).
+// the radix-16 register passes of the first version.
 #include "common.hpp"
 #include "fft_device_real.hpp"
 
@@ -155,43 +155,13 @@ __global__ void k_c2r_order0(const C* in, real_of<C>* out, int64_t batch)
 }
 
 // ---------------------------------------------------------------------------
-// Large transforms: one global-memory Stockham pass of radix R.
+// Large transforms: two-level twiddle W_n^e from the split table (e = hi * 2^lo_bits + lo).
 // ---------------------------------------------------------------------------
 template<class C>
 __device__ __forceinline__ C split_twiddle(const C* tw, int lo_bits, int64_t e)
 {
     const int64_t mask = (int64_t(1) << lo_bits) - 1;
     return cmul(tw[(int64_t(1) << lo_bits) + (e >> lo_bits)], tw[e & mask]);
-}
-
-template<int R, int DIR, class C = cf>
-__global__ __launch_bounds__(256) void k_pass(const C* __restrict__ in, C* __restrict__ out,
-                                              const C* __restrict__ tw, int lo_bits, int64_t n, int64_t ns,
-                                              int64_t total)
-{
-    const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x;
-    if (gid >= total) return;
-    const int64_t nb = n / R;
-    const int64_t b = gid / nb, j = gid - b * nb;
-    in += b * n;
-    out += b * n;
-    C v[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
-    const int64_t jm = j & (ns - 1);
-    if (ns > 1) {
-        const int64_t step = jm * (n / (ns * R));
-#pragma unroll
-        for (int r = 1; r < R; ++r) {
-            C w = split_twiddle(tw, lo_bits, step * r);
-            if (DIR > 0) w.y = -w.y;
-            v[r] = cmul(v[r], w);
-        }
-    }
-    dft<R, DIR>(v);
-    const int64_t base = (j / ns) * ns * R + jm;
-#pragma unroll
-    for (int r = 0; r < R; ++r) out[base + r * ns] = v[r];
 }
 
 // One global Stockham pass of a large radix R (64..512) with the R-point DFTs done in LDS
