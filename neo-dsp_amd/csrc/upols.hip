@@ -563,8 +563,10 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     // A/B on MI355X: 1024 beat 512/768/2048/4096 at C4 and C5), <= 64 partial slabs
     int target = 1024;
     if (const char* e = std::getenv("NEO_HIP_SPLIT_WGS")) target = std::max(1, std::atoi(e));
-    // >= 8 rows per split keeps the out kernel's slab sum short at small C (C3: 24 splits)
-    int S = std::max(1, std::min({(target + channels - 1) / channels, (partitions + 7) / 8, 64}));
+    // >= 8 rows per split keeps the slab sum short at small C; the one-launch (latency) form
+    // takes >= 16 (C3: 12 splits, 9.6 vs 10.6 us per block with 24)
+    const int min_rows = h->fused ? 16 : 8;
+    int S = std::max(1, std::min({(target + channels - 1) / channels, (partitions + min_rows - 1) / min_rows, 64}));
     h->rows = (partitions + S - 1) / S;
     h->S = (partitions + h->rows - 1) / h->rows;
     // batched passes: same workgroup target, >= 2T partitions per split so the sliding FDL

@@ -225,6 +225,7 @@ def test_multirow_splits_with_wraparound(neo_gpu, oracle):
     ref = oracle.dense_convolve(sig, oracle.uniform_partition(oracle.normalize_impulse(ir), B))
     for target in ("6", "1", "64"):
         os.environ["NEO_HIP_SPLIT_WGS"] = target
+        os.environ["NEO_HIP_FUSED"] = "0"  # the MAC + finish form (>= 8 rows per split)
         try:
             P = neo_gpu.num_partitions(L, B)
             conv = neo_gpu.UpolsConvolver(C, B, P)
@@ -235,7 +236,7 @@ def test_multirow_splits_with_wraparound(neo_gpu, oracle):
                 conv(blk)
                 out[:, t * B:(t + 1) * B] = blk
         finally:
-            del os.environ["NEO_HIP_SPLIT_WGS"]
+            del os.environ["NEO_HIP_SPLIT_WGS"], os.environ["NEO_HIP_FUSED"]
         # S = ceil(P / ceil(P / min(ceil(t/C), ceil(P/8), 64)))
         assert conv.splits == {"6": 3, "1": 1, "64": 7}[target]
         assert peak_err(out, ref) <= TOL, (target, conv.splits)
