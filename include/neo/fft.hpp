@@ -22,6 +22,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <functional>
 #include <type_traits>
 #include <vector>
 
@@ -262,6 +263,89 @@ constexpr auto rfftfreq(Vec vec, double inv_sample_rate) noexcept -> void
 }  // namespace neo
 
 namespace neo::fft {
+
+/// norm.hpp (Python scaling modes)
+enum struct norm
+{
+    backward,
+    ortho,
+    forward,
+};
+
+/// stft.hpp:30-37
+template<std::floating_point Float>
+struct stft_options {
+    std::size_t frame_size{};
+    std::size_t transform_size{};
+    std::size_t overlap_size{};
+    std::function<Float(std::size_t, std::size_t)> window{[](std::size_t i, std::size_t n) {
+        // hann_window (math/windowing.hpp:29-41)
+        auto const two_pi = static_cast<Float>(3.14159265358979323846) * Float(2);
+        return Float(0.5) * (Float(1) - std::cos(two_pi * static_cast<Float>(i) / static_cast<Float>(n - 1)));
+    }};
+};
+
+/// stft_plan (stft.hpp:40-109): x [C][L] -> [C][F][N/2+1] on the GPU (framing + batched r2c)
+template<std::floating_point Float, typename Complex = std::complex<Float>>
+struct stft_plan {
+    static_assert(std::same_as<Float, float> || std::same_as<Float, double>);
+
+    explicit stft_plan(std::size_t transform_size)
+        : stft_plan(stft_options<Float>{transform_size, transform_size, transform_size / 2})
+    {}
+
+    explicit stft_plan(stft_options<Float> options) : _options{std::move(options)}
+    {
+        auto const n = fft::size(fft::next_order(_options.transform_size));
+        _window.resize(n);
+        for (std::size_t i = 0; i < n; ++i) _window[i] = _options.window(i, n);  // fill_window
+    }
+
+    template<typename InMat>
+        requires neo::hip::detail::matrix_like<InMat>
+    [[nodiscard]] auto operator()(InMat x) -> neo::hip::array<Complex, 3>
+    {
+        auto const C = std::size_t(x.extent(0)), L = std::size_t(x.extent(1));
+        std::vector<Float> buf(C * L);
+        for (std::size_t c = 0; c < C; ++c)
+            for (std::size_t i = 0; i < L; ++i) buf[c * L + i] = Float(neo::hip::detail::at(x, c, i));
+        std::int64_t frames = 0;
+        neo::hip::check(neo_hip_stft_num_frames(std::int64_t(L), int(_options.frame_size), int(_options.overlap_size),
+                                                &frames));
+        neo::hip::array<Complex, 3> out;
+        out.ext[0] = C;
+        out.ext[1] = std::size_t(frames);
+        out.ext[2] = _window.size() / 2 + 1;
+        out.buf.resize(out.ext[0] * out.ext[1] * out.ext[2]);
+        auto const f = [] {
+            if constexpr (std::same_as<Float, double>) return neo_hip_stft_f64;
+            else return neo_hip_stft;
+        }();
+        neo::hip::check(f(buf.data(), int(C), std::int64_t(L), int(_options.frame_size),
+                          int(_options.transform_size), int(_options.overlap_size), _window.data(), out.data(), 0,
+                          neo::hip::detail::default_device()));
+        return out;
+    }
+
+private:
+    stft_options<Float> _options;
+    std::vector<Float> _window;
+};
+
+/// stft.hpp:111-125
+template<typename InMat>
+[[nodiscard]] auto stft(InMat x, stft_options<std::remove_cvref_t<decltype(neo::hip::detail::at(x, 0, 0))>> options)
+{
+    using Float = std::remove_cvref_t<decltype(neo::hip::detail::at(x, 0, 0))>;
+    return stft_plan<Float>{std::move(options)}(x);
+}
+
+template<typename InMat>
+[[nodiscard]] auto stft(InMat x, std::size_t window_size)
+{
+    using Float = std::remove_cvref_t<decltype(neo::hip::detail::at(x, 0, 0))>;
+    return stft_plan<Float>{window_size}(x);
+}
 
 /// rfft.hpp:41-62: split the c2c spectrum of a + ib into rfft(a), rfft(b) (host utility)
 template<typename InVec, typename OutVecX, typename OutVecY>

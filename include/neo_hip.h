@@ -157,6 +157,18 @@ NEO_HIP_API int neo_hip_fft_convolve_f64(const double* signal, int64_t n, const 
 NEO_HIP_API int neo_hip_direct_convolve_f64(const double* signal, int64_t n, const double* patch, int64_t m,
                                             double* out, int is_device, int device);
 
+/* -- STFT (stft_plan, src/neo/fft/stft.hpp:40-109) ------------------------------
+ * x [C][L] -> out [C][F][N/2+1] complex (float or double), N = 2^next_order(transform_size),
+ * hop = frame_size - overlap, F = neo_hip_stft_num_frames(L, frame_size, overlap)
+ * (detail::num_sftf_frames, :21-25). Frame f = x[f*hop, +min(L - f*hop, frame_size))
+ * zero-padded to N, times window[0, N) (NULL = hann_window over N, windowing.hpp:29-41),
+ * then rfft. Host or device pointers (window in the same memory as x). */
+NEO_HIP_API int neo_hip_stft_num_frames(int64_t length, int frame_size, int overlap, int64_t* frames);
+NEO_HIP_API int neo_hip_stft(const float* x, int channels, int64_t length, int frame_size, int transform_size,
+                             int overlap, const float* window, void* out, int is_device, int device);
+NEO_HIP_API int neo_hip_stft_f64(const double* x, int channels, int64_t length, int frame_size, int transform_size,
+                                 int overlap, const double* window, void* out, int is_device, int device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,7 @@
-// convolve.hip — one-shot full linear convolution on MI355X: fft_convolve and
-// direct_convolve, the reference's Python `neo.convolve` methods
-// (extra/python/src/neo/__init__.py:43-48 -> main.cpp:169-198).
+// convolve.hip — one-shot transforms built on the FFT plans: full linear convolution
+// (fft_convolve, direct_convolve; the reference's Python `neo.convolve` methods,
+// extra/python/src/neo/__init__.py:43-48 -> main.cpp:169-198) and the STFT
+// (stft_plan, src/neo/fft/stft.hpp:40-109, the general form of uniform_partition).
 //
 //   fft_convolve    (src/neo/convolution/fft_convolver.hpp:19-93): zero-pad both inputs
 //                   to N = 2^next_order(n+m-1), r2c both (one batched plan), complex
@@ -11,6 +12,8 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cmath>
+#include <vector>
 #include <type_traits>
 
 namespace neo_hip {
@@ -64,6 +67,22 @@ __global__ void k_direct_convolve(const R* __restrict__ a, int64_t na, const R* 
             acc = acc + prod;
         }
         out[k] = acc;
+    }
+}
+
+// stft_plan::operator() framing (stft.hpp:56-99): frame f of channel c starts at f*hop,
+// takes min(L - start, frame) samples, zero-pads to N and multiplies by window[0, N)
+// (the reference multiplies the whole zero-padded buffer, :92); rows [C][F][N].
+template<class R>
+__global__ void k_stft_frames(const R* __restrict__ x, int64_t L, int64_t F, int64_t frame, int64_t hop, int64_t N,
+                              const R* __restrict__ window, R* __restrict__ rows, int64_t total)
+{
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t n = i % N, cf_ = i / N, f = cf_ % F, c = cf_ / F;
+        const int64_t start = f * hop;
+        const int64_t cnt = L - start < frame ? L - start : frame;
+        const R v = n < cnt ? x[c * L + start + n] : R(0);
+        rows[i] = v * window[n];
     }
 }
 
@@ -192,6 +211,78 @@ int direct_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, 
     return rc;
 }
 
+// detail::num_sftf_frames (stft.hpp:21-25): idiv(L - frame + overlap, frame - overlap) + 1,
+// clamped to one frame where the reference's unsigned arithmetic would underflow
+int64_t stft_frames(int64_t L, int64_t frame, int64_t overlap)
+{
+    const int64_t hop = frame - overlap;
+    if (L <= frame) return 1;
+    return (L - frame + overlap + hop - 1) / hop + 1;
+}
+
+template<class R>
+int stft_impl(const R* x, int channels, int64_t length, int frame, int transform, int overlap, const R* window,
+              void* out, int is_device, int device)
+{
+    using C = std::conditional_t<sizeof(R) == 8, cd, cf>;
+    const int f64 = sizeof(R) == 8 ? NEO_HIP_F64 : 0;
+    if (!x || !out || channels < 1 || length < 1 || frame < 1 || transform < 1 || overlap < 0 || overlap >= frame)
+        return fail(NEO_HIP_EINVAL, "bad stft arguments");
+    int order = 0;
+    while ((int64_t(1) << order) < transform) ++order;  // rfft_plan{from_order, next_order(transform_size)}
+    const int64_t N = int64_t(1) << order, bins = N / 2 + 1;
+    if (frame > N) return fail(NEO_HIP_EINVAL, "frame_size %d exceeds the transform size %lld", frame, (long long)N);
+    if (order > 27) return fail(NEO_HIP_EINVAL, "transform size exceeds max order 27");
+    const int64_t F = stft_frames(length, frame, overlap), rows_n = int64_t(channels) * F;
+    device_guard g(device);
+    if (g.rc) return g.rc;
+    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());
+    hipStream_t s = nullptr;
+    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    int rc = NEO_HIP_OK;
+    R *d_x = nullptr, *d_w = nullptr, *rows = nullptr;
+    C* d_out = static_cast<C*>(out);
+    neo_hip_fft_plan* plan = nullptr;
+    std::vector<R> hann;
+    if (!window) {  // hann_window (windowing.hpp:29-41) over the transform size, in R
+        hann.resize(size_t(N));
+        const R n1 = R(N - 1), two_pi = R(3.14159265358979323846) * R(2);
+        for (int64_t i = 0; i < N; ++i) hann[size_t(i)] = R(0.5) * (R(1) - std::cos(two_pi * R(i) / n1));
+    }
+    const size_t xbytes = size_t(channels) * size_t(length) * sizeof(R), obytes = size_t(rows_n * bins) * sizeof(C);
+    if (hipMalloc(reinterpret_cast<void**>(&rows), size_t(rows_n * N) * sizeof(R)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_w), size_t(N) * sizeof(R)) != hipSuccess ||
+        (!is_device && (hipMalloc(reinterpret_cast<void**>(&d_x), xbytes) != hipSuccess ||
+                        hipMalloc(reinterpret_cast<void**>(&d_out), obytes) != hipSuccess)))
+        rc = fail(NEO_HIP_ENOMEM, "stft buffers");
+    const R* xin = is_device ? x : d_x;
+    if (!rc && !is_device && hipMemcpyAsync(d_x, x, xbytes, hipMemcpyHostToDevice, s) != hipSuccess)
+        rc = fail(NEO_HIP_ERUNTIME, "input copy failed");
+    if (!rc && hipMemcpyAsync(d_w, window ? window : hann.data(), size_t(N) * sizeof(R),
+                              window && is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s) != hipSuccess)
+        rc = fail(NEO_HIP_ERUNTIME, "window copy failed");
+    if (!rc) {
+        const int64_t total = rows_n * N;
+        hipLaunchKernelGGL((k_stft_frames<R>), dim3(grid_for(total)), dim3(256), 0, s, xin, length, F, int64_t(frame),
+                           int64_t(frame - overlap), N, d_w, rows, total);
+        rc = hipGetLastError() == hipSuccess ? NEO_HIP_OK : fail(NEO_HIP_ERUNTIME, "framing launch failed");
+    }
+    if (!rc) rc = neo_hip_fft_plan_create(order, rows_n, NEO_HIP_R2C | f64, device, &plan);
+    if (!rc) rc = neo_hip_fft_execute(plan, rows, d_out, -1, s);
+    if (!rc && !is_device && hipMemcpyAsync(out, d_out, obytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
+    neo_hip_fft_plan_destroy(plan);
+    (void)hipFree(rows);
+    (void)hipFree(d_w);
+    if (!is_device) {
+        (void)hipFree(d_x);
+        (void)hipFree(d_out);
+    }
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
 }  // namespace neo_hip
 
 using namespace neo_hip;
@@ -220,6 +311,26 @@ NEO_HIP_API int neo_hip_direct_convolve_f64(const double* signal, int64_t n, con
                                             double* out, int is_device, int device)
 {
     return direct_convolve_impl(signal, n, patch, m, out, is_device, device);
+}
+
+NEO_HIP_API int neo_hip_stft_num_frames(int64_t length, int frame_size, int overlap, int64_t* frames)
+{
+    if (!frames || length < 0 || frame_size < 1 || overlap < 0 || overlap >= frame_size)
+        return fail(NEO_HIP_EINVAL, "bad stft arguments");
+    *frames = stft_frames(length, frame_size, overlap);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_stft(const float* x, int channels, int64_t length, int frame_size, int transform_size,
+                             int overlap, const float* window, void* out, int is_device, int device)
+{
+    return stft_impl(x, channels, length, frame_size, transform_size, overlap, window, out, is_device, device);
+}
+
+NEO_HIP_API int neo_hip_stft_f64(const double* x, int channels, int64_t length, int frame_size, int transform_size,
+                                 int overlap, const double* window, void* out, int is_device, int device)
+{
+    return stft_impl(x, channels, length, frame_size, transform_size, overlap, window, out, is_device, device);
 }
 
 }  // extern "C"

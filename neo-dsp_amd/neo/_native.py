@@ -56,6 +56,9 @@ SIGNATURES = {
     "neo_hip_direct_convolve": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
     "neo_hip_fft_convolve_f64": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
     "neo_hip_direct_convolve_f64": (_i, [_vp, _i64, _vp, _i64, _vp, _i, _i]),
+    "neo_hip_stft_num_frames": (_i, [_i64, _i, _i, ctypes.POINTER(_i64)]),
+    "neo_hip_stft": (_i, [_vp, _i, _i64, _i, _i, _i, _vp, _vp, _i, _i]),
+    "neo_hip_stft_f64": (_i, [_vp, _i, _i64, _i, _i, _i, _vp, _vp, _i, _i]),
 }
 
 _lib = None

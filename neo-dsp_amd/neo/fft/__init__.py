@@ -20,7 +20,8 @@ import numpy as np
 from .. import _native
 from ._plan import FFTPlan, get_plan
 
-__all__ = ["fft", "ifft", "rfft", "irfft", "rfftfreq", "FFTPlan", "get_plan", "next_order", "size", "max_order"]
+__all__ = ["fft", "ifft", "rfft", "irfft", "rfftfreq", "stft", "stft_num_frames", "FFTPlan", "get_plan", "next_order",
+           "size", "max_order"]
 
 _NORMS = ("backward", "ortho", "forward")
 
@@ -168,3 +169,48 @@ def rfftfreq(n: int, d: float = 1.0) -> np.ndarray:
     fs = 1.0 / float(d)
     inv = 1.0 / float(n) if n else 0.0
     return np.arange(n, dtype=np.float64) * fs * inv
+
+
+def stft_num_frames(length: int, frame_size: int, overlap_size: int) -> int:
+    """detail::num_sftf_frames (src/neo/fft/stft.hpp:21-25)."""
+    f = ctypes.c_int64()
+    _native.check(_native.load().neo_hip_stft_num_frames(int(length), int(frame_size), int(overlap_size),
+                                                         ctypes.byref(f)))
+    return f.value
+
+
+def stft(x, frame_size: int, transform_size=None, overlap_size=None, window="hann", device: int = 0):
+    """stft_plan / stft (src/neo/fft/stft.hpp:40-125) on the GPU: x [C][L] (or [L]) ->
+    [C][F][N/2+1], N = 2^next_order(transform_size). `stft(x, n)` is the reference's
+    stft(x, window_size): frame = transform = n, overlap n/2, hann window. `window`:
+    "hann", "rectangular", an array of N values or a callable window(index, size) (the
+    stft_options::window signature, evaluated over N like fill_window)."""
+    a = np.asarray(x)
+    f64 = a.dtype == np.float64
+    rt = np.float64 if f64 else np.float32
+    a = np.ascontiguousarray(np.atleast_2d(a), dtype=rt)
+    C, L = a.shape
+    frame = int(frame_size)
+    transform = frame if transform_size is None else int(transform_size)
+    overlap = frame // 2 if overlap_size is None else int(overlap_size)
+    N = 1 << next_order(transform)
+    if isinstance(window, str):
+        if window == "hann":
+            w = None  # computed by the library in the transform's precision
+        elif window == "rectangular":
+            w = np.ones(N, rt)
+        else:
+            raise ValueError(f"unknown window {window!r}")
+    elif callable(window):
+        w = np.array([window(i, N) for i in range(N)], dtype=rt)
+    else:
+        w = np.ascontiguousarray(window, dtype=rt)
+        if w.shape != (N,):
+            raise ValueError(f"window must have {N} values (the transform size)")
+    F = stft_num_frames(L, frame, overlap)
+    out = np.empty((C, F, N // 2 + 1), np.complex128 if f64 else np.complex64)
+    fn = _native.load().neo_hip_stft_f64 if f64 else _native.load().neo_hip_stft
+    wp = None if w is None else w.ctypes.data_as(ctypes.c_void_p)
+    _native.check(fn(a.ctypes.data_as(ctypes.c_void_p), C, L, frame, transform, overlap, wp,
+                     out.ctypes.data_as(ctypes.c_void_p), 0, int(device)))
+    return out

@@ -655,6 +655,49 @@ void oracle_direct_convolve(const float* signal, size_t n, const float* patch, s
 }
 
 /* ------------------------------------------------------------------------ */
+/* stft_plan (src/neo/fft/stft.hpp:40-109) with hann_window / any window      */
+/* ------------------------------------------------------------------------ */
+/* hann_window::operator() (math/windowing.hpp:29-41) in float, filled over size */
+void oracle_hann(size_t size, float* w)
+{
+    const float n = (float)(size - 1);
+    const float two_pi = (float)3.14159265358979323846 * 2.0f;
+    for (size_t i = 0; i < size; ++i) w[i] = 0.5f * (1.0f - cosf(two_pi * (float)i / n));
+}
+
+/* detail::num_sftf_frames (:21-25): idiv(L - frame + overlap, frame - overlap) + 1 */
+size_t oracle_stft_frames(size_t L, size_t frame, size_t overlap)
+{
+    const size_t hop = frame - overlap;
+    if (L <= frame) return 1; /* the reference underflows here; the build clamps */
+    return (L - frame + overlap + hop - 1) / hop + 1;
+}
+
+/* operator()(x) (:56-99): out [C][F][N/2+1] complex, window [N] */
+int oracle_stft(const float* x, size_t C, size_t L, size_t frame, size_t transform, size_t overlap,
+                const float* window, float* out)
+{
+    int order = 0;
+    while (((size_t)1 << order) < transform) ++order;
+    const size_t N = (size_t)1 << order, bins = N / 2 + 1, F = oracle_stft_frames(L, frame, overlap);
+    float* in = (float*)malloc(sizeof(float) * N);
+    if (!in) return -2;
+    for (size_t c = 0; c < C; ++c) {
+        for (size_t f = 0; f < F; ++f) {
+            const size_t start = f * frame - f * overlap;
+            const size_t cnt = L - start < frame ? L - start : frame;
+            memset(in, 0, sizeof(float) * N);                                   /* fill(in, 0) */
+            memcpy(in, x + c * L + start, sizeof(float) * cnt);                 /* copy */
+            for (size_t i = 0; i < N; ++i) in[i] = in[i] * window[i];           /* multiply */
+            int rc = oracle_rfft(order, in, out + 2 * bins * (c * F + f));      /* _rfft(in, out) */
+            if (rc) { free(in); return rc; }
+        }
+    }
+    free(in);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
 /* splitmix64 -> U[-1,1) float32 (the documented generator)      */
 /* ------------------------------------------------------------------------ */
 static uint64_t splitmix64(uint64_t* s)

@@ -19,6 +19,10 @@ typedef struct oracle_upola2 oracle_upola2;
 oracle_upola2* oracle_upola2_create(size_t P, size_t bins, const float* H);
 void oracle_upola2_destroy(oracle_upola2* u);
 int oracle_upola2_process(oracle_upola2* u, float* inout, size_t num_samples);
+void oracle_hann(size_t size, float* w);
+size_t oracle_stft_frames(size_t L, size_t frame, size_t overlap);
+int oracle_stft(const float* x, size_t C, size_t L, size_t frame, size_t transform, size_t overlap,
+                const float* window, float* out);
 int oracle_fft_c2c_f64(int order, int dir, double* x);
 int oracle_rfft_f64(int order, const double* in, double* out);
 int oracle_irfft_f64(int order, const double* in, double* out);

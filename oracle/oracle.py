@@ -63,6 +63,10 @@ def lib():
         L.oracle_upola2_create.restype = ctypes.c_void_p
         L.oracle_upola2_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_upola2_process.argtypes = [ctypes.c_void_p, _f32p, _sz]
+        L.oracle_hann.argtypes = [_sz, _f32p]
+        L.oracle_stft_frames.argtypes = [_sz, _sz, _sz]
+        L.oracle_stft_frames.restype = _sz
+        L.oracle_stft.argtypes = [_f32p, _sz, _sz, _sz, _sz, _sz, _f32p, _f32p]
         L.oracle_fft_c2c_f64.argtypes = [ctypes.c_int, ctypes.c_int, _f64p]
         L.oracle_rfft_f64.argtypes = [ctypes.c_int, _f64p, _f64p]
         L.oracle_irfft_f64.argtypes = [ctypes.c_int, _f64p, _f64p]
@@ -344,3 +348,28 @@ def direct_convolve_f64(signal: np.ndarray, patch: np.ndarray) -> np.ndarray:
     out = np.empty(a.size + b.size - 1, np.float64)
     lib().oracle_direct_convolve_f64(a, a.size, b, b.size, out)
     return out
+
+
+# ---------------------------------------------------------------- STFT
+def hann(size: int) -> np.ndarray:
+    """hann_window (math/windowing.hpp:29-41) in float over `size` points."""
+    w = np.empty(size, np.float32)
+    lib().oracle_hann(size, w)
+    return w
+
+
+def stft_frames(length: int, frame: int, overlap: int) -> int:
+    return int(lib().oracle_stft_frames(length, frame, overlap))
+
+
+def stft(x: np.ndarray, frame: int, transform: int, overlap: int, window: np.ndarray) -> np.ndarray:
+    """stft_plan::operator() (stft.hpp:56-99): [C][L] -> [C][F][N/2+1] complex64."""
+    x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
+    C, L = x.shape
+    N = 1 << (int(transform) - 1).bit_length()
+    F = stft_frames(L, frame, overlap)
+    out = np.empty(C * F * (N // 2 + 1) * 2, np.float32)
+    w = np.ascontiguousarray(window, dtype=np.float32)
+    if lib().oracle_stft(x, C, L, frame, transform, overlap, w, out):
+        raise RuntimeError("oracle stft failed")
+    return out.view(np.complex64).reshape(C, F, N // 2 + 1)

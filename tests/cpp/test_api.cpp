@@ -261,6 +261,31 @@ static void test_double_precision()
     }
 }
 
+static void test_stft()
+{
+    // stft_test.cpp:15-37 shapes, and values against the restatement (hann over N)
+    for (std::size_t len : {2040, 2048}) {
+        std::vector<float> x(len, 0.0F);
+        auto const no_overlap = neo::fft::stft(neo::hip::make_matrix_view(x.data(), 1, len),
+                                               neo::fft::stft_options<float>{256, 256, 0});
+        REQUIRE(no_overlap.extent(0) == 1 && no_overlap.extent(1) == 8 && no_overlap.extent(2) == 129);
+        auto const half = neo::fft::stft(neo::hip::make_matrix_view(x.data(), 1, len), 256);
+        REQUIRE(half.extent(0) == 1 && half.extent(1) == 16 && half.extent(2) == 129);
+    }
+    auto const x = rnoise(71, 3000);
+    auto const S = neo::fft::stft(neo::hip::make_matrix_view(x.data(), 1, 3000), 256);
+    std::vector<float> w(256), ref(S.size() * 2);
+    oracle_hann(256, w.data());
+    oracle_stft(x.data(), 1, 3000, 256, 256, 128, w.data(), ref.data());
+    double peak = 0, err = 0;
+    for (std::size_t i = 0; i < S.size(); ++i) {
+        cf const r{ref[2 * i], ref[2 * i + 1]};
+        peak = std::max(peak, double(std::abs(r)));
+        err = std::max(err, double(std::abs(S.buf[i] - r)));
+    }
+    REQUIRE(err / peak <= 1e-5);
+}
+
 static void test_one_shot_convolve()
 {
     auto const x = rnoise(55, 1000), p = rnoise(56, 333);
@@ -322,6 +347,7 @@ int main()
     test_one_shot_convolve();
     test_upola_v2_pieces_vs_oracle();
     test_double_precision();
+    test_stft();
     std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);
     return failures ? 1 : 0;
 }

@@ -248,3 +248,57 @@ def test_max_order_round_trips(neo_gpu):
     neo_gpu.fft.FFTPlan(2, order, 1).execute_device(R.data_ptr(), back.data_ptr(), +1, 0)
     torch.cuda.synchronize()
     assert ((back / n - r).abs().max() / r.abs().max()).item() <= 1e-5
+
+
+# ------------------------------------------------------------------ STFT (stft.hpp:40-125)
+@pytest.mark.parametrize("length", [2040, 2048])
+def test_stft_reference_shapes(neo_gpu, length):
+    """stft_test.cpp:15-37: no overlap -> 8 x 129, stft(x, 256) (half overlap) -> 16 x 129."""
+    x = np.zeros((1, length), np.float32)
+    assert neo_gpu.fft.stft(x, 256, 256, 0).shape == (1, 8, 129)
+    assert neo_gpu.fft.stft(x, 256).shape == (1, 16, 129)
+    assert neo_gpu.fft.stft(x.astype(np.float64), 256).shape == (1, 16, 129)
+
+
+@pytest.mark.parametrize("C,L,frame,transform,overlap", [(1, 2040, 256, 256, 128), (3, 5000, 300, 512, 100),
+                                                         (2, 100, 64, 64, 0), (1, 48000, 1024, 2048, 512),
+                                                         (2, 10, 16, 16, 8)])
+@pytest.mark.parametrize("window", ["hann", "rectangular", "custom"])
+def test_stft_vs_oracle(neo_gpu, oracle, C, L, frame, transform, overlap, window):
+    x = np.stack([oracle.noise(900 + c, L) for c in range(C)])
+    N = 1 << (transform - 1).bit_length()
+    if window == "hann":
+        w, arg = oracle.hann(N), "hann"
+    elif window == "rectangular":
+        w = np.ones(N, np.float32)
+        arg = "rectangular"
+    else:
+        w = (oracle.noise(77, N) * 0.5 + 1).astype(np.float32)
+        arg = w
+    got = neo_gpu.fft.stft(x, frame, transform, overlap, window=arg)
+    ref = oracle.stft(x, frame, transform, overlap, w)
+    assert got.shape == ref.shape
+    assert peak_err(got, ref) <= TOL
+
+
+def test_stft_f64(neo_gpu, oracle):
+    rng = np.random.default_rng(5)
+    x = rng.random((2, 3000)) * 2 - 1
+    got = neo_gpu.fft.stft(x, 256, 512, 64, window="rectangular")
+    assert got.dtype == np.complex128
+    F = got.shape[1]
+    truth = np.empty_like(got)
+    for c in range(2):
+        for f in range(F):
+            seg = x[c, f * 192:f * 192 + 256]
+            truth[c, f] = np.fft.rfft(np.pad(seg, (0, 512 - len(seg))))
+    assert peak_err(got, truth) <= 1e-12
+
+
+def test_uniform_partition_is_a_rectangular_stft(neo_gpu, oracle):
+    """uniform_partition.hpp:12-26 = stft(frame B, transform 2B, overlap 0, rectangular)."""
+    ir = np.stack([oracle.noise(950 + c, 3000) for c in range(2)])
+    H = neo_gpu.uniform_partition(ir, 256)
+    S = neo_gpu.fft.stft(ir, 256, 512, 0, window="rectangular")
+    assert H.shape == S.shape
+    assert peak_err(H, S) <= TOL

@@ -350,3 +350,21 @@ def test_convolve_f64_matches_numpy(oracle, n, m):
     truth = np.convolve(x, p)
     assert peak_err(oracle.direct_convolve_f64(x, p), truth) < 1e-13
     assert peak_err(oracle.fft_convolve_f64(x, p), truth) < 1e-13
+
+
+def test_stft_frames_and_values(oracle):
+    """stft_test.cpp:8-13 (num_sftf_frames KATs) and the restatement of stft_plan against
+    float64 numpy on the same frames and hann window."""
+    assert oracle.stft_frames(1024, 128, 0) == 8
+    assert oracle.stft_frames(1024, 256, 0) == 4
+    assert oracle.stft_frames(1024, 256, 128) == 8
+    x = oracle.noise(5, 2040)
+    w = oracle.hann(256)
+    S = oracle.stft(x, 256, 256, 128, w)
+    assert S.shape == (1, 16, 129)
+    xs, w64 = x.astype(np.float64), w.astype(np.float64)
+    truth = []
+    for f in range(16):
+        seg = xs[f * 128:f * 128 + 256]
+        truth.append(np.fft.rfft(np.pad(seg, (0, 256 - len(seg))) * w64))
+    assert peak_err(S[0], np.stack(truth)) < 1e-6
