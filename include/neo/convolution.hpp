@@ -38,6 +38,21 @@ enum struct method
     upols,
 };
 
+/// mode.hpp:12-29 (only `full` has an output size, like the reference)
+enum struct mode
+{
+    full,
+    valid,
+    same,
+};
+
+template<mode Mode, std::integral Int>
+[[nodiscard]] constexpr auto output_size(Int signal, Int patch) -> Int
+{
+    static_assert(Mode == mode::full, "the reference defines output_size for mode::full only");
+    return static_cast<Int>(signal + patch - Int(1));
+}
+
 /// fdl_index.hpp:12-41 — insert(write_pos), then for segment s: multiply(s, (write_pos + P - s) % P)
 template<typename IndexType = std::size_t>
 struct fdl_index {

@@ -321,6 +321,8 @@ static void test_uniform_partition_shapes()
     }
 }
 
+static_assert(neo::convolution::output_size<neo::convolution::mode::full>(1000, 333) == 1332);
+
 static void test_rfftfreq()
 {
     // extra/python/test/test.py:65-68 through the C++ header (host arithmetic)
