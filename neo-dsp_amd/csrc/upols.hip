@@ -578,7 +578,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     const int bt = batch_t(block, h->bNB, h->bT);
     int Sb = std::max(1, std::min({(btarget + channels - 1) / channels, partitions / (2 * bt), 64}));
     if (h->ring - partitions < bt - 1) h->batch = false;  // ring too short for a batch
-    h->rows_b = (partitions + Sb - 1) / Sb;
+    h->rows_b = ((partitions + Sb - 1) / Sb + kMaxBatch - 1) / kMaxBatch * kMaxBatch;  // whole chunks of any T
     h->Sb = (partitions + h->rows_b - 1) / h->rows_b;
     const size_t rowbytes = size_t(block) * sizeof(cf);
     const size_t nrows = size_t(channels) * size_t(h->ring);  // H uses the first P rows of each channel

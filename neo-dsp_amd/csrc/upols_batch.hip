@@ -67,13 +67,12 @@ __device__ __forceinline__ void batch_step(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)
 {
     constexpr int slot = U % D;
     bvec<NB> hv[VPT];
-    const bool valid = p < p1;  // the last chunk of a split may run past p1: zero filter row
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
         f[(T - U) % T][v] = pf[slot][v];
-        hv[v] = valid ? ph[slot][v] : bvec<NB>(0.0f);
+        hv[v] = ph[slot][v];
     }
-    const int pn = p + D < p1 ? p + D : p1 - 1;  // past the end: a harmless re-read, no branch
+    const int pn = p + D < ring ? p + D : ring - 1;  // stay inside the allocated rows
     {
         int r = w - pn;
         r = r < 0 ? r + ring : r;
@@ -148,7 +147,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
     V ph[D][VPT], pf[D][VPT];
 #pragma unroll
     for (int d = 0; d < D; ++d) {  // prefetch partitions p0 .. p0 + D - 1
-        const int p = p0 + d < p1 ? p0 + d : p0;
+        const int p = p0 + d < ring ? p0 + d : ring - 1;  // past P: zero filter rows
         int r = w - p;
         r = r < 0 ? r + ring : r;
 #pragma unroll
@@ -157,6 +156,8 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
             ph[d][v] = __builtin_nontemporal_load(Hv + int64_t(p) * psv + tid + v * L);
         }
     }
+    // splits hold a multiple of T partitions; the last split's final chunk runs past P into
+    // the ring's spare filter rows, which are zero (so those steps add nothing)
     for (int pb = p0; pb < p1; pb += T)
         batch_chunk<T, NB, VPT, L, D>(a, f, ph, pf, Hv, Fv, psv, tid, ring, w, pb, p1,
                                       std::make_integer_sequence<int, T>{});
