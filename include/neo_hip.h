@@ -129,7 +129,9 @@ NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in,
                                               int64_t ld_out, int64_t num_samples, int is_device, void* stream);
 NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
 /* MAC-kernel timing with HIP events recorded on the launch stream (for the
- * roofline in bench.py): enable, then read the accumulated ms / launch count. */
+ * roofline in bench.py): enable = n > 0 brackets every n-th MAC launch with an
+ * event pair (0 = off); timing() returns the summed ms and the count of timed
+ * launches. */
 NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable);
 NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches);
 NEO_HIP_API int neo_hip_upols_info(neo_hip_upols* h, int* channels, int* block, int* partitions, int* splits);

@@ -416,7 +416,8 @@ void destroy(upols_t* h)
 int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (h->timing) {
+    const bool timed = h->timing && h->tick++ % h->timing == 0;
+    if (timed) {
         if (h->events_used == h->events.size()) {
             NEO_HIP_CHECK(hipEventCreate(&ev.first));
             NEO_HIP_CHECK(hipEventCreate(&ev.second));
@@ -438,7 +439,7 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
     }
 #undef NEO_STEP
     NEO_HIP_LAUNCH_CHECK();
-    if (h->timing) {
+    if (timed) {
         NEO_HIP_CHECK(hipEventRecord(ev.second, s));
         ++h->events_used;
     }
@@ -806,7 +807,9 @@ NEO_HIP_API int neo_hip_upols_set_batch(neo_hip_upols* h, int enable)
 NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable)
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
-    h->timing = enable != 0;
+    if (enable < 0) return fail(NEO_HIP_EINVAL, "timing stride %d < 0", enable);
+    h->timing = enable;
+    h->tick = 0;
     return NEO_HIP_OK;
 }
 

@@ -307,7 +307,8 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     }
     NEO_HIP_LAUNCH_CHECK();
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (h->timing) {
+    const bool timed = h->timing && h->tick++ % h->timing == 0;
+    if (timed) {
         if (h->events_used == h->events.size()) {
             NEO_HIP_CHECK(hipEventCreate(&ev.first));
             NEO_HIP_CHECK(hipEventCreate(&ev.second));
@@ -323,7 +324,7 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s)))
     }
     if (rc) return rc;
-    if (h->timing) {
+    if (timed) {
         NEO_HIP_CHECK(hipEventRecord(ev.second, s));
         ++h->events_used;
     }

@@ -36,7 +36,8 @@ struct neo_hip_upols {
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
     size_t samples_cap = 0;
-    bool timing = false;
+    int timing = 0;          // 0: off; n: HIP events around every n-th MAC launch
+    int64_t tick = 0;        // MAC launches seen while timing
     bool ola = false;  // upola_convolver (overlap-add stage) instead of upols (overlap-save)
     bool v2 = false;   // upola_convolver_v2: sub-block input (implies ola)
     int in_pos = 0;    // v2: samples of the current block already consumed (_input_pos)

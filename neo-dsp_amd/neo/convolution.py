@@ -206,8 +206,11 @@ class UpolsConvolver:
         return t.value, s.value
 
     # -- instrumentation ------------------------------------------------------
-    def set_timing(self, enable: bool) -> None:
-        _native.check(_native.load().neo_hip_upols_set_timing(self._h, int(enable)))
+    def set_timing(self, enable, every: int = 1) -> None:
+        """HIP events around every `every`-th MAC launch while enabled (bench instrumentation)."""
+        if every < 1:
+            raise ValueError("every must be >= 1")
+        _native.check(_native.load().neo_hip_upols_set_timing(self._h, int(every) if enable else 0))
 
     def timing(self):
         """(accumulated MAC-kernel ms, launches) since the last call."""

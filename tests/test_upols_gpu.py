@@ -402,7 +402,7 @@ def test_process_samples_errors(neo_gpu):
                                       (128, 128 * 40, 2, 100)])
 def test_batched_blocks_vs_oracle(neo_gpu, oracle, method, B, L, C, nb):
     """process_blocks runs batch_cfg<B>::T blocks per MAC pass (sliding FDL window, ring of
-    P + 15 rows); leftover blocks and the FDL wraparound (nb > P) included."""
+    P + 31 rows); leftover blocks and the FDL wraparound (nb > P) included."""
     torch = pytest.importorskip("torch")
     ir = np.stack([oracle.noise(230 + c, L) for c in range(C)])
     parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
@@ -474,3 +474,22 @@ def test_every_batch_size(neo_gpu, oracle, monkeypatch, T, nbins):
         conv.process_blocks(t)
         torch.cuda.synchronize()
         assert peak_err(t.cpu().numpy(), ref) <= TOL, method
+
+
+def test_timing_stride(neo_gpu):
+    """set_timing(every=n) brackets every n-th MAC launch with a HIP event pair."""
+    torch = pytest.importorskip("torch")
+    conv = neo_gpu.UpolsConvolver(2, 128, 5)
+    conv.set_batch(False)
+    x = torch.zeros((2, 128 * 10), device="cuda")
+    conv.set_timing(True, every=4)
+    conv.process_blocks(x)
+    conv.set_timing(False)
+    ms, n = conv.timing()
+    assert n == 3 and ms > 0  # launches 0, 4, 8
+    conv.set_timing(True)
+    conv.process_blocks(x)
+    conv.set_timing(False)
+    assert conv.timing()[1] == 10
+    with pytest.raises(ValueError):
+        conv.set_timing(True, every=0)
