@@ -765,8 +765,6 @@ NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in,
     const size_t count = size_t(h->C) * size_t(num_samples);
     if (count > h->samples_cap) {
         (void)hipFree(h->samples_dev);
-    (void)hipFree(h->part_b);
-    (void)hipFree(h->tail);
         if (h->samples_host) (void)hipHostFree(h->samples_host);
         h->samples_dev = nullptr;
         h->samples_host = nullptr;

@@ -493,3 +493,32 @@ def test_timing_stride(neo_gpu):
     assert conv.timing()[1] == 10
     with pytest.raises(ValueError):
         conv.set_timing(True, every=0)
+
+
+def test_host_staging_growth_keeps_batch_buffers(neo_gpu, oracle):
+    """Host process() with a growing staging buffer between batched device passes: the
+    batched partial / tail buffers stay valid (regression: the staging growth path freed
+    them)."""
+    torch = pytest.importorskip("torch")
+    B, L, C = 128, 3000, 2
+    ir = np.stack([oracle.noise(300 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    for method in ("upols", "upola"):
+        sig = np.stack([oracle.noise(310 + c, B * 120) for c in range(C)])
+        ref = oracle.dense_convolve(sig, parts, method=method)
+        conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
+        conv.filter(parts)
+        out = np.empty_like(sig)
+        pos = 0
+        for kind, n in [("dev", 32), ("host", 2), ("dev", 32), ("host", 16), ("dev", 32), ("host", 6)]:
+            seg = np.ascontiguousarray(sig[:, pos * B:(pos + n) * B])
+            if kind == "dev":
+                t = torch.from_numpy(seg).cuda()
+                conv.process_blocks(t)
+                torch.cuda.synchronize()
+                seg = t.cpu().numpy()
+            else:
+                conv.process(seg)  # staging grows 2 -> 16 blocks
+            out[:, pos * B:(pos + n) * B] = seg
+            pos += n
+        assert peak_err(out, ref) <= TOL, method
