@@ -9,7 +9,15 @@ channels are independent, so there is no collective on the data path — torch
 .distributed (gloo) only carries the timing barrier and the max-over-ranks).
 
 A "step" = one block of B samples through the whole convolver for every channel
-(r2c + FDL insert + partitioned MAC + c2r), inputs already resident in HBM.
+(r2c + FDL insert + partitioned MAC + c2r), inputs already resident in HBM, one
+block per call as a real-time caller runs it. The convolver's default streaming
+form is the lookahead (neo_hip_upols_set_ahead): the first block of every 32-block
+window runs one pass over filter + FDL (k_batch_mac) that also accumulates, for the
+window's later blocks, every partition whose FDL row already exists; each block then
+adds the partitions of the window's own blocks (k_upols_ahead). Every block's output
+is complete when its step returns (same latency, same products as the plain step).
+`roofline` is that window pass; `per_block_step` is the plain one-pass-per-block
+step (k_upols_step) timed in the same run; `offline` has all blocks up front.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c4|c3|c2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -43,10 +51,12 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=128)  # 4 lookahead windows of 32 blocks
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS) + ["c2"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ahead", action="store_true", help="headline = the plain one-pass-per-block step")
+    ap.add_argument("--no-offline", action="store_true", help="skip the batched (blocks up front) line")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--host-io", action="store_true",
                     help="time the host-buffer boundary (neo_hip_upols_process on pinned-staged host memory): "
@@ -99,16 +109,16 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def load_pmc_traffic(workload: str):
-    """HBM bytes per MAC launch from the committed rocprofv3 --pmc summary (separate
-    passes; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+def load_pmc_traffic(workload: str, kernel: str = ""):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 --pmc summary
+    for `workload` (separate passes; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            if d.get("workload") == workload and kernel in d.get("kernel", "") and d.get("hbm_bytes_per_launch"):
                 return float(d["hbm_bytes_per_launch"])
         except (OSError, ValueError):
             continue
@@ -195,7 +205,7 @@ def run_upols(args, world, rank, local):
     torch.cuda.set_device(dev)
     P = neo.num_partitions(L, B)
     conv = neo.UpolsConvolver(C, B, P, device=local)
-    conv.set_batch(False)  # streaming: one MAC pass per block, as a real-time caller runs it
+    conv.set_batch(False)  # streaming: one block per step, as a real-time caller runs it
     g = torch.Generator(device=dev).manual_seed(8 + rank)
     ir = torch.rand((C, L), generator=g, device=dev).mul_(2).sub_(1)  # synthetic white-noise IR
     conv.set_impulse(ir, normalize=True)
@@ -209,36 +219,62 @@ def run_upols(args, world, rank, local):
 
     # the block loop runs in the C-ABI (neo_hip_upols_process_blocks), one step = one block
     wb = max(args.warmup, 1)
-    t_warm = time.perf_counter()
-    conv.process_blocks_ptr(xp, yp, ld, wb, stream)
-    torch.cuda.synchronize()
-    while time.perf_counter() - t_warm < WARM_SECONDS:  # untimed; re-runs the warm-up blocks
+    off = 4 * wb * B  # timed blocks follow the warm-up blocks
+
+    def timed_steps():
+        """Warm up, then time args.steps single-block steps; MAC-kernel duration from HIP
+        events recorded on the launch stream around every n-th MAC launch of the timed
+        steps (the C-ABI's timing mode; sampled so that the event records stay a small
+        part of a launch-bound step like C3's)."""
+        t_warm = time.perf_counter()
         conv.process_blocks_ptr(xp, yp, ld, wb, stream)
         torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    # MAC-kernel duration: HIP events recorded on the launch stream around every n-th MAC
-    # launch of the timed steps (the C-ABI's timing mode; sampled so that the event
-    # records stay a small part of a launch-bound step like C3's)
-    conv.timing()  # drain
-    conv.set_timing(True, every=timing_stride(args.steps))
-    t0 = time.perf_counter()
-    off = 4 * max(args.warmup, 1) * B
-    conv.process_blocks_ptr(xp + off, yp + off, ld, args.steps, stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    t1 = time.perf_counter()
-    conv.set_timing(False)
-    mac_ms, launches = conv.timing()
-    assert torch.isfinite(y[:, max(args.warmup, 1) * B:]).all().item()
-    elapsed = max_over_ranks(t1 - t0, world)
-    mac_avg_ms = max_over_ranks(mac_ms / max(launches, 1), world)
+        while time.perf_counter() - t_warm < WARM_SECONDS:  # untimed; re-runs the warm-up blocks
+            conv.process_blocks_ptr(xp, yp, ld, wb, stream)
+            torch.cuda.synchronize()
+        if conv.ahead_info()[0]:
+            conv.set_ahead(True)  # the timed steps start a lookahead window (phase 0)
+        barrier(world)
+        torch.cuda.synchronize()
+        conv.timing()  # drain
+        conv.set_timing(True, every=timing_stride(args.steps))
+        t0 = time.perf_counter()
+        conv.process_blocks_ptr(xp + off, yp + off, ld, args.steps, stream)
+        torch.cuda.synchronize()
+        barrier(world)
+        t1 = time.perf_counter()
+        conv.set_timing(False)
+        mac_ms, launches = conv.timing()
+        assert torch.isfinite(y[:, wb * B:]).all().item()
+        return max_over_ranks(t1 - t0, world), max_over_ranks(mac_ms / max(launches, 1), world)
+
+    samples = world * C * B * args.steps
+    bytes_step = C * (16 * P * B + 20 * B)  # filter + FDL stream (packed bins) + FDL row write + in/prev
+    # the plain single-block step: one pass over filter + FDL per block (k_upols_step)
+    conv.set_ahead(False)
+    el_plain, mac_plain = timed_steps()
+    gbs_plain = bytes_step / (mac_plain * 1e-3) / 1e9
+    plain = {"value": samples / el_plain / 1e6, "ms_per_step": el_plain * 1e3 / args.steps,
+             "kernel": f"k_upols_step<{B}>", "kernel_avg_ms": mac_plain, "algorithmic_bytes_per_launch": bytes_step,
+             "achieved_gbs": gbs_plain, "frac": gbs_plain / PEAK_HBM_GBS,
+             "traffic": load_pmc_traffic(args.workload + "_plain", "k_upols_step")}
+    ahead, _, T, sb = conv.ahead_info()
+    ahead = not args.no_ahead
+    conv.set_ahead(ahead)
+    if ahead:
+        # streaming lookahead (the default): one k_batch_mac pass per T-block window over
+        # filter + FDL that also accumulates every partition already available for the
+        # window's later blocks; each block step (k_upols_ahead) adds the rest
+        elapsed, mac_avg_ms = timed_steps()
+        bytes_mac = C * 8 * B * (2 * P + sb * T)  # filter rows + FDL rows read, T partial slabs per split written
+        kernel = f"k_batch_mac<{B},{T},1> (lookahead window pass, 1 per {T} blocks)"
+        steps_per_launch = T
+    else:
+        elapsed, mac_avg_ms, bytes_mac, kernel, steps_per_launch = el_plain, mac_plain, bytes_step, plain["kernel"], 1
+    achieved = bytes_mac / (mac_avg_ms * 1e-3) / 1e9
 
     offline = run_upols_offline(args, conv, C, B, P, xp, yp, ld, stream, world)
 
-    samples = world * C * B * args.steps
-    bytes_mac = C * (16 * P * B + 20 * B)  # filter + FDL stream (packed bins) + FDL row write + in/prev
-    achieved = bytes_mac / (mac_avg_ms * 1e-3) / 1e9
     res = {
         "metric": "Msamples/sec UPOLS convolver (block=512, IR=10s@48k); achieved HBM GB/s",
         "value": samples / elapsed / 1e6,
@@ -253,14 +289,17 @@ def run_upols(args, world, rank, local):
         "dtype": "f32",
         "data": "synthetic (U[-1,1) white-noise input and IR, torch.rand on device)",
         "config": {"workload": f"UPOLS {args.workload}: {C} ch/GPU x {world} GPU, B={B}, L={L} taps (P={P}), "
-                               f"channel-sharded",
+                               f"channel-sharded, one block per step",
                    "channels_per_gpu": C, "channels_total": C * world, "block": B, "taps": L, "partitions": P,
-                   "splits": conv.splits, "parallelism": f"channel-shard x{world} (no collective)"},
+                   "splits": sb if ahead else conv.splits, "lookahead_window": T if ahead else 1,
+                   "parallelism": f"channel-shard x{world} (no collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS, "traffic": load_pmc_traffic(args.workload),
-                     "kernel": f"k_upols_step<{B}>", "kernel_avg_ms": mac_avg_ms,
+                     "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": (load_pmc_traffic(args.workload, "k_batch_mac") if ahead
+                                 else load_pmc_traffic(args.workload + "_plain", "k_upols_step")),
+                     "kernel": kernel, "kernel_avg_ms": mac_avg_ms, "steps_per_launch": steps_per_launch,
                      "algorithmic_bytes_per_launch": bytes_mac, "d2d_copy_gbs": copy_ceiling_gbs(dev)},
-        "effective_hbm_gbs_step": bytes_mac * world / (elapsed / args.steps) / 1e9 / world,
+        "per_block_step": plain,
         "offline": offline,
     }
     if args.workload == "c3":
@@ -277,7 +316,7 @@ def run_upols_offline(args, conv, C, B, P, xp, yp, ld, stream, world):
     conv.set_batch(True)
     T, splits = conv.batch_info()
     nb = (args.steps // T) * T
-    if nb == 0:
+    if nb == 0 or args.no_offline:
         conv.set_batch(False)
         return None
     t_warm = time.perf_counter()
@@ -300,10 +339,11 @@ def run_upols_offline(args, conv, C, B, P, xp, yp, ld, stream, world):
     mac_avg_ms = max_over_ranks(mac_ms / max(launches, 1), world)
     bytes_pass = C * 16 * P * B  # filter + FDL streamed once per pass of T blocks
     gbs = bytes_pass / (mac_avg_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.workload + "_offline")
+    traffic = load_pmc_traffic(args.workload + "_offline", "k_batch_mac")
     return {"value": world * C * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": T,
             "traffic": traffic, "traffic_over_algorithmic": traffic / bytes_pass if traffic else None,
             "ms_per_block": elapsed * 1e3 / nb, "splits": splits, "kernel": f"k_batch_mac<{B},{T},1>",
+            "algorithmic_bytes_per_launch": bytes_pass,
             "kernel_avg_ms": mac_avg_ms,
             "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS}
 

@@ -128,6 +128,16 @@ NEO_HIP_API int neo_hip_upols_batch_info(neo_hip_upols* h, int* blocks_per_pass,
 NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
                                               int64_t ld_out, int64_t num_samples, int is_device, void* stream);
 NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
+/* Streaming lookahead for single-block steps (upols / upola): the first block of
+ * each T-block window runs one batched pass over the filter and the FDL that also
+ * accumulates every partition already available for the window's later blocks;
+ * each block then adds only the partitions of the window's own blocks. Output is
+ * the same block by block (summation order differs), latency stays one block.
+ * Default on where a step is HBM-bound (not the one-launch form); v2 handles
+ * refuse it. Switching is allowed at any block boundary. */
+NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable);
+/* enabled, block position in the current window, window length T, splits of the pass */
+NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* phase, int* window, int* splits);
 /* MAC-kernel timing with HIP events recorded on the launch stream (for the
  * roofline in bench.py): enable = n > 0 brackets every n-th MAC launch with an
  * event pair (0 = off); timing() returns the summed ms and the count of timed

@@ -117,7 +117,7 @@ template<int B, int T, int NB, int D = (T < NEO_BATCH_D ? T : NEO_BATCH_D)>  // 
 __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf* __restrict__ H,
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
-                                                                   int64_t cstride, int64_t pstride)
+                                                                   int64_t cstride, int64_t pstride, int ahead)
 {
     using K = batch_cfg<B, NB>;
     using V = bvec<NB>;
@@ -136,13 +136,18 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
     for (int j = 0; j < T; ++j)
 #pragma unroll
         for (int v = 0; v < NB * VPT; ++v) a[j][v] = {f2v(0.0f), f2v(0.0f)};
+    // ahead (streaming lookahead, see k_upols_ahead): blocks 0..T-1 are not in the FDL yet,
+    // so rows w .. w+T-1 (the prologue window and the first row entering it) count as zero
+    // and block j collects partitions p > j only
+    const bool future = ahead && p0 == 0;
     V f[T][VPT];
 #pragma unroll
     for (int sl = 1; sl < T; ++sl) {  // rows block sl needs at p0
         int r = w + sl - p0;
         r = r < 0 ? r + ring : (r >= ring ? r - ring : r);
 #pragma unroll
-        for (int v = 0; v < VPT; ++v) f[sl][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
+        for (int v = 0; v < VPT; ++v)
+            f[sl][v] = future ? V{} : __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
     }
     V ph[D][VPT], pf[D][VPT];
 #pragma unroll
@@ -152,7 +157,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
         r = r < 0 ? r + ring : r;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-            pf[d][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
+            pf[d][v] = future && d == 0 ? V{} : __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
             ph[d][v] = __builtin_nontemporal_load(Hv + int64_t(p) * psv + tid + v * L);
         }
     }
@@ -259,9 +264,83 @@ __global__ __launch_bounds__(256) void k_batch_ola(float* __restrict__ out, int6
     }
 }
 
+// Streaming lookahead: one block step of a T-block window (block j = 0..T-1 of the window
+// that started at FDL row w0 = w - j; grid C, 256 lanes). At j = 0 a k_batch_mac pass with
+// `ahead` already accumulated, for every block of the window, the partitions whose FDL rows
+// existed then (p > j for block j) into the slabs part[c][s][j]. This step completes block j
+// with the rest, p = 0..j, whose rows are the window's own blocks:
+//   X = rfft(window) -> FDL row w;  Y = sum_s slab[s][j] + H0 X + sum_{p=1..j} H_p FDL[w - p]
+//   out = irfft(Y) / 2B (OLS: last B samples; OLA: first B + overlap)
+// The same products as a single-block step, in a different summation order; per block the
+// HBM traffic is the slabs and j <= T-1 row pairs instead of all P partitions.
+template<int B, bool OLA>
+__global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ in, int64_t ld_in,
+                                                     float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
+                                                     const cf* __restrict__ H, cf* __restrict__ fdl,
+                                                     const cf* __restrict__ part, int S, int T, int j,
+                                                     const cf* __restrict__ twg, int ring, int w, int64_t cstride,
+                                                     int64_t pstride)
+{
+    using K = upols_cfg<B>;
+    __shared__ __attribute__((aligned(16))) cf X[B];
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    const int tid = threadIdx.x, c = blockIdx.x;
+    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+    const float* in_c = in + int64_t(c) * ld_in;
+    float* prev_c = prev + int64_t(c) * B;
+    window_fft<B, OLA>(prev_c, in_c, fft, tw, tid);
+    const int64_t crow = int64_t(c) * cstride;
+    cf* row = fdl + crow + int64_t(w) * pstride;
+    for (int k = tid; k < B; k += 256) {
+        const cf x = r2c_split<B>(fft, tw + K::TW1, k);
+        X[k] = x;
+        row[k] = x;
+    }
+    if constexpr (!OLA) {  // the window's second half becomes the next call's first half
+        for (int i = tid; i < B / 4; i += 256)
+            reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
+    }
+    __syncthreads();
+    const int64_t ps4 = pstride / 2;
+    const float4* H4 = reinterpret_cast<const float4*>(H + crow);
+    const float4* F4 = reinterpret_cast<const float4*>(fdl + crow);
+    const float4* S4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * T * B + int64_t(j) * B);
+    const int64_t ss4 = int64_t(T) * K::Q;  // float4 between the slabs of one block
+    for (int q = tid; q < K::Q; q += 256) {  // lane-private bins 2q, 2q + 1
+        acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+        mac2(a0, a1, H4[q], reinterpret_cast<const float4*>(X)[q]);
+        int p = 1;
+        for (; p + 3 <= j; p += 4) {  // four row pairs in flight
+            float4 hv[4], xv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = w - p - u < 0 ? w - p - u + ring : w - p - u;
+                hv[u] = H4[int64_t(p + u) * ps4 + q];
+                xv[u] = F4[int64_t(r) * ps4 + q];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) mac2(a0, a1, hv[u], xv[u]);
+        }
+        for (; p <= j; ++p) {
+            const int r = w - p < 0 ? w - p + ring : w - p;
+            mac2(a0, a1, H4[int64_t(p) * ps4 + q], F4[int64_t(r) * ps4 + q]);
+        }
+        float4 sum = S4[q];
+        for (int t = 1; t < S; ++t) {
+            const float4 r = S4[t * ss4 + q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
+        reinterpret_cast<float4*>(X)[q] = make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
+    }
+    __syncthreads();
+    c2r_tail<B, OLA>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
+}
+
 // dispatch k_batch_mac over (B, NB, T) for the valid combinations
 template<int BB, int NB>
-int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
+int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead)
 {
     constexpr int L = batch_cfg<BB, NB>::L;
     const unsigned grid = unsigned(h->C) * unsigned(h->Sb) * unsigned(batch_cfg<BB, NB>::G);
@@ -269,7 +348,7 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
     case TT:                                                                                                     \
         if constexpr (batch_t(BB, NB, TT) == TT) {                                                               \
             hipLaunchKernelGGL((k_batch_mac<BB, TT, NB>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, \
-                               h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride);                      \
+                               h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride, ahead);               \
             break;                                                                                               \
         }                                                                                                        \
         return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);
@@ -288,15 +367,76 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
 
 // T consecutive blocks: window r2c + insert (C x T), one MAC pass (C x Sb), per-block
 // finish (C x T), OLA overlap chain (C).
+static int batch_buffers(upols_t* h)
+{
+    if (!h->part_b) {
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
+                                size_t(h->C) * h->Sb * kMaxBatch * h->B * sizeof(cf)));
+        if (h->ola)
+            NEO_HIP_CHECK(
+                hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * h->B * sizeof(float)));
+    }
+    return NEO_HIP_OK;
+}
+
+// timing events (neo_hip_upols_set_timing) around every n-th MAC launch
+static int mac_event(upols_t* h, bool timed, bool second, std::pair<hipEvent_t, hipEvent_t>& ev, hipStream_t s)
+{
+    if (!timed) return NEO_HIP_OK;
+    if (!second) {
+        if (h->events_used == h->events.size()) {
+            NEO_HIP_CHECK(hipEventCreate(&ev.first));
+            NEO_HIP_CHECK(hipEventCreate(&ev.second));
+            h->events.push_back(ev);
+        }
+        ev = h->events[h->events_used];
+        NEO_HIP_CHECK(hipEventRecord(ev.first, s));
+    } else {
+        NEO_HIP_CHECK(hipEventRecord(ev.second, s));
+        ++h->events_used;
+    }
+    return NEO_HIP_OK;
+}
+
+// One streaming block step in lookahead mode: at the first block of each T-block window a
+// k_batch_mac pass (ahead) over the filter and the FDL; then k_upols_ahead for the block.
+int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
+{
+    const int B = h->B, T = batch_blocks(h);
+    int rc = batch_buffers(h);
+    if (rc) return rc;
+    if (h->phase == 0) {
+        std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+        const bool timed = h->timing && h->tick++ % h->timing == 0;
+        if ((rc = mac_event(h, timed, false, ev, s))) return rc;
+        if (h->bNB == 2) {
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 1)))
+        } else {
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 1)))
+        }
+        if (rc) return rc;
+        if ((rc = mac_event(h, timed, true, ev, s))) return rc;
+    }
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_upols_ahead<BB, true>), dim3(unsigned(h->C)), dim3(256), 0, s, in,
+                                                 ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T,
+                                                 h->phase, h->tw, h->ring, h->wpos, h->cstride, h->pstride))
+    } else {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_upols_ahead<BB, false>), dim3(unsigned(h->C)), dim3(256), 0, s, in,
+                                                 ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T,
+                                                 h->phase, h->tw, h->ring, h->wpos, h->cstride, h->pstride))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
+    h->phase = h->phase + 1 >= T ? 0 : h->phase + 1;
+    return NEO_HIP_OK;
+}
+
 int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s)
 {
     const int B = h->B;
-    if (!h->part_b) {
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
-                                size_t(h->C) * h->Sb * kMaxBatch * B * sizeof(cf)));
-        if (h->ola)
-            NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * B * sizeof(float)));
-    }
+    int rc0 = batch_buffers(h);
+    if (rc0) return rc0;
     const unsigned gCT = unsigned(h->C) * unsigned(T);
     if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, true>), dim3(gCT), dim3(256), 0, s, in, ld_in,
@@ -308,26 +448,15 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     NEO_HIP_LAUNCH_CHECK();
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     const bool timed = h->timing && h->tick++ % h->timing == 0;
-    if (timed) {
-        if (h->events_used == h->events.size()) {
-            NEO_HIP_CHECK(hipEventCreate(&ev.first));
-            NEO_HIP_CHECK(hipEventCreate(&ev.second));
-            h->events.push_back(ev);
-        }
-        ev = h->events[h->events_used];
-        NEO_HIP_CHECK(hipEventRecord(ev.first, s));
-    }
-    int rc = NEO_HIP_OK;
+    int rc = mac_event(h, timed, false, ev, s);
+    if (rc) return rc;
     if (h->bNB == 2) {
-        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s)))
+        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 0)))
     } else {
-        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s)))
+        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 0)))
     }
     if (rc) return rc;
-    if (timed) {
-        NEO_HIP_CHECK(hipEventRecord(ev.second, s));
-        ++h->events_used;
-    }
+    if ((rc = mac_event(h, timed, true, ev, s))) return rc;
     if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_finish<BB, true>), dim3(gCT), dim3(256), 0, s, h->part_b,
                                                  h->Sb, T, in, ld_in, out, ld_out, h->prev, h->tail, h->tw))

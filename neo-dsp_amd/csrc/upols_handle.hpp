@@ -32,6 +32,10 @@ struct neo_hip_upols {
     int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
     int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
     neo_hip::cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
+    // streaming lookahead (k_upols_ahead): one batched pass per T blocks, phase = block of
+    // the current window; on for HBM-bound shapes (not fused), NEO_HIP_AHEAD / set_ahead
+    bool ahead = false;
+    int phase = 0;
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
@@ -101,6 +105,8 @@ inline int batch_blocks(const upols_t* h) { return batch_t(h->B, h->bNB, h->bT);
 
 // upols_batch.hip: T whole blocks in one pass over the filter and the FDL
 int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s);
+// upols_batch.hip: one streaming block step in lookahead mode
+int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
 // upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device
 int upload_tw(cf** d, int B);
 int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s,

@@ -46,6 +46,8 @@ SIGNATURES = {
     "neo_hip_upols_process_device": (_i, [_vp, _vp, _i64, _vp, _i64, _vp]),
     "neo_hip_upols_process_blocks": (_i, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "neo_hip_upols_reset": (_i, [_vp]),
+    "neo_hip_upols_set_ahead": (_i, [_vp, _i]),
+    "neo_hip_upols_get_ahead": (_i, [_vp] + [ctypes.POINTER(_i)] * 4),
     "neo_hip_upols_set_timing": (_i, [_vp, _i]),
     "neo_hip_upols_timing": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "neo_hip_upols_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),

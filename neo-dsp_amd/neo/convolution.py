@@ -205,6 +205,17 @@ class UpolsConvolver:
         _native.check(_native.load().neo_hip_upols_batch_info(self._h, ctypes.byref(t), ctypes.byref(s)))
         return t.value, s.value
 
+    def set_ahead(self, enable: bool) -> None:
+        """Streaming lookahead for single-block steps (neo_hip_upols_set_ahead)."""
+        _native.check(_native.load().neo_hip_upols_set_ahead(self._h, int(bool(enable))))
+
+    def ahead_info(self):
+        """(lookahead enabled, block position in the current window, window length T,
+        splits of the window pass)."""
+        v = [ctypes.c_int() for _ in range(4)]
+        _native.check(_native.load().neo_hip_upols_get_ahead(self._h, *[ctypes.byref(x) for x in v]))
+        return bool(v[0].value), v[1].value, v[2].value, v[3].value
+
     # -- instrumentation ------------------------------------------------------
     def set_timing(self, enable, every: int = 1) -> None:
         """HIP events around every `every`-th MAC launch while enabled (bench instrumentation)."""

@@ -522,3 +522,84 @@ def test_host_staging_growth_keeps_batch_buffers(neo_gpu, oracle):
             out[:, pos * B:(pos + n) * B] = seg
             pos += n
         assert peak_err(out, ref) <= TOL, method
+
+
+# ------------------------------------------------ streaming lookahead (k_batch_mac ahead + k_upols_ahead)
+@pytest.mark.parametrize("method", ["upols", "upola"])
+@pytest.mark.parametrize("B,L,C,nb", [(512, 20000, 3, 75), (256, 2560, 2, 70), (16, 100, 2, 40), (64, 64, 1, 37),
+                                      (1024, 30000, 2, 33), (4096, 12000, 1, 9), (128, 128 * 40, 2, 100)])
+def test_ahead_steps_vs_oracle(neo_gpu, oracle, method, B, L, C, nb):
+    """Single-block steps with lookahead: one batched pass per T-block window (p > j for
+    block j), the window's own partitions per step; P < T, P = 1 and ring wraparound."""
+    torch = pytest.importorskip("torch")
+    ir = np.stack([oracle.noise(320 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    sig = np.stack([oracle.noise(330 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts, method=method)
+    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
+    conv.filter(parts)
+    conv.set_batch(False)
+    conv.set_ahead(True)
+    assert conv.ahead_info()[:2] == (True, 0)
+    t = torch.from_numpy(sig).cuda()
+    conv.process_blocks(t)
+    torch.cuda.synchronize()
+    assert conv.ahead_info()[1] == nb % conv.ahead_info()[2]
+    assert peak_err(t.cpu().numpy(), ref) <= TOL
+
+
+def test_ahead_mixed_paths(neo_gpu, oracle):
+    """Lookahead steps, batched passes, plain steps and host blocks share one state; the
+    lookahead can be switched at any block boundary."""
+    torch = pytest.importorskip("torch")
+    B, L, C = 256, 9000, 3
+    ir = np.stack([oracle.noise(340 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    for method in ("upols", "upola"):
+        sig = np.stack([oracle.noise(350 + c, B * 150) for c in range(C)])
+        ref = oracle.dense_convolve(sig, parts, method=method)
+        conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
+        conv.filter(parts)
+        conv.set_ahead(True)
+        t = torch.from_numpy(sig).cuda()
+        pos = 0
+        for kind, n in [("one", 5), ("batch", 40), ("host", 3), ("off", 4), ("on", 0), ("one", 33), ("batch", 64),
+                        ("one", 1)]:
+            if kind == "on":
+                conv.set_ahead(True)
+                continue
+            seg = t[:, pos * B:(pos + n) * B].contiguous()
+            if kind == "off":
+                conv.set_ahead(False)
+                conv.set_batch(False)
+                conv.process_blocks(seg)
+                conv.set_batch(True)
+            elif kind == "batch":
+                conv.process_blocks(seg)  # lookahead steps up to the window end, then batches
+            elif kind == "one":
+                for i in range(n):
+                    blk = seg[:, i * B:(i + 1) * B].contiguous()
+                    conv(blk)
+                    seg[:, i * B:(i + 1) * B] = blk
+            else:
+                torch.cuda.synchronize()
+                h = seg.cpu().numpy().copy()
+                conv.process(h)
+                seg = torch.from_numpy(h).cuda()
+            t[:, pos * B:(pos + n) * B] = seg
+            pos += n
+        torch.cuda.synchronize()
+        assert peak_err(t[:, :pos * B].cpu().numpy(), ref[:, :pos * B]) <= TOL, method
+
+
+def test_ahead_defaults_and_errors(neo_gpu):
+    big = neo_gpu.UpolsConvolver(64, 512, 300)  # filter + FDL 157 MB: HBM-bound step
+    assert big.ahead_info()[0]
+    assert neo_gpu.UpolsConvolver(1, 512, 188).ahead_info()[0]  # C3
+    small = neo_gpu.UpolsConvolver(1, 128, 20)  # P < 2T: the plain step
+    assert not small.ahead_info()[0]
+    v2 = neo_gpu.UpolsConvolver(2, 128, 4, method="upola_v2")
+    assert not v2.ahead_info()[0]
+    with pytest.raises(RuntimeError):
+        v2.set_ahead(True)
+    v2.set_ahead(False)

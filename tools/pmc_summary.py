@@ -1,9 +1,13 @@
-"""Summarize rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into profiles/<tag>_pmc_<workload>.json.
+"""Summarize rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into profiles/<tag>_pmc_<label>.json.
 
 HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: rocprofv3 reports
 both in KiB, and on gfx950 FETCH_SIZE counts exactly half the bytes of a wide
 (16 B/lane) coalesced streaming read (MI355X_MICROARCH.md §HBM), so it is doubled.
-Usage: python tools/pmc_summary.py <tag> <workload> <kernel-substring> <algorithmic-bytes-per-launch>
+
+Usage:
+  python tools/pmc_summary.py <tag>      every pass of tools/gpu_pmc.sh <tag>, algorithmic
+                                         bytes taken from the same round's bench lines
+  python tools/pmc_summary.py <tag> <pmc-dir-workload> <kernel-substring> <alg-bytes> [label]
 """
 import csv
 import json
@@ -11,6 +15,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(REPO, "gpurun_out")
 
 
 def mean_counter(path, kernel):
@@ -22,21 +27,44 @@ def mean_counter(path, kernel):
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
 
-def main():
-    tag, workload, kernel, alg = sys.argv[1], sys.argv[2], sys.argv[3], float(sys.argv[4])
-    out = os.path.join(REPO, "gpurun_out")
-    fetch, nf = mean_counter(os.path.join(out, f"pmc_{workload}_FETCH_SIZE_{tag}", "run_counter_collection.csv"), kernel)
-    write, nw = mean_counter(os.path.join(out, f"pmc_{workload}_WRITE_SIZE_{tag}", "run_counter_collection.csv"), kernel)
+def summarize(tag, workload, kernel, alg, label=None):
+    label = label or workload
+    fetch, nf = mean_counter(os.path.join(OUT, f"pmc_{workload}_FETCH_SIZE_{tag}", "run_counter_collection.csv"), kernel)
+    write, nw = mean_counter(os.path.join(OUT, f"pmc_{workload}_WRITE_SIZE_{tag}", "run_counter_collection.csv"), kernel)
+    if fetch is None or write is None:
+        print(f"{label}: no dispatches of {kernel!r}", file=sys.stderr)
+        return None
     hbm = 2 * fetch * 1024 + write * 1024
-    res = {"workload": workload, "kernel": kernel, "tag": tag, "dispatches": [nf, nw],
+    res = {"workload": label, "kernel": kernel, "tag": tag, "dispatches": [nf, nw],
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": hbm / alg,
            "method": "separate rocprofv3 --pmc passes; 2*FETCH_SIZE (gfx950 16-B stream calibration) + WRITE_SIZE"}
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
-    path = os.path.join(REPO, "profiles", f"{tag}_pmc_{workload}.json")
-    with open(path, "w") as f:
+    with open(os.path.join(REPO, "profiles", f"{tag}_pmc_{label}.json"), "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps(res))
+    return res
+
+
+def bench_line(tag, workload):
+    with open(os.path.join(OUT, f"bench_{workload}_{tag}.json")) as f:
+        return json.loads(f.read().strip().splitlines()[-1])
+
+
+def main():
+    tag = sys.argv[1]
+    if len(sys.argv) > 2:
+        summarize(tag, sys.argv[2], sys.argv[3], float(sys.argv[4]), sys.argv[5] if len(sys.argv) > 5 else None)
+        return
+    for w in ("c5", "c4"):
+        b = bench_line(tag, w)
+        summarize(tag, w, "k_batch_mac", b["roofline"]["algorithmic_bytes_per_launch"], w)
+        summarize(tag, w, "k_upols_step", b["per_block_step"]["algorithmic_bytes_per_launch"], w + "_plain")
+    b = bench_line(tag, "c2")
+    summarize(tag, "c2", "k_c2c_lds<4096", b["roofline"]["algorithmic_bytes_per_launch"], "c2")
+    b = bench_line(tag, "c5")
+    if b.get("offline"):
+        summarize(tag, "c5o", "k_batch_mac", b["offline"]["algorithmic_bytes_per_launch"], "c5_offline")
 
 
 if __name__ == "__main__":
