@@ -213,7 +213,18 @@ __host__ __device__ constexpr int pass_radix()
 // Stockham passes from sub-length Ns upward. v[m] = element t + m*T on entry
 // (T = N/E); on exit v[m] = X[t + m*T]. `lds` holds lds_len(N) complex and is
 // reused by every pass; all threads of the block must call (barriers inside).
-template<int N, int E, int DIR, int Ns = 1, class C>
+// Wave-level LDS ordering for transforms run by ONE wave (WS = true in stockham): a
+// wave's LDS accesses execute in order, so a compiler-level barrier plus wavefront-scope
+// fences replaces the workgroup barrier, and the other waves of the workgroup need not
+// take part.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template<int N, int E, int DIR, int Ns = 1, bool WS = false, class C>
 __device__ __forceinline__ void stockham(C (&v)[E], C* lds, const C* tw, int t, bool active)
 {
     if constexpr (N == 1 || Ns >= N) {
@@ -247,13 +258,13 @@ __device__ __forceinline__ void stockham(C (&v)[E], C* lds, const C* tw, int t, 
             }
         }
         if constexpr (!last) {
-            __syncthreads();
+            if constexpr (WS) wave_sync(); else __syncthreads();
             if (active) {
 #pragma unroll
                 for (int m = 0; m < E; ++m) v[m] = lds[lpad(t + m * T)];
             }
-            __syncthreads();
-            stockham<N, E, DIR, Ns * R>(v, lds, tw, t, active);
+            if constexpr (WS) wave_sync(); else __syncthreads();
+            stockham<N, E, DIR, Ns * R, WS>(v, lds, tw, t, active);
         }
     }
 }

@@ -396,8 +396,7 @@ void destroy(upols_t* h)
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
-    (void)hipFree(h->H);
-    (void)hipFree(h->fdl);
+    (void)hipFree(h->H);  // the FDL shares H's allocation (rows [nrows, 2 nrows))
     (void)hipFree(h->part);
     (void)hipFree(h->prev);
     (void)hipFree(h->arrivals);
@@ -576,10 +575,24 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     // window's warm-up (T - 1 extra rows per split) stays under half the split's rows
     if (const char* e = std::getenv("NEO_HIP_BATCH_T")) h->bT = std::max(2, std::min(kMaxBatch, std::atoi(e)));
     if (const char* e = std::getenv("NEO_HIP_BATCH_NB")) h->bNB = std::atoi(e) == 1 ? 1 : 2;
-    int btarget = target;
+    if (const char* e = std::getenv("NEO_HIP_BATCH_VAR")) h->bvar = std::max(0, std::min(6, std::atoi(e)));
+    if (h->bvar == 3 && (int64_t(h->ring - 1) * h->pstride + block) * int64_t(sizeof(cf)) >= (int64_t(1) << 31))
+        h->bvar = 2;  // buffer-load rows need one channel's span below 2 GiB
+    // LDS-DMA variants: one descriptor spans a channel's H rows up to its FDL rows
+    if (h->bvar >= 4 && (int64_t(channels) * h->ring * block + int64_t(h->ring) * h->pstride) * int64_t(sizeof(cf)) >=
+                            (int64_t(1) << 31))
+        h->bvar = 2;
+    if (const char* e = std::getenv("NEO_HIP_AHEAD_KERNEL")) h->akern = std::atoi(e) == 1 ? 1 : 2;
+    // batched MAC: 256-lane workgroups at 2 waves/SIMD -> 2 resident per CU, so 512 fills the
+    // chip once with no second round (A/B, bmac_var 3: C5 0.409 -> 0.367 ms per pass, C4 0.369
+    // -> 0.379 ms, within run-to-run spread)
+    int btarget = 512;
     if (const char* e = std::getenv("NEO_HIP_BATCH_WGS")) btarget = std::max(1, std::atoi(e));
     const int bt = batch_t(block, h->bNB, h->bT);
-    int Sb = std::max(1, std::min({(btarget + channels - 1) / channels, partitions / (2 * bt), 64}));
+    if (const char* e = std::getenv("NEO_HIP_BATCH_CACHE_ROWS")) h->pcb = std::max(0, std::atoi(e));
+    // workgroups per (channel, split): the batched MAC has one lane per bin, <= 256 lanes
+    const int bgroups = std::max(1, block / h->bNB / 256);
+    int Sb = std::max(1, std::min({(btarget + channels * bgroups - 1) / (channels * bgroups), partitions / (2 * bt), 64}));
     if (h->ring - partitions < bt - 1) h->batch = false;  // ring too short for a batch
     // streaming lookahead: one filter + FDL pass per T-block window instead of per block
     // (MI355X, 1 block per step: C5 0.286 -> 0.024 ms, C4 0.285 -> 0.021, C3 10.0 -> 7.8 us);
@@ -596,8 +609,9 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     };
     if (hipStreamCreateWithFlags(&h->stream, hipStreamDefault) != hipSuccess)
         return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
-    if (hipMalloc(reinterpret_cast<void**>(&h->H), nrows * rowbytes) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&h->fdl), nrows * rowbytes) != hipSuccess ||
+    // filter and FDL in ONE allocation (FDL = rows [nrows, 2 nrows)): the LDS-DMA batched MAC
+    // reaches both of a channel through a single buffer descriptor
+    if (hipMalloc(reinterpret_cast<void**>(&h->H), 2 * nrows * rowbytes) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->part), size_t(channels) * h->S * rowbytes) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->prev), size_t(channels) * block * sizeof(float)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&h->arrivals), size_t(channels) * sizeof(int)) != hipSuccess ||
@@ -605,6 +619,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
                     hipSuccess ||
                 hipMalloc(reinterpret_cast<void**>(&h->tmp), size_t(channels) * rowbytes) != hipSuccess)))
         return bail(fail(NEO_HIP_ENOMEM, "device allocation of %zu bytes failed", 2 * nrows * rowbytes));
+    h->fdl = h->H + nrows * size_t(block);
     int rc = upload_tw(&h->tw, block);
     if (rc) return bail(rc);
     if (hipMemset(h->H, 0, nrows * rowbytes) != hipSuccess) return bail(fail(NEO_HIP_ERUNTIME, "memset failed"));

@@ -55,15 +55,52 @@ struct acc3 {
     f2v d, x;
 };
 
+// Row loads of the batched MAC. BUF = false: flat global loads (64-bit address per lane
+// and row). BUF = true: buffer loads over a per-channel descriptor, the lane's byte
+// offset fixed in a VGPR and the row offset in an SGPR (no per-row address VALU).
+template<class V, bool BUF>
+struct row_src {
+    const V* Hv;
+    const V* Fv;
+    int64_t psv;                   // row stride in vectors
+    __amdgpu_buffer_rsrc_t Hr, Fr;
+    int prow;                      // row stride in bytes
+    int pc;                        // filter rows p < pc are read cacheable (BUF only; the rest nontemporal)
+    __device__ __forceinline__ V h(int p, int lane) const
+    {
+        if constexpr (BUF) {
+            const auto u = p < pc ? __builtin_amdgcn_raw_buffer_load_b64(Hr, lane * int(sizeof(V)), p * prow, 0)
+                                  : __builtin_amdgcn_raw_buffer_load_b64(Hr, lane * int(sizeof(V)), p * prow, 2 /* nt */);
+            return __builtin_bit_cast(V, u);
+        } else {
+            return __builtin_nontemporal_load(Hv + int64_t(p) * psv + lane);
+        }
+    }
+    __device__ __forceinline__ V f(int r, int lane) const
+    {
+        if constexpr (BUF) {
+            auto u = __builtin_amdgcn_raw_buffer_load_b64(Fr, lane * int(sizeof(V)), r * prow, 2 /* nt */);
+            return __builtin_bit_cast(V, u);
+        } else {
+            return __builtin_nontemporal_load(Fv + int64_t(r) * psv + lane);
+        }
+    }
+};
+
 // Step U of a T-step chunk (p = pb + U; U is a template argument so every slot index
 // is static and the arrays stay in registers): take H row p and FDL row (w - p) from
 // prefetch slot U mod D (loaded D steps earlier) into window slot (T - U) mod T, issue
 // the loads for p + D, then MAC all T blocks; block j reads window slot (j - U) mod T.
 // D bounds the loads in flight per lane (and so the registers they hold).
-template<int T, int NB, int VPT, int L, int D, int U>
+//   A2 = false: four partial products per bin in two packed pairs (acc3 d and x).
+//   A2 = true:  one packed pair per bin, the complex product itself: (re, im) +=
+//     (hr, hr)(xr, xi) + (-hi, hi)(xi, xr) -- two v_pk_fma_f32 as before, half the
+//     accumulator registers. The lane holding the packed bin 0 (DC, Nyquist: two real
+//     products) takes the operands (hr, hi) and (0, 0) instead, so its pair sums
+//     (hr xr, hi xi) = (DC, Nyquist) exactly as the four-product form does.
+template<int T, int NB, int VPT, int L, int D, bool A2, int U, class SRC>
 __device__ __forceinline__ void batch_step(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)[T][VPT], bvec<NB> (&ph)[D][VPT],
-                                           bvec<NB> (&pf)[D][VPT], const bvec<NB>* Hv, const bvec<NB>* Fv,
-                                           int64_t psv, int tid, int ring, int w, int p, int p1)
+                                           bvec<NB> (&pf)[D][VPT], const SRC& src, int tid, int ring, int w, int p)
 {
     constexpr int slot = U % D;
     bvec<NB> hv[VPT];
@@ -78,46 +115,96 @@ __device__ __forceinline__ void batch_step(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)
         r = r < 0 ? r + ring : r;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-            pf[slot][v] = __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
-            ph[slot][v] = __builtin_nontemporal_load(Hv + int64_t(pn) * psv + tid + v * L);
+            pf[slot][v] = src.f(r, tid + v * L);
+            ph[slot][v] = src.h(pn, tid + v * L);
         }
     }
+    if constexpr (A2) {
+        f2v h1[VPT][NB], h2[VPT][NB];
 #pragma unroll
-    for (int j = 0; j < T; ++j)
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            const bvec<NB> x = f[(j - U + T) % T][v], h = hv[v];
+        for (int v = 0; v < VPT; ++v)
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                acc3& A = a[j][v * NB + b];
-                const f2v hb = {h[2 * b], h[2 * b + 1]}, xb = {x[2 * b], x[2 * b + 1]};
-                A.d = __builtin_elementwise_fma(hb, xb, A.d);
-                A.x = __builtin_elementwise_fma(hb, xb.yx, A.x);
+                const float hr = hv[v][2 * b], hi = hv[v][2 * b + 1];
+                const bool z = b == 0 && tid + v * L == 0;  // packed bin 0
+                const float s = z ? 0.0f : hi;
+                h1[v][b] = {hr, z ? hi : hr};
+                h2[v][b] = {-s, s};
             }
-        }
+        // two sweeps over the blocks, so consecutive FMAs never chain on one accumulator
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) {
+                    const bvec<NB> x = f[(j - U + T) % T][v];
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) {
+                        acc3& A = a[j][v * NB + b];
+                        const f2v xb = {x[2 * b], x[2 * b + 1]};
+                        A.d = k == 0 ? __builtin_elementwise_fma(h1[v][b], xb, A.d)
+                                     : __builtin_elementwise_fma(h2[v][b], xb.yx, A.d);
+                    }
+                }
+    } else {
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+                const bvec<NB> x = f[(j - U + T) % T][v], h = hv[v];
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    acc3& A = a[j][v * NB + b];
+                    const f2v hb = {h[2 * b], h[2 * b + 1]}, xb = {x[2 * b], x[2 * b + 1]};
+                    A.d = __builtin_elementwise_fma(hb, xb, A.d);
+                    A.x = __builtin_elementwise_fma(hb, xb.yx, A.x);
+                }
+            }
+    }
     __builtin_amdgcn_sched_barrier(0);  // keep each step's loads D steps ahead, not all hoisted
 }
 
-template<int T, int NB, int VPT, int L, int D, int... U>
+template<int T, int NB, int VPT, int L, int D, bool A2, class SRC, int... U>
 __device__ __forceinline__ void batch_chunk(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)[T][VPT], bvec<NB> (&ph)[D][VPT],
-                                            bvec<NB> (&pf)[D][VPT], const bvec<NB>* Hv, const bvec<NB>* Fv,
-                                            int64_t psv, int tid, int ring, int w, int pb, int p1,
+                                            bvec<NB> (&pf)[D][VPT], const SRC& src, int tid, int ring, int w, int pb,
                                             std::integer_sequence<int, U...>)
 {
-    (batch_step<T, NB, VPT, L, D, U>(a, f, ph, pf, Hv, Fv, psv, tid, ring, w, pb + U, p1), ...);
+    (batch_step<T, NB, VPT, L, D, A2, U>(a, f, ph, pf, src, tid, ring, w, pb + U), ...);
 }
 
 // MAC pass for T blocks (grid C x S, batch_cfg<B, NB>::L lanes, NB bins per lane-vector):
 // workgroup (c, s) walks partitions [p0, p1) and writes T partial spectra to
 // part[c][s][j][B].
-#ifndef NEO_BATCH_D
-#define NEO_BATCH_D 4
-#endif
-template<int B, int T, int NB, int D = (T < NEO_BATCH_D ? T : NEO_BATCH_D)>  // D divides T: slots line up across chunks
-__global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf* __restrict__ H,
+// Variants (h->bvar, NEO_HIP_BATCH_VAR): accumulator form, prefetch depth D (divides T, so
+// slots line up across chunks) and the waves per SIMD the register budget is sized for.
+template<int V>
+struct bmac_var;
+template<>
+struct bmac_var<0> {  // four partial products per bin (acc3), D = 4, 256 VGPRs
+    static constexpr bool A2 = false, BUF = false;
+    static constexpr int D = 4, W = 2;
+};
+template<>
+struct bmac_var<1> {  // complex accumulators, D = 4, <= 168 VGPRs (3 waves/SIMD)
+    static constexpr bool A2 = true, BUF = false;
+    static constexpr int D = 4, W = 3;
+};
+template<>
+struct bmac_var<2> {  // complex accumulators, D = 8, 256 VGPRs
+    static constexpr bool A2 = true, BUF = false;
+    static constexpr int D = 8, W = 2;
+};
+template<>
+struct bmac_var<3> {  // as 2 with buffer loads (row offsets in SGPRs)
+    static constexpr bool A2 = true, BUF = true;
+    static constexpr int D = 8, W = 2;
+};
+template<int B, int T, int NB, int VAR, int D0 = bmac_var<VAR>::D, int D = (T < D0 ? T : D0)>
+__global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_batch_mac(const cf* __restrict__ H,
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
-                                                                   int64_t cstride, int64_t pstride, int ahead)
+                                                                   int64_t cstride, int64_t pstride, int ahead, int pc)
 {
     using K = batch_cfg<B, NB>;
     using V = bvec<NB>;
@@ -130,6 +217,11 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
     const int64_t psv = pstride / NB;  // row stride in vectors
     const V* Hv = reinterpret_cast<const V*>(H + int64_t(c) * cstride);
     const V* Fv = reinterpret_cast<const V*>(fdl + int64_t(c) * cstride);
+    constexpr bool BUF = bmac_var<VAR>::BUF;
+    const int span = BUF ? int(((ring - 1) * pstride + B) * int64_t(sizeof(cf))) : 0;  // < 2 GiB (host check)
+    const row_src<V, BUF> src{Hv, Fv, psv, __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Hv), 0, span, 0x00020000),
+                              __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Fv), 0, span, 0x00020000),
+                              int(pstride * int64_t(sizeof(cf))), pc};
 
     acc3 a[T][NB * VPT];
 #pragma unroll
@@ -147,7 +239,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
         r = r < 0 ? r + ring : (r >= ring ? r - ring : r);
 #pragma unroll
         for (int v = 0; v < VPT; ++v)
-            f[sl][v] = future ? V{} : __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
+            f[sl][v] = future ? V{} : src.f(r, tid + v * L);
     }
     V ph[D][VPT], pf[D][VPT];
 #pragma unroll
@@ -157,15 +249,15 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
         r = r < 0 ? r + ring : r;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-            pf[d][v] = future && d == 0 ? V{} : __builtin_nontemporal_load(Fv + int64_t(r) * psv + tid + v * L);
-            ph[d][v] = __builtin_nontemporal_load(Hv + int64_t(p) * psv + tid + v * L);
+            pf[d][v] = future && d == 0 ? V{} : src.f(r, tid + v * L);
+            ph[d][v] = src.h(p, tid + v * L);
         }
     }
     // splits hold a multiple of T partitions; the last split's final chunk runs past P into
     // the ring's spare filter rows, which are zero (so those steps add nothing)
     for (int pb = p0; pb < p1; pb += T)
-        batch_chunk<T, NB, VPT, L, D>(a, f, ph, pf, Hv, Fv, psv, tid, ring, w, pb, p1,
-                                      std::make_integer_sequence<int, T>{});
+        batch_chunk<T, NB, VPT, L, D, bmac_var<VAR>::A2>(a, f, ph, pf, src, tid, ring, w, pb,
+                                                          std::make_integer_sequence<int, T>{});
 
     cf* slab = part + (int64_t(c) * S + s) * T * B;
 #pragma unroll
@@ -177,11 +269,154 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), 2) void k_batch_mac(const cf
             for (int b = 0; b < NB; ++b) {
                 const acc3& A = a[j][v * NB + b];
                 const bool bin0 = tid + v * L == 0 && b == 0;
-                o[2 * b] = bin0 ? A.d.x : A.d.x - A.d.y;
-                o[2 * b + 1] = bin0 ? A.d.y : A.x.x + A.x.y;
+                if constexpr (bmac_var<VAR>::A2) {
+                    o[2 * b] = A.d.x;
+                    o[2 * b + 1] = A.d.y;
+                } else {
+                    o[2 * b] = bin0 ? A.d.x : A.d.x - A.d.y;
+                    o[2 * b + 1] = bin0 ? A.d.y : A.x.x + A.x.y;
+                }
             }
             *reinterpret_cast<V*>(slab + int64_t(j) * B + (tid + v * L) * NB) = o;
         }
+}
+
+// k_batch_mac with the row stream through an LDS-DMA ring (B = 256 / 512, T = 32, one
+// complex bin per lane): each wave owns 64 bins and a private ring of D slots of 1 KB;
+// one buffer_load_dwordx4 ... lds per partition fills a slot (lanes 0-31: the H row's 64
+// bins, lanes 32-63: the FDL row's), issued D partitions ahead, so D KB per wave are in
+// flight without holding registers. H and the FDL share one allocation, so one buffer
+// descriptor per channel covers both; a lane's byte offset is its bin plus its row times
+// the row pitch. The wave reads back only its own slots (counted vmcnt, no barrier); the
+// accumulators and the sliding window of T FDL values stay in registers (complex
+// accumulators, bmac_var<2>'s arithmetic). Prefetches past the last consumed partition
+// may read junk rows or out of range (buffer loads return 0 there); they are never used.
+template<int D, int W>
+struct lds_var {
+    static constexpr int depth = D, waves = W;
+};
+template<int V>
+using lds_var_t = std::conditional_t<V == 4, lds_var<8, 3>, std::conditional_t<V == 5, lds_var<16, 2>, lds_var<8, 4>>>;
+
+template<int N>
+__device__ __forceinline__ void wait_vm()  // s_waitcnt vmcnt(N), other counters untouched
+{
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// H and FDL values of this lane's bin from ring slot OFF (bytes; the FDL half 512 B
+// further). Inline asm: the compiler would otherwise wait for every LDS-DMA in flight
+// before an LDS read it cannot tell apart from their destinations.
+template<int OFF>
+__device__ __forceinline__ void ring_read(unsigned lane_addr, f2v& h, f2v& x)
+{
+    asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(h), "=v"(x)
+                 : "v"(lane_addr), "i"(OFF), "i"(OFF + 512)
+                 : "memory");
+}
+
+struct lds_src {
+    __amdgpu_buffer_rsrc_t rs;  // channel's H rows ... FDL rows
+    int voff;                   // next DMA's byte offset: H lanes row p, FDL lanes row (w - p) mod R
+    int delta;                  // per partition: +row (H lanes), -row (FDL lanes)
+    int wrap;                   // FDL lanes: + R rows when w - p drops below 0 (H lanes: 0)
+    unsigned wring;             // wave's ring (LDS byte address, wave-uniform)
+    unsigned lane_addr;         // wring + 8 * lane
+};
+
+// DMA partition p into ring slot `slot`; q.voff holds p's offsets and then moves to p + 1
+// (one add per partition; the FDL lanes wrap once, when p passes w)
+__device__ __forceinline__ void lds_fill(lds_src& q, int slot, int p, int w)
+{
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(q.rs, (__attribute__((address_space(3))) void*)(uintptr_t)(q.wring + slot * 1024),
+                                             16, q.voff, 0, 0, 2 /* nt */);
+    q.voff += q.delta + (p == w ? q.wrap : 0);
+}
+
+template<int T, int D, int U>
+__device__ __forceinline__ void lds_step(acc3 (&a)[T], f2v (&f)[T], lds_src& q, int w, int p, bool zero, bool bin0)
+{
+    constexpr int slot = U % D;
+    wait_vm<D - 1>();  // the DMA of partition p (D - 1 newer ones stay in flight)
+    f2v hv, xv;
+    ring_read<slot * 1024>(q.lane_addr, hv, xv);
+    if (zero) xv = f2v(0.0f);
+    f[(T - U) % T] = xv;
+    lds_fill(q, slot, p + D, w);  // refill the slot with partition p + D
+    const float s = bin0 ? 0.0f : hv.y;
+    const f2v h1 = {hv.x, bin0 ? hv.y : hv.x}, h2 = {-s, s};
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const f2v x = f[(j - U + T) % T];
+            a[j].d = k == 0 ? __builtin_elementwise_fma(h1, x, a[j].d) : __builtin_elementwise_fma(h2, x.yx, a[j].d);
+        }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template<int T, int D, int... U>
+__device__ __forceinline__ void lds_chunk(acc3 (&a)[T], f2v (&f)[T], lds_src& q, int w, int pb, bool zero0, bool bin0,
+                                          std::integer_sequence<int, U...>)
+{
+    (lds_step<T, D, U>(a, f, q, w, pb + U, U == 0 && zero0, bin0), ...);
+}
+
+template<int B, int T, int VAR>
+__global__ __launch_bounds__(256, lds_var_t<VAR>::waves) void k_batch_mac_lds(
+    const cf* __restrict__ H, const cf* __restrict__ fdl, cf* __restrict__ part, int P, int ring, int S, int rows, int w,
+    int64_t cstride, int64_t pstride, int ahead)
+{
+    constexpr int D = lds_var_t<VAR>::depth, G = B / 256;
+    static_assert(B == 256 || B == 512, "one bin per lane, 64 bins per wave");
+    __shared__ __attribute__((aligned(1024))) char lring[4 * D * 1024];
+    const int cs = blockIdx.x / G, gch = blockIdx.x - cs * G;
+    const int tid = gch * 256 + threadIdx.x;  // bin
+    const int c = cs / S, s = cs - c * S;
+    const int p0 = s * rows, p1 = min(P, p0 + rows);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+    const cf* Hc = H + int64_t(c) * cstride;
+    const cf* Fc = fdl + int64_t(c) * cstride;
+    const int foff = int((fdl - H) * int64_t(sizeof(cf)));  // FDL of a channel, bytes past its H (host-checked < 2 GiB)
+    const int rowbytes = int(pstride * int64_t(sizeof(cf)));
+    const bool hl = lane < 32;  // lanes 0-31 fetch the H half of a slot, 32-63 the FDL half
+    lds_src q;
+    q.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<cf*>(Hc), 0, foff + ring * rowbytes, 0x00020000);
+    {
+        int r0 = w - p0;
+        r0 = r0 < 0 ? r0 + ring : r0;
+        q.voff = (hl ? p0 * rowbytes : foff + r0 * rowbytes) + (gch * 256 + wv * 64 + 2 * (lane & 31)) * int(sizeof(cf));
+    }
+    q.delta = hl ? rowbytes : -rowbytes;
+    q.wrap = hl ? 0 : ring * rowbytes;
+    q.wring = unsigned(reinterpret_cast<uintptr_t>(lring)) + unsigned(wv * D * 1024);
+    q.lane_addr = q.wring + 8u * unsigned(lane);
+    const bool bin0 = tid == 0;
+
+    acc3 a[T];
+#pragma unroll
+    for (int j = 0; j < T; ++j) a[j] = {f2v(0.0f), f2v(0.0f)};
+    const bool future = ahead && p0 == 0;  // see k_batch_mac
+    f2v f[T];
+#pragma unroll
+    for (int sl = 1; sl < T; ++sl) {
+        int r = w + sl - p0;
+        r = r < 0 ? r + ring : (r >= ring ? r - ring : r);
+        f[sl] = future ? f2v(0.0f) : __builtin_nontemporal_load(reinterpret_cast<const f2v*>(Fc + int64_t(r) * pstride + tid));
+    }
+    wait_vm<0>();
+#pragma unroll
+    for (int d = 0; d < D; ++d) lds_fill(q, d, p0 + d, w);  // partitions p0 .. p0 + D - 1
+    for (int pb = p0; pb < p1; pb += T)
+        lds_chunk<T, D>(a, f, q, w, pb, future && pb == p0, bin0, std::make_integer_sequence<int, T>{});
+    wait_vm<0>();  // no DMA outstanding at exit
+
+    cf* slab = part + (int64_t(c) * S + s) * T * B;
+#pragma unroll
+    for (int j = 0; j < T; ++j) *reinterpret_cast<f2v*>(slab + int64_t(j) * B + tid) = a[j].d;
 }
 
 // Sum the S slabs of block j in order, c2r, 1/2B (grid C x T, 256 lanes).
@@ -338,6 +573,123 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
     c2r_tail<B, OLA>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
 }
 
+// k_upols_ahead with the work spread over one workgroup of 64 + NG*Q lanes per channel
+// (Q = B/2 float4 per row): wave 0 runs the window r2c alone (wave-synchronous, no
+// workgroup barriers) while NG groups of Q lanes sum the slabs and MAC the partitions
+// p = 1..j (group g takes p = 1 + g, 1 + g + NG, ...; up to KC row pairs in flight per
+// lane); after one barrier group 0 adds H0 X and the groups' partials, and after a second
+// wave 0 runs the c2r. The serial chain per block is one window transform, one burst of
+// row loads (overlapped with it) and one inverse transform; the per-channel MAC no longer
+// walks j partitions four at a time.
+template<int B>
+struct ahead_cfg {
+    static constexpr int Q = B / 2;                                  // float4 (2 bins) per row
+    static constexpr int NG = Q >= 768 ? 1 : (768 / Q > 6 ? 6 : 768 / Q);  // MAC groups
+    static constexpr int EW = B >= 512 ? B / 64 : 8;                 // transform elements per lane
+    static constexpr int TW = B / EW;                                // transform lanes (<= 64)
+    static constexpr int NT = 64 + NG * Q;                           // workgroup size
+    static constexpr int KC = 8;                                     // row pairs in flight per lane
+};
+
+template<int B, bool OLA>
+__global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
+    const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
+    const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
+    const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride)
+{
+    using K = upols_cfg<B>;
+    using A = ahead_cfg<B>;
+    constexpr int Q = A::Q, NG = A::NG, EW = A::EW, TW = A::TW, KC = A::KC;
+    static_assert(TW <= 64 && A::NT <= 1024, "ahead2 geometry");
+    __shared__ __attribute__((aligned(16))) cf X[B];
+    __shared__ __attribute__((aligned(16))) float4 acc[NG][Q];
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    const int tid = threadIdx.x, c = blockIdx.x;
+    const int64_t crow = int64_t(c) * cstride;
+    const float* in_c = in + int64_t(c) * ld_in;
+    float* prev_c = prev + int64_t(c) * B;
+    const int64_t ps4 = pstride / 2;
+    const float4* H4 = reinterpret_cast<const float4*>(H + crow);
+    float4 h0 = {0.f, 0.f, 0.f, 0.f};
+    if (tid < 64) {  // wave 0: window r2c, FDL row w, previous block
+        for (int i = tid; i < K::TW1 + K::TW2; i += 64) tw[i] = twg[i];
+        cf v[EW];
+        if (tid < TW) {
+            const cf* pz = reinterpret_cast<const cf*>(prev_c);
+            const cf* iz = reinterpret_cast<const cf*>(in_c);
+#pragma unroll
+            for (int m = 0; m < EW; ++m) {
+                const int n = tid + m * TW;
+                if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
+                else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+            }
+        }
+        wave_sync();
+        stockham<B, EW, -1, 1, true>(v, fft, tw, tid, tid < TW);
+        if (tid < TW) {
+#pragma unroll
+            for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
+        }
+        wave_sync();
+        cf* row = fdl + crow + int64_t(w) * pstride;
+        for (int k = tid; k < B; k += 64) {
+            const cf x = r2c_split<B>(fft, tw + K::TW1, k);
+            X[k] = x;
+            row[k] = x;
+        }
+        if constexpr (!OLA) {  // the window's second half becomes the next call's first half
+            for (int i = tid; i < B / 4; i += 64)
+                reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
+        }
+    } else {  // MAC groups: slabs + partitions 1..j
+        const int u = tid - 64, g = u / Q, q = u - g * Q;
+        if (g == 0) h0 = H4[q];
+        const float4* F4 = reinterpret_cast<const float4*>(fdl + crow);
+        const float4* S4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * T * B + int64_t(j) * B);
+        const int64_t ss4 = int64_t(T) * K::Q;  // float4 between the slabs of one block
+        float4 sum = {0.f, 0.f, 0.f, 0.f};
+        for (int s = g; s < S; s += NG) {
+            const float4 r = S4[s * ss4 + q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+        for (int pb = 1 + g; pb <= j; pb += NG * KC) {
+            float4 hv[KC], xv[KC];
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                const int p = pb + k * NG;
+                if (p <= j) {
+                    const int r = w - p < 0 ? w - p + ring : w - p;
+                    hv[k] = H4[int64_t(p) * ps4 + q];
+                    xv[k] = F4[int64_t(r) * ps4 + q];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KC; ++k)
+                if (pb + k * NG <= j) mac2(a0, a1, hv[k], xv[k]);
+        }
+        const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
+        acc[g][q] = make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
+    }
+    __syncthreads();
+    if (tid >= 64 && tid < 64 + Q) {  // group 0: + H0 X + the other groups
+        const int q = tid - 64;
+        acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+        mac2(a0, a1, h0, reinterpret_cast<const float4*>(X)[q]);
+        const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
+        float4 y = acc[0][q];
+#pragma unroll
+        for (int g = 1; g < NG; ++g) {
+            const float4 r = acc[g][q];
+            y.x += r.x; y.y += r.y; y.z += r.z; y.w += r.w;
+        }
+        reinterpret_cast<float4*>(X)[q] = make_float4(y.x + b0.x, y.y + b0.y, y.z + b1.x, y.w + b1.y);
+    }
+    __syncthreads();
+    if (tid < 64) c2r_tail<B, OLA, EW, true>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
+}
+
 // dispatch k_batch_mac over (B, NB, T) for the valid combinations
 template<int BB, int NB>
 int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead)
@@ -347,8 +699,26 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead)
 #define NEO_BATCH_T(TT)                                                                                          \
     case TT:                                                                                                     \
         if constexpr (batch_t(BB, NB, TT) == TT) {                                                               \
-            hipLaunchKernelGGL((k_batch_mac<BB, TT, NB>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, \
-                               h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride, ahead);               \
+            if constexpr (TT == 32 && NB == 1 && (BB == 256 || BB == 512)) {                                     \
+                if (h->bvar >= 4) {                                                                              \
+                    hipLaunchKernelGGL(h->bvar == 4   ? (k_batch_mac_lds<BB, TT, 4>)                            \
+                                       : h->bvar == 5 ? (k_batch_mac_lds<BB, TT, 5>)                            \
+                                                      : (k_batch_mac_lds<BB, TT, 6>),                           \
+                                       dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, h->ring, h->Sb, \
+                                       h->rows_b, h->wpos, h->cstride, h->pstride, ahead);                       \
+                    break;                                                                                       \
+                }                                                                                                \
+                if (h->bvar != 0) {                                                                              \
+                    hipLaunchKernelGGL(h->bvar == 1   ? (k_batch_mac<BB, TT, NB, 1>)                            \
+                                       : h->bvar == 2 ? (k_batch_mac<BB, TT, NB, 2>)                            \
+                                                      : (k_batch_mac<BB, TT, NB, 3>),                           \
+                                       dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, h->ring, h->Sb, \
+                                       h->rows_b, h->wpos, h->cstride, h->pstride, ahead, h->pcb);                       \
+                    break;                                                                                       \
+                }                                                                                                \
+            }                                                                                                    \
+            hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 0>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b,  \
+                               h->P, h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride, ahead, h->pcb);         \
             break;                                                                                               \
         }                                                                                                        \
         return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);
@@ -417,7 +787,19 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         if (rc) return rc;
         if ((rc = mac_event(h, timed, true, ev, s))) return rc;
     }
-    if (h->ola) {
+    if (h->akern == 2 && B <= 1024) {
+        if (h->ola) {
+            NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
+                                      (k_upols_ahead2<BB, true>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
+                                      ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
+                                      h->ring, h->wpos, h->cstride, h->pstride))
+        } else {
+            NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
+                                      (k_upols_ahead2<BB, false>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
+                                      ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
+                                      h->ring, h->wpos, h->cstride, h->pstride))
+        }
+    } else if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_upols_ahead<BB, true>), dim3(unsigned(h->C)), dim3(256), 0, s, in,
                                                  ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T,
                                                  h->phase, h->tw, h->ring, h->wpos, h->cstride, h->pstride))

@@ -92,12 +92,13 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
 //   OLS: out = window samples [B, 2B)                       (overlap_save.hpp:104-111)
 //   OLA: out = samples [0, B) + overlap; overlap = [B, 2B)  (overlap_add.hpp:92-106)
 // E = 4 keeps the fused kernel inside its 64-VGPR budget (T = B/E <= 256 lanes).
-template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256)>
+// WS = true: run by one wave (T <= 64 lanes), no workgroup barriers.
+template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256), bool WS = false>
 __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, float* ovl_c, int tid)
 {
     using K = upols_cfg<B>;
     constexpr int T = B / E;
-    static_assert(T <= 256 && B % E == 0, "c2r must fit one 256-lane workgroup");
+    static_assert(T <= (WS ? 64 : 256) && B % E == 0, "c2r must fit one 256-lane workgroup (one wave for WS)");
     const bool active = tid < T;
     cf v[E];
     if (active) {
@@ -109,7 +110,7 @@ __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, flo
                           : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
         }
     }
-    stockham<B, E, +1>(v, fft, tw, tid, active);
+    stockham<B, E, +1, 1, WS>(v, fft, tw, tid, active);
     if (active) {
         const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108 / overlap_add.hpp:98
         cf* o = reinterpret_cast<cf*>(out_c);

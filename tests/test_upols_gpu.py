@@ -528,10 +528,13 @@ def test_host_staging_growth_keeps_batch_buffers(neo_gpu, oracle):
 @pytest.mark.parametrize("method", ["upols", "upola"])
 @pytest.mark.parametrize("B,L,C,nb", [(512, 20000, 3, 75), (256, 2560, 2, 70), (16, 100, 2, 40), (64, 64, 1, 37),
                                       (1024, 30000, 2, 33), (4096, 12000, 1, 9), (128, 128 * 40, 2, 100)])
-def test_ahead_steps_vs_oracle(neo_gpu, oracle, method, B, L, C, nb):
+@pytest.mark.parametrize("akern", ["1", "2"])
+def test_ahead_steps_vs_oracle(neo_gpu, oracle, monkeypatch, method, B, L, C, nb, akern):
     """Single-block steps with lookahead: one batched pass per T-block window (p > j for
-    block j), the window's own partitions per step; P < T, P = 1 and ring wraparound."""
+    block j), the window's own partitions per step; P < T, P = 1 and ring wraparound.
+    akern: the per-block kernel (1 = k_upols_ahead, 2 = k_upols_ahead2, B <= 1024)."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("NEO_HIP_AHEAD_KERNEL", akern)
     ir = np.stack([oracle.noise(320 + c, L) for c in range(C)])
     parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
     sig = np.stack([oracle.noise(330 + c, B * nb) for c in range(C)])

@@ -1,5 +1,5 @@
 """A/B the batched MAC pass (process_blocks, T blocks per pass) in one process, interleaved.
-usage: python tools/batchbench.py [c5|c4|c3] [rounds] [blocks] spec...   spec = ENV=V[,ENV=V]"""
+usage: python tools/batchbench.py [c5|c4|c3|CxBxL] [rounds] [blocks] spec...   spec = ENV=V[,ENV=V]"""
 import os
 import sys
 import time
@@ -13,7 +13,7 @@ import bench  # noqa: E402
 wl = sys.argv[1] if len(sys.argv) > 1 else "c5"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 nb = int(sys.argv[3]) if len(sys.argv) > 3 else 96
-C, B, L = bench.WORKLOADS[wl]
+C, B, L = bench.WORKLOADS[wl] if wl in bench.WORKLOADS else map(int, wl.split("x"))  # or CxBxL
 P = neo.num_partitions(L, B)
 g = torch.Generator(device="cuda").manual_seed(1)
 ir = torch.rand((C, L), generator=g, device="cuda") * 2 - 1
@@ -50,7 +50,9 @@ bytes_pass = C * 16 * P * B
 for name in variants:
     v, w = sorted(res[name]), sorted(wall[name])
     med, wm = v[len(v) // 2], w[len(w) // 2]
-    print(f"{wl} {name:44s} MAC/pass {med:.4f} ms ({bytes_pass / med / 1e6:.0f} GB/s H+FDL) "
+    flop_pass = 8.0 * C * P * B * min(32, nb)
+    print(f"{wl} {name:44s} MAC/pass {med:.4f} ms ({bytes_pass / med / 1e6:.0f} GB/s H+FDL, "
+          f"{flop_pass / med / 1e9:.1f} TFLOP/s) "
           f"wall/block {wm:.4f} ms -> {C * B / wm / 1e3:.0f} Msamples/s")
 first = next(iter(outs.values()))
 print("max |y - y_first| per variant:", [float((o - first).abs().max()) for o in outs.values()],
