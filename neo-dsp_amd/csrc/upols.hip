@@ -575,7 +575,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     // window's warm-up (T - 1 extra rows per split) stays under half the split's rows
     if (const char* e = std::getenv("NEO_HIP_BATCH_T")) h->bT = std::max(2, std::min(kMaxBatch, std::atoi(e)));
     if (const char* e = std::getenv("NEO_HIP_BATCH_NB")) h->bNB = std::atoi(e) == 1 ? 1 : 2;
-    if (const char* e = std::getenv("NEO_HIP_BATCH_VAR")) h->bvar = std::max(0, std::min(6, std::atoi(e)));
+    if (const char* e = std::getenv("NEO_HIP_BATCH_VAR")) h->bvar = std::max(0, std::min(5, std::atoi(e)));
     if (h->bvar == 3 && (int64_t(h->ring - 1) * h->pstride + block) * int64_t(sizeof(cf)) >= (int64_t(1) << 31))
         h->bvar = 2;  // buffer-load rows need one channel's span below 2 GiB
     // LDS-DMA variants: one descriptor spans a channel's H rows up to its FDL rows
@@ -589,7 +589,6 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     int btarget = 512;
     if (const char* e = std::getenv("NEO_HIP_BATCH_WGS")) btarget = std::max(1, std::atoi(e));
     const int bt = batch_t(block, h->bNB, h->bT);
-    if (const char* e = std::getenv("NEO_HIP_BATCH_CACHE_ROWS")) h->pcb = std::max(0, std::atoi(e));
     // workgroups per (channel, split): the batched MAC has one lane per bin, <= 256 lanes
     const int bgroups = std::max(1, block / h->bNB / 256);
     int Sb = std::max(1, std::min({(btarget + channels * bgroups - 1) / (channels * bgroups), partitions / (2 * bt), 64}));

@@ -65,12 +65,11 @@ struct row_src {
     int64_t psv;                   // row stride in vectors
     __amdgpu_buffer_rsrc_t Hr, Fr;
     int prow;                      // row stride in bytes
-    int pc;                        // filter rows p < pc are read cacheable (BUF only; the rest nontemporal)
     __device__ __forceinline__ V h(int p, int lane) const
     {
         if constexpr (BUF) {
-            const auto u = p < pc ? __builtin_amdgcn_raw_buffer_load_b64(Hr, lane * int(sizeof(V)), p * prow, 0)
-                                  : __builtin_amdgcn_raw_buffer_load_b64(Hr, lane * int(sizeof(V)), p * prow, 2 /* nt */);
+            // (a per-row cacheable/nontemporal select here costs 54 spilled VGPRs at 256)
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(Hr, lane * int(sizeof(V)), p * prow, 2 /* nt */);
             return __builtin_bit_cast(V, u);
         } else {
             return __builtin_nontemporal_load(Hv + int64_t(p) * psv + lane);
@@ -204,7 +203,7 @@ template<int B, int T, int NB, int VAR, int D0 = bmac_var<VAR>::D, int D = (T < 
 __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_batch_mac(const cf* __restrict__ H,
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
-                                                                   int64_t cstride, int64_t pstride, int ahead, int pc)
+                                                                   int64_t cstride, int64_t pstride, int ahead)
 {
     using K = batch_cfg<B, NB>;
     using V = bvec<NB>;
@@ -221,7 +220,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     const int span = BUF ? int(((ring - 1) * pstride + B) * int64_t(sizeof(cf))) : 0;  // < 2 GiB (host check)
     const row_src<V, BUF> src{Hv, Fv, psv, __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Hv), 0, span, 0x00020000),
                               __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Fv), 0, span, 0x00020000),
-                              int(pstride * int64_t(sizeof(cf))), pc};
+                              int(pstride * int64_t(sizeof(cf)))};
 
     acc3 a[T][NB * VPT];
 #pragma unroll
@@ -296,7 +295,7 @@ struct lds_var {
     static constexpr int depth = D, waves = W;
 };
 template<int V>
-using lds_var_t = std::conditional_t<V == 4, lds_var<8, 3>, std::conditional_t<V == 5, lds_var<16, 2>, lds_var<8, 4>>>;
+using lds_var_t = std::conditional_t<V == 4, lds_var<8, 3>, lds_var<16, 2>>;  // (8, 4 waves): 1200 spilled VGPRs
 
 template<int N>
 __device__ __forceinline__ void wait_vm()  // s_waitcnt vmcnt(N), other counters untouched
@@ -701,9 +700,7 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead)
         if constexpr (batch_t(BB, NB, TT) == TT) {                                                               \
             if constexpr (TT == 32 && NB == 1 && (BB == 256 || BB == 512)) {                                     \
                 if (h->bvar >= 4) {                                                                              \
-                    hipLaunchKernelGGL(h->bvar == 4   ? (k_batch_mac_lds<BB, TT, 4>)                            \
-                                       : h->bvar == 5 ? (k_batch_mac_lds<BB, TT, 5>)                            \
-                                                      : (k_batch_mac_lds<BB, TT, 6>),                           \
+                    hipLaunchKernelGGL(h->bvar == 4 ? (k_batch_mac_lds<BB, TT, 4>) : (k_batch_mac_lds<BB, TT, 5>),   \
                                        dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, h->ring, h->Sb, \
                                        h->rows_b, h->wpos, h->cstride, h->pstride, ahead);                       \
                     break;                                                                                       \
@@ -713,12 +710,12 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead)
                                        : h->bvar == 2 ? (k_batch_mac<BB, TT, NB, 2>)                            \
                                                       : (k_batch_mac<BB, TT, NB, 3>),                           \
                                        dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, h->ring, h->Sb, \
-                                       h->rows_b, h->wpos, h->cstride, h->pstride, ahead, h->pcb);                       \
+                                       h->rows_b, h->wpos, h->cstride, h->pstride, ahead);                       \
                     break;                                                                                       \
                 }                                                                                                \
             }                                                                                                    \
             hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 0>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b,  \
-                               h->P, h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride, ahead, h->pcb);         \
+                               h->P, h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride, ahead);         \
             break;                                                                                               \
         }                                                                                                        \
         return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);
