@@ -407,6 +407,7 @@ void destroy(upols_t* h)
     if (h->io_host) (void)hipHostFree(h->io_host);
     (void)hipFree(h->samples_dev);
     (void)hipFree(h->part_b);
+    (void)hipFree(h->part_s);
     (void)hipFree(h->tail);
     if (h->samples_host) (void)hipHostFree(h->samples_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -582,6 +583,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     if (h->bvar >= 4 && (int64_t(channels) * h->ring * block + int64_t(h->ring) * h->pstride) * int64_t(sizeof(cf)) >=
                             (int64_t(1) << 31))
         h->bvar = 2;
+    if (const char* e = std::getenv("NEO_HIP_AHEAD_SUB")) h->asub = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_KERNEL")) h->akern = std::atoi(e) == 1 ? 1 : 2;
     // batched MAC: 256-lane workgroups at 2 waves/SIMD -> 2 resident per CU, so 512 fills the
     // chip once with no second round (A/B, bmac_var 3: C5 0.409 -> 0.367 ms per pass, C4 0.369

@@ -65,6 +65,13 @@ struct row_src {
     int64_t psv;                   // row stride in vectors
     __amdgpu_buffer_rsrc_t Hr, Fr;
     int prow;                      // row stride in bytes
+    int emax, rz;                  // FDL rows entering past partition emax read row rz (zero: an H spare row / out of range)
+    // FDL row entering the sliding window at partition pn (write position w)
+    __device__ __forceinline__ int frow(int w, int pn, int ring) const
+    {
+        const int r = w - pn;
+        return pn > emax ? rz : (r < 0 ? r + ring : r);
+    }
     __device__ __forceinline__ V h(int p, int lane) const
     {
         if constexpr (BUF) {
@@ -110,8 +117,7 @@ __device__ __forceinline__ void batch_step(acc3 (&a)[T][NB * VPT], bvec<NB> (&f)
     }
     const int pn = p + D < ring ? p + D : ring - 1;  // stay inside the allocated rows
     {
-        int r = w - pn;
-        r = r < 0 ? r + ring : r;
+        const int r = src.frow(w, pn, ring);
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
             pf[slot][v] = src.f(r, tid + v * L);
@@ -203,7 +209,8 @@ template<int B, int T, int NB, int VAR, int D0 = bmac_var<VAR>::D, int D = (T < 
 __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_batch_mac(const cf* __restrict__ H,
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
-                                                                   int64_t cstride, int64_t pstride, int ahead)
+                                                                   int64_t cstride, int64_t pstride, int ahead,
+                                                                   int emax, int rz)
 {
     using K = batch_cfg<B, NB>;
     using V = bvec<NB>;
@@ -220,7 +227,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     const int span = BUF ? int(((ring - 1) * pstride + B) * int64_t(sizeof(cf))) : 0;  // < 2 GiB (host check)
     const row_src<V, BUF> src{Hv, Fv, psv, __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Hv), 0, span, 0x00020000),
                               __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Fv), 0, span, 0x00020000),
-                              int(pstride * int64_t(sizeof(cf)))};
+                              int(pstride * int64_t(sizeof(cf))), emax, rz};
 
     acc3 a[T][NB * VPT];
 #pragma unroll
@@ -233,9 +240,10 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     const bool future = ahead && p0 == 0;
     V f[T][VPT];
 #pragma unroll
-    for (int sl = 1; sl < T; ++sl) {  // rows block sl needs at p0
+    for (int sl = 1; sl < T; ++sl) {  // rows block sl needs at p0 (entered at partition p0 - sl)
         int r = w + sl - p0;
         r = r < 0 ? r + ring : (r >= ring ? r - ring : r);
+        r = p0 - sl > emax ? rz : r;
 #pragma unroll
         for (int v = 0; v < VPT; ++v)
             f[sl][v] = future ? V{} : src.f(r, tid + v * L);
@@ -244,8 +252,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
 #pragma unroll
     for (int d = 0; d < D; ++d) {  // prefetch partitions p0 .. p0 + D - 1
         const int p = p0 + d < ring ? p0 + d : ring - 1;  // past P: zero filter rows
-        int r = w - p;
-        r = r < 0 ? r + ring : r;
+        const int r = src.frow(w, p, ring);
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
             pf[d][v] = future && d == 0 ? V{} : src.f(r, tid + v * L);
@@ -572,7 +579,13 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
     c2r_tail<B, OLA>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
 }
 
-// k_upols_ahead with the work spread over one workgroup of 64 + NG*Q lanes per channel
+// k_upols_ahead with the work spread over one workgroup of 64 + NG*Q lanes per channel.
+// Sub-windows (sub != nullptr): at the first block of each kSubWindow-block sub-window
+// after the first, a small k_batch_mac pass (T = kSubWindow, FDL rows limited to the
+// window's own) accumulates for the sub-window's blocks the partitions whose rows are the
+// window's blocks before it; a block step then adds that slab and runs only the
+// partitions 1..jr (jr = its position in the sub-window) itself. Per 32-block window the
+// rows a block step reads drop from 496 to 112 row pairs per channel.
 // (Q = B/2 float4 per row): wave 0 runs the window r2c alone (wave-synchronous, no
 // workgroup barriers) while NG groups of Q lanes sum the slabs and MAC the partitions
 // p = 1..j (group g takes p = 1 + g, 1 + g + NG, ...; up to KC row pairs in flight per
@@ -580,6 +593,21 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
 // wave 0 runs the c2r. The serial chain per block is one window transform, one burst of
 // row loads (overlapped with it) and one inverse transform; the per-channel MAC no longer
 // walks j partitions four at a time.
+#ifdef NEO_AHEAD_PROBE
+// diagnostic build only (make PROBE=1): s_memrealtime stamps of channel 0's phases
+__device__ unsigned long long g_probe[16];
+#define NEO_PROBE(i, cond)                                                                     \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        if (c == 0 && (cond)) g_probe[i] = __builtin_amdgcn_s_memrealtime();                   \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+    } while (0)
+#else
+#define NEO_PROBE(i, cond) (void)0
+#endif
+
+constexpr int kSubWindow = 8;  // lookahead sub-window (blocks)
+
 template<int B>
 struct ahead_cfg {
     static constexpr int Q = B / 2;                                  // float4 (2 bins) per row
@@ -594,12 +622,12 @@ template<int B, bool OLA>
 __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
-    const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride)
+    const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int jr)
 {
     using K = upols_cfg<B>;
     using A = ahead_cfg<B>;
     constexpr int Q = A::Q, NG = A::NG, EW = A::EW, TW = A::TW, KC = A::KC;
-    static_assert(TW <= 64 && A::NT <= 1024, "ahead2 geometry");
+    static_assert(TW <= 64 && A::NT <= 1024 && EW % 2 == 0, "ahead2 geometry");
     __shared__ __attribute__((aligned(16))) cf X[B];
     __shared__ __attribute__((aligned(16))) float4 acc[NG][Q];
     __shared__ cf fft[K::LL];
@@ -611,6 +639,8 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     const int64_t ps4 = pstride / 2;
     const float4* H4 = reinterpret_cast<const float4*>(H + crow);
     float4 h0 = {0.f, 0.f, 0.f, 0.f};
+    NEO_PROBE(0, tid == 0);
+    NEO_PROBE(8, tid == 64);
     if (tid < 64) {  // wave 0: window r2c, FDL row w, previous block
         for (int i = tid; i < K::TW1 + K::TW2; i += 64) tw[i] = twg[i];
         cf v[EW];
@@ -623,9 +653,20 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
                 if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
                 else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
             }
+            if constexpr (!OLA) {
+                // the window's second half (this block, v[EW/2..EW-1]) becomes the next call's
+                // first half, stored from registers (a re-load cost a ~1 us round trip). Lanes
+                // read prev_c[n] in load m - EW/2 of the same wave, which has completed (loads
+                // return in order) by the time the store of load m's value issues.
+                cf* pw = reinterpret_cast<cf*>(prev_c);
+#pragma unroll
+                for (int m = EW / 2; m < EW; ++m) pw[tid + m * TW - B / 2] = v[m];
+            }
         }
         wave_sync();
+        NEO_PROBE(1, tid == 0);
         stockham<B, EW, -1, 1, true>(v, fft, tw, tid, tid < TW);
+        NEO_PROBE(2, tid == 0);
         if (tid < TW) {
 #pragma unroll
             for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
@@ -636,10 +677,6 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
             const cf x = r2c_split<B>(fft, tw + K::TW1, k);
             X[k] = x;
             row[k] = x;
-        }
-        if constexpr (!OLA) {  // the window's second half becomes the next call's first half
-            for (int i = tid; i < B / 4; i += 64)
-                reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
         }
     } else {  // MAC groups: slabs + partitions 1..j
         const int u = tid - 64, g = u / Q, q = u - g * Q;
@@ -652,13 +689,17 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
             const float4 r = S4[s * ss4 + q];
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
+        if (sub && g == NG - 1) {  // sub-window pass: the window's rows before this sub-window
+            const float4 r = reinterpret_cast<const float4*>(sub + (int64_t(c) * kSubWindow + jr) * B)[q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
         acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
-        for (int pb = 1 + g; pb <= j; pb += NG * KC) {
+        for (int pb = 1 + g; pb <= jr; pb += NG * KC) {
             float4 hv[KC], xv[KC];
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
                 const int p = pb + k * NG;
-                if (p <= j) {
+                if (p <= jr) {
                     const int r = w - p < 0 ? w - p + ring : w - p;
                     hv[k] = H4[int64_t(p) * ps4 + q];
                     xv[k] = F4[int64_t(r) * ps4 + q];
@@ -666,12 +707,15 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
             }
 #pragma unroll
             for (int k = 0; k < KC; ++k)
-                if (pb + k * NG <= j) mac2(a0, a1, hv[k], xv[k]);
+                if (pb + k * NG <= jr) mac2(a0, a1, hv[k], xv[k]);
         }
         const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
         acc[g][q] = make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
+        NEO_PROBE(9, tid == 64);
     }
+    NEO_PROBE(3, tid == 0);
     __syncthreads();
+    NEO_PROBE(4, tid == 0);
     if (tid >= 64 && tid < 64 + Q) {  // group 0: + H0 X + the other groups
         const int q = tid - 64;
         acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
@@ -686,36 +730,59 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
         reinterpret_cast<float4*>(X)[q] = make_float4(y.x + b0.x, y.y + b0.y, y.z + b1.x, y.w + b1.y);
     }
     __syncthreads();
+    NEO_PROBE(5, tid == 0);
     if (tid < 64) c2r_tail<B, OLA, EW, true>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
+    NEO_PROBE(6, tid == 0);
+}
+
+// one k_batch_mac launch: T blocks at write position h->wpos into slabs `part` [C][S][T][B],
+// splits of `rows` partitions over [0, P); FDL rows entering past partition `emax` count as
+// zero (the lookahead's sub-window passes take only the rows of the current window)
+struct mac_pass {
+    cf* part;
+    int P, S, rows, emax;
+};
+
+static mac_pass full_pass(const upols_t* h) { return {h->part_b, h->P, h->Sb, h->rows_b, 0x7fffffff}; }
+
+// zero FDL row for entering rows past emax, as a row index relative to a channel's FDL base:
+// H's first spare row of the same channel (H rows P .. ring-1 are zero; H and FDL share one
+// allocation, FDL = H + nrows * B), negative, so buffer loads also see it out of range (0)
+static int zero_row(const upols_t* h)
+{
+    const int64_t fdl_rows = int64_t(h->C) * h->ring * h->B / h->pstride;  // FDL offset in rows
+    return int(h->P - fdl_rows);
 }
 
 // dispatch k_batch_mac over (B, NB, T) for the valid combinations
 template<int BB, int NB>
-int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead)
+int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead, const mac_pass& mp)
 {
     constexpr int L = batch_cfg<BB, NB>::L;
-    const unsigned grid = unsigned(h->C) * unsigned(h->Sb) * unsigned(batch_cfg<BB, NB>::G);
+    const unsigned grid = unsigned(h->C) * unsigned(mp.S) * unsigned(batch_cfg<BB, NB>::G);
+    const int rz = zero_row(h);
+    const bool lds_ok = mp.emax == 0x7fffffff;  // the LDS-DMA variants take whole passes only
 #define NEO_BATCH_T(TT)                                                                                          \
     case TT:                                                                                                     \
         if constexpr (batch_t(BB, NB, TT) == TT) {                                                               \
             if constexpr (TT == 32 && NB == 1 && (BB == 256 || BB == 512)) {                                     \
-                if (h->bvar >= 4) {                                                                              \
+                if (h->bvar >= 4 && lds_ok) {                                                                    \
                     hipLaunchKernelGGL(h->bvar == 4 ? (k_batch_mac_lds<BB, TT, 4>) : (k_batch_mac_lds<BB, TT, 5>),   \
-                                       dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, h->ring, h->Sb, \
-                                       h->rows_b, h->wpos, h->cstride, h->pstride, ahead);                       \
+                                       dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part, mp.P, h->ring, mp.S,   \
+                                       mp.rows, h->wpos, h->cstride, h->pstride, ahead);                         \
                     break;                                                                                       \
                 }                                                                                                \
                 if (h->bvar != 0) {                                                                              \
                     hipLaunchKernelGGL(h->bvar == 1   ? (k_batch_mac<BB, TT, NB, 1>)                            \
                                        : h->bvar == 2 ? (k_batch_mac<BB, TT, NB, 2>)                            \
                                                       : (k_batch_mac<BB, TT, NB, 3>),                           \
-                                       dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b, h->P, h->ring, h->Sb, \
-                                       h->rows_b, h->wpos, h->cstride, h->pstride, ahead);                       \
+                                       dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part, mp.P, h->ring, mp.S,   \
+                                       mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz);            \
                     break;                                                                                       \
                 }                                                                                                \
             }                                                                                                    \
-            hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 0>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, h->part_b,  \
-                               h->P, h->ring, h->Sb, h->rows_b, h->wpos, h->cstride, h->pstride, ahead);         \
+            hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 0>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part,    \
+                               mp.P, h->ring, mp.S, mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz); \
             break;                                                                                               \
         }                                                                                                        \
         return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);
@@ -732,13 +799,12 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead)
     return NEO_HIP_OK;
 }
 
-// T consecutive blocks: window r2c + insert (C x T), one MAC pass (C x Sb), per-block
-// finish (C x T), OLA overlap chain (C).
 static int batch_buffers(upols_t* h)
 {
     if (!h->part_b) {
         NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
                                 size_t(h->C) * h->Sb * kMaxBatch * h->B * sizeof(cf)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_s), size_t(h->C) * kSubWindow * h->B * sizeof(cf)));
         if (h->ola)
             NEO_HIP_CHECK(
                 hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * h->B * sizeof(float)));
@@ -777,24 +843,34 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         const bool timed = h->timing && h->tick++ % h->timing == 0;
         if ((rc = mac_event(h, timed, false, ev, s))) return rc;
         if (h->bNB == 2) {
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 1)))
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 1, full_pass(h))))
         } else {
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 1)))
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 1, full_pass(h))))
         }
         if (rc) return rc;
         if ((rc = mac_event(h, timed, true, ev, s))) return rc;
     }
     if (h->akern == 2 && B <= 1024) {
+        // sub-windows (kSubWindow blocks): at the first block of each after the first, one pass
+        // over the window's rows so far; the block step then walks its sub-window's rows only
+        const bool sub = h->asub && T % kSubWindow == 0 && T > kSubWindow;
+        const int jr = sub ? h->phase % kSubWindow : h->phase;
+        if (sub && h->phase >= kSubWindow && jr == 0) {
+            const mac_pass mp{h->part_s, h->phase + kSubWindow, 1, h->phase + kSubWindow, h->phase};
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, kSubWindow, s, 1, mp)))
+            if (rc) return rc;
+        }
+        const cf* subp = sub && h->phase >= kSubWindow ? h->part_s : nullptr;
         if (h->ola) {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, true>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, jr))
         } else {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, false>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, jr))
         }
     } else if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_upols_ahead<BB, true>), dim3(unsigned(h->C)), dim3(256), 0, s, in,
@@ -830,9 +906,9 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     int rc = mac_event(h, timed, false, ev, s);
     if (rc) return rc;
     if (h->bNB == 2) {
-        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 0)))
+        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 0, full_pass(h))))
     } else {
-        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 0)))
+        NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 0, full_pass(h))))
     }
     if (rc) return rc;
     if ((rc = mac_event(h, timed, true, ev, s))) return rc;
@@ -853,3 +929,11 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
 
 
 }  // namespace neo_hip
+
+#ifdef NEO_AHEAD_PROBE
+// diagnostic build only: copy channel 0's k_upols_ahead2 phase stamps (s_memrealtime, 100 MHz)
+extern "C" __attribute__((visibility("default"))) int neo_hip_debug_probe(unsigned long long* dst)
+{
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(neo_hip::g_probe), sizeof(neo_hip::g_probe)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -1,0 +1,45 @@
+"""Phase stamps of k_upols_ahead2 (channel 0) from the diagnostic build (tools/probe/,
+-DNEO_AHEAD_PROBE): s_memrealtime (100 MHz) at kernel entry, after the input loads,
+after the window FFT, before/after each workgroup barrier, after the c2r; wave 1 (MAC
+group) at entry and when its slab sum + rows are done. usage: python tools/probebench.py [c5|c4]"""
+import ctypes
+import os
+import sys
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["NEO_HIP_LIBRARY"] = os.path.join(R, "tools", "probe", "libneo_hip_probe.so")
+sys.path[:0] = [os.path.join(R, "neo-dsp_amd"), R]
+import torch  # noqa: E402
+import neo  # noqa: E402
+import bench  # noqa: E402
+from neo import _native  # noqa: E402
+
+wl = sys.argv[1] if len(sys.argv) > 1 else "c5"
+C, B, L = bench.WORKLOADS[wl]
+P = neo.num_partitions(L, B)
+g = torch.Generator(device="cuda").manual_seed(1)
+ir = torch.rand((C, L), generator=g, device="cuda") * 2 - 1
+cv = neo.UpolsConvolver(C, B, P)
+cv.set_impulse(ir)
+cv.set_batch(False)
+cv.set_ahead(True)
+lib = _native.load()
+buf = (ctypes.c_ulonglong * 16)()
+x = torch.rand((C, B), generator=g, device="cuda") * 2 - 1
+y = torch.empty_like(x)
+names = ["entry", "loaded", "fft", "r2c+row", "bar1", "bar2", "c2r"]
+rows = {}
+for it in range(4 * 32):
+    ph = cv.ahead_info()[1]
+    cv.process_device(x.data_ptr(), B, y.data_ptr(), B, 0)
+    torch.cuda.synchronize()
+    assert lib.neo_hip_debug_probe(buf) == 0
+    t = list(buf)
+    if it >= 64:
+        rows.setdefault(ph, []).append([(t[k] - t[0]) * 10 for k in range(7)] + [(t[8] - t[0]) * 10, (t[9] - t[0]) * 10])
+print(f"{wl}: ns since wave-0 entry, median over 2 windows; MAC wave: entry / done")
+print("  j " + " ".join(f"{n:>8s}" for n in names) + "  macIn  macDone")
+for j in sorted(rows):
+    v = rows[j]
+    med = [sorted(c)[len(c) // 2] for c in zip(*v)]
+    print(f"{j:3d} " + " ".join(f"{m:8d}" for m in med[:7]) + f" {med[7]:6d} {med[8]:8d}")
