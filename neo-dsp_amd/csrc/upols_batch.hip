@@ -58,7 +58,9 @@ struct acc3 {
 // Row loads of the batched MAC. BUF = false: flat global loads (64-bit address per lane
 // and row). BUF = true: buffer loads over a per-channel descriptor, the lane's byte
 // offset fixed in a VGPR and the row offset in an SGPR (no per-row address VALU).
-template<class V, bool BUF>
+// HNT: filter rows nontemporal (true) or with the default policy, so that the first rows of
+// each channel stay resident in the Infinity Cache across passes (false).
+template<class V, bool BUF, bool HNT = true>
 struct row_src {
     const V* Hv;
     const V* Fv;
@@ -75,11 +77,13 @@ struct row_src {
     __device__ __forceinline__ V h(int p, int lane) const
     {
         if constexpr (BUF) {
-            // (a per-row cacheable/nontemporal select here costs 54 spilled VGPRs at 256)
-            const auto u = __builtin_amdgcn_raw_buffer_load_b64(Hr, lane * int(sizeof(V)), p * prow, 2 /* nt */);
+            // (a per-row cacheable/nontemporal select here cost 54 spilled VGPRs at 256: the policy
+            // is a template argument and the partition loop runs in two ranges instead)
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(Hr, lane * int(sizeof(V)), p * prow, HNT ? 2 : 0);
             return __builtin_bit_cast(V, u);
         } else {
-            return __builtin_nontemporal_load(Hv + int64_t(p) * psv + lane);
+            if constexpr (HNT) return __builtin_nontemporal_load(Hv + int64_t(p) * psv + lane);
+            else return Hv[int64_t(p) * psv + lane];
         }
     }
     __device__ __forceinline__ V f(int r, int lane) const
@@ -205,13 +209,41 @@ struct bmac_var<3> {  // as 2 with buffer loads (row offsets in SGPRs)
     static constexpr bool A2 = true, BUF = true;
     static constexpr int D = 8, W = 2;
 };
+#ifdef NEO_AHEAD_PROBE
+// diagnostic build only (make probe): s_memrealtime stamps of channel 0's phases;
+// k_batch_mac: s_memtime + s_memrealtime at entry and exit of workgroup 0 (clock)
+__device__ unsigned long long g_probe[16];
+__device__ unsigned long long g_wgspan[4096][2];  // k_batch_mac (T = 32): per-workgroup entry / exit, s_memrealtime
+#define NEO_PROBE(i, cond)                                                                     \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        if (c == 0 && (cond)) g_probe[i] = __builtin_amdgcn_s_memrealtime();                   \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+    } while (0)
+#define NEO_CLOCK_STAMP(i)                                                                     \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                             \
+            g_probe[i] = __builtin_amdgcn_s_memtime();                                         \
+            g_probe[i + 1] = __builtin_amdgcn_s_memrealtime();                                 \
+        }                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                             \
+            g_wgspan[blockIdx.x][(i) == 10 ? 0 : 1] = __builtin_amdgcn_s_memrealtime();        \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+    } while (0)
+#else
+#define NEO_CLOCK_STAMP(i) (void)0
+#define NEO_PROBE(i, cond) (void)0
+#endif
+
 template<int B, int T, int NB, int VAR, int D0 = bmac_var<VAR>::D, int D = (T < D0 ? T : D0)>
 __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_batch_mac(const cf* __restrict__ H,
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
                                                                    int64_t cstride, int64_t pstride, int ahead,
-                                                                   int emax, int rz)
+                                                                   int emax, int rz, int pc)
 {
+    if constexpr (T == 32) NEO_CLOCK_STAMP(10);
     using K = batch_cfg<B, NB>;
     using V = bvec<NB>;
     constexpr int VPT = K::VPT, L = K::L;
@@ -228,6 +260,9 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     const row_src<V, BUF> src{Hv, Fv, psv, __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Hv), 0, span, 0x00020000),
                               __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(Fv), 0, span, 0x00020000),
                               int(pstride * int64_t(sizeof(cf))), emax, rz};
+    // filter rows p < pc with the default (cacheable) policy: the same rows every pass, kept
+    // in the Infinity Cache; the nontemporal stream of the rest does not evict them
+    const row_src<V, BUF, false> src_c{src.Hv, src.Fv, src.psv, src.Hr, src.Fr, src.prow, emax, rz};
 
     acc3 a[T][NB * VPT];
 #pragma unroll
@@ -256,12 +291,17 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
             pf[d][v] = future && d == 0 ? V{} : src.f(r, tid + v * L);
-            ph[d][v] = src.h(p, tid + v * L);
+            ph[d][v] = BUF && p < pc ? src_c.h(p, tid + v * L) : src.h(p, tid + v * L);
         }
     }
     // splits hold a multiple of T partitions; the last split's final chunk runs past P into
-    // the ring's spare filter rows, which are zero (so those steps add nothing)
-    for (int pb = p0; pb < p1; pb += T)
+    // the ring's spare filter rows, which are zero (so those steps add nothing). Chunks
+    // starting below pc load filter rows cacheable, the rest nontemporally.
+    int pb = p0;
+    for (; BUF && pb < p1 && pb < pc; pb += T)  // (flat-load variants: all nontemporal, no spills)
+        batch_chunk<T, NB, VPT, L, D, bmac_var<VAR>::A2>(a, f, ph, pf, src_c, tid, ring, w, pb,
+                                                          std::make_integer_sequence<int, T>{});
+    for (; pb < p1; pb += T)
         batch_chunk<T, NB, VPT, L, D, bmac_var<VAR>::A2>(a, f, ph, pf, src, tid, ring, w, pb,
                                                           std::make_integer_sequence<int, T>{});
 
@@ -285,6 +325,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
             }
             *reinterpret_cast<V*>(slab + int64_t(j) * B + (tid + v * L) * NB) = o;
         }
+    if constexpr (T == 32) NEO_CLOCK_STAMP(12);
 }
 
 // k_batch_mac with the row stream through an LDS-DMA ring (B = 256 / 512, T = 32, one
@@ -593,18 +634,6 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
 // wave 0 runs the c2r. The serial chain per block is one window transform, one burst of
 // row loads (overlapped with it) and one inverse transform; the per-channel MAC no longer
 // walks j partitions four at a time.
-#ifdef NEO_AHEAD_PROBE
-// diagnostic build only (make PROBE=1): s_memrealtime stamps of channel 0's phases
-__device__ unsigned long long g_probe[16];
-#define NEO_PROBE(i, cond)                                                                     \
-    do {                                                                                       \
-        __builtin_amdgcn_sched_barrier(0);                                                     \
-        if (c == 0 && (cond)) g_probe[i] = __builtin_amdgcn_s_memrealtime();                   \
-        __builtin_amdgcn_sched_barrier(0);                                                     \
-    } while (0)
-#else
-#define NEO_PROBE(i, cond) (void)0
-#endif
 
 constexpr int kSubWindow = 8;  // lookahead sub-window (blocks)
 
@@ -740,10 +769,10 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
 // zero (the lookahead's sub-window passes take only the rows of the current window)
 struct mac_pass {
     cf* part;
-    int P, S, rows, emax;
+    int P, S, rows, emax, pc;  // pc: filter rows per channel loaded cacheable
 };
 
-static mac_pass full_pass(const upols_t* h) { return {h->part_b, h->P, h->Sb, h->rows_b, 0x7fffffff}; }
+static mac_pass full_pass(const upols_t* h) { return {h->part_b, h->P, h->Sb, h->rows_b, 0x7fffffff, h->pcb}; }
 
 // zero FDL row for entering rows past emax, as a row index relative to a channel's FDL base:
 // H's first spare row of the same channel (H rows P .. ring-1 are zero; H and FDL share one
@@ -777,12 +806,13 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead, const ma
                                        : h->bvar == 2 ? (k_batch_mac<BB, TT, NB, 2>)                            \
                                                       : (k_batch_mac<BB, TT, NB, 3>),                           \
                                        dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part, mp.P, h->ring, mp.S,   \
-                                       mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz);            \
+                                       mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz, mp.pc);      \
                     break;                                                                                       \
                 }                                                                                                \
             }                                                                                                    \
             hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 0>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part,    \
-                               mp.P, h->ring, mp.S, mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz); \
+                               mp.P, h->ring, mp.S, mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz,   \
+                               mp.pc);                                                                          \
             break;                                                                                               \
         }                                                                                                        \
         return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);
@@ -856,7 +886,7 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         const bool sub = h->asub && T % kSubWindow == 0 && T > kSubWindow;
         const int jr = sub ? h->phase % kSubWindow : h->phase;
         if (sub && h->phase >= kSubWindow && jr == 0) {
-            const mac_pass mp{h->part_s, h->phase + kSubWindow, 1, h->phase + kSubWindow, h->phase};
+            const mac_pass mp{h->part_s, h->phase + kSubWindow, 1, h->phase + kSubWindow, h->phase, h->P};
             NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, kSubWindow, s, 1, mp)))
             if (rc) return rc;
         }
@@ -935,5 +965,9 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
 extern "C" __attribute__((visibility("default"))) int neo_hip_debug_probe(unsigned long long* dst)
 {
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(neo_hip::g_probe), sizeof(neo_hip::g_probe)) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int neo_hip_debug_wgspan(unsigned long long* dst)
+{
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(neo_hip::g_wgspan), sizeof(neo_hip::g_wgspan)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -31,6 +31,7 @@ struct neo_hip_upols {
     bool batch = true;      // process_blocks runs T blocks per MAC pass (neo_hip_upols_set_batch)
     int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
     int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
+    int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kCacheBudgetBytes; NEO_HIP_BATCH_CACHE_ROWS)
     int bvar = 3;           // batched MAC variant at T = 32, B = 256/512 (bmac_var in upols_batch.hip; NEO_HIP_BATCH_VAR)
     neo_hip::cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
     // streaming lookahead (k_upols_ahead): one batched pass per T blocks, phase = block of

@@ -43,3 +43,34 @@ for j in sorted(rows):
     v = rows[j]
     med = [sorted(c)[len(c) // 2] for c in zip(*v)]
     print(f"{j:3d} " + " ".join(f"{m:8d}" for m in med[:7]) + f" {med[7]:6d} {med[8]:8d}")
+
+# clock during the window pass under sustained load: 8 windows back to back, stamps of the
+# last pass (workgroup 0: s_memtime shader cycles over s_memrealtime 100 MHz ticks)
+xs = torch.rand((C, 256 * B), generator=g, device="cuda") * 2 - 1
+ys = torch.empty_like(xs)
+for rep in range(3):
+    while cv.ahead_info()[1] != 0:
+        cv.process_device(x.data_ptr(), B, y.data_ptr(), B, 0)
+    cv.process_blocks_ptr(xs.data_ptr(), ys.data_ptr(), 256 * B, 256, 0)
+    torch.cuda.synchronize()
+    assert lib.neo_hip_debug_probe(buf) == 0
+    t = list(buf)
+    cyc, rt = t[12] - t[10], t[13] - t[11]
+    print(f"window pass (workgroup 0): {rt * 10 / 1e3:.1f} us, {cyc} cycles -> {cyc / (rt * 10):.3f} GHz")
+
+# per-workgroup entry/exit of the last window pass: how many workgroups run at once
+span = (ctypes.c_ulonglong * (4096 * 2))()
+assert lib.neo_hip_debug_wgspan(span) == 0
+nwg = C * cv.ahead_info()[3] * max(1, B // 256)
+ent = [span[2 * i] for i in range(nwg)]
+ext = [span[2 * i + 1] for i in range(nwg)]
+t0 = min(ent)
+ent = [(e - t0) * 10 / 1e3 for e in ent]
+ext = [(e - t0) * 10 / 1e3 for e in ext]
+dur = sorted(b - a for a, b in zip(ent, ext))
+print(f"{nwg} workgroups: entry us min/median/max {min(ent):.1f}/{sorted(ent)[nwg // 2]:.1f}/{max(ent):.1f}; "
+      f"exit max {max(ext):.1f}; duration min/median/max {dur[0]:.1f}/{dur[nwg // 2]:.1f}/{dur[-1]:.1f}")
+hist = [0] * 10
+for e in ent:
+    hist[min(9, int(e / (max(ext) / 10)))] += 1
+print("entry histogram over the pass (10 bins):", hist)
