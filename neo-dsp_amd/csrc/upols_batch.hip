@@ -702,11 +702,17 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
         }
         wave_sync();
         cf* row = fdl + crow + int64_t(w) * pstride;
-        for (int k = tid; k < B; k += 64) {
-            const cf x = r2c_split<B>(fft, tw + K::TW1, k);
-            X[k] = x;
-            row[k] = x;
-        }
+        constexpr int NK = (B + 63) / 64;
+        cf xs[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i)  // all LDS reads first, then the stores
+            if (tid + 64 * i < B) xs[i] = r2c_split<B>(fft, tw + K::TW1, tid + 64 * i);
+#pragma unroll
+        for (int i = 0; i < NK; ++i)
+            if (tid + 64 * i < B) {
+                X[tid + 64 * i] = xs[i];
+                row[tid + 64 * i] = xs[i];
+            }
     } else {  // MAC groups: slabs + partitions 1..j
         const int u = tid - 64, g = u / Q, q = u - g * Q;
         if (g == 0) h0 = H4[q];

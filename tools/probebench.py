@@ -74,3 +74,15 @@ hist = [0] * 10
 for e in ent:
     hist[min(9, int(e / (max(ext) / 10)))] += 1
 print("entry histogram over the pass (10 bins):", hist)
+by_xcd = {}
+for i in range(nwg):
+    by_xcd.setdefault(i % 8, []).append(ext[i] - ent[i])
+print("duration by blockIdx % 8 (XCD):", {k: round(sum(v) / len(v), 1) for k, v in sorted(by_xcd.items())})
+by_g = {}
+for i in range(nwg):
+    by_g.setdefault(i % 2, []).append(ext[i] - ent[i])
+print("duration by bin half (blockIdx % 2):", {k: round(sum(v) / len(v), 1) for k, v in sorted(by_g.items())})
+d16 = [round(ext[i] - ent[i]) for i in range(64)]
+print("first 64 workgroups:", d16)
+print("mean duration per 32 consecutive workgroups:", [round(sum(ext[i] - ent[i] for i in range(k, k + 32)) / 32) for k in range(0, nwg, 32)])
+print("exit time per 32 consecutive workgroups (max):", [round(max(ext[i] for i in range(k, k + 32))) for k in range(0, nwg, 32)])
