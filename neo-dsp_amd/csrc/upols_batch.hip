@@ -651,7 +651,8 @@ template<int B, bool OLA>
 __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
-    const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int jr)
+    const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int ssub,
+    int jr)
 {
     using K = upols_cfg<B>;
     using A = ahead_cfg<B>;
@@ -724,8 +725,8 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
             const float4 r = S4[s * ss4 + q];
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
-        if (sub && g == NG - 1) {  // sub-window pass: the window's rows before this sub-window
-            const float4 r = reinterpret_cast<const float4*>(sub + (int64_t(c) * kSubWindow + jr) * B)[q];
+        for (int s = NG - 1 - g; s < ssub; s += NG) {  // sub-window pass slabs (the window's earlier rows)
+            const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + s) * kSubWindow + jr) * B)[q];
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
@@ -840,7 +841,8 @@ static int batch_buffers(upols_t* h)
     if (!h->part_b) {
         NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
                                 size_t(h->C) * h->Sb * kMaxBatch * h->B * sizeof(cf)));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_s), size_t(h->C) * kSubWindow * h->B * sizeof(cf)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_s),
+                                size_t(h->C) * (kMaxBatch / kSubWindow) * kSubWindow * h->B * sizeof(cf)));
         if (h->ola)
             NEO_HIP_CHECK(
                 hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * h->B * sizeof(float)));
@@ -891,22 +893,25 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         // over the window's rows so far; the block step then walks its sub-window's rows only
         const bool sub = h->asub && T % kSubWindow == 0 && T > kSubWindow;
         const int jr = sub ? h->phase % kSubWindow : h->phase;
-        if (sub && h->phase >= kSubWindow && jr == 0) {
-            const mac_pass mp{h->part_s, h->phase + kSubWindow, 1, h->phase + kSubWindow, h->phase, h->P};
+        // one split per kSubWindow partitions (each walks one chunk): the pass is latency-bound
+        const int ssub = sub && h->phase >= kSubWindow ? (h->ssplit ? h->phase / kSubWindow + 1 : 1) : 0;
+        if (ssub && jr == 0) {
+            const int srows = (h->phase + kSubWindow) / ssub;
+            const mac_pass mp{h->part_s, h->phase + kSubWindow, ssub, srows, h->phase, h->P};
             NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, kSubWindow, s, 1, mp)))
             if (rc) return rc;
         }
-        const cf* subp = sub && h->phase >= kSubWindow ? h->part_s : nullptr;
+        const cf* subp = h->part_s;
         if (h->ola) {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, true>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride, subp, jr))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr))
         } else {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, false>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride, subp, jr))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr))
         }
     } else if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_upols_ahead<BB, true>), dim3(unsigned(h->C)), dim3(256), 0, s, in,

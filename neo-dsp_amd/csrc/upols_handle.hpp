@@ -37,8 +37,9 @@ struct neo_hip_upols {
     // streaming lookahead (k_upols_ahead): one batched pass per T blocks, phase = block of
     // the current window; on for HBM-bound shapes (not fused), NEO_HIP_AHEAD / set_ahead
     bool ahead = false;
-    bool asub = true;   // lookahead sub-windows (k_upols_ahead2 only; NEO_HIP_AHEAD_SUB=0 disables)
-    neo_hip::cf* part_s = nullptr;  // sub-window pass slabs [C][kSubWindow][B]
+    bool asub = true;
+    bool ssplit = false;  // sub-window passes: one split per chunk (NEO_HIP_SUB_SPLIT=1; A/B on one box: slower)   // lookahead sub-windows (k_upols_ahead2 only; NEO_HIP_AHEAD_SUB=0 disables)
+    neo_hip::cf* part_s = nullptr;  // sub-window pass slabs [C][ssub <= kMaxBatch / kSubWindow][kSubWindow][B]
     int akern = 2;  // per-block lookahead kernel: 2 = k_upols_ahead2 (B <= 1024), 1 = k_upols_ahead (NEO_HIP_AHEAD_KERNEL)
     int phase = 0;
     float* tail = nullptr;  // batched OLA tails [C][T][B]
