@@ -241,7 +241,7 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
                                                                    const cf* __restrict__ fdl, cf* __restrict__ part,
                                                                    int P, int ring, int S, int rows, int w,
                                                                    int64_t cstride, int64_t pstride, int ahead,
-                                                                   int emax, int rz, int pc)
+                                                                   int emax, int rz, int pc, int prio)
 {
     if constexpr (T == 32) NEO_CLOCK_STAMP(10);
     using K = batch_cfg<B, NB>;
@@ -297,13 +297,30 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     // splits hold a multiple of T partitions; the last split's final chunk runs past P into
     // the ring's spare filter rows, which are zero (so those steps add nothing). Chunks
     // starting below pc load filter rows cacheable, the rest nontemporally.
+    // prio: two workgroups share a CU (blockIdx i and i + grid/2, the dispatch order) and the
+    // SQ favours the older one's waves, which finish ~30 % early and leave one wave per SIMD
+    // for the rest of the pass; with prio they trade issue priority in 20 us slices
+    // (s_memrealtime, 100 MHz). (Locking the two together with a barrier per chunk instead —
+    // one 8-wave workgroup per CU — was 30 % slower: both stall on memory at the same time.)
+    const int half = blockIdx.x >= gridDim.x / 2;
+    auto share = [&]() {
+        if (prio) {
+            if (((__builtin_amdgcn_s_memrealtime() >> 11) + half) & 1) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+    };
     int pb = p0;
-    for (; BUF && pb < p1 && pb < pc; pb += T)  // (flat-load variants: all nontemporal, no spills)
+    for (; BUF && pb < p1 && pb < pc; pb += T) {  // (flat-load variants: all nontemporal, no spills)
+        share();
         batch_chunk<T, NB, VPT, L, D, bmac_var<VAR>::A2>(a, f, ph, pf, src_c, tid, ring, w, pb,
                                                           std::make_integer_sequence<int, T>{});
-    for (; pb < p1; pb += T)
+    }
+    for (; pb < p1; pb += T) {
+        share();
         batch_chunk<T, NB, VPT, L, D, bmac_var<VAR>::A2>(a, f, ph, pf, src, tid, ring, w, pb,
                                                           std::make_integer_sequence<int, T>{});
+    }
+    if (prio) __builtin_amdgcn_s_setprio(0);
 
     cf* slab = part + (int64_t(c) * S + s) * T * B;
 #pragma unroll
@@ -813,13 +830,13 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead, const ma
                                        : h->bvar == 2 ? (k_batch_mac<BB, TT, NB, 2>)                            \
                                                       : (k_batch_mac<BB, TT, NB, 3>),                           \
                                        dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part, mp.P, h->ring, mp.S,   \
-                                       mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz, mp.pc);      \
+                                       mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz, mp.pc, h->bprio); \
                     break;                                                                                       \
                 }                                                                                                \
             }                                                                                                    \
             hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 0>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part,    \
                                mp.P, h->ring, mp.S, mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz,   \
-                               mp.pc);                                                                          \
+                               mp.pc, h->bprio);                                                                \
             break;                                                                                               \
         }                                                                                                        \
         return fail(NEO_HIP_EINVAL, "batch of %d blocks not available at block %d", TT, BB);

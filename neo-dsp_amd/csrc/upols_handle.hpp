@@ -32,13 +32,14 @@ struct neo_hip_upols {
     int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
     int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
     int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kCacheBudgetBytes; NEO_HIP_BATCH_CACHE_ROWS)
+    int bprio = 1;          // batched MAC: co-resident workgroups trade issue priority (NEO_HIP_BATCH_PRIO=0 off)
     int bvar = 3;           // batched MAC variant at T = 32, B = 256/512 (bmac_var in upols_batch.hip; NEO_HIP_BATCH_VAR)
     neo_hip::cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
     // streaming lookahead (k_upols_ahead): one batched pass per T blocks, phase = block of
     // the current window; on for HBM-bound shapes (not fused), NEO_HIP_AHEAD / set_ahead
     bool ahead = false;
-    bool asub = true;
-    bool ssplit = false;  // sub-window passes: one split per chunk (NEO_HIP_SUB_SPLIT=1; A/B on one box: slower)   // lookahead sub-windows (k_upols_ahead2 only; NEO_HIP_AHEAD_SUB=0 disables)
+    bool asub = true;     // lookahead sub-windows (k_upols_ahead2 only; NEO_HIP_AHEAD_SUB=0 disables)
+    bool ssplit = false;  // sub-window passes: one split per chunk (NEO_HIP_SUB_SPLIT=1; A/B on one box: slower)
     neo_hip::cf* part_s = nullptr;  // sub-window pass slabs [C][ssub <= kMaxBatch / kSubWindow][kSubWindow][B]
     int akern = 2;  // per-block lookahead kernel: 2 = k_upols_ahead2 (B <= 1024), 1 = k_upols_ahead (NEO_HIP_AHEAD_KERNEL)
     int phase = 0;
