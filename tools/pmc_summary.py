@@ -58,13 +58,15 @@ def main():
         return
     for w in ("c5", "c4"):
         b = bench_line(tag, w)
-        summarize(tag, w, "k_batch_mac", b["roofline"]["algorithmic_bytes_per_launch"], w)
+        # the window pass only (T = 32), not the lookahead's sub-window passes (T = 8)
+        summarize(tag, w, f"k_batch_mac<{b['config']['block']}, 32", b["roofline"]["algorithmic_bytes_per_launch"], w)
         summarize(tag, w, "k_upols_step", b["per_block_step"]["algorithmic_bytes_per_launch"], w + "_plain")
     b = bench_line(tag, "c2")
     summarize(tag, "c2", "k_c2c_lds<4096", b["roofline"]["algorithmic_bytes_per_launch"], "c2")
     b = bench_line(tag, "c5")
     if b.get("offline"):
-        summarize(tag, "c5o", "k_batch_mac", b["offline"]["algorithmic_bytes_per_launch"], "c5_offline")
+        summarize(tag, "c5o", f"k_batch_mac<{b['config']['block']}, 32", b["offline"]["algorithmic_bytes_per_launch"],
+                  "c5_offline")
 
 
 if __name__ == "__main__":
