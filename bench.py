@@ -35,6 +35,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, "neo-dsp_amd")]
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 vector (packed FMA) peak, 256 CU x 4 SIMD x 64 flop/clk x 2.4 GHz
 # Untimed warm-up: at least --warmup steps AND at least this much GPU time. MI355X runs
 # the first ~20 ms of sustained HBM load measurably slower (clock ramp; measured 0.93 vs
 # 0.74 ms for the 4096 x 65536 FFT), which a few warm-up steps do not cover.
@@ -302,6 +303,11 @@ def run_upols(args, world, rank, local):
         "per_block_step": plain,
         "offline": offline,
     }
+    if ahead:
+        # the window pass is also an fp32 FMA stream: 8 flop per complex MAC, T blocks per pass
+        tflops = 8.0 * C * P * B * T / (mac_avg_ms * 1e-3) / 1e12
+        res["roofline"]["valu"] = {"achieved_tflops": tflops, "peak_tflops": PEAK_FP32_TFLOPS, "frac": tflops / PEAK_FP32_TFLOPS,
+                                   "note": "packed-FMA peak at 2.4 GHz; the pass holds 1.6-1.7 GHz (DESIGN.md section 5)"}
     if args.workload == "c3":
         res["roofline"]["note"] = "working set L2/MALL-resident: effective GB/s, launch-latency bound"
     return res

@@ -408,6 +408,8 @@ void destroy(upols_t* h)
     (void)hipFree(h->samples_dev);
     (void)hipFree(h->part_b);
     (void)hipFree(h->part_s);
+    (void)hipFree(h->h0t);
+    (void)hipFree(h->h0tail);
     (void)hipFree(h->tail);
     if (h->samples_host) (void)hipHostFree(h->samples_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -587,6 +589,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     if (const char* e = std::getenv("NEO_HIP_BATCH_CACHE_ROWS")) h->pcb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("NEO_HIP_SUB_SPLIT")) h->ssplit = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_BATCH_PRIO")) h->bprio = std::atoi(e) != 0;
+    if (const char* e = std::getenv("NEO_HIP_AHEAD_DIRECT")) h->adirect = std::atoi(e) != 0 ? 2 : 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_SUB")) h->asub = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_KERNEL")) h->akern = std::atoi(e) == 1 ? 1 : 2;
     // batched MAC: 256-lane workgroups at 2 waves/SIMD -> 2 resident per CU, so 512 fills the
@@ -698,6 +701,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
         src = tmp;
     }
     int rc = pack_filter(h, src, h->stream);
+    if (!rc) rc = update_head(h, h->stream);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     if (tmp) (void)hipFree(tmp);
@@ -723,6 +727,7 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
         rc = fail(NEO_HIP_ERUNTIME, "impulse copy failed");
     if (!rc && normalize) rc = normalize_device(d, h->C, length, h->stream);
     if (!rc) rc = partition_device(d, h->C, length, h->B, true, h->H, h->tw, h->stream, h->cstride, h->pstride);
+    if (!rc) rc = update_head(h, h->stream);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     (void)hipFree(d);

@@ -5,6 +5,9 @@
 #include "upols_device.hpp"
 #include "upols_handle.hpp"
 
+#include <algorithm>
+#include <vector>
+
 #include <type_traits>
 #include <utility>
 
@@ -788,6 +791,314 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     NEO_PROBE(6, tid == 0);
 }
 
+// ---------------------------------------------------------------------------------------
+// Direct-head lookahead block step (OLS, B = 256 / 512): the output no longer waits for the
+// window transform. Partition 0's contribution H0 X is the linear convolution of the window
+// with the time-domain head h0 (irfft(H0) / 2B; the first B taps, its second half zero for
+// a zero-padded partition), y0[n] = sum_k h0[k] x[n - k] for the output samples n in
+// [B, 2B) -- the same products the overlap-save irfft of H0 X evaluates, summed directly.
+// The rest of block j's spectrum (window-pass slabs, sub-window slab, partitions 1..jr) does
+// not depend on this block's input at all. So, one workgroup per channel, by wave role:
+//   wave 0        window load -> LDS (for the convolution), previous block from registers,
+//                 r2c, FDL row w insert (for later blocks; off the output path)
+//   MAC waves     slabs + partitions 1..jr -> rest spectrum R in LDS
+//   c2r wave      waits for R, irfft(R) / 2B -> z in LDS
+//   conv waves    taps into LDS, wait for the window, B/4 taps each over all B outputs
+//                 (8 outputs per lane, two packed accumulator sets: even taps on output
+//                 pairs (2i, 2i+1), odd taps on (2i+1, 2i+2), one float4 of the window per
+//                 four taps), partial sums in LDS; then out = sum of the four partials + z
+// Roles hand over through LDS counters (release / acquire at workgroup scope); all waves of
+// a workgroup are resident together, so the waits always end.
+template<int B>
+struct ahead3_cfg {
+    static constexpr int Q = B / 2;                    // float4 (2 bins) per row
+    static constexpr int MW = Q / 64;                  // MAC waves
+    static constexpr int CW = B >= 512 ? 8 : 4;        // convolution waves (taps split CW ways)
+    static constexpr int R = 8;                        // outputs per convolution lane
+    static constexpr int CL = B / R;                   // convolution lanes (<= 64)
+    static constexpr int KW = B / CW;                  // taps per convolution wave
+    static constexpr int EW = B >= 512 ? B / 64 : 8;   // transform elements per lane
+    static constexpr int TW = B / EW;                  // transform lanes (<= 64)
+    static constexpr int NT = 64 * (1 + MW + 1 + CW);  // workgroup size
+    static constexpr int XPAD = 8;                     // zero floats before the window (prefetch underrun)
+};
+
+__device__ __forceinline__ void lds_signal(int* cnt)  // all lanes of a wave, after its LDS writes
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void lds_wait(int* cnt, int n)
+{
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < n) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template<int B>
+__global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
+    const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
+    const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
+    const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int ssub,
+    int jr, const float* __restrict__ h0t)
+{
+    using K = upols_cfg<B>;
+    using A = ahead3_cfg<B>;
+    constexpr int MW = A::MW, CW = A::CW, EW = A::EW, TW = A::TW, KW = A::KW, XP = A::XPAD;
+    static_assert(TW <= 64 && A::CL <= 64 && A::NT <= 1024 && EW % 2 == 0 && KW % 4 == 0, "ahead3 geometry");
+    __shared__ cf tw_f[K::TW1 + K::TW2];
+    __shared__ cf fft_f[K::LL];
+    __shared__ cf tw_c[K::TW1 + K::TW2];
+    __shared__ cf fft_c[K::LL];
+    __shared__ __attribute__((aligned(16))) cf Rs[B];                 // rest spectrum (packed)
+    __shared__ __attribute__((aligned(16))) float xw[XP + 2 * B + 8];  // window, XP zeros in front
+    __shared__ __attribute__((aligned(16))) float hh[B];               // head taps
+    __shared__ __attribute__((aligned(16))) float Pc[CW][B];           // convolution partials
+    __shared__ __attribute__((aligned(16))) float zs[B];               // irfft(R) / 2B, samples [B, 2B)
+    __shared__ int cnt[4];                                             // window, R, partials, z
+    const int tid = threadIdx.x, c = blockIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int64_t crow = int64_t(c) * cstride;
+    const float* in_c = in + int64_t(c) * ld_in;
+    float* prev_c = prev + int64_t(c) * B;
+    NEO_PROBE(0, tid == 0);
+    if (tid < 4) cnt[tid] = 0;
+    if (tid < XP) xw[tid] = 0.f;
+    if (tid < 8) xw[XP + 2 * B + tid] = 0.f;
+    __syncthreads();
+    if (wave == 0) {  // window -> LDS + registers, previous block, r2c, FDL row w
+        for (int i = lane; i < K::TW1 + K::TW2; i += 64) tw_f[i] = twg[i];
+        cf v[EW];
+        if (lane < TW) {
+            const cf* pz = reinterpret_cast<const cf*>(prev_c);
+            const cf* iz = reinterpret_cast<const cf*>(in_c);
+#pragma unroll
+            for (int m = 0; m < EW; ++m) {
+                const int n = lane + m * TW;
+                v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+            }
+            cf* xc = reinterpret_cast<cf*>(xw + XP);
+#pragma unroll
+            for (int m = 0; m < EW; ++m) xc[lane + m * TW] = v[m];
+            cf* pw = reinterpret_cast<cf*>(prev_c);  // this block becomes the next call's first half
+#pragma unroll
+            for (int m = EW / 2; m < EW; ++m) pw[lane + m * TW - B / 2] = v[m];
+        }
+        lds_signal(&cnt[0]);
+        NEO_PROBE(1, tid == 0);
+        wave_sync();
+        stockham<B, EW, -1, 1, true>(v, fft_f, tw_f, lane, lane < TW);
+        NEO_PROBE(2, tid == 0);
+        if (lane < TW) {
+#pragma unroll
+            for (int m = 0; m < EW; ++m) fft_f[lpad(lane + m * TW)] = v[m];
+        }
+        wave_sync();
+        cf* row = fdl + crow + int64_t(w) * pstride;
+        constexpr int NK = B / 64;
+        cf xs[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i) xs[i] = r2c_split<B>(fft_f, tw_f + K::TW1, lane + 64 * i);
+#pragma unroll
+        for (int i = 0; i < NK; ++i) row[lane + 64 * i] = xs[i];
+        NEO_PROBE(3, tid == 0);
+    } else if (wave <= MW) {  // rest spectrum: slabs + sub-window slabs + partitions 1..jr
+        const int q = tid - 64;
+        const int64_t ps4 = pstride / 2;
+        const float4* H4 = reinterpret_cast<const float4*>(H + crow);
+        const float4* F4 = reinterpret_cast<const float4*>(fdl + crow);
+        const float4* S4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * T * B + int64_t(j) * B);
+        const int64_t ss4 = int64_t(T) * K::Q;
+        float4 sum = {0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < S; ++t) {
+            const float4 r = S4[t * ss4 + q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        for (int t = 0; t < ssub; ++t) {
+            const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + t) * kSubWindow + jr) * B)[q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+        float4 hv[kSubWindow], xv[kSubWindow];
+#pragma unroll
+        for (int p = 1; p < kSubWindow; ++p)
+            if (p <= jr) {
+                const int r = w - p < 0 ? w - p + ring : w - p;
+                hv[p] = H4[int64_t(p) * ps4 + q];
+                xv[p] = F4[int64_t(r) * ps4 + q];
+            }
+#pragma unroll
+        for (int p = 1; p < kSubWindow; ++p)
+            if (p <= jr) mac2(a0, a1, hv[p], xv[p]);
+        const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
+        reinterpret_cast<float4*>(Rs)[q] = make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
+        lds_signal(&cnt[1]);
+        NEO_PROBE(4, tid == 64);
+    } else if (wave == MW + 1) {  // irfft(R) / 2B -> zs
+        for (int i = lane; i < K::TW1 + K::TW2; i += 64) tw_c[i] = twg[i];
+        lds_wait(&cnt[1], MW);
+        NEO_PROBE(5, lane == 0);
+        cf v[EW];
+        if (lane < TW) {
+#pragma unroll
+            for (int m = 0; m < EW; ++m) {
+                const int k = lane + m * TW;
+                const cf x0 = Rs[0];
+                v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw_c + K::TW1, 0)
+                              : c2r_join<B>(Rs[k], Rs[B - k], tw_c + K::TW1, k);
+            }
+        }
+        stockham<B, EW, +1, 1, true>(v, fft_c, tw_c, lane, lane < TW);
+        if (lane < TW) {
+            const float scale = 1.0f / float(2 * B);  // overlap_save.hpp:107-108
+            cf* zc = reinterpret_cast<cf*>(zs);
+#pragma unroll
+            for (int m = EW / 2; m < EW; ++m) zc[lane + m * TW - B / 2] = {v[m].x * scale, v[m].y * scale};
+        }
+        lds_signal(&cnt[3]);
+        NEO_PROBE(6, lane == 0);
+    } else {  // convolution with the head taps
+        const int cw = wave - MW - 2;
+        const int ka = cw * KW;
+        for (int i = lane * 4; i < KW; i += 256)
+            *reinterpret_cast<float4*>(hh + ka + i) = *reinterpret_cast<const float4*>(h0t + int64_t(c) * B + ka + i);
+        lds_wait(&cnt[0], 1);  // the window (wave 0); the taps are this wave's own writes
+        NEO_PROBE(7, lane == 0 && cw == 0);
+        f2v ya[4] = {}, yb[4] = {};  // even taps on output pairs (2i, 2i+1); odd taps on (2i+1, 2i+2)
+        float y0o = 0.f;              // odd taps of output 0
+        const int n0 = B + A::R * lane;
+        if (lane < A::CL) {
+            const float* x = xw + XP;
+            int b = n0 - ka;  // window floats [b - 4, b + 8) cover four taps from ka
+            float4 Fm = *reinterpret_cast<const float4*>(x + b - 4);
+            float4 F0 = *reinterpret_cast<const float4*>(x + b);
+            float4 F1 = *reinterpret_cast<const float4*>(x + b + 4);
+#pragma unroll 4
+            for (int kc = ka; kc < ka + KW; kc += 4) {
+                const float4 hq = *reinterpret_cast<const float4*>(hh + kc);
+                const float4 Fn = *reinterpret_cast<const float4*>(x + b - 8);  // next chunk (zeros before the window)
+                const f2v s0[4] = {{F0.x, F0.y}, {F0.z, F0.w}, {F1.x, F1.y}, {F1.z, F1.w}};  // x[b .. b+7]
+                const f2v s1[4] = {{Fm.z, Fm.w}, {F0.x, F0.y}, {F0.z, F0.w}, {F1.x, F1.y}};  // x[b-2 .. b+5]
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    ya[i] = __builtin_elementwise_fma(f2v{hq.x, hq.x}, s0[i], ya[i]);  // tap kc
+                    yb[i] = __builtin_elementwise_fma(f2v{hq.y, hq.y}, s0[i], yb[i]);  // tap kc + 1
+                    ya[i] = __builtin_elementwise_fma(f2v{hq.z, hq.z}, s1[i], ya[i]);  // tap kc + 2
+                    yb[i] = __builtin_elementwise_fma(f2v{hq.w, hq.w}, s1[i], yb[i]);  // tap kc + 3
+                }
+                y0o = __builtin_fmaf(hq.y, Fm.w, y0o);  // x[n0 - kc - 1]
+                y0o = __builtin_fmaf(hq.w, Fm.y, y0o);  // x[n0 - kc - 3]
+                F1 = F0;
+                F0 = Fm;
+                Fm = Fn;
+                b -= 4;
+            }
+            // y[2i] = ya[i].x + yb[i-1].y (i > 0) or + y0o; y[2i+1] = ya[i].y + yb[i].x
+            float* pc = Pc[cw] + (n0 - B);
+            const float4 o0 = {ya[0].x + y0o, ya[0].y + yb[0].x, ya[1].x + yb[0].y, ya[1].y + yb[1].x};
+            const float4 o1 = {ya[2].x + yb[1].y, ya[2].y + yb[2].x, ya[3].x + yb[2].y, ya[3].y + yb[3].x};
+            reinterpret_cast<float4*>(pc)[0] = o0;
+            reinterpret_cast<float4*>(pc)[1] = o1;
+        }
+        lds_signal(&cnt[2]);
+        NEO_PROBE(8, lane == 0 && cw == 0);
+        lds_wait(&cnt[2], CW);
+        lds_wait(&cnt[3], 1);
+        NEO_PROBE(9, lane == 0 && cw == 0);
+        float* out_c = out + int64_t(c) * ld_out;
+        for (int m = cw * (B / CW) + lane * 4; m < (cw + 1) * (B / CW); m += 256) {
+            float4 r = *reinterpret_cast<const float4*>(zs + m);
+#pragma unroll
+            for (int t = 0; t < CW; ++t) {
+                const float4 u = *reinterpret_cast<const float4*>(Pc[t] + m);
+                r.x += u.x; r.y += u.y; r.z += u.z; r.w += u.w;
+            }
+            *reinterpret_cast<float4*>(out_c + m) = r;
+        }
+        NEO_PROBE(10, lane == 0 && cw == 0);
+    }
+}
+
+// Time-domain head taps for k_upols_ahead3 (grid C, 256 lanes): irfft(H0) / 2B of each
+// channel's packed partition 0; taps [0, B) -> h0t, the second half's magnitude relative to
+// the first (zero-padded partitions: rounding only) -> tail[c].
+template<int B>
+__global__ __launch_bounds__(256) void k_head_taps(const cf* __restrict__ H, int64_t cstride, const cf* __restrict__ twg,
+                                                   float* __restrict__ h0t, float* __restrict__ tail)
+{
+    using K = upols_cfg<B>;
+    constexpr int E = K::E, T = B / E;
+    __shared__ cf X[B];
+    __shared__ cf fft[K::LL];
+    __shared__ cf tw[K::TW1 + K::TW2];
+    __shared__ float red[2][256];
+    const int tid = threadIdx.x, c = blockIdx.x;
+    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
+    for (int k = tid; k < B; k += 256) X[k] = H[int64_t(c) * cstride + k];
+    __syncthreads();
+    cf v[E];
+    const bool active = tid < T;
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int k = tid + m * T;
+            v[m] = k == 0 ? c2r_join<B>(cf{X[0].x, 0.f}, cf{X[0].y, 0.f}, tw + K::TW1, 0)
+                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
+        }
+    }
+    stockham<B, E, +1>(v, fft, tw, tid, active);
+    float head = 0.f, tl = 0.f;
+    if (active) {
+        const float scale = 1.0f / float(2 * B);
+        cf* o = reinterpret_cast<cf*>(h0t + int64_t(c) * B);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const cf z = {v[m].x * scale, v[m].y * scale};
+            const float a = fmaxf(fabsf(z.x), fabsf(z.y));
+            if (m < E / 2) {
+                o[tid + m * T] = z;
+                head = fmaxf(head, a);
+            } else {
+                tl = fmaxf(tl, a);
+            }
+        }
+    }
+    red[0][tid] = head;
+    red[1][tid] = tl;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st) {
+            red[0][tid] = fmaxf(red[0][tid], red[0][tid + st]);
+            red[1][tid] = fmaxf(red[1][tid], red[1][tid + st]);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) tail[c] = red[1][0] > 1e-6f * red[0][0] ? 1.f : 0.f;
+}
+
+int update_head(upols_t* h, hipStream_t s)
+{
+    h->direct_ok = false;
+    if (h->ola || h->v2 || (h->B != 256 && h->B != 512)) return NEO_HIP_OK;
+    if (!h->h0t) {
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->h0t), size_t(h->C) * h->B * sizeof(float)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->h0tail), size_t(h->C) * sizeof(float)));
+    }
+    if (h->B == 256)
+        hipLaunchKernelGGL((k_head_taps<256>), dim3(unsigned(h->C)), dim3(256), 0, s, h->H, h->cstride, h->tw, h->h0t,
+                           h->h0tail);
+    else
+        hipLaunchKernelGGL((k_head_taps<512>), dim3(unsigned(h->C)), dim3(256), 0, s, h->H, h->cstride, h->tw, h->h0t,
+                           h->h0tail);
+    NEO_HIP_LAUNCH_CHECK();
+    std::vector<float> t(size_t(h->C));
+    NEO_HIP_CHECK(hipMemcpyAsync(t.data(), h->h0tail, t.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    NEO_HIP_CHECK(hipStreamSynchronize(s));
+    // a head with a non-zero second half (a filter not from zero-padded partitions) keeps the
+    // transform path for partition 0
+    h->direct_ok = std::all_of(t.begin(), t.end(), [](float v) { return v == 0.f; });
+    return NEO_HIP_OK;
+}
+
 // one k_batch_mac launch: T blocks at write position h->wpos into slabs `part` [C][S][T][B],
 // splits of `rows` partitions over [0, P); FDL rows entering past partition `emax` count as
 // zero (the lookahead's sub-window passes take only the rows of the current window)
@@ -919,7 +1230,17 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
             if (rc) return rc;
         }
         const cf* subp = h->part_s;
-        if (h->ola) {
+        const bool direct = sub && h->direct_ok && !h->ola && (B == 256 ? h->adirect >= 1 : B == 512 && h->adirect == 2);
+        if (direct) {  // (needs jr < kSubWindow)
+            if (B == 256)
+                hipLaunchKernelGGL((k_upols_ahead3<256>), dim3(unsigned(h->C)), dim3(ahead3_cfg<256>::NT), 0, s, in,
+                                   ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
+                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, h->h0t);
+            else
+                hipLaunchKernelGGL((k_upols_ahead3<512>), dim3(unsigned(h->C)), dim3(ahead3_cfg<512>::NT), 0, s, in,
+                                   ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
+                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, h->h0t);
+        } else if (h->ola) {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, true>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,

@@ -41,6 +41,13 @@ struct neo_hip_upols {
     bool asub = true;     // lookahead sub-windows (k_upols_ahead2 only; NEO_HIP_AHEAD_SUB=0 disables)
     bool ssplit = false;  // sub-window passes: one split per chunk (NEO_HIP_SUB_SPLIT=1; A/B on one box: slower)
     neo_hip::cf* part_s = nullptr;  // sub-window pass slabs [C][ssub <= kMaxBatch / kSubWindow][kSubWindow][B]
+    // direct-head block step k_upols_ahead3 (OLS): 1 = at B = 256 (same-box A/B: C4 +3.5 %; at
+    // B = 512 the 512 x 512-tap convolution costs what it saves), 2 = at B = 256 and 512,
+    // 0 = off (NEO_HIP_AHEAD_DIRECT=1 / 0)
+    int adirect = 1;
+    bool direct_ok = false; // partition 0's time-domain head is B taps (update_head)
+    float* h0t = nullptr;   // head taps [C][B] (k_head_taps)
+    float* h0tail = nullptr;
     int akern = 2;  // per-block lookahead kernel: 2 = k_upols_ahead2 (B <= 1024), 1 = k_upols_ahead (NEO_HIP_AHEAD_KERNEL)
     int phase = 0;
     float* tail = nullptr;  // batched OLA tails [C][T][B]
@@ -121,5 +128,7 @@ int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf
 int normalize_device(float* d_ir, int C, int64_t L, hipStream_t s);
 // filter [C][P][B+1] (reference layout, device) -> packed H rows of the handle
 int pack_filter(upols_t* h, const cf* src, hipStream_t s);
+// time-domain head taps of partition 0 for the direct-head block step (after every filter change)
+int update_head(upols_t* h, hipStream_t s);
 
 }  // namespace neo_hip

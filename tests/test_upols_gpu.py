@@ -551,6 +551,36 @@ def test_ahead_steps_vs_oracle(neo_gpu, oracle, monkeypatch, method, B, L, C, nb
     assert peak_err(t.cpu().numpy(), ref) <= TOL
 
 
+@pytest.mark.parametrize("B", [256, 512])
+@pytest.mark.parametrize("direct", ["0", "1"])
+@pytest.mark.parametrize("head", ["partitioned", "arbitrary"])
+def test_ahead_direct_head(neo_gpu, oracle, monkeypatch, B, direct, head):
+    """Direct-head block step (k_upols_ahead3, OLS): partition 0 as a B-tap time-domain
+    convolution when its head comes from a zero-padded partition; an arbitrary head
+    spectrum (second half of irfft(H0) not zero) keeps the transform path. Both must match
+    the reference restatement, which takes any spectra. NEO_HIP_AHEAD_DIRECT=1 forces the
+    direct head at B = 512 too (off by default there: no gain in a same-box A/B)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("NEO_HIP_AHEAD_DIRECT", direct)
+    C, L, nb = 2, 40 * B, 70
+    ir = np.stack([oracle.noise(370 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    if head == "arbitrary":
+        rng = np.random.default_rng(5)
+        noise = (rng.standard_normal((C, B + 1)) + 1j * rng.standard_normal((C, B + 1))).astype(np.complex64)
+        parts[:, 0] += 0.05 * noise
+    sig = np.stack([oracle.noise(380 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts)
+    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1])
+    conv.filter(parts)
+    conv.set_batch(False)
+    conv.set_ahead(True)
+    t = torch.from_numpy(sig).cuda()
+    conv.process_blocks(t)
+    torch.cuda.synchronize()
+    assert peak_err(t.cpu().numpy(), ref) <= TOL
+
+
 def test_ahead_mixed_paths(neo_gpu, oracle):
     """Lookahead steps, batched passes, plain steps and host blocks share one state; the
     lookahead can be switched at any block boundary."""
