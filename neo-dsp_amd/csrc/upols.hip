@@ -69,10 +69,9 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
     const int64_t ps4 = pstride / 2;            // row stride in float4 units
 
     if (!TAIL && s == 0) {
-        for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
         const float* in_c = in + int64_t(c) * ld_in;
         float* prev_c = prev + int64_t(c) * B;
-        window_fft<B, OLA>(prev_c, in_c, fft, tw, tid);
+        window_fft<B, OLA>(prev_c, in_c, fft, tw, tid, twg);
         cf* row = fdl + crow + int64_t(w) * pstride;
         for (int k = tid; k < B; k += 256) {
             const cf x = r2c_split<B>(fft, tw + K::TW1, k);

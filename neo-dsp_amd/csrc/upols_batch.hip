@@ -42,10 +42,9 @@ __global__ __launch_bounds__(256) void k_batch_window(const float* __restrict__ 
     __shared__ cf fft[K::LL];
     __shared__ cf tw[K::TW1 + K::TW2];
     const int tid = threadIdx.x, c = blockIdx.x / T, j = blockIdx.x - c * T;
-    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
     const float* in_c = in + int64_t(c) * ld_in + int64_t(j) * B;
     const float* prev_c = j == 0 ? prev + int64_t(c) * B : in_c - B;
-    window_fft<B, OLA>(prev_c, in_c, fft, tw, tid);
+    window_fft<B, OLA>(prev_c, in_c, fft, tw, tid, twg);
     const int r = w + j < ring ? w + j : w + j - ring;
     cf* row = fdl + int64_t(c) * cstride + int64_t(r) * pstride;
     for (int k = tid; k < B; k += 256) row[k] = r2c_split<B>(fft, tw + K::TW1, k);
@@ -588,10 +587,9 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
     __shared__ cf fft[K::LL];
     __shared__ cf tw[K::TW1 + K::TW2];
     const int tid = threadIdx.x, c = blockIdx.x;
-    for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
     const float* in_c = in + int64_t(c) * ld_in;
     float* prev_c = prev + int64_t(c) * B;
-    window_fft<B, OLA>(prev_c, in_c, fft, tw, tid);
+    window_fft<B, OLA>(prev_c, in_c, fft, tw, tid, twg);
     const int64_t crow = int64_t(c) * cstride;
     cf* row = fdl + crow + int64_t(w) * pstride;
     for (int k = tid; k < B; k += 256) {
@@ -692,7 +690,8 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     NEO_PROBE(0, tid == 0);
     NEO_PROBE(8, tid == 64);
     if (tid < 64) {  // wave 0: window r2c, FDL row w, previous block
-        for (int i = tid; i < K::TW1 + K::TW2; i += 64) tw[i] = twg[i];
+        tw_regs<K::TW1 + K::TW2, 64> twr;
+        twr.load(twg, tid);
         cf v[EW];
         if (tid < TW) {
             const cf* pz = reinterpret_cast<const cf*>(prev_c);
@@ -713,6 +712,7 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
                 for (int m = EW / 2; m < EW; ++m) pw[tid + m * TW - B / 2] = v[m];
             }
         }
+        twr.store(tw, tid);
         wave_sync();
         NEO_PROBE(1, tid == 0);
         stockham<B, EW, -1, 1, true>(v, fft, tw, tid, tid < TW);
@@ -866,7 +866,8 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
     if (tid < 8) xw[XP + 2 * B + tid] = 0.f;
     __syncthreads();
     if (wave == 0) {  // window -> LDS + registers, previous block, r2c, FDL row w
-        for (int i = lane; i < K::TW1 + K::TW2; i += 64) tw_f[i] = twg[i];
+        tw_regs<K::TW1 + K::TW2, 64> twr;
+        twr.load(twg, lane);
         cf v[EW];
         if (lane < TW) {
             const cf* pz = reinterpret_cast<const cf*>(prev_c);
@@ -883,6 +884,7 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
 #pragma unroll
             for (int m = EW / 2; m < EW; ++m) pw[lane + m * TW - B / 2] = v[m];
         }
+        twr.store(tw_f, lane);
         lds_signal(&cnt[0]);
         NEO_PROBE(1, tid == 0);
         wave_sync();

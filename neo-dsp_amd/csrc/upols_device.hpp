@@ -32,6 +32,27 @@ struct upols_cfg {
     static constexpr int LL = lds_len(B);
 };
 
+// Twiddle table staged global -> registers -> LDS: the loads issue together with the
+// window loads that follow, instead of a load / wait / ds_write round trip per iteration
+// ahead of them (a copy loop with a runtime trip count is not hoisted by the compiler).
+template<int N, int LANES>
+struct tw_regs {
+    static constexpr int R = (N + LANES - 1) / LANES;
+    cf v[R];
+    __device__ __forceinline__ void load(const cf* __restrict__ g, int t)
+    {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (t + LANES * i < N) v[i] = g[t + LANES * i];
+    }
+    __device__ __forceinline__ void store(cf* l, int t) const
+    {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (t + LANES * i < N) l[t + LANES * i] = v[i];
+    }
+};
+
 struct acc4 {  // 4 partial products per bin keep the packed bin 0 exact
     float rr, ii, ri, ir;
 };
@@ -63,11 +84,15 @@ __device__ __forceinline__ cf finish(const acc4& a, bool bin0)
 // OLS window = [previous block | new block] (overlap_save.hpp:90-95);
 // OLA window = [new block | zeros]          (overlap_add.hpp:84-86).
 template<int B, bool OLA, int E = (B / 8 <= 256 ? 8 : B / 256)>
-__device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, const cf* tw1, int tid)
+__device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, cf* tw1, int tid,
+                                           const cf* __restrict__ twg = nullptr)
 {
     constexpr int T = B / E;
     static_assert(T <= 256 && B % E == 0, "window FFT must fit one 256-lane workgroup");
+    using K = upols_cfg<B>;
     const bool active = tid < T;
+    tw_regs<K::TW1 + K::TW2, 256> twr;  // twg: stage the twiddles here, loads issued with the window's
+    if (twg) twr.load(twg, tid);
     cf v[E];
     if (active) {
         const cf* pz = reinterpret_cast<const cf*>(prev_c);
@@ -79,7 +104,8 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
             else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
         }
     }
-    __syncthreads();  // twiddles staged by the caller
+    if (twg) twr.store(tw1, tid);
+    __syncthreads();  // twiddles staged (here or by the caller)
     stockham<B, E, -1>(v, fft, tw1, tid, active);
     if (active) {
 #pragma unroll
