@@ -1147,6 +1147,14 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead, const ma
                     break;                                                                                       \
                 }                                                                                                \
             }                                                                                                    \
+            if constexpr (TT == 8 && NB == 1 && (BB == 256 || BB == 512)) {                                      \
+                if (h->b8var == 3) { /* 8-block passes (sub-windows, leftovers): buffer loads, D = 8 */          \
+                    hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 3>), dim3(grid), dim3(L), 0, s, h->H, h->fdl,    \
+                                       mp.part, mp.P, h->ring, mp.S, mp.rows, h->wpos, h->cstride, h->pstride,   \
+                                       ahead, mp.emax, rz, mp.pc, h->bprio);                                     \
+                    break;                                                                                       \
+                }                                                                                                \
+            }                                                                                                    \
             hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 0>), dim3(grid), dim3(L), 0, s, h->H, h->fdl, mp.part,    \
                                mp.P, h->ring, mp.S, mp.rows, h->wpos, h->cstride, h->pstride, ahead, mp.emax, rz,   \
                                mp.pc, h->bprio);                                                                \
