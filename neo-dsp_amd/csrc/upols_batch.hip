@@ -301,13 +301,13 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     // starting below pc load filter rows cacheable, the rest nontemporally.
     // prio: two workgroups share a CU (blockIdx i and i + grid/2, the dispatch order) and the
     // SQ favours the older one's waves, which finish ~30 % early and leave one wave per SIMD
-    // for the rest of the pass; with prio they trade issue priority in 20 us slices
-    // (s_memrealtime, 100 MHz). (Locking the two together with a barrier per chunk instead —
+    // for the rest of the pass; with prio they trade issue priority in slices of 2^prio
+    // s_memrealtime ticks (100 MHz; 11 = 20 us). (Locking the two together with a barrier per chunk instead —
     // one 8-wave workgroup per CU — was 30 % slower: both stall on memory at the same time.)
     const int half = blockIdx.x >= gridDim.x / 2;
     auto share = [&]() {
         if (prio) {
-            if (((__builtin_amdgcn_s_memrealtime() >> 11) + half) & 1) __builtin_amdgcn_s_setprio(2);
+            if (((__builtin_amdgcn_s_memrealtime() >> prio) + half) & 1) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
     };

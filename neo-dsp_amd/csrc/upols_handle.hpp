@@ -32,7 +32,8 @@ struct neo_hip_upols {
     int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
     int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
     int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kCacheBudgetBytes; NEO_HIP_BATCH_CACHE_ROWS)
-    int bprio = 1;          // batched MAC: co-resident workgroups trade issue priority (NEO_HIP_BATCH_PRIO=0 off)
+    int bprio = 11;         // batched MAC: co-resident workgroups trade issue priority every 2^bprio
+                            // 10-ns ticks (NEO_HIP_BATCH_PRIO=0 off)
     int b8var = 3;          // 8-block passes: bmac_var 3 (buffer loads, D = 8) or 0 (NEO_HIP_BATCH8_VAR)
     int bvar = 3;           // batched MAC variant at T = 32, B = 256/512 (bmac_var in upols_batch.hip; NEO_HIP_BATCH_VAR)
     neo_hip::cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
