@@ -46,17 +46,19 @@ for j in sorted(rows):
 
 # clock during the window pass under sustained load: 8 windows back to back, stamps of the
 # last pass (workgroup 0: s_memtime shader cycles over s_memrealtime 100 MHz ticks)
-xs = torch.rand((C, 256 * B), generator=g, device="cuda") * 2 - 1
+xs = torch.rand((C, 255 * B), generator=g, device="cuda") * 2 - 1  # ends mid-window
 ys = torch.empty_like(xs)
 for rep in range(3):
     while cv.ahead_info()[1] != 0:
         cv.process_device(x.data_ptr(), B, y.data_ptr(), B, 0)
-    cv.process_blocks_ptr(xs.data_ptr(), ys.data_ptr(), 256 * B, 256, 0)
+    cv.process_blocks_ptr(xs.data_ptr(), ys.data_ptr(), 255 * B, 255, 0)
     torch.cuda.synchronize()
     assert lib.neo_hip_debug_probe(buf) == 0
     t = list(buf)
     cyc, rt = t[12] - t[10], t[13] - t[11]
     print(f"window pass (workgroup 0): {rt * 10 / 1e3:.1f} us, {cyc} cycles -> {cyc / (rt * 10):.3f} GHz")
+    print("  last block step of the sustained run (ns):", [(t[k] - t[0]) * 10 for k in range(7)],
+          "MAC wave:", (t[8] - t[0]) * 10, (t[9] - t[0]) * 10)
 
 # per-workgroup entry/exit of the last window pass: how many workgroups run at once
 span = (ctypes.c_ulonglong * (4096 * 2))()
