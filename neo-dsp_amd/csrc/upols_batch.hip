@@ -686,7 +686,14 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     float* prev_c = prev + int64_t(c) * B;
     const int64_t ps4 = pstride / 2;
     const float4* H4 = reinterpret_cast<const float4*>(H + crow);
-    float4 h0 = {0.f, 0.f, 0.f, 0.f};
+    // group 0 lane i owns the mirror pair of bins (k0, k1) = (i, B - i), (0, B/2) for i = 0:
+    // the r2c split, H0 X and the c2r join all pair bin k with bin B - k
+    const int i0 = tid - 64, k0 = i0, k1 = i0 == 0 ? B / 2 : B - i0;
+    cf h0a = {0.f, 0.f}, h0b = h0a;
+    if (tid >= 64 && tid < 64 + Q) {
+        h0a = H[crow + k0];
+        h0b = H[crow + k1];
+    }
     NEO_PROBE(0, tid == 0);
     NEO_PROBE(8, tid == 64);
     if (tid < 64) {  // wave 0: window r2c, FDL row w, previous block
@@ -721,22 +728,8 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
 #pragma unroll
             for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
         }
-        wave_sync();
-        cf* row = fdl + crow + int64_t(w) * pstride;
-        constexpr int NK = (B + 63) / 64;
-        cf xs[NK];
-#pragma unroll
-        for (int i = 0; i < NK; ++i)  // all LDS reads first, then the stores
-            if (tid + 64 * i < B) xs[i] = r2c_split<B>(fft, tw + K::TW1, tid + 64 * i);
-#pragma unroll
-        for (int i = 0; i < NK; ++i)
-            if (tid + 64 * i < B) {
-                X[tid + 64 * i] = xs[i];
-                row[tid + 64 * i] = xs[i];
-            }
     } else {  // MAC groups: slabs + partitions 1..j
         const int u = tid - 64, g = u / Q, q = u - g * Q;
-        if (g == 0) h0 = H4[q];
         const float4* F4 = reinterpret_cast<const float4*>(fdl + crow);
         const float4* S4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * T * B + int64_t(j) * B);
         const int64_t ss4 = int64_t(T) * K::Q;  // float4 between the slabs of one block
@@ -772,22 +765,36 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     NEO_PROBE(3, tid == 0);
     __syncthreads();
     NEO_PROBE(4, tid == 0);
-    if (tid >= 64 && tid < 64 + Q) {  // group 0: + H0 X + the other groups
-        const int q = tid - 64;
-        acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
-        mac2(a0, a1, h0, reinterpret_cast<const float4*>(X)[q]);
-        const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
-        float4 y = acc[0][q];
+    if (tid >= 64 && tid < 64 + Q) {
+        // group 0, bin pair (k0, k1): r2c split of the window transform, FDL row w, Y = the
+        // groups' partial sums + H0 X, then the c2r join -- 2 bins per lane over Q lanes
+        // instead of B/64 per lane in wave 0, between the two barriers
+        const cf xa = r2c_split<B>(fft, tw + K::TW1, k0), xb = r2c_split<B>(fft, tw + K::TW1, k1);
+        cf* row = fdl + crow + int64_t(w) * pstride;
+        row[k0] = xa;
+        row[k1] = xb;
+        const cf* accb = reinterpret_cast<const cf*>(&acc[0][0]);  // acc[g] as B bins
+        cf ya = accb[k0], yb = accb[k1];
 #pragma unroll
         for (int g = 1; g < NG; ++g) {
-            const float4 r = acc[g][q];
-            y.x += r.x; y.y += r.y; y.z += r.z; y.w += r.w;
+            const cf ra = accb[g * B + k0], rb = accb[g * B + k1];
+            ya.x += ra.x; ya.y += ra.y; yb.x += rb.x; yb.y += rb.y;
         }
-        reinterpret_cast<float4*>(X)[q] = make_float4(y.x + b0.x, y.y + b0.y, y.z + b1.x, y.w + b1.y);
+        if (k0 == 0) {  // packed {DC, Nyquist}: two real products
+            ya.x += h0a.x * xa.x;
+            ya.y += h0a.y * xa.y;
+        } else {
+            ya.x += h0a.x * xa.x - h0a.y * xa.y;
+            ya.y += h0a.x * xa.y + h0a.y * xa.x;
+        }
+        yb.x += h0b.x * xb.x - h0b.y * xb.y;
+        yb.y += h0b.x * xb.y + h0b.y * xb.x;
+        X[k0] = k0 == 0 ? c2r_join<B>(cf{ya.x, 0.f}, cf{ya.y, 0.f}, tw + K::TW1, 0) : c2r_join<B>(ya, yb, tw + K::TW1, k0);
+        X[k1] = c2r_join<B>(yb, k0 == 0 ? yb : ya, tw + K::TW1, k1);
     }
     __syncthreads();
     NEO_PROBE(5, tid == 0);
-    if (tid < 64) c2r_tail<B, OLA, EW, true>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
+    if (tid < 64) c2r_tail<B, OLA, EW, true, true>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
     NEO_PROBE(6, tid == 0);
 }
 

@@ -119,7 +119,8 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
 //   OLA: out = samples [0, B) + overlap; overlap = [B, 2B)  (overlap_add.hpp:92-106)
 // E = 4 keeps the fused kernel inside its 64-VGPR budget (T = B/E <= 256 lanes).
 // WS = true: run by one wave (T <= 64 lanes), no workgroup barriers.
-template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256), bool WS = false>
+// JOINED = true: X already holds the joined c2r input Z[k] (c2r_join applied by the caller).
+template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256), bool WS = false, bool JOINED = false>
 __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, float* ovl_c, int tid)
 {
     using K = upols_cfg<B>;
@@ -131,9 +132,13 @@ __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, flo
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int k = tid + m * T;
-            const cf x0 = X[0];
-            v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
-                          : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
+            if constexpr (JOINED) {
+                v[m] = X[k];
+            } else {
+                const cf x0 = X[0];
+                v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw + K::TW1, 0)
+                              : c2r_join<B>(X[k], X[B - k], tw + K::TW1, k);
+            }
         }
     }
     stockham<B, E, +1, 1, WS>(v, fft, tw, tid, active);
