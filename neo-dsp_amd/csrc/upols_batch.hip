@@ -639,8 +639,8 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
 }
 
 // k_upols_ahead with the work spread over one workgroup of 64 + NG*Q lanes per channel.
-// Sub-windows (sub != nullptr): at the first block of each kSubWindow-block sub-window
-// after the first, a small k_batch_mac pass (T = kSubWindow, FDL rows limited to the
+// Sub-windows (ssub > 0): at the first block of each sw-block sub-window after the
+// first, a small k_batch_mac pass (T = sw, FDL rows limited to the
 // window's own) accumulates for the sub-window's blocks the partitions whose rows are the
 // window's blocks before it; a block step then adds that slab and runs only the
 // partitions 1..jr (jr = its position in the sub-window) itself. Per 32-block window the
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
 // row loads (overlapped with it) and one inverse transform; the per-channel MAC no longer
 // walks j partitions four at a time.
 
-constexpr int kSubWindow = 8;  // lookahead sub-window (blocks)
+// lookahead sub-window length sw (blocks) is per handle: h->subw, 8 or 16
 
 template<int B>
 struct ahead_cfg {
@@ -670,7 +670,7 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
     const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int ssub,
-    int jr)
+    int jr, int sw)
 {
     using K = upols_cfg<B>;
     using A = ahead_cfg<B>;
@@ -739,7 +739,7 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         for (int s = NG - 1 - g; s < ssub; s += NG) {  // sub-window pass slabs (the window's earlier rows)
-            const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + s) * kSubWindow + jr) * B)[q];
+            const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + s) * sw + jr) * B)[q];
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
@@ -847,7 +847,7 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
     const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int ssub,
-    int jr, const float* __restrict__ h0t)
+    int jr, int sw, const float* __restrict__ h0t)
 {
     using K = upols_cfg<B>;
     using A = ahead3_cfg<B>;
@@ -923,21 +923,23 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         for (int t = 0; t < ssub; ++t) {
-            const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + t) * kSubWindow + jr) * B)[q];
+            const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + t) * sw + jr) * B)[q];
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
-        float4 hv[kSubWindow], xv[kSubWindow];
+        for (int pb = 1; pb <= jr; pb += 8) {  // up to 8 row pairs in flight
+            float4 hv[8], xv[8];
 #pragma unroll
-        for (int p = 1; p < kSubWindow; ++p)
-            if (p <= jr) {
-                const int r = w - p < 0 ? w - p + ring : w - p;
-                hv[p] = H4[int64_t(p) * ps4 + q];
-                xv[p] = F4[int64_t(r) * ps4 + q];
-            }
+            for (int k = 0; k < 8; ++k)
+                if (pb + k <= jr) {
+                    const int p = pb + k, r = w - p < 0 ? w - p + ring : w - p;
+                    hv[k] = H4[int64_t(p) * ps4 + q];
+                    xv[k] = F4[int64_t(r) * ps4 + q];
+                }
 #pragma unroll
-        for (int p = 1; p < kSubWindow; ++p)
-            if (p <= jr) mac2(a0, a1, hv[p], xv[p]);
+            for (int k = 0; k < 8; ++k)
+                if (pb + k <= jr) mac2(a0, a1, hv[k], xv[k]);
+        }
         const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
         reinterpret_cast<float4*>(Rs)[q] = make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
         lds_signal(&cnt[1]);
@@ -1154,7 +1156,7 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s, int ahead, const ma
                     break;                                                                                       \
                 }                                                                                                \
             }                                                                                                    \
-            if constexpr (TT == 8 && NB == 1 && (BB == 256 || BB == 512)) {                                      \
+            if constexpr ((TT == 8 || TT == 16) && NB == 1 && (BB == 256 || BB == 512)) {                       \
                 if (h->b8var == 3) { /* 8-block passes (sub-windows, leftovers): buffer loads, D = 8 */          \
                     hipLaunchKernelGGL((k_batch_mac<BB, TT, NB, 3>), dim3(grid), dim3(L), 0, s, h->H, h->fdl,    \
                                        mp.part, mp.P, h->ring, mp.S, mp.rows, h->wpos, h->cstride, h->pstride,   \
@@ -1186,8 +1188,7 @@ static int batch_buffers(upols_t* h)
     if (!h->part_b) {
         NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
                                 size_t(h->C) * h->Sb * kMaxBatch * h->B * sizeof(cf)));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_s),
-                                size_t(h->C) * (kMaxBatch / kSubWindow) * kSubWindow * h->B * sizeof(cf)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_s), size_t(h->C) * kMaxBatch * h->B * sizeof(cf)));
         if (h->ola)
             NEO_HIP_CHECK(
                 hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * h->B * sizeof(float)));
@@ -1234,39 +1235,40 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         if ((rc = mac_event(h, timed, true, ev, s))) return rc;
     }
     if (h->akern == 2 && B <= 1024) {
-        // sub-windows (kSubWindow blocks): at the first block of each after the first, one pass
-        // over the window's rows so far; the block step then walks its sub-window's rows only
-        const bool sub = h->asub && T % kSubWindow == 0 && T > kSubWindow;
-        const int jr = sub ? h->phase % kSubWindow : h->phase;
-        // one split per kSubWindow partitions (each walks one chunk): the pass is latency-bound
-        const int ssub = sub && h->phase >= kSubWindow ? (h->ssplit ? h->phase / kSubWindow + 1 : 1) : 0;
+        // sub-windows (sw blocks): at the first block of each after the first, one pass over the
+        // window's rows so far; the block step then walks its sub-window's rows only
+        const int sw = h->subw;
+        const bool sub = h->asub && T % sw == 0 && T > sw;
+        const int jr = sub ? h->phase % sw : h->phase;
+        // (ssplit: one split per sw partitions, each walks one chunk)
+        const int ssub = sub && h->phase >= sw ? (h->ssplit ? h->phase / sw + 1 : 1) : 0;
         if (ssub && jr == 0) {
-            const int srows = (h->phase + kSubWindow) / ssub;
-            const mac_pass mp{h->part_s, h->phase + kSubWindow, ssub, srows, h->phase, h->P};
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, kSubWindow, s, 1, mp)))
+            const int srows = (h->phase + sw) / ssub;
+            const mac_pass mp{h->part_s, h->phase + sw, ssub, srows, h->phase, h->P};
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, sw, s, 1, mp)))
             if (rc) return rc;
         }
         const cf* subp = h->part_s;
         const bool direct = sub && h->direct_ok && !h->ola && (B == 256 ? h->adirect >= 1 : B == 512 && h->adirect == 2);
-        if (direct) {  // (needs jr < kSubWindow)
+        if (direct) {
             if (B == 256)
                 hipLaunchKernelGGL((k_upols_ahead3<256>), dim3(unsigned(h->C)), dim3(ahead3_cfg<256>::NT), 0, s, in,
                                    ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, h->h0t);
+                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, h->h0t);
             else
                 hipLaunchKernelGGL((k_upols_ahead3<512>), dim3(unsigned(h->C)), dim3(ahead3_cfg<512>::NT), 0, s, in,
                                    ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, h->h0t);
+                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, h->h0t);
         } else if (h->ola) {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, true>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw))
         } else {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, false>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw))
         }
     } else if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_upols_ahead<BB, true>), dim3(unsigned(h->C)), dim3(256), 0, s, in,

@@ -42,7 +42,9 @@ struct neo_hip_upols {
     bool ahead = false;
     bool asub = true;     // lookahead sub-windows (k_upols_ahead2 only; NEO_HIP_AHEAD_SUB=0 disables)
     bool ssplit = false;  // sub-window passes: one split per chunk (NEO_HIP_SUB_SPLIT=1; A/B on one box: slower)
-    neo_hip::cf* part_s = nullptr;  // sub-window pass slabs [C][ssub <= kMaxBatch / kSubWindow][kSubWindow][B]
+    int subw = 8;         // lookahead sub-window (blocks): 16 at B >= 512 (rocprof totals: C5 -1.7 %), 8 below
+                          // (C4 +1 % with 16); NEO_HIP_SUBWINDOW=8/16
+    neo_hip::cf* part_s = nullptr;  // sub-window pass slabs [C][ssub][subw][B], ssub * subw <= kMaxBatch
     // direct-head block step k_upols_ahead3 (OLS): 1 = at B = 256 (same-box A/B: C4 +3.5 %; at
     // B = 512 the 512 x 512-tap convolution costs what it saves), 2 = at B = 256 and 512,
     // 0 = off (NEO_HIP_AHEAD_DIRECT=1 / 0)
