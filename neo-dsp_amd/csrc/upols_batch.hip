@@ -769,7 +769,11 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
         // group 0, bin pair (k0, k1): r2c split of the window transform, FDL row w, Y = the
         // groups' partial sums + H0 X, then the c2r join -- 2 bins per lane over Q lanes
         // instead of B/64 per lane in wave 0, between the two barriers
-        const cf xa = r2c_split<B>(fft, tw + K::TW1, k0), xb = r2c_split<B>(fft, tw + K::TW1, k1);
+        // one twiddle lookup serves all four: w(B - k) = -conj(w(k)) (w(B/2) = -i for the k0 = 0
+        // lane), the inverse twiddles are the conjugates
+        const cf wa = k0 == 0 ? cf{1.f, 0.f} : twiddle<2 * B, -1>(tw + K::TW1, k0);
+        const cf wb = k0 == 0 ? cf{0.f, -1.f} : cf{-wa.x, wa.y};
+        const cf xa = r2c_split_w<B>(fft, wa, k0), xb = r2c_split_w<B>(fft, wb, k1);
         cf* row = fdl + crow + int64_t(w) * pstride;
         row[k0] = xa;
         row[k1] = xb;
@@ -789,8 +793,9 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
         }
         yb.x += h0b.x * xb.x - h0b.y * xb.y;
         yb.y += h0b.x * xb.y + h0b.y * xb.x;
-        X[k0] = k0 == 0 ? c2r_join<B>(cf{ya.x, 0.f}, cf{ya.y, 0.f}, tw + K::TW1, 0) : c2r_join<B>(ya, yb, tw + K::TW1, k0);
-        X[k1] = c2r_join<B>(yb, k0 == 0 ? yb : ya, tw + K::TW1, k1);
+        X[k0] = k0 == 0 ? c2r_join_w<B>(cf{ya.x, 0.f}, cf{ya.y, 0.f}, cf{1.f, 0.f}, 0)
+                        : c2r_join_w<B>(ya, yb, cf{wa.x, -wa.y}, k0);
+        X[k1] = c2r_join_w<B>(yb, k0 == 0 ? yb : ya, cf{wb.x, -wb.y}, k1);
     }
     __syncthreads();
     NEO_PROBE(5, tid == 0);
