@@ -2,6 +2,9 @@
 // T consecutive blocks of every channel share ONE pass over the filter and the FDL
 // (window r2c + insert, MAC with a sliding FDL window in registers, per-block finish,
 // OLA overlap chain). Same results as T single-block steps up to summation order.
+// Also the streaming lookahead built on the same pass (one block per call): the window
+// pass at the first block of every T-block window (k_batch_mac, ahead), the sub-window
+// passes, and the per-block steps k_upols_ahead / k_upols_ahead2 / k_upols_ahead3.
 #include "upols_device.hpp"
 #include "upols_handle.hpp"
 
