@@ -870,13 +870,13 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
     __shared__ __attribute__((aligned(16))) float hh[B];               // head taps
     __shared__ __attribute__((aligned(16))) float Pc[CW][B];           // convolution partials
     __shared__ __attribute__((aligned(16))) float zs[B];               // irfft(R) / 2B, samples [B, 2B)
-    __shared__ int cnt[4];                                             // window, R, partials, z
+    __shared__ int cnt[5];                                             // window, R, partials, z, joined R
     const int tid = threadIdx.x, c = blockIdx.x, wave = tid >> 6, lane = tid & 63;
     const int64_t crow = int64_t(c) * cstride;
     const float* in_c = in + int64_t(c) * ld_in;
     float* prev_c = prev + int64_t(c) * B;
     NEO_PROBE(0, tid == 0);
-    if (tid < 4) cnt[tid] = 0;
+    if (tid < 5) cnt[tid] = 0;
     if (tid < XP) xw[tid] = 0.f;
     if (tid < 8) xw[XP + 2 * B + tid] = 0.f;
     __syncthreads();
@@ -951,20 +951,28 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
         const cf b0 = finish(a0, q == 0), b1 = finish(a1, false);
         reinterpret_cast<float4*>(Rs)[q] = make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
         lds_signal(&cnt[1]);
+        // c2r join on mirror pairs (k, B - k), in place: lane q owns (q, B - q), (0, B/2) for q = 0
+        lds_wait(&cnt[1], MW);
+        lds_wait(&cnt[0], 1);  // wave 0's twiddle table
+        {
+            const int k0 = q, k1 = q == 0 ? B / 2 : B - q;
+            const cf wa = k0 == 0 ? cf{1.f, 0.f} : twiddle<2 * B, -1>(tw_f + K::TW1, k0);
+            const cf wb = k0 == 0 ? cf{0.f, -1.f} : cf{-wa.x, wa.y};
+            const cf ya = Rs[k0], yb = Rs[k1];
+            Rs[k0] = k0 == 0 ? c2r_join_w<B>(cf{ya.x, 0.f}, cf{ya.y, 0.f}, cf{1.f, 0.f}, 0)
+                             : c2r_join_w<B>(ya, yb, cf{wa.x, -wa.y}, k0);
+            Rs[k1] = c2r_join_w<B>(yb, k0 == 0 ? yb : ya, cf{wb.x, -wb.y}, k1);
+        }
+        lds_signal(&cnt[4]);
         NEO_PROBE(4, tid == 64);
     } else if (wave == MW + 1) {  // irfft(R) / 2B -> zs
         for (int i = lane; i < K::TW1 + K::TW2; i += 64) tw_c[i] = twg[i];
-        lds_wait(&cnt[1], MW);
+        lds_wait(&cnt[4], MW);  // the joined rest spectrum
         NEO_PROBE(5, lane == 0);
         cf v[EW];
         if (lane < TW) {
 #pragma unroll
-            for (int m = 0; m < EW; ++m) {
-                const int k = lane + m * TW;
-                const cf x0 = Rs[0];
-                v[m] = k == 0 ? c2r_join<B>(cf{x0.x, 0.f}, cf{x0.y, 0.f}, tw_c + K::TW1, 0)
-                              : c2r_join<B>(Rs[k], Rs[B - k], tw_c + K::TW1, k);
-            }
+            for (int m = 0; m < EW; ++m) v[m] = Rs[lane + m * TW];
         }
         stockham<B, EW, +1, 1, true>(v, fft_c, tw_c, lane, lane < TW);
         if (lane < TW) {
