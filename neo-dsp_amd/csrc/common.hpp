@@ -57,15 +57,24 @@ struct device_guard {
     }
 };
 
-// Two-level forward twiddle table for an FFT of size n (see twiddle<> in
-// fft_device.hpp): [0,64) = W^e, [64, 64+n/64) = W^(64h), W = exp(-2*pi*i/n),
-// computed in double (long double for the f64 tables) and rounded once.
+// Forward twiddle table for an FFT of size n (see twiddle<> in fft_device.hpp): n <=
+// kTwFull: W^e for e < max(64, n) (e mod n); larger: [0,64) = W^e, [64, 64+n/64) =
+// W^(64h); W = exp(-2*pi*i/n), computed in double (long double for the f64 tables) and
+// rounded once.
 template<class C = cf>
 inline std::vector<C> make_twiddle_table(int64_t n)
 {
     using R = real_of<C>;
     using W = std::conditional_t<sizeof(R) == 8, long double, double>;
     const W pi2 = W(2) * W(3.14159265358979323846264338327950288L);
+    if (n <= kTwFull) {
+        std::vector<C> t(static_cast<size_t>(n < 64 ? 64 : n));
+        for (int64_t e = 0; e < int64_t(t.size()); ++e) {
+            const W a = -pi2 * W(e % (n > 0 ? n : 1)) / W(n > 0 ? n : 1);
+            t[size_t(e)] = {R(std::cos(a)), R(std::sin(a))};
+        }
+        return t;
+    }
     const int64_t lo = 64, hi = n <= 64 ? 0 : n / 64;
     std::vector<C> t(static_cast<size_t>(lo + hi));
     for (int64_t e = 0; e < lo; ++e) {

@@ -182,13 +182,17 @@ __device__ __forceinline__ void dft(C (&v)[R])
 __device__ __forceinline__ int lpad(int a) { return a + (a >> 4); }
 __host__ __device__ constexpr int lds_len(int n) { return n + n / 16 + 1; }
 
-// Two-level twiddle table for an FFT of size N: tw[0..63] = W^e (e < 64),
-// tw[64..64+N/64) = W^(64*h); W = exp(-2*pi*i/N) (forward). DIR=+1 conjugates.
+// Twiddle table for an FFT of size N, W = exp(-2*pi*i/N) (forward); DIR=+1 conjugates.
+// N <= kTwFull: one entry per exponent, tw[e] = W^e (64 entries at least, e mod N); one LDS
+// read per twiddle in the block steps' B-point transforms. Larger N: two levels,
+// tw[0..63] = W^e (e < 64), tw[64..64+N/64) = W^(64*h), a read pair and a complex multiply.
+constexpr int kTwFull = 512;
+
 template<int N, int DIR, class C>
 __device__ __forceinline__ C twiddle(const C* tw, int e)
 {
     C w;
-    if constexpr (N <= 64) {
+    if constexpr (N <= kTwFull) {
         w = tw[e];
     } else {
         w = cmul(tw[64 + (e >> 6)], tw[e & 63]);
@@ -200,7 +204,7 @@ __device__ __forceinline__ C twiddle(const C* tw, int e)
 template<int N>
 __host__ __device__ constexpr int twiddle_len()
 {
-    return N <= 64 ? 64 : 64 + N / 64;
+    return N <= 64 ? 64 : (N <= kTwFull ? N : 64 + N / 64);
 }
 
 // Radix chosen for the pass that starts with sub-transform length Ns.
