@@ -587,7 +587,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->pcb = h->pc;  // same Infinity Cache budget as the single-block step
     if (const char* e = std::getenv("NEO_HIP_BATCH_CACHE_ROWS")) h->pcb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("NEO_HIP_SUB_SPLIT")) h->ssplit = std::atoi(e) != 0;
-    if (const char* e = std::getenv("NEO_HIP_BATCH_PRIO")) h->bprio = std::max(0, std::min(20, std::atoi(e)));
+    if (const char* e = std::getenv("NEO_HIP_BATCH_PRIO")) h->bprio = std::max(0, std::min(95, std::atoi(e)));
     if (const char* e = std::getenv("NEO_HIP_AHEAD_DIRECT")) h->adirect = std::atoi(e) != 0 ? 2 : 0;
     if (const char* e = std::getenv("NEO_HIP_BATCH8_VAR")) h->b8var = std::atoi(e) == 3 ? 3 : 0;
     h->subw = block >= 512 ? 16 : 8;

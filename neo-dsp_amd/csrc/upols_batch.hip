@@ -308,9 +308,16 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     // s_memrealtime ticks (100 MHz; 11 = 20 us). (Locking the two together with a barrier per chunk instead —
     // one 8-wave workgroup per CU — was 30 % slower: both stall on memory at the same time.)
     const int half = blockIdx.x >= gridDim.x / 2;
+    // prio = shift + 32 * m: m = 0 alternates slices 1:1; m = 1 gives the younger workgroup
+    // 2 slices of 3, m = 2 3 slices of 5
     auto share = [&]() {
         if (prio) {
-            if (((__builtin_amdgcn_s_memrealtime() >> prio) + half) & 1) __builtin_amdgcn_s_setprio(2);
+            const unsigned sh = prio & 31, m = unsigned(prio) >> 5;
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime() >> sh;
+            const unsigned period = m == 0 ? 2 : (m == 1 ? 3 : 5), older = m == 2 ? 2 : 1;
+            const bool mine_old = t % period < older;  // slices held by the older workgroup
+            const bool hi = half ? !mine_old : mine_old;
+            if (hi) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
     };
