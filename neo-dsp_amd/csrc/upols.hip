@@ -584,7 +584,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     if (h->bvar >= 4 && (int64_t(channels) * h->ring * block + int64_t(h->ring) * h->pstride) * int64_t(sizeof(cf)) >=
                             (int64_t(1) << 31))
         h->bvar = 2;
-    h->pcb = h->pc;  // same Infinity Cache budget as the single-block step
+    h->pcb = int(std::min<double>(partitions, kBatchCacheBudgetBytes / (double(channels) * block * sizeof(cf))));
     if (const char* e = std::getenv("NEO_HIP_BATCH_CACHE_ROWS")) h->pcb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("NEO_HIP_SUB_SPLIT")) h->ssplit = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_BATCH_PRIO")) h->bprio = std::max(0, std::min(95, std::atoi(e)));

@@ -13,6 +13,9 @@ namespace neo_hip {
 constexpr int kMaxBatch = 32;                          // most blocks one batched MAC pass consumes
 constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch
 constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read cacheable (256 MiB Infinity Cache)
+// the lookahead / batched passes leave more of the Infinity Cache to the block steps' rows and
+// slabs (same-box A/B at C5, 4 runs each: 168 MiB 17.8 us/step, 216 MiB 18.3, 126 MiB 18.1)
+constexpr double kBatchCacheBudgetBytes = 168.0 * 1024 * 1024;
 }  // namespace neo_hip
 
 struct neo_hip_upols {
@@ -31,7 +34,7 @@ struct neo_hip_upols {
     bool batch = true;      // process_blocks runs T blocks per MAC pass (neo_hip_upols_set_batch)
     int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
     int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
-    int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kCacheBudgetBytes; NEO_HIP_BATCH_CACHE_ROWS)
+    int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kBatchCacheBudgetBytes; NEO_HIP_BATCH_CACHE_ROWS)
     int bprio = 11;         // batched MAC: co-resident workgroups trade issue priority every 2^bprio
                             // 10-ns ticks (NEO_HIP_BATCH_PRIO=0 off)
     int b8var = 3;          // 8-block passes: bmac_var 3 (buffer loads, D = 8) or 0 (NEO_HIP_BATCH8_VAR)
