@@ -592,6 +592,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     if (const char* e = std::getenv("NEO_HIP_BATCH8_VAR")) h->b8var = std::atoi(e) == 3 ? 3 : 0;
     h->subw = block >= 512 ? 16 : 8;
     if (const char* e = std::getenv("NEO_HIP_SUBWINDOW")) h->subw = std::atoi(e) == 16 ? 16 : 8;
+    if (const char* e = std::getenv("NEO_HIP_SLAB_NT")) h->snt = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_SUB")) h->asub = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_KERNEL")) h->akern = std::atoi(e) == 1 ? 1 : 2;
     // batched MAC: 256-lane workgroups at 2 waves/SIMD -> 2 resident per CU, so 512 fills the

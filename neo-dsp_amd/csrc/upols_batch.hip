@@ -277,7 +277,8 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
     // ahead (streaming lookahead, see k_upols_ahead): blocks 0..T-1 are not in the FDL yet,
     // so rows w .. w+T-1 (the prologue window and the first row entering it) count as zero
     // and block j collects partitions p > j only
-    const bool future = ahead && p0 == 0;
+    const bool future = (ahead & 1) && p0 == 0;
+    const bool nts = (ahead & 2) != 0;  // slabs stored nontemporally (they are read once, next steps)
     V f[T][VPT];
 #pragma unroll
     for (int sl = 1; sl < T; ++sl) {  // rows block sl needs at p0 (entered at partition p0 - sl)
@@ -352,7 +353,8 @@ __global__ __launch_bounds__((batch_cfg<B, NB>::L), bmac_var<VAR>::W) void k_bat
                     o[2 * b + 1] = bin0 ? A.d.y : A.x.x + A.x.y;
                 }
             }
-            *reinterpret_cast<V*>(slab + int64_t(j) * B + (tid + v * L) * NB) = o;
+            if (nts) __builtin_nontemporal_store(o, reinterpret_cast<V*>(slab + int64_t(j) * B + (tid + v * L) * NB));
+            else *reinterpret_cast<V*>(slab + int64_t(j) * B + (tid + v * L) * NB) = o;
         }
     if constexpr (T == 32) NEO_CLOCK_STAMP(12);
 }
@@ -1250,9 +1252,9 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         const bool timed = h->timing && h->tick++ % h->timing == 0;
         if ((rc = mac_event(h, timed, false, ev, s))) return rc;
         if (h->bNB == 2) {
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 1, full_pass(h))))
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 1 | (h->snt ? 2 : 0), full_pass(h))))
         } else {
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 1, full_pass(h))))
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 1 | (h->snt ? 2 : 0), full_pass(h))))
         }
         if (rc) return rc;
         if ((rc = mac_event(h, timed, true, ev, s))) return rc;
@@ -1268,7 +1270,7 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
         if (ssub && jr == 0) {
             const int srows = (h->phase + sw) / ssub;
             const mac_pass mp{h->part_s, h->phase + sw, ssub, srows, h->phase, h->P};
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, sw, s, 1, mp)))
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, sw, s, 1 | (h->snt ? 2 : 0), mp)))
             if (rc) return rc;
         }
         const cf* subp = h->part_s;

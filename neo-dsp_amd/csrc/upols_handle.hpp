@@ -37,6 +37,7 @@ struct neo_hip_upols {
     int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kBatchCacheBudgetBytes; NEO_HIP_BATCH_CACHE_ROWS)
     int bprio = 11;         // batched MAC: co-resident workgroups trade issue priority every 2^bprio
                             // 10-ns ticks (NEO_HIP_BATCH_PRIO=0 off)
+    bool snt = false;       // lookahead passes store their slabs nontemporally (NEO_HIP_SLAB_NT)
     int b8var = 3;          // 8-block passes: bmac_var 3 (buffer loads, D = 8) or 0 (NEO_HIP_BATCH8_VAR)
     int bvar = 3;           // batched MAC variant at T = 32, B = 256/512 (bmac_var in upols_batch.hip; NEO_HIP_BATCH_VAR)
     neo_hip::cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]

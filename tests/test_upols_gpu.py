@@ -581,6 +581,32 @@ def test_ahead_direct_head(neo_gpu, oracle, monkeypatch, B, direct, head):
     assert peak_err(t.cpu().numpy(), ref) <= TOL
 
 
+@pytest.mark.parametrize("method", ["upols", "upola"])
+@pytest.mark.parametrize("B", [256, 512])
+@pytest.mark.parametrize("subw", ["8", "16"])
+@pytest.mark.parametrize("slab_nt", ["0", "1"])
+def test_ahead_subwindow_lengths(neo_gpu, oracle, monkeypatch, method, B, subw, slab_nt):
+    """Lookahead sub-windows of 8 and 16 blocks (one or three sub-window passes per window;
+    block steps walk up to 7 / 15 row pairs), slabs stored with either cache policy, over
+    three windows with ring wraparound."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("NEO_HIP_SUBWINDOW", subw)
+    monkeypatch.setenv("NEO_HIP_SLAB_NT", slab_nt)
+    C, L, nb = 2, 45 * B, 100
+    ir = np.stack([oracle.noise(390 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    sig = np.stack([oracle.noise(395 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts, method=method)
+    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
+    conv.filter(parts)
+    conv.set_batch(False)
+    conv.set_ahead(True)
+    t = torch.from_numpy(sig).cuda()
+    conv.process_blocks(t)
+    torch.cuda.synchronize()
+    assert peak_err(t.cpu().numpy(), ref) <= TOL
+
+
 def test_ahead_mixed_paths(neo_gpu, oracle):
     """Lookahead steps, batched passes, plain steps and host blocks share one state; the
     lookahead can be switched at any block boundary."""
