@@ -670,7 +670,12 @@ __global__ __launch_bounds__(256) void k_upols_ahead(const float* __restrict__ i
 template<int B>
 struct ahead_cfg {
     static constexpr int Q = B / 2;                                  // float4 (2 bins) per row
+#ifdef NEO_AHEAD_NG
+    static constexpr int NG0 = Q >= 768 ? 1 : (768 / Q > 6 ? 6 : 768 / Q);
+    static constexpr int NG = NEO_AHEAD_NG < NG0 ? NEO_AHEAD_NG : NG0;  // (A/B builds)
+#else
     static constexpr int NG = Q >= 768 ? 1 : (768 / Q > 6 ? 6 : 768 / Q);  // MAC groups
+#endif
     static constexpr int EW = B >= 512 ? B / 64 : 8;                 // transform elements per lane
     static constexpr int TW = B / EW;                                // transform lanes (<= 64)
     static constexpr int NT = 64 + NG * Q;                           // workgroup size
