@@ -385,6 +385,7 @@ int reset_state(upols_t* h, hipStream_t s)
     h->wpos = 0;
     h->in_pos = 0;
     h->phase = 0;
+    h->fwin = -1;
     return NEO_HIP_OK;
 }
 
@@ -410,6 +411,10 @@ void destroy(upols_t* h)
     (void)hipFree(h->h0t);
     (void)hipFree(h->h0tail);
     (void)hipFree(h->tail);
+    (void)hipFree(h->hf);
+    (void)hipFree(h->hf0);
+    (void)hipFree(h->ff);
+    (void)hipFree(h->twf);
     if (h->samples_host) (void)hipHostFree(h->samples_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -594,6 +599,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     if (const char* e = std::getenv("NEO_HIP_SUBWINDOW")) h->subw = std::atoi(e) == 16 ? 16 : 8;
     if (const char* e = std::getenv("NEO_HIP_SLAB_NT")) h->snt = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_SUB")) h->asub = std::atoi(e) != 0;
+    if (const char* e = std::getenv("NEO_HIP_FAR")) h->far = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_KERNEL")) h->akern = std::atoi(e) == 1 ? 1 : 2;
     // batched MAC: 256-lane workgroups at 2 waves/SIMD -> 2 resident per CU, so 512 fills the
     // chip once with no second round (A/B, bmac_var 3: C5 0.409 -> 0.367 ms per pass, C4 0.369
@@ -705,6 +711,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
     }
     int rc = pack_filter(h, src, h->stream);
     if (!rc) rc = update_head(h, h->stream);
+    if (!rc) rc = far_filter(h, h->stream);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     if (tmp) (void)hipFree(tmp);
@@ -731,6 +738,7 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
     if (!rc && normalize) rc = normalize_device(d, h->C, length, h->stream);
     if (!rc) rc = partition_device(d, h->C, length, h->B, true, h->H, h->tw, h->stream, h->cstride, h->pstride);
     if (!rc) rc = update_head(h, h->stream);
+    if (!rc) rc = far_filter(h, h->stream);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     (void)hipFree(d);
@@ -843,7 +851,8 @@ NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable)
     if (enable && h->v2) return fail(NEO_HIP_EINVAL, "lookahead steps are for whole-block upols / upola handles");
     if (enable && h->ring - h->P < batch_blocks(h) - 1) return fail(NEO_HIP_EINVAL, "FDL ring too short for lookahead");
     h->ahead = enable != 0;
-    h->phase = 0;  // the FDL is complete at any block boundary: the next step opens a window
+    h->phase = 0;
+    h->fwin = -1;  // the FDL is complete at any block boundary: the next step opens a window
     return NEO_HIP_OK;
 }
 

@@ -687,7 +687,7 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
     const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int ssub,
-    int jr, int sw)
+    int jr, int sw, const cf* __restrict__ far, int fj)
 {
     using K = upols_cfg<B>;
     using A = ahead_cfg<B>;
@@ -757,6 +757,10 @@ __global__ __launch_bounds__(ahead_cfg<B>::NT) void k_upols_ahead2(
         }
         for (int s = NG - 1 - g; s < ssub; s += NG) {  // sub-window pass slabs (the window's earlier rows)
             const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + s) * sw + jr) * B)[q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        if (far && g == NG - 1) {  // two-level lookahead: the far partitions (upols_far.hip)
+            const float4 r = reinterpret_cast<const float4*>(far + (int64_t(c) * kFarT + fj) * B)[q];
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
@@ -869,7 +873,7 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ part, int S, int T, int j,
     const cf* __restrict__ twg, int ring, int w, int64_t cstride, int64_t pstride, const cf* __restrict__ sub, int ssub,
-    int jr, int sw, const float* __restrict__ h0t)
+    int jr, int sw, const float* __restrict__ h0t, const cf* __restrict__ far, int fj)
 {
     using K = upols_cfg<B>;
     using A = ahead3_cfg<B>;
@@ -946,6 +950,10 @@ __global__ __launch_bounds__(ahead3_cfg<B>::NT) void k_upols_ahead3(
         }
         for (int t = 0; t < ssub; ++t) {
             const float4 r = reinterpret_cast<const float4*>(sub + ((int64_t(c) * ssub + t) * sw + jr) * B)[q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+        if (far) {  // two-level lookahead: the far partitions (upols_far.hip)
+            const float4 r = reinterpret_cast<const float4*>(far + (int64_t(c) * kFarT + fj) * B)[q];
             sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
         }
         acc4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
@@ -1252,14 +1260,35 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     const int B = h->B, T = batch_blocks(h);
     int rc = batch_buffers(h);
     if (rc) return rc;
+    // two-level lookahead: partitions >= kFarT once per kFarT blocks (upols_far.hip), the
+    // level-1 pass over partitions < kFarT only
+    const bool far = far_usable(h);
+    if (far && h->phase == 0) {
+        if (h->fwin <= 0) {
+            if ((rc = far_window(h, s))) return rc;
+            h->fwin = 0;
+            h->fbase = 0;
+        } else {
+            h->fbase += T;
+        }
+        h->fwin = (h->fwin + 1) % (kFarT / T);
+    }
+    const cf* farp = far ? h->ff : nullptr;
+    const int fj = far ? h->fbase + h->phase : 0;
     if (h->phase == 0) {
         std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
         const bool timed = h->timing && h->tick++ % h->timing == 0;
         if ((rc = mac_event(h, timed, false, ev, s))) return rc;
+        mac_pass mp = full_pass(h);
+        if (far) {  // partitions [0, kFarT) in splits of whole 32-partition chunks; splits past it store zeros
+            mp.P = kFarT;
+            mp.rows = std::max(kMaxBatch, (kFarT / h->Sb + kMaxBatch - 1) / kMaxBatch * kMaxBatch);
+            mp.pc = std::min(mp.pc, kFarT);
+        }
         if (h->bNB == 2) {
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 1 | (h->snt ? 2 : 0), full_pass(h))))
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 2>(h, T, s, 1 | (h->snt ? 2 : 0), mp)))
         } else {
-            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 1 | (h->snt ? 2 : 0), full_pass(h))))
+            NEO_UPOLS_DISPATCH(B, rc = (launch_batch_mac<BB, 1>(h, T, s, 1 | (h->snt ? 2 : 0), mp)))
         }
         if (rc) return rc;
         if ((rc = mac_event(h, timed, true, ev, s))) return rc;
@@ -1284,21 +1313,21 @@ int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
             if (B == 256)
                 hipLaunchKernelGGL((k_upols_ahead3<256>), dim3(unsigned(h->C)), dim3(ahead3_cfg<256>::NT), 0, s, in,
                                    ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, h->h0t);
+                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, h->h0t, farp, fj);
             else
                 hipLaunchKernelGGL((k_upols_ahead3<512>), dim3(unsigned(h->C)), dim3(ahead3_cfg<512>::NT), 0, s, in,
                                    ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, h->h0t);
+                                   h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, h->h0t, farp, fj);
         } else if (h->ola) {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, true>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, farp, fj))
         } else {
             NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                       (k_upols_ahead2<BB, false>), dim3(unsigned(h->C)), dim3(ahead_cfg<BB>::NT), 0, s, in,
                                       ld_in, out, ld_out, h->prev, h->H, h->fdl, h->part_b, h->Sb, T, h->phase, h->tw,
-                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw))
+                                      h->ring, h->wpos, h->cstride, h->pstride, subp, ssub, jr, sw, farp, fj))
         }
     } else if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_upols_ahead<BB, true>), dim3(unsigned(h->C)), dim3(256), 0, s, in,
@@ -1321,6 +1350,7 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     int rc0 = batch_buffers(h);
     if (rc0) return rc0;
     const unsigned gCT = unsigned(h->C) * unsigned(T);
+    h->fwin = -1;  // the far window restarts at the next lookahead window
     if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, true>), dim3(gCT), dim3(256), 0, s, in, ld_in,
                                                  h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))

@@ -11,6 +11,7 @@
 
 namespace neo_hip {
 constexpr int kMaxBatch = 32;                          // most blocks one batched MAC pass consumes
+constexpr int kFarT = 128;                             // two-level lookahead: blocks per far-field window
 constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch
 constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read cacheable (256 MiB Infinity Cache)
 // the lookahead / batched passes leave more of the Infinity Cache to the block steps' rows and
@@ -58,6 +59,15 @@ struct neo_hip_upols {
     float* h0tail = nullptr;
     int akern = 2;  // per-block lookahead kernel: 2 = k_upols_ahead2 (B <= 1024), 1 = k_upols_ahead (NEO_HIP_AHEAD_KERNEL)
     int phase = 0;
+    // two-level lookahead (upols_far.hip, NEO_HIP_FAR=1): partitions >= kFarT by a partition-axis
+    // transform once per kFarT blocks; the level-1 pass then walks partitions < kFarT only
+    bool far = false;
+    int fwin = -1;                 // level-1 windows done in the current far window (-1: recompute)
+    int fbase = 0;                 // first block of the current level-1 window within the far window
+    neo_hip::cf* hf = nullptr;     // segment spectra [C][Q-1][2 kFarT][B]
+    neo_hip::cf* hf0 = nullptr;    // bin 0's second coefficient [C][Q-1][2 kFarT]
+    neo_hip::cf* ff = nullptr;     // far field of the current window [C][kFarT][B]
+    neo_hip::cf* twf = nullptr;    // 2 kFarT-point twiddles
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
@@ -129,6 +139,11 @@ inline int batch_blocks(const upols_t* h) { return batch_t(h->B, h->bNB, h->bT);
 int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s);
 // upols_batch.hip: one streaming block step in lookahead mode
 int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
+// upols_far.hip: two-level lookahead (segment spectra after every filter change; one far
+// window per kFarT blocks)
+bool far_usable(const upols_t* h);
+int far_filter(upols_t* h, hipStream_t s);
+int far_window(upols_t* h, hipStream_t s);
 // upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device
 int upload_tw(cf** d, int B);
 int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s,

@@ -551,6 +551,62 @@ def test_ahead_steps_vs_oracle(neo_gpu, oracle, monkeypatch, method, B, L, C, nb
     assert peak_err(t.cpu().numpy(), ref) <= TOL
 
 
+@pytest.mark.parametrize("method", ["upols", "upola"])
+@pytest.mark.parametrize("B,P,C,nb", [(256, 300, 2, 420), (512, 200, 2, 300), (32, 700, 1, 900), (64, 129, 2, 300),
+                                      (128, 256, 1, 520)])
+def test_far_field_steps_vs_oracle(neo_gpu, oracle, monkeypatch, method, B, P, C, nb):
+    """Two-level lookahead (NEO_HIP_FAR=1, upols_far.hip): partitions >= 128 by a 256-point
+    transform along the partition axis once per 128 blocks, the level-1 pass over partitions
+    < 128. Several far windows, ring wraparound, P just above 128, a last segment of one
+    partition, the packed DC/Nyquist bin; OLS and OLA."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("NEO_HIP_FAR", "1")
+    L = B * (P - 1) + B // 2 + 1
+    ir = np.stack([oracle.noise(520 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    assert parts.shape[1] == P
+    sig = np.stack([oracle.noise(530 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts, method=method)
+    conv = neo_gpu.UpolsConvolver(C, B, P, method=method)
+    conv.filter(parts)
+    conv.set_batch(False)
+    conv.set_ahead(True)
+    t = torch.from_numpy(sig).cuda()
+    conv.process_blocks(t)
+    torch.cuda.synchronize()
+    assert peak_err(t.cpu().numpy(), ref) <= TOL
+
+
+def test_far_field_mixed_and_refilter(neo_gpu, oracle, monkeypatch):
+    """Far field across batched passes, lookahead toggles at arbitrary blocks and a filter
+    change: the far window restarts at the next lookahead window."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("NEO_HIP_FAR", "1")
+    B, P, C = 256, 290, 2
+    L = B * P
+    irs = [np.stack([oracle.noise(540 + 7 * k + c, L) for c in range(C)]) for k in range(2)]
+    parts = [oracle.uniform_partition(oracle.normalize_impulse(ir), B) for ir in irs]
+    conv = neo_gpu.UpolsConvolver(C, B, P)
+    for k in range(2):
+        nb = 480
+        sig = np.stack([oracle.noise(560 + 3 * k + c, B * nb) for c in range(C)])
+        ref = oracle.dense_convolve(sig, parts[k])
+        conv.filter(parts[k])
+        out = np.empty_like(sig)
+        pos = 0
+        for ahead, batch, n in [(True, False, 150), (False, True, 64), (True, False, 37), (True, True, 32),
+                                (True, False, 197)]:
+            conv.set_batch(batch)
+            conv.set_ahead(ahead)
+            seg = torch.from_numpy(np.ascontiguousarray(sig[:, pos * B:(pos + n) * B])).cuda()
+            conv.process_blocks(seg)
+            torch.cuda.synchronize()
+            out[:, pos * B:(pos + n) * B] = seg.cpu().numpy()
+            pos += n
+        assert pos == nb
+        assert peak_err(out, ref) <= TOL, k
+
+
 @pytest.mark.parametrize("B", [256, 512])
 @pytest.mark.parametrize("direct", ["0", "1"])
 @pytest.mark.parametrize("head", ["partitioned", "arbitrary"])
