@@ -267,8 +267,17 @@ def run_upols(args, world, rank, local):
         # filter + FDL that also accumulates every partition already available for the
         # window's later blocks; each block step (k_upols_ahead) adds the rest
         elapsed, mac_avg_ms = timed_steps()
-        bytes_mac = C * 8 * B * (2 * P + sb * T)  # filter rows + FDL rows read, T partial slabs per split written
-        kernel = f"k_batch_mac<{B},{T},1> (lookahead window pass, 1 per {T} blocks)"
+        # two-level lookahead (upols_far.hip; default from 1536 partitions, NEO_HIP_FAR overrides):
+        # the window pass walks partitions < 128; k_far_mac takes the rest once per 128 blocks
+        far_env = os.environ.get("NEO_HIP_FAR")
+        far = P > 128 and (far_env != "0" if far_env is not None and far_env != "" else P >= 1536)
+        if far and args.steps % 128:
+            print(f"bench: two-level lookahead on and --steps {args.steps} is not a multiple of 128: "
+                  "the timed region holds a partial far-window share", file=sys.stderr)
+        P1 = 128 if far else P
+        bytes_mac = C * 8 * B * (2 * P1 + sb * T)  # filter rows + FDL rows read, T partial slabs per split written
+        kernel = f"k_batch_mac<{B},{T},1> (lookahead window pass, 1 per {T} blocks" + \
+            (", partitions < 128; far field: k_far_mac once per 128 blocks)" if far else ")")
         steps_per_launch = T
     else:
         elapsed, mac_avg_ms, bytes_mac, kernel, steps_per_launch = el_plain, mac_plain, bytes_step, plain["kernel"], 1

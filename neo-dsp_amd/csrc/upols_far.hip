@@ -25,6 +25,18 @@
 
 namespace neo_hip {
 
+#ifndef NEO_FAR_WAVES
+#define NEO_FAR_WAVES 2  // A/B builds: waves per SIMD the far MAC is register-capped for
+#endif
+#ifndef NEO_FAR_PLAIN
+#define NEO_FAR_PLAIN 0  // A/B builds: 1 = default-policy loads in the far MAC
+#endif
+__device__ __forceinline__ cf far_ld(const cf* p)
+{
+    if constexpr (NEO_FAR_PLAIN) return *p;
+    else return ld_nt(p);
+}
+
 constexpr int kFarN = 2 * kFarT;  // partition-axis transform length
 constexpr int kFarL = 256;        // lanes per workgroup: 16 row groups x 16 bin pairs (32 bins)
 
@@ -110,7 +122,7 @@ __global__ __launch_bounds__(kFarL) void k_far_filter(const cf* __restrict__ H, 
 // filter taps and read 0). Segment q + 1's rows 128..255 are segment q's rows 0..127, so each
 // lane keeps them in registers: the FDL is read once per window (a 2-bin-per-lane first
 // version held 300 registers, ran at 1 wave/SIMD and took 2.0 ms at C5).
-__global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(2))) void k_far_mac(const cf* __restrict__ fdl, const cf* __restrict__ hf,
+__global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(NEO_FAR_WAVES))) void k_far_mac(const cf* __restrict__ fdl, const cf* __restrict__ hf,
                                                    const cf* __restrict__ hf0, cf* __restrict__ ff,
                                                    const cf* __restrict__ twg, int B, int P, int Q1, int ring, int w,
                                                    int64_t cstride, int64_t pstride)
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(2))) void
         const int d = (q + 1) * kFarT - (a + 16 * n2);  // blocks before t0 (>= 1)
         if (d >= P) return cf{0.f, 0.f};
         const int r = w - d < 0 ? w - d + ring : w - d;
-        return ld_nt(F + int64_t(r) * pstride);
+        return far_ld(F + int64_t(r) * pstride);
     };
     cf acc[16], v[16];
 #pragma unroll
@@ -144,7 +156,7 @@ __global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(2))) void
         const cf* hq = hf + (int64_t(c) * Q1 + (q - 1)) * kFarN * B + kb;
         cf h[16], nx[8];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) h[k] = ld_nt(hq + int64_t(16 * k + a) * B);
+        for (int k = 0; k < 16; ++k) h[k] = far_ld(hq + int64_t(16 * k + a) * B);
 #pragma unroll
         for (int n2 = 0; n2 < 8; ++n2) nx[n2] = q < Q1 ? row(q + 1, n2) : cf{0.f, 0.f};
         cf keep[8];

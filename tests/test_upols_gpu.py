@@ -214,6 +214,28 @@ def test_full_size_properties(neo_gpu, oracle, C, B, L):
         assert peak_err(ox[c].cpu().numpy(), ref[0]) <= TOL
 
 
+def test_full_size_far_field_default(neo_gpu, oracle):
+    """C4 shape (P = 1875 >= kFarAutoP) in lookahead mode with the environment default, i.e.
+    the two-level lookahead on: 300 blocks (three far windows, 14 segments each), two channels
+    checked against the oracle."""
+    torch = pytest.importorskip("torch")
+    C, B, L, nb = 256, 256, 480000, 300
+    g = torch.Generator(device="cuda").manual_seed(77)
+    ir = (torch.rand((C, L), generator=g, device="cuda") * 2 - 1).contiguous()
+    x = (torch.rand((C, B * nb), generator=g, device="cuda") * 2 - 1).contiguous()
+    conv = neo_gpu.UpolsConvolver(C, B, neo_gpu.num_partitions(L, B))
+    conv.set_impulse(ir, normalize=True)
+    conv.set_batch(False)
+    conv.set_ahead(True)
+    xh = x.cpu().numpy()
+    conv.process_blocks(x)
+    torch.cuda.synchronize()
+    irh = oracle.normalize_impulse(ir.cpu().numpy())
+    for c in (0, C - 1):
+        ref = oracle.dense_convolve(xh[c:c + 1], oracle.uniform_partition(irh[c:c + 1], B))
+        assert peak_err(x[c].cpu().numpy(), ref[0]) <= TOL
+
+
 def test_multirow_splits_with_wraparound(neo_gpu, oracle):
     """More blocks than partitions and several partitions per split (every split carries
     nonzero FDL rows, ring wraps), forced via NEO_HIP_SPLIT_WGS read at create time."""
