@@ -267,10 +267,10 @@ def run_upols(args, world, rank, local):
         # filter + FDL that also accumulates every partition already available for the
         # window's later blocks; each block step (k_upols_ahead) adds the rest
         elapsed, mac_avg_ms = timed_steps()
-        # two-level lookahead (upols_far.hip; default from 1536 partitions, NEO_HIP_FAR overrides):
+        # two-level lookahead (upols_far.hip; default from 512 partitions, NEO_HIP_FAR overrides):
         # the window pass walks partitions < 128; k_far_mac takes the rest once per 128 blocks
         far_env = os.environ.get("NEO_HIP_FAR")
-        far = P > 128 and (far_env != "0" if far_env is not None and far_env != "" else P >= 1536)
+        far = P > 128 and (far_env != "0" if far_env is not None and far_env != "" else P >= 512)
         if far and args.steps % 128:
             print(f"bench: two-level lookahead on and --steps {args.steps} is not a multiple of 128: "
                   "the timed region holds a partial far-window share", file=sys.stderr)

@@ -599,8 +599,8 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     if (const char* e = std::getenv("NEO_HIP_SUBWINDOW")) h->subw = std::atoi(e) == 16 ? 16 : 8;
     if (const char* e = std::getenv("NEO_HIP_SLAB_NT")) h->snt = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_SUB")) h->asub = std::atoi(e) != 0;
-    // two-level lookahead: on by default from kFarAutoP partitions (same-box A/B, C4 P = 1875:
-    // 4200-4228 vs 3365-3747 Msamples/s; C5 P = 938: 7330-7363 vs 7081-7430, left off)
+    // two-level lookahead: on by default from kFarAutoP partitions (same-box A/B: C5 P = 938 9995 vs 7020,
+    // C4 P = 1875 5204-5244 vs 3365-3747 Msamples/s)
     h->far = partitions >= kFarAutoP;
     if (const char* e = std::getenv("NEO_HIP_FAR")) h->far = std::atoi(e) != 0;
     if (const char* e = std::getenv("NEO_HIP_AHEAD_KERNEL")) h->akern = std::atoi(e) == 1 ? 1 : 2;

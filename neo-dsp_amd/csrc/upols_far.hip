@@ -129,6 +129,7 @@ __global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(NEO_FAR_W
 {
     __shared__ cf lds[16 * 16 * 16];
     __shared__ cf z[kFarN];
+    __shared__ cf z0[kFarN];  // bin 0's Bv coefficients of the current segment
     __shared__ cf tw[kFarN];
     const int t = threadIdx.x, a = t >> 4, cp = t & 15;
     const int ng = B / 16, bg = blockIdx.x % ng, c = blockIdx.x / ng;
@@ -159,6 +160,7 @@ __global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(NEO_FAR_W
         for (int k = 0; k < 16; ++k) h[k] = far_ld(hq + int64_t(16 * k + a) * B);
 #pragma unroll
         for (int n2 = 0; n2 < 8; ++n2) nx[n2] = q < Q1 ? row(q + 1, n2) : cf{0.f, 0.f};
+        const cf b0v = b0 ? hf0[(int64_t(c) * Q1 + (q - 1)) * kFarN + t] : cf{0.f, 0.f};
         cf keep[8];
 #pragma unroll
         for (int n2 = 0; n2 < 8; ++n2) keep[n2] = v[n2];
@@ -168,6 +170,7 @@ __global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(NEO_FAR_W
 #pragma unroll
                 for (int k = 0; k < 16; ++k) z[16 * k + a] = v[k];
             }
+            z0[t] = b0v;  // the previous segment's reads of z / z0 ended before col_fft's barriers
             __syncthreads();
         }
 #pragma unroll
@@ -175,8 +178,7 @@ __global__ __launch_bounds__(kFarL) __attribute__((amdgpu_waves_per_eu(NEO_FAR_W
             const int f = 16 * k + a;
             acc[k] = cadd(acc[k], cmul(v[k], h[k]));
             if (b0 && cp == 0)
-                acc[k] = cadd(acc[k], cmul(cconj(z[(kFarN - f) & (kFarN - 1)]),
-                                           hf0[(int64_t(c) * Q1 + (q - 1)) * kFarN + f]));
+                acc[k] = cadd(acc[k], cmul(cconj(z[(kFarN - f) & (kFarN - 1)]), z0[f]));
         }
 #pragma unroll
         for (int n2 = 0; n2 < 8; ++n2) {  // segment q + 1's rows 128.. are this segment's rows 0..127

@@ -12,7 +12,7 @@
 namespace neo_hip {
 constexpr int kMaxBatch = 32;                          // most blocks one batched MAC pass consumes
 constexpr int kFarT = 128;                             // two-level lookahead: blocks per far-field window
-constexpr int kFarAutoP = 1536;                        // partitions from which it is on by default
+constexpr int kFarAutoP = 512;                         // partitions from which it is on by default
 constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch
 constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read cacheable (256 MiB Infinity Cache)
 // the lookahead / batched passes leave more of the Infinity Cache to the block steps' rows and
