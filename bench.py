@@ -8,16 +8,18 @@ At N = 1 that is one GPU's shard; at N GPUs, N x 256 channels (weak scaling; the
 channels are independent, so there is no collective on the data path — torch
 .distributed (gloo) only carries the timing barrier and the max-over-ranks).
 
-A "step" = one block of B samples through the whole convolver for every channel
-(r2c + FDL insert + partitioned MAC + c2r), inputs already resident in HBM, one
-block per call as a real-time caller runs it. The convolver's default streaming
-form is the lookahead (neo_hip_upols_set_ahead): the first block of every 32-block
-window runs one pass over filter + FDL (k_batch_mac) that also accumulates, for the
-window's later blocks, every partition whose FDL row already exists; each block then
-adds the partitions of the window's own blocks (k_upols_ahead). Every block's output
-is complete when its step returns (same latency, same products as the plain step).
-`roofline` is that window pass; `per_block_step` is the plain one-pass-per-block
-step (k_upols_step) timed in the same run; `offline` has all blocks up front.
+A "step" = one block of B samples through the whole convolver for every channel,
+inputs already resident in HBM, one block per call as a real-time caller runs it
+(block t + 1 is not given to the convolver before block t's output is complete). The
+convolver's default streaming form is the level pipeline (upols_levels.hip): every step
+runs the block step (window r2c, FDL insert, the 15 newest partitions, c2r) plus 1/T of
+the next window of each partition level, so every step does the same work and the line
+is the same at any --steps. `roofline` holds every part of the step (block step,
+Toeplitz level slices, far slice) with its HIP-event time, algorithmic bytes and share of
+the step; its top-level fields are the dominant part's. `latency` is the per-step time
+distribution, `parity` the last timed blocks against the oracle, `per_block_step` the
+plain one-pass-per-block step and `offline` the batched form (blocks up front), both
+timed in the same run; `c2_fft` the 4096 x 65536 batched FFT.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c4|c3|c2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -52,12 +54,14 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=128)  # 4 lookahead windows of 32 blocks
+    ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS) + ["c2"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ahead", action="store_true", help="headline = the plain one-pass-per-block step")
     ap.add_argument("--no-offline", action="store_true", help="skip the batched (blocks up front) line")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed output")
+    ap.add_argument("--no-fft", action="store_true", help="skip the c2_fft sub-object of UPOLS runs")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--host-io", action="store_true",
                     help="time the host-buffer boundary (neo_hip_upols_process on pinned-staged host memory): "
@@ -110,16 +114,31 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def code_tag() -> str:
+    """Hash of the kernel sources: PMC summaries count only for the code they measured."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha1()
+    for path in sorted(glob.glob(os.path.join(REPO, "neo-dsp_amd", "csrc", "*.[hc]*"))):
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:12]
+
+
 def load_pmc_traffic(workload: str, kernel: str = ""):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 --pmc summary
-    for `workload` (separate passes; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    """HBM bytes per launch (per step for the streaming parts) of `kernel` from a committed
+    rocprofv3 --pmc summary (tools/pmc_summary.py) for `workload` measured on THIS code
+    (same code_tag), or None."""
     import glob
 
+    tag = code_tag()
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            if d.get("workload") == workload and kernel in d.get("kernel", "") and d.get("hbm_bytes_per_launch"):
+            if (d.get("code_tag") == tag and d.get("workload") == workload and kernel in d.get("kernel", "")
+                    and d.get("hbm_bytes_per_launch")):
                 return float(d["hbm_bytes_per_launch"])
         except (OSError, ValueError):
             continue
@@ -127,7 +146,7 @@ def load_pmc_traffic(workload: str, kernel: str = ""):
 
 
 def timing_stride(steps: int) -> int:
-    """Time every n-th MAC launch of the timed region: >= 12 samples, at most every 16th."""
+    """Time every n-th step of the timed region: >= 12 samples, at most every 16th."""
     return max(1, min(16, steps // 12))
 
 
@@ -196,7 +215,65 @@ def device_for(local: int) -> int:
     return local % max(1, torch.cuda.device_count())
 
 
+class Feed:
+    """Feeds the convolver the blocks of a cyclic input x [C][NX*B] (block g of the stream is
+    block g mod NX of x; outputs land in y at the same place), so that the input history of
+    any output block is known — the parity check replays it through the oracle."""
+
+    def __init__(self, conv, x, y, nx, B, stream):
+        self.conv, self.x, self.y, self.nx, self.B, self.stream = conv, x, y, nx, B, stream
+        self.ld = nx * B
+        self.g = 0  # blocks processed so far
+
+    def run(self, n):
+        while n > 0:
+            i = self.g % self.nx
+            k = min(n, self.nx - i)
+            off = 4 * i * self.B
+            self.conv.process_blocks_ptr(self.x.data_ptr() + off, self.y.data_ptr() + off, self.ld, k, self.stream)
+            self.g += k
+            n -= k
+
+
+def algorithmic_bytes(C, B, P, plan):
+    """Algorithmic bytes per streaming step, per part:
+    block step: in + previous block read + write + out (4 x 4B) + FDL row write and H0 (2 x 8B)
+                + a0 - 1 filter/FDL row pairs (16B each) + one slab per level (8B)
+    Toeplitz level l (window T, band [a, b)), C*B/T columns per step: per column b - a filter
+                rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
+    far level, C*B/128 columns per step: per column 256 FDL rows, 256 stored + nseg - 1 older
+                row-pair spectra, nseg segment spectra (256 f each) and 128 far-field entries."""
+    nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
+    block = C * B * (16 + 16 + 16 * (plan["a0"] - 1) + 8 + 8 * nlev)
+    toep = sum(C * B / T * 8 * (2 * (b - a) + 2 * T - 1) for T, a, b in zip(plan["T"], plan["a"], plan["b"]))
+    ns = plan["nseg"]
+    far = C * B / 128 * 8 * (256 * (2 * ns + 1) + 128) if ns else 0.0
+    return block, toep, far
+
+
+def oracle_parity(x, y, feed, irh, B, chans, K=4, threads=16):
+    """Peak-normalized error of the last K processed blocks of channels `chans` against the
+    oracle's dense_convolve over their full input history (the P + 1 blocks before them: an
+    output block depends on no older input, fdl_index.hpp:23-36)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    P = O.uniform_partition(irh[:1], B).shape[1]
+    G = feed.g
+    start = max(0, G - K - P - 1)
+    idx = [g % feed.nx for g in range(start, G)]
+    worst = 0.0
+    for c in chans:
+        xc = x[c].view(feed.nx, B)[idx].cpu().numpy().reshape(1, -1)
+        yc = y[c].view(feed.nx, B)[idx[-K:]].cpu().numpy().reshape(-1)
+        ref = O.dense_convolve(xc, O.uniform_partition(irh[c:c + 1], B), threads=threads)[0, -K * B:]
+        worst = max(worst, float(np.abs(yc - ref).max() / np.abs(ref).max()))
+    return worst
+
+
 def run_upols(args, world, rank, local):
+    import numpy as np
     import torch
     import neo
 
@@ -207,84 +284,114 @@ def run_upols(args, world, rank, local):
     P = neo.num_partitions(L, B)
     conv = neo.UpolsConvolver(C, B, P, device=local)
     conv.set_batch(False)  # streaming: one block per step, as a real-time caller runs it
+    levels = conv.ahead_info()[0] and not args.no_ahead
+    plan = neo.convolution.level_plan(P)
     g = torch.Generator(device=dev).manual_seed(8 + rank)
     ir = torch.rand((C, L), generator=g, device=dev).mul_(2).sub_(1)  # synthetic white-noise IR
+    irh = ir.cpu().numpy() if (rank == 0 and not args.no_parity) else None
     conv.set_impulse(ir, normalize=True)
     del ir
-    nblk = max(args.warmup, 1) + args.steps
-    x = torch.rand((C, nblk * B), generator=g, device=dev).mul_(2).sub_(1)
+    nx = P + 192  # cyclic input: covers the parity check's history window (P + 5 blocks)
+    x = torch.rand((C, nx * B), generator=g, device=dev).mul_(2).sub_(1)
     y = torch.empty_like(x)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    ld = x.shape[1]
-    xp, yp = x.data_ptr(), y.data_ptr()
+    feed = Feed(conv, x, y, nx, B, stream)
+    stride = timing_stride(args.steps)
 
-    # the block loop runs in the C-ABI (neo_hip_upols_process_blocks), one step = one block
-    wb = max(args.warmup, 1)
-    off = 4 * wb * B  # timed blocks follow the warm-up blocks
+    def warm():
+        t_warm = time.perf_counter()
+        feed.run(max(args.warmup, 1))
+        torch.cuda.synchronize()
+        while time.perf_counter() - t_warm < WARM_SECONDS:  # untimed
+            feed.run(64)
+            torch.cuda.synchronize()
 
     def timed_steps():
-        """Warm up, then time args.steps single-block steps; MAC-kernel duration from HIP
-        events recorded on the launch stream around every n-th MAC launch of the timed
-        steps (the C-ABI's timing mode; sampled so that the event records stay a small
-        part of a launch-bound step like C3's)."""
-        t_warm = time.perf_counter()
-        conv.process_blocks_ptr(xp, yp, ld, wb, stream)
-        torch.cuda.synchronize()
-        while time.perf_counter() - t_warm < WARM_SECONDS:  # untimed; re-runs the warm-up blocks
-            conv.process_blocks_ptr(xp, yp, ld, wb, stream)
-            torch.cuda.synchronize()
-        if conv.ahead_info()[0]:
-            conv.set_ahead(True)  # the timed steps start a lookahead window (phase 0)
+        """args.steps single-block steps; per-part kernel time from HIP events the C-ABI
+        records on the launch stream around every `stride`-th step."""
         barrier(world)
         torch.cuda.synchronize()
-        conv.timing()  # drain
-        conv.set_timing(True, every=timing_stride(args.steps))
+        conv.timing_detail()  # drain
+        conv.set_timing(True, every=stride)
         t0 = time.perf_counter()
-        conv.process_blocks_ptr(xp + off, yp + off, ld, args.steps, stream)
+        feed.run(args.steps)
         torch.cuda.synchronize()
         barrier(world)
         t1 = time.perf_counter()
         conv.set_timing(False)
-        mac_ms, launches = conv.timing()
-        assert torch.isfinite(y[:, wb * B:]).all().item()
-        return max_over_ranks(t1 - t0, world), max_over_ranks(mac_ms / max(launches, 1), world)
+        det = [(ms / n if n else None) for ms, n in conv.timing_detail()]
+        assert torch.isfinite(y).all().item()
+        return max_over_ranks(t1 - t0, world), [max_over_ranks(d, world) if d is not None else None for d in det]
 
     samples = world * C * B * args.steps
-    bytes_step = C * (16 * P * B + 20 * B)  # filter + FDL stream (packed bins) + FDL row write + in/prev
     # the plain single-block step: one pass over filter + FDL per block (k_upols_step)
     conv.set_ahead(False)
-    el_plain, mac_plain = timed_steps()
-    gbs_plain = bytes_step / (mac_plain * 1e-3) / 1e9
+    warm()
+    el_plain, det_plain = timed_steps()
+    bytes_plain = C * (16 * P * B + 20 * B)  # filter + FDL stream (packed bins) + FDL row write + in/prev
+    gbs_plain = bytes_plain / (det_plain[0] * 1e-3) / 1e9
     plain = {"value": samples / el_plain / 1e6, "ms_per_step": el_plain * 1e3 / args.steps,
-             "kernel": f"k_upols_step<{B}>", "kernel_avg_ms": mac_plain, "algorithmic_bytes_per_launch": bytes_step,
+             "kernel": f"k_upols_step<{B}>", "kernel_avg_ms": det_plain[0], "algorithmic_bytes_per_launch": bytes_plain,
              "achieved_gbs": gbs_plain, "frac": gbs_plain / PEAK_HBM_GBS,
              "traffic": load_pmc_traffic(args.workload + "_plain", "k_upols_step")}
-    ahead, _, T, sb = conv.ahead_info()
-    ahead = not args.no_ahead
-    conv.set_ahead(ahead)
-    if ahead:
-        # streaming lookahead (the default): one k_batch_mac pass per T-block window over
-        # filter + FDL that also accumulates every partition already available for the
-        # window's later blocks; each block step (k_upols_ahead) adds the rest
-        elapsed, mac_avg_ms = timed_steps()
-        # two-level lookahead (upols_far.hip; default from 512 partitions, NEO_HIP_FAR overrides):
-        # the window pass walks partitions < 128; k_far_mac takes the rest once per 128 blocks
-        far_env = os.environ.get("NEO_HIP_FAR")
-        far = P > 128 and (far_env != "0" if far_env is not None and far_env != "" else P >= 512)
-        if far and args.steps % 128:
-            print(f"bench: two-level lookahead on and --steps {args.steps} is not a multiple of 128: "
-                  "the timed region holds a partial far-window share", file=sys.stderr)
-        P1 = 128 if far else P
-        bytes_mac = C * 8 * B * (2 * P1 + sb * T)  # filter rows + FDL rows read, T partial slabs per split written
-        kernel = f"k_batch_mac<{B},{T},1> (lookahead window pass, 1 per {T} blocks" + \
-            (", partitions < 128; far field: k_far_mac once per 128 blocks)" if far else ")")
-        steps_per_launch = T
+    if levels:
+        conv.set_ahead(True)
+    warm()
+    elapsed, det = timed_steps()
+    parity = None
+    if irh is not None:
+        irn = None
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+
+        irn = O.normalize_impulse(irh)
+        parity = {"parity_err": oracle_parity(x, y, feed, irn, B, sorted({0, C // 2, C - 1}), threads=args.cpu_threads),
+                  "channels": sorted({0, C // 2, C - 1}), "blocks": 4,
+                  "what": "last 4 blocks of the timed region vs oracle dense_convolve over their input history "
+                          "(peak-normalized; bar 1e-5)"}
+    # per-step latency: every step of a separate 256-step run bracketed by events (GPU time of the
+    # step, first to last event), the distribution a per-block real-time caller sees
+    conv.step_times()
+    conv.set_timing(True, every=1)
+    feed.run(256)
+    torch.cuda.synchronize()
+    conv.set_timing(False)
+    st = np.array(conv.step_times())
+    latency = {"steps": int(st.size), "mean_ms": float(st.mean()), "p50_ms": float(np.percentile(st, 50)),
+               "p99_ms": float(np.percentile(st, 99)), "max_ms": float(st.max()),
+               "max_over_mean": float(st.max() / st.mean()),
+               "note": "GPU time per step (HIP events around every step, which add their own records)"}
+
+    if levels:
+        bs, tp, fr = algorithmic_bytes(C, B, P, plan)
+        parts = [("block step k_upols_lvl<%d>" % B, det[0], bs),
+                 ("Toeplitz level slices k_lvl_toep (T = %s)" % "/".join(map(str, plan["T"])), det[1], tp),
+                 ("far slice k_lvf_slice (%d segments)" % plan["nseg"], det[2], fr)]
+        step_ms = det[3]
+        kernels = []
+        for name, ms, by in parts:
+            if not by:
+                continue
+            gbs = by / (ms * 1e-3) / 1e9
+            kernels.append({"kernel": name, "ms_per_step": ms, "share_of_step": ms / step_ms,
+                            "algorithmic_bytes_per_step": by, "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS,
+                            "traffic": load_pmc_traffic(args.workload, name.split()[-2] if "(" in name else name)})
+        dom = max(kernels, key=lambda k: k["ms_per_step"])
+        step_bytes = bs + tp + fr
+        roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
+                "kernel_avg_ms": dom["ms_per_step"], "steps_per_launch": 1,
+                "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_step"],
+                "step": {"ms": step_ms, "algorithmic_bytes": step_bytes,
+                         "achieved_gbs": step_bytes / (step_ms * 1e-3) / 1e9,
+                         "frac": step_bytes / (step_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+                "kernels": kernels, "d2d_copy_gbs": copy_ceiling_gbs(dev)}
     else:
-        elapsed, mac_avg_ms, bytes_mac, kernel, steps_per_launch = el_plain, mac_plain, bytes_step, plain["kernel"], 1
-    achieved = bytes_mac / (mac_avg_ms * 1e-3) / 1e9
-
-    offline = run_upols_offline(args, conv, C, B, P, xp, yp, ld, stream, world)
-
+        roof = {"bound": "hbm", "achieved": gbs_plain, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": gbs_plain / PEAK_HBM_GBS, "traffic": plain["traffic"], "kernel": plain["kernel"],
+                "kernel_avg_ms": det_plain[0], "steps_per_launch": 1, "algorithmic_bytes_per_launch": bytes_plain,
+                "d2d_copy_gbs": copy_ceiling_gbs(dev)}
+    offline = run_upols_offline(args, conv, C, B, P, x, y, nx * B, stream, world)
     res = {
         "metric": "Msamples/sec UPOLS convolver (block=512, IR=10s@48k); achieved HBM GB/s",
         "value": samples / elapsed / 1e6,
@@ -301,49 +408,43 @@ def run_upols(args, world, rank, local):
         "config": {"workload": f"UPOLS {args.workload}: {C} ch/GPU x {world} GPU, B={B}, L={L} taps (P={P}), "
                                f"channel-sharded, one block per step",
                    "channels_per_gpu": C, "channels_total": C * world, "block": B, "taps": L, "partitions": P,
-                   "splits": sb if ahead else conv.splits, "lookahead_window": T if ahead else 1,
+                   "streaming": ("levels: block step p<%d, Toeplitz %s, far %d segments" %
+                                 (plan["a0"], list(zip(plan["T"], plan["a"], plan["b"])), plan["nseg"])
+                                 if levels else "plain step"),
                    "parallelism": f"channel-shard x{world} (no collective)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS,
-                     "traffic": (load_pmc_traffic(args.workload, "k_batch_mac") if ahead
-                                 else load_pmc_traffic(args.workload + "_plain", "k_upols_step")),
-                     "kernel": kernel, "kernel_avg_ms": mac_avg_ms, "steps_per_launch": steps_per_launch,
-                     "algorithmic_bytes_per_launch": bytes_mac, "d2d_copy_gbs": copy_ceiling_gbs(dev)},
+        "roofline": roof,
+        "latency": latency,
+        "parity": parity,
         "per_block_step": plain,
         "offline": offline,
     }
-    if ahead:
-        # the window pass is also an fp32 FMA stream: 8 flop per complex MAC, T blocks per pass
-        tflops = 8.0 * C * P * B * T / (mac_avg_ms * 1e-3) / 1e12
-        res["roofline"]["valu"] = {"achieved_tflops": tflops, "peak_tflops": PEAK_FP32_TFLOPS, "frac": tflops / PEAK_FP32_TFLOPS,
-                                   "note": "packed-FMA peak at 2.4 GHz; the pass holds 1.6-1.7 GHz (DESIGN.md section 5)"}
     if args.workload == "c3":
         res["roofline"]["note"] = "working set L2/MALL-resident: effective GB/s, launch-latency bound"
     return res
 
 
-def run_upols_offline(args, conv, C, B, P, xp, yp, ld, stream, world):
+def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world):
     """Same convolver and input, blocks available up front (dense_convolve / process_blocks):
     T blocks share one pass over the filter and the FDL. Not the headline (which is the
-    real-time one-block-per-pass step); reported beside it."""
+    real-time one-block-per-pass step); reported beside it. 128 blocks per timed run."""
     import torch
 
+    if args.no_offline:
+        return None
     conv.set_batch(True)
     T, splits = conv.batch_info()
-    nb = (args.steps // T) * T
-    if nb == 0 or args.no_offline:
-        conv.set_batch(False)
-        return None
+    nb = 128
+    conv.reset()
     t_warm = time.perf_counter()
     while time.perf_counter() - t_warm < WARM_SECONDS:
-        conv.process_blocks_ptr(xp, yp, ld, nb, stream)
+        conv.process_blocks_ptr(x.data_ptr(), y.data_ptr(), ld, nb, stream)
         torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     conv.timing()
     conv.set_timing(True)
     t0 = time.perf_counter()
-    conv.process_blocks_ptr(xp, yp, ld, nb, stream)
+    conv.process_blocks_ptr(x.data_ptr(), y.data_ptr(), ld, nb, stream)
     torch.cuda.synchronize()
     barrier(world)
     t1 = time.perf_counter()
@@ -358,8 +459,7 @@ def run_upols_offline(args, conv, C, B, P, xp, yp, ld, stream, world):
     return {"value": world * C * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": T,
             "traffic": traffic, "traffic_over_algorithmic": traffic / bytes_pass if traffic else None,
             "ms_per_block": elapsed * 1e3 / nb, "splits": splits, "kernel": f"k_batch_mac<{B},{T},1>",
-            "algorithmic_bytes_per_launch": bytes_pass,
-            "kernel_avg_ms": mac_avg_ms,
+            "algorithmic_bytes_per_launch": bytes_pass, "kernel_avg_ms": mac_avg_ms,
             "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS}
 
 
@@ -456,6 +556,12 @@ def main():
         args.no_cpu_baseline = True
     else:
         res = run_upols(args, world, rank, local)
+        if not args.no_fft:
+            import argparse as _ap
+
+            f = run_fft(_ap.Namespace(steps=20, warmup=5), world, rank, local)
+            res["c2_fft"] = {"value": f["value"], "unit": f["unit"], "ms_per_step": f["ms_per_step"],
+                             "metric": f["metric"], "roofline": f["roofline"]}
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             C, B, L = WORKLOADS.get(args.workload, (0, 0, 0))

@@ -93,6 +93,19 @@ NEO_HIP_API int neo_hip_upola_create(int channels, int block, int partitions, in
  * window state (the irfft result is written back into the real window, :114). Whole
  * blocks through the other process calls behave like neo_hip_upola_create. */
 NEO_HIP_API int neo_hip_upola2_create(int channels, int block, int partitions, int device, neo_hip_upols** h);
+/* Any of the three with explicit choices instead of the shape-based defaults
+ * (method 0 = upols, 1 = upola, 2 = upola v2; opts NULL = all defaults). Results are the
+ * same for every choice up to float summation order; they exist so that every code path
+ * can be exercised and timed on any shape. */
+typedef struct neo_hip_upols_opts {
+    int fused;            /* plain step: -1 auto (one launch below 64 MiB of filter + FDL), 0 MAC + finish, 1 one launch */
+    int split_workgroups; /* plain step: 0 auto (1024 workgroups), else the workgroup target for its partition splits */
+    int batch_blocks;     /* batched passes: 0 auto (32), else blocks per pass (power of two, 2..32) */
+    int batch_bins;       /* batched passes: 0 auto (1), else bins per lane vector (1 or 2) */
+    int levels;           /* single-block steps: -1 auto (streaming levels from 64 partitions), 0 plain step, 1 levels */
+} neo_hip_upols_opts;
+NEO_HIP_API int neo_hip_upols_create_ex(int channels, int block, int partitions, int device, int method,
+                                        const neo_hip_upols_opts* opts, neo_hip_upols** h);
 NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h);
 /* filter [C][P][B+1] complex (uniform_partition layout), host or device memory;
  * like uniform_partitioned_convolver::filter() it also resets all state. */
@@ -128,22 +141,34 @@ NEO_HIP_API int neo_hip_upols_batch_info(neo_hip_upols* h, int* blocks_per_pass,
 NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in, int64_t ld_in, float* out,
                                               int64_t ld_out, int64_t num_samples, int is_device, void* stream);
 NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
-/* Streaming lookahead for single-block steps (upols / upola): the first block of
- * each T-block window runs one batched pass over the filter and the FDL that also
- * accumulates every partition already available for the window's later blocks;
- * each block then adds only the partitions of the window's own blocks. Output is
- * the same block by block (summation order differs), latency stays one block.
- * Default on where a step is HBM-bound (not the one-launch form); v2 handles
- * refuse it. Switching is allowed at any block boundary. */
+/* Streaming levels for single-block steps (upols / upola; upols_levels.hip): the
+ * partitions are cut into bands (block step p < 16; Toeplitz windows of 8 / 16 / 32 blocks
+ * for [16, 32) / [32, 64) / [64, 256); a 128-block partition-axis transform for
+ * [256, P)); every band's contribution to the blocks of its next window is computed
+ * during the current window, 1/T of the bins per block step, so every call does the
+ * same work. Output is the same block by block (summation order differs), latency stays
+ * one block. Default on from 64 partitions (B <= 1024); v2 handles refuse it. Switching
+ * is allowed at any block boundary (the next step computes the current windows whole). */
 NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable);
-/* enabled, block position in the current window, window length T, splits of the pass */
+/* enabled, block position in the current far window, longest window, number of levels */
 NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* phase, int* window, int* splits);
-/* MAC-kernel timing with HIP events recorded on the launch stream (for the
- * roofline in bench.py): enable = n > 0 brackets every n-th MAC launch with an
- * event pair (0 = off); timing() returns the summed ms and the count of timed
- * launches. */
+/* The level plan for `partitions` (no device needed): the block step takes [0, a0);
+ * Toeplitz level l < nlevels has a window of T[l] blocks and the band [a[l], b[l]);
+ * nseg far segments of 128 partitions from 256 (arrays of >= 3 entries). */
+NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, int* T, int* a, int* b, int* nseg);
+/* Kernel timing with HIP events recorded on the launch stream (for the roofline in
+ * bench.py): enable = n > 0 brackets every n-th launch group with events (0 = off).
+ * timing() returns the summed ms of the bracketed part and the count of timed groups:
+ * the MAC kernel of a plain or batched step, the whole step of a streaming-level step.
+ * timing_detail() returns per part (ms[4], launches[4]): streaming steps 0 = block
+ * step, 1 = Toeplitz level slices, 2 = far slice, 3 = whole step; plain / batched steps
+ * 0 = MAC kernel. Both drain the events. */
 NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable);
 NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches);
+NEO_HIP_API int neo_hip_upols_timing_detail(neo_hip_upols* h, double* ms, int64_t* launches);
+/* the duration of every timed launch group in order (first to last event; a streaming
+ * step: the whole step), up to cap into ms; count = groups recorded. Drains the events. */
+NEO_HIP_API int neo_hip_upols_step_times(neo_hip_upols* h, double* ms, int64_t cap, int64_t* count);
 NEO_HIP_API int neo_hip_upols_info(neo_hip_upols* h, int* channels, int* block, int* partitions, int* splits);
 
 /* -- setup path (uniform_partition.hpp:12-26, normalize_impulse.hpp:11-33) -- */

@@ -384,18 +384,15 @@ int reset_state(upols_t* h, hipStream_t s)
     }
     h->wpos = 0;
     h->in_pos = 0;
-    h->phase = 0;
-    h->fwin = -1;
+    h->lv_n = -1;  // streaming levels re-prime at the next step
     return NEO_HIP_OK;
 }
 
 void destroy(upols_t* h)
 {
     if (!h) return;
-    for (auto& e : h->events) {
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
-    }
+    for (auto& g : h->events)
+        for (auto& e : g.e) (void)hipEventDestroy(e);
     (void)hipFree(h->H);  // the FDL shares H's allocation (rows [nrows, 2 nrows))
     (void)hipFree(h->part);
     (void)hipFree(h->prev);
@@ -407,14 +404,8 @@ void destroy(upols_t* h)
     if (h->io_host) (void)hipHostFree(h->io_host);
     (void)hipFree(h->samples_dev);
     (void)hipFree(h->part_b);
-    (void)hipFree(h->part_s);
-    (void)hipFree(h->h0t);
-    (void)hipFree(h->h0tail);
     (void)hipFree(h->tail);
-    (void)hipFree(h->hf);
-    (void)hipFree(h->hf0);
-    (void)hipFree(h->ff);
-    (void)hipFree(h->twf);
+    lvl_free(h);
     if (h->samples_host) (void)hipHostFree(h->samples_host);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -422,18 +413,10 @@ void destroy(upols_t* h)
 
 int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
-    if (h->ahead) return launch_ahead(h, in, ld_in, out, ld_out, s);
-    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    const bool timed = h->timing && h->tick++ % h->timing == 0;
-    if (timed) {
-        if (h->events_used == h->events.size()) {
-            NEO_HIP_CHECK(hipEventCreate(&ev.first));
-            NEO_HIP_CHECK(hipEventCreate(&ev.second));
-            h->events.push_back(ev);
-        }
-        ev = h->events[h->events_used];
-        NEO_HIP_CHECK(hipEventRecord(ev.first, s));
-    }
+    if (h->ahead) return launch_levels(h, in, ld_in, out, ld_out, s);
+    upols_t::ev_group* ev = nullptr;
+    if (int rc = timing_begin(h, 2, &ev)) return rc;
+    if (int rc = timing_mark(ev, 0, s)) return rc;
     const unsigned grid = unsigned(h->C) * unsigned(h->S);
 #define NEO_STEP(FU, OL)                                                                                      \
     NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, FU, OL>), dim3(grid), dim3(256), 0, s, in, ld_in, \
@@ -447,10 +430,7 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
     }
 #undef NEO_STEP
     NEO_HIP_LAUNCH_CHECK();
-    if (timed) {
-        NEO_HIP_CHECK(hipEventRecord(ev.second, s));
-        ++h->events_used;
-    }
+    if (int rc = timing_mark(ev, 1, s)) return rc;
     if (!h->fused) {
         if (h->ola) {
             NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_finish<BB, true>), dim3(unsigned(h->C)), dim3(256), 0,
@@ -462,6 +442,7 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
         NEO_HIP_LAUNCH_CHECK();
     }
     h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;  // fdl_index.hpp:35-37
+    h->lv_n = -1;
     return NEO_HIP_OK;
 }
 
@@ -469,6 +450,7 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
 int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int n, hipStream_t s)
 {
     const int sum_first = h->in_pos == 0;
+    h->lv_n = -1;
     if (sum_first) {  // tail MAC over partitions p >= 1 into the split slabs
         const unsigned grid = unsigned(h->C) * unsigned(h->S);
         NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, false, true, true>), dim3(grid), dim3(256), 0, s,
@@ -511,7 +493,7 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
         // the largest power-of-two batch (<= T) of whole blocks left, one pass over H + FDL
         int tb = 1;
         while (tb * 2 <= T && n - done >= int64_t(tb) * 2 * B) tb *= 2;
-        if (h->in_pos == 0 && h->phase == 0 && tb > 1 && a16 && done % 4 == 0) {
+        if (h->in_pos == 0 && tb > 1 && a16 && done % 4 == 0) {
             rc = launch_batch(h, ip, ld_in, op, ld_out, tb, s);
             done += int64_t(tb) * B;
         } else if (!h->v2) {
@@ -535,9 +517,15 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
 
 
 namespace {
-int create_convolver(int channels, int block, int partitions, int device, bool ola, bool v2, neo_hip_upols** out)
+int create_convolver(int channels, int block, int partitions, int device, bool ola, bool v2,
+                     const neo_hip_upols_opts* opt, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
+    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1};
+    if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.split_workgroups < 0 ||
+        (o.batch_blocks && (o.batch_blocks < 2 || o.batch_blocks > kMaxBatch || (o.batch_blocks & (o.batch_blocks - 1)))) ||
+        o.batch_bins < 0 || o.batch_bins > 2)
+        return fail(NEO_HIP_EINVAL, "invalid convolver options");
     *out = nullptr;
     if (channels < 1) return fail(NEO_HIP_EINVAL, "channels must be >= 1");
     if (!valid_block(block)) return fail(NEO_HIP_EINVAL, "block must be a power of two in [16, 4096], got %d", block);
@@ -550,28 +538,24 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->B = block;
     h->P = partitions;
     h->ring = partitions + kMaxBatch - 1;
-    if (const char* e = std::getenv("NEO_HIP_RING_EXTRA"))  // A/B: ring rows beyond P
-        h->ring = partitions + std::max(0, std::min(kMaxBatch - 1, std::atoi(e)));
+    plan_levels(partitions, h->lv);
+    if (h->lv.nseg) h->ring = std::max(h->ring, kFarRing);  // far slices read 383 blocks back
     h->ola = ola || v2;
     h->v2 = v2;
     h->fused = 2.0 * 8.0 * double(channels) * double(partitions) * double(block) < double(kFusedMaxBytes);
-    if (const char* e = std::getenv("NEO_HIP_FUSED")) h->fused = std::atoi(e) != 0;
+    if (o.fused >= 0) h->fused = o.fused != 0;
+    if (o.batch_blocks) h->bT = o.batch_blocks;
+    if (o.batch_bins) h->bNB = o.batch_bins;
     // filter rows kept resident in the Infinity Cache across steps: the first pc rows of
     // every channel are read with the default policy, ~216 MiB in all (A/B on MI355X: C5
     // 0.302 -> 0.286 ms per MAC at 220 rows, C4 0.295 -> 0.282 at 400; past ~250 MiB
     // the cached rows start evicting each other)
     h->pc = int(std::min<double>(partitions, kCacheBudgetBytes / (double(channels) * block * sizeof(cf))));
-    if (const char* e = std::getenv("NEO_HIP_CACHE_ROWS")) h->pc = std::max(0, std::atoi(e));
     h->cstride = int64_t(h->ring) * block;
     h->pstride = block;
-    if (const char* e = std::getenv("NEO_HIP_LAYOUT"); e && std::string(e) == "pcb") {
-        h->cstride = block;
-        h->pstride = int64_t(channels) * block;
-    }
     // splits per channel: aim for ~1024 workgroups (4 per CU, all resident at 8 waves/SIMD;
     // A/B on MI355X: 1024 beat 512/768/2048/4096 at C4 and C5), <= 64 partial slabs
-    int target = 1024;
-    if (const char* e = std::getenv("NEO_HIP_SPLIT_WGS")) target = std::max(1, std::atoi(e));
+    const int target = o.split_workgroups ? o.split_workgroups : 1024;
     // >= 8 rows per split keeps the slab sum short at small C; the one-launch (latency) form
     // takes >= 16 (C3: 12 splits, 9.6 vs 10.6 us per block with 24)
     const int min_rows = h->fused ? 16 : 8;
@@ -580,45 +564,21 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->S = (partitions + h->rows - 1) / h->rows;
     // batched passes: same workgroup target, >= 2T partitions per split so the sliding FDL
     // window's warm-up (T - 1 extra rows per split) stays under half the split's rows
-    if (const char* e = std::getenv("NEO_HIP_BATCH_T")) h->bT = std::max(2, std::min(kMaxBatch, std::atoi(e)));
-    if (const char* e = std::getenv("NEO_HIP_BATCH_NB")) h->bNB = std::atoi(e) == 1 ? 1 : 2;
-    if (const char* e = std::getenv("NEO_HIP_BATCH_VAR")) h->bvar = std::max(0, std::min(5, std::atoi(e)));
-    if (h->bvar == 3 && (int64_t(h->ring - 1) * h->pstride + block) * int64_t(sizeof(cf)) >= (int64_t(1) << 31))
-        h->bvar = 2;  // buffer-load rows need one channel's span below 2 GiB
-    // LDS-DMA variants: one descriptor spans a channel's H rows up to its FDL rows
-    if (h->bvar >= 4 && (int64_t(channels) * h->ring * block + int64_t(h->ring) * h->pstride) * int64_t(sizeof(cf)) >=
-                            (int64_t(1) << 31))
-        h->bvar = 2;
+    h->bufload = (int64_t(h->ring - 1) * h->pstride + block) * int64_t(sizeof(cf)) < (int64_t(1) << 31);
     h->pcb = int(std::min<double>(partitions, kBatchCacheBudgetBytes / (double(channels) * block * sizeof(cf))));
-    if (const char* e = std::getenv("NEO_HIP_BATCH_CACHE_ROWS")) h->pcb = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("NEO_HIP_SUB_SPLIT")) h->ssplit = std::atoi(e) != 0;
-    if (const char* e = std::getenv("NEO_HIP_BATCH_PRIO")) h->bprio = std::max(0, std::min(95, std::atoi(e)));
-    if (const char* e = std::getenv("NEO_HIP_AHEAD_DIRECT")) h->adirect = std::atoi(e) != 0 ? 2 : 0;
-    if (const char* e = std::getenv("NEO_HIP_BATCH8_VAR")) h->b8var = std::atoi(e) == 3 ? 3 : 0;
-    h->subw = block >= 512 ? 16 : 8;
-    if (const char* e = std::getenv("NEO_HIP_SUBWINDOW")) h->subw = std::atoi(e) == 16 ? 16 : 8;
-    if (const char* e = std::getenv("NEO_HIP_SLAB_NT")) h->snt = std::atoi(e) != 0;
-    if (const char* e = std::getenv("NEO_HIP_AHEAD_SUB")) h->asub = std::atoi(e) != 0;
-    // two-level lookahead: on by default from kFarAutoP partitions (same-box A/B: C5 P = 938 9995 vs 7020,
-    // C4 P = 1875 5204-5244 vs 3365-3747 Msamples/s)
-    h->far = partitions >= kFarAutoP;
-    if (const char* e = std::getenv("NEO_HIP_FAR")) h->far = std::atoi(e) != 0;
-    if (const char* e = std::getenv("NEO_HIP_AHEAD_KERNEL")) h->akern = std::atoi(e) == 1 ? 1 : 2;
     // batched MAC: 256-lane workgroups at 2 waves/SIMD -> 2 resident per CU, so 512 fills the
     // chip once with no second round (A/B, bmac_var 3: C5 0.409 -> 0.367 ms per pass, C4 0.369
     // -> 0.379 ms, within run-to-run spread)
-    int btarget = 512;
-    if (const char* e = std::getenv("NEO_HIP_BATCH_WGS")) btarget = std::max(1, std::atoi(e));
+    const int btarget = 512;
     const int bt = batch_t(block, h->bNB, h->bT);
     // workgroups per (channel, split): the batched MAC has one lane per bin, <= 256 lanes
     const int bgroups = std::max(1, block / h->bNB / 256);
     int Sb = std::max(1, std::min({(btarget + channels * bgroups - 1) / (channels * bgroups), partitions / (2 * bt), 64}));
     if (h->ring - partitions < bt - 1) h->batch = false;  // ring too short for a batch
-    // streaming lookahead: one filter + FDL pass per T-block window instead of per block
-    // (MI355X, 1 block per step: C5 0.286 -> 0.024 ms, C4 0.285 -> 0.021, C3 10.0 -> 7.8 us);
-    // short filters (P < 2T) keep the plain step, whose one pass is already small
-    h->ahead = !v2 && h->batch && partitions >= 2 * bt;
-    if (const char* e = std::getenv("NEO_HIP_AHEAD")) h->ahead = std::atoi(e) != 0 && !v2 && h->batch;
+    // streaming levels (upols_levels.hip) instead of one pass over filter + FDL per block,
+    // from 64 partitions, blocks up to 1024; short filters keep the plain step, whose one pass
+    // is already small (its working set sits in the Infinity Cache)
+    h->ahead = !v2 && block <= 1024 && (o.levels >= 0 ? o.levels != 0 : partitions >= 64);
     h->rows_b = ((partitions + Sb - 1) / Sb + kMaxBatch - 1) / kMaxBatch * kMaxBatch;  // whole chunks of any T
     h->Sb = (partitions + h->rows_b - 1) / h->rows_b;
     const size_t rowbytes = size_t(block) * sizeof(cf);
@@ -654,17 +614,24 @@ extern "C" {
 
 NEO_HIP_API int neo_hip_upols_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
 {
-    return create_convolver(channels, block, partitions, device, false, false, out);
+    return create_convolver(channels, block, partitions, device, false, false, nullptr, out);
 }
 
 NEO_HIP_API int neo_hip_upola_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
 {
-    return create_convolver(channels, block, partitions, device, true, false, out);
+    return create_convolver(channels, block, partitions, device, true, false, nullptr, out);
 }
 
 NEO_HIP_API int neo_hip_upola2_create(int channels, int block, int partitions, int device, neo_hip_upols** out)
 {
-    return create_convolver(channels, block, partitions, device, true, true, out);
+    return create_convolver(channels, block, partitions, device, true, true, nullptr, out);
+}
+
+NEO_HIP_API int neo_hip_upols_create_ex(int channels, int block, int partitions, int device, int method,
+                                        const neo_hip_upols_opts* opts, neo_hip_upols** out)
+{
+    if (method < 0 || method > 2) return fail(NEO_HIP_EINVAL, "method must be 0 (upols), 1 (upola) or 2 (upola v2)");
+    return create_convolver(channels, block, partitions, device, method >= 1, method == 2, opts, out);
 }
 
 NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h)
@@ -713,8 +680,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
         src = tmp;
     }
     int rc = pack_filter(h, src, h->stream);
-    if (!rc) rc = update_head(h, h->stream);
-    if (!rc) rc = far_filter(h, h->stream);
+    lvl_filter_changed(h);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     if (tmp) (void)hipFree(tmp);
@@ -740,8 +706,7 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
         rc = fail(NEO_HIP_ERUNTIME, "impulse copy failed");
     if (!rc && normalize) rc = normalize_device(d, h->C, length, h->stream);
     if (!rc) rc = partition_device(d, h->C, length, h->B, true, h->H, h->tw, h->stream, h->cstride, h->pstride);
-    if (!rc) rc = update_head(h, h->stream);
-    if (!rc) rc = far_filter(h, h->stream);
+    lvl_filter_changed(h);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     (void)hipFree(d);
@@ -851,11 +816,10 @@ NEO_HIP_API int neo_hip_upols_set_batch(neo_hip_upols* h, int enable)
 NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable)
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
-    if (enable && h->v2) return fail(NEO_HIP_EINVAL, "lookahead steps are for whole-block upols / upola handles");
-    if (enable && h->ring - h->P < batch_blocks(h) - 1) return fail(NEO_HIP_EINVAL, "FDL ring too short for lookahead");
+    if (enable && h->v2) return fail(NEO_HIP_EINVAL, "streaming levels are for whole-block upols / upola handles");
+    if (enable && h->B > 1024) return fail(NEO_HIP_EINVAL, "streaming levels take blocks up to 1024");
     h->ahead = enable != 0;
-    h->phase = 0;
-    h->fwin = -1;  // the FDL is complete at any block boundary: the next step opens a window
+    h->lv_n = -1;  // the FDL is complete at any block boundary: the next step primes the levels
     return NEO_HIP_OK;
 }
 
@@ -863,9 +827,9 @@ NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* pha
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     if (enabled) *enabled = h->ahead;
-    if (phase) *phase = h->phase;
-    if (window) *window = batch_blocks(h);
-    if (splits) *splits = h->Sb;
+    if (phase) *phase = int(h->lv_n < 0 ? 0 : h->lv_n % kFarT);
+    if (window) *window = h->lv.nseg ? kFarT : (h->lv.n ? h->lv.T[h->lv.n - 1] : 1);
+    if (splits) *splits = h->lv.n + (h->lv.nseg ? 1 : 0);
     return NEO_HIP_OK;
 }
 
@@ -878,23 +842,70 @@ NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable)
     return NEO_HIP_OK;
 }
 
-NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches)
+// fold the recorded event groups into the per-part sums and the per-group totals
+static int drain_events(upols_t* h)
+{
+    for (size_t i = 0; i < h->events_used; ++i) {
+        const auto& e = h->events[i];
+        NEO_HIP_CHECK(hipEventSynchronize(e.e[e.n - 1]));
+        float tot = 0.f;
+        NEO_HIP_CHECK(hipEventElapsedTime(&tot, e.e[0], e.e[e.n - 1]));
+        h->group_ms.push_back(tot);
+        for (int k = 0; k + 1 < e.n; ++k) {
+            float t = 0.f;
+            NEO_HIP_CHECK(hipEventElapsedTime(&t, e.e[k], e.e[k + 1]));
+            h->part_ms[k] += t;
+            ++h->part_n[k];
+        }
+        if (e.n == 4) {
+            h->part_ms[3] += tot;
+            ++h->part_n[3];
+        }
+    }
+    h->events_used = 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_timing_detail(neo_hip_upols* h, double* ms, int64_t* launches)
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     device_guard g(h->device);
-    for (size_t i = 0; i < h->events_used; ++i) {
-        auto& e = h->events[i];
-        NEO_HIP_CHECK(hipEventSynchronize(e.second));
-        float ms = 0.f;
-        NEO_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
-        h->mac_ms += ms;
-        ++h->launches;
+    if (int rc = drain_events(h)) return rc;
+    h->group_ms.clear();
+    for (int k = 0; k < 4; ++k) {
+        if (ms) ms[k] = h->part_ms[k];
+        if (launches) launches[k] = h->part_n[k];
+        h->part_ms[k] = 0.0;
+        h->part_n[k] = 0;
     }
-    h->events_used = 0;
-    if (mac_ms) *mac_ms = h->mac_ms;
-    if (launches) *launches = h->launches;
-    h->mac_ms = 0.0;
-    h->launches = 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_step_times(neo_hip_upols* h, double* ms, int64_t cap, int64_t* count)
+{
+    if (!h || (cap > 0 && !ms)) return fail(NEO_HIP_EINVAL, "null handle or buffer");
+    device_guard g(h->device);
+    if (int rc = drain_events(h)) return rc;
+    const int64_t n = int64_t(h->group_ms.size());
+    for (int64_t i = 0; i < std::min(n, cap); ++i) ms[i] = h->group_ms[size_t(i)];
+    if (count) *count = n;
+    h->group_ms.clear();
+    for (int k = 0; k < 4; ++k) {
+        h->part_ms[k] = 0.0;
+        h->part_n[k] = 0;
+    }
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches)
+{
+    double ms[4];
+    int64_t n[4];
+    int rc = neo_hip_upols_timing_detail(h, ms, n);
+    if (rc) return rc;
+    const int k = n[3] ? 3 : 0;  // streaming-level steps: the whole step; else the MAC kernel
+    if (mac_ms) *mac_ms = ms[k];
+    if (launches) *launches = n[k];
     return NEO_HIP_OK;
 }
 

@@ -11,18 +11,30 @@
 
 namespace neo_hip {
 constexpr int kMaxBatch = 32;                          // most blocks one batched MAC pass consumes
-constexpr int kFarT = 128;                             // two-level lookahead: blocks per far-field window
-constexpr int kFarAutoP = 512;                         // partitions from which it is on by default
 constexpr double kFusedMaxBytes = 64.0 * 1024 * 1024;  // filter + FDL bytes below which a step is one launch
 constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read cacheable (256 MiB Infinity Cache)
-// the lookahead / batched passes leave more of the Infinity Cache to the block steps' rows and
-// slabs (same-box A/B at C5, 4 runs each: 168 MiB 17.8 us/step, 216 MiB 18.3, 126 MiB 18.1)
+// the batched passes leave more of the Infinity Cache to the slabs (same-box A/B at C5, 4 runs
+// each: 168 MiB 17.8 us/step, 216 MiB 18.3, 126 MiB 18.1)
 constexpr double kBatchCacheBudgetBytes = 168.0 * 1024 * 1024;
+// streaming levels (upols_levels.hip)
+constexpr int kLvA0 = 16;    // partitions of the block step itself
+constexpr int kLvMax = 4;    // Toeplitz levels + far
+constexpr int kFarT = 128;   // far level: blocks per window (256-point partition-axis transform)
+constexpr int kFarA = 256;   // far level: first partition (2 kFarT)
+constexpr int kFarSPG = 2;   // far level: segments per sub-unit workgroup
+constexpr int kFarRing = 2 * kFarA;  // far level: FDL ring rows needed (a slice reads back 383 blocks)
+
+struct level_plan {
+    int a0 = 1;                      // the block step takes partitions [0, a0)
+    int n = 0;                       // Toeplitz levels
+    int T[3] = {}, a[3] = {}, b[3] = {};  // window (blocks) and partition band [a, b) per level
+    int nseg = 0;                    // far segments of kFarT partitions from kFarA (0: no far level)
+};
 }  // namespace neo_hip
 
 struct neo_hip_upols {
     int device = 0, C = 0, B = 0, P = 0, S = 1, rows = 1;
-    int ring = 0;  // FDL ring rows R = P + kMaxBatch - 1
+    int ring = 0;  // FDL ring rows R = P + kMaxBatch - 1 (at least kFarRing with a far level)
     hipStream_t stream = nullptr;
     neo_hip::cf* H = nullptr;
     neo_hip::cf* fdl = nullptr;
@@ -36,45 +48,31 @@ struct neo_hip_upols {
     bool batch = true;      // process_blocks runs T blocks per MAC pass (neo_hip_upols_set_batch)
     int Sb = 1, rows_b = 1; // batched-pass splits per channel and partitions per split
     int bT = 32, bNB = 1;   // batched pass: blocks per pass (capped by batch_t), bins per lane-vector
-    int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kBatchCacheBudgetBytes; NEO_HIP_BATCH_CACHE_ROWS)
-    int bprio = 11;         // batched MAC: co-resident workgroups trade issue priority every 2^bprio
-                            // 10-ns ticks (NEO_HIP_BATCH_PRIO=0 off)
-    bool snt = false;       // lookahead passes store their slabs nontemporally (NEO_HIP_SLAB_NT)
-    int b8var = 3;          // 8-block passes: bmac_var 3 (buffer loads, D = 8) or 0 (NEO_HIP_BATCH8_VAR)
-    int bvar = 3;           // batched MAC variant at T = 32, B = 256/512 (bmac_var in upols_batch.hip; NEO_HIP_BATCH_VAR)
+    int pcb = 0;            // filter rows per channel the batched MAC loads cacheable (kBatchCacheBudgetBytes)
+    bool bufload = true;    // batched MAC with buffer loads (one channel's rows span < 2 GiB)
     neo_hip::cf* part_b = nullptr;   // batched partial spectra [C][Sb][T][B]
-    // streaming lookahead (k_upols_ahead): one batched pass per T blocks, phase = block of
-    // the current window; on for HBM-bound shapes (not fused), NEO_HIP_AHEAD / set_ahead
+    // streaming levels (upols_levels.hip): on for HBM-bound shapes (neo_hip_upols_set_ahead)
     bool ahead = false;
-    bool asub = true;     // lookahead sub-windows (k_upols_ahead2 only; NEO_HIP_AHEAD_SUB=0 disables)
-    bool ssplit = false;  // sub-window passes: one split per chunk (NEO_HIP_SUB_SPLIT=1; A/B on one box: slower)
-    int subw = 8;         // lookahead sub-window (blocks): 16 at B >= 512 (rocprof totals: C5 -1.7 %), 8 below
-                          // (C4 +1 % with 16); NEO_HIP_SUBWINDOW=8/16
-    neo_hip::cf* part_s = nullptr;  // sub-window pass slabs [C][ssub][subw][B], ssub * subw <= kMaxBatch
-    // direct-head block step k_upols_ahead3 (OLS): 1 = at B = 256 (same-box A/B: C4 +3.5 %; at
-    // B = 512 the 512 x 512-tap convolution costs what it saves), 2 = at B = 256 and 512,
-    // 0 = off (NEO_HIP_AHEAD_DIRECT=1 / 0)
-    int adirect = 1;
-    bool direct_ok = false; // partition 0's time-domain head is B taps (update_head)
-    float* h0t = nullptr;   // head taps [C][B] (k_head_taps)
-    float* h0tail = nullptr;
-    int akern = 2;  // per-block lookahead kernel: 2 = k_upols_ahead2 (B <= 1024), 1 = k_upols_ahead (NEO_HIP_AHEAD_KERNEL)
-    int phase = 0;
-    // two-level lookahead (upols_far.hip, NEO_HIP_FAR=1): partitions >= kFarT by a partition-axis
-    // transform once per kFarT blocks; the level-1 pass then walks partitions < kFarT only
-    bool far = false;
-    int fwin = -1;                 // level-1 windows done in the current far window (-1: recompute)
-    int fbase = 0;                 // first block of the current level-1 window within the far window
-    neo_hip::cf* hf = nullptr;     // segment spectra [C][Q-1][2 kFarT][B]
-    neo_hip::cf* hf0 = nullptr;    // bin 0's second coefficient [C][Q-1][2 kFarT]
-    neo_hip::cf* ff = nullptr;     // far field of the current window [C][kFarT][B]
-    neo_hip::cf* twf = nullptr;    // 2 kFarT-point twiddles
+    neo_hip::level_plan lv;
+    int64_t lv_n = -1;              // blocks since the levels were primed (-1: prime at the next step)
+    bool lv_ready = false;          // level buffers allocated
+    neo_hip::cf* lv_slab[3] = {};   // Toeplitz level slabs [2][C][T][B]
+    neo_hip::cf* fv_hf = nullptr;   // far segment spectra [C][nseg][256][B]
+    neo_hip::cf* fv_hf0 = nullptr;  // far bin 0 second coefficient [C][nseg][256]
+    neo_hip::cf* fv_xf = nullptr;   // far FDL row-pair spectra, ring of nseg slots [C][nseg][256][B]
+    neo_hip::cf* fv_xf0m = nullptr; // bin 0 conj(Z[-f]) of each slot [C][nseg][256]
+    neo_hip::cf* fv_ff = nullptr;   // far field [2][C][128][B]
+    neo_hip::cf* fv_part = nullptr; // far sub-unit partial spectra of one slice
+    int* fv_cnt = nullptr;          // far sub-unit arrival counters of one slice
+    neo_hip::cf* fv_tw = nullptr;   // 256-point twiddles
+    int fv_nsub = 1;                // far sub-units per unit
+    bool fv_dirty = true;           // far segment spectra to recompute (filter changed)
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
     size_t samples_cap = 0;
-    int timing = 0;          // 0: off; n: HIP events around every n-th MAC launch
-    int64_t tick = 0;        // MAC launches seen while timing
+    int timing = 0;          // 0: off; n: HIP events around every n-th launch group
+    int64_t tick = 0;        // launch groups seen while timing
     bool ola = false;  // upola_convolver (overlap-add stage) instead of upols (overlap-save)
     bool v2 = false;   // upola_convolver_v2: sub-block input (implies ola)
     int in_pos = 0;    // v2: samples of the current block already consumed (_input_pos)
@@ -88,10 +86,15 @@ struct neo_hip_upols {
     // Default [C][P][B]; NEO_HIP_LAYOUT=pcb selects partition-major [P][C][B] (A/B).
     int64_t cstride = 0, pstride = 0;
     int pc = 0;  // filter rows per channel read with the cacheable policy (kCacheBudgetBytes; NEO_HIP_CACHE_ROWS)
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool, reused across timing windows
+    struct ev_group {
+        hipEvent_t e[4] = {};
+        int n = 0;
+    };
+    std::vector<ev_group> events;  // pool, reused across timing windows
     size_t events_used = 0;
-    double mac_ms = 0.0;
-    int64_t launches = 0;
+    double part_ms[4] = {};        // drained event time per part (see neo_hip_upols_timing_detail)
+    int64_t part_n[4] = {};
+    std::vector<float> group_ms;   // whole-group durations, in order (neo_hip_upols_step_times)
 };
 
 
@@ -138,13 +141,33 @@ inline int batch_blocks(const upols_t* h) { return batch_t(h->B, h->bNB, h->bT);
 
 // upols_batch.hip: T whole blocks in one pass over the filter and the FDL
 int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s);
-// upols_batch.hip: one streaming block step in lookahead mode
-int launch_ahead(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
-// upols_far.hip: two-level lookahead (segment spectra after every filter change; one far
-// window per kFarT blocks)
-bool far_usable(const upols_t* h);
-int far_filter(upols_t* h, hipStream_t s);
-int far_window(upols_t* h, hipStream_t s);
+// Timing (neo_hip_upols_set_timing): the next event group of nev events if this launch
+// group is a timed one (every h->timing-th), else nullptr; mark(g, i, s) records event i.
+inline int timing_begin(upols_t* h, int nev, upols_t::ev_group** out)
+{
+    *out = nullptr;
+    if (!h->timing || h->tick++ % h->timing != 0) return NEO_HIP_OK;
+    if (h->events_used == h->events.size()) {
+        upols_t::ev_group g;
+        for (auto& e : g.e) NEO_HIP_CHECK(hipEventCreate(&e));
+        h->events.push_back(g);
+    }
+    *out = &h->events[h->events_used++];
+    (*out)->n = nev;
+    return NEO_HIP_OK;
+}
+inline int timing_mark(upols_t::ev_group* g, int i, hipStream_t s)
+{
+    if (g) NEO_HIP_CHECK(hipEventRecord(g->e[i], s));
+    return NEO_HIP_OK;
+}
+
+// upols_levels.hip: one streaming block step (level slabs + the newest partitions) and 1/T
+// of every level's next window; the level plan; buffers; filter-change hook
+int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
+void plan_levels(int P, level_plan& lp);
+void lvl_free(upols_t* h);
+void lvl_filter_changed(upols_t* h);
 // upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device
 int upload_tw(cf** d, int B);
 int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s,
@@ -152,7 +175,5 @@ int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf
 int normalize_device(float* d_ir, int C, int64_t L, hipStream_t s);
 // filter [C][P][B+1] (reference layout, device) -> packed H rows of the handle
 int pack_filter(upols_t* h, const cf* src, hipStream_t s);
-// time-domain head taps of partition 0 for the direct-head block step (after every filter change)
-int update_head(upols_t* h, hipStream_t s);
 
 }  // namespace neo_hip

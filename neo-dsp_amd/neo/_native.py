@@ -22,6 +22,12 @@ NEO_HIP_ENODEV = 4
 C2C, R2C, C2R = 0, 1, 2
 F64 = 16  # OR into the kind: complex128 / float64 plans
 
+class UpolsOpts(ctypes.Structure):
+    """neo_hip_upols_opts (include/neo_hip.h)."""
+    _fields_ = [("fused", ctypes.c_int), ("split_workgroups", ctypes.c_int), ("batch_blocks", ctypes.c_int),
+                ("batch_bins", ctypes.c_int), ("levels", ctypes.c_int)]
+
+
 # every symbol declared in include/neo_hip.h: (name, restype, argtypes)
 _vp, _i, _i64, _fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_float)
 SIGNATURES = {
@@ -39,6 +45,7 @@ SIGNATURES = {
     "neo_hip_upols_process_samples": (_i, [_vp, _vp, _i64, _vp, _i64, _i64, _i, _vp]),
     "neo_hip_upols_set_batch": (_i, [_vp, _i]),
     "neo_hip_upols_batch_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "neo_hip_upols_create_ex": (_i, [_i, _i, _i, _i, _i, _vp, ctypes.POINTER(_vp)]),
     "neo_hip_upols_destroy": (_i, [_vp]),
     "neo_hip_upols_set_filter": (_i, [_vp, _vp, _i]),
     "neo_hip_upols_set_impulse": (_i, [_vp, _vp, _i64, _i, _i]),
@@ -50,6 +57,9 @@ SIGNATURES = {
     "neo_hip_upols_get_ahead": (_i, [_vp] + [ctypes.POINTER(_i)] * 4),
     "neo_hip_upols_set_timing": (_i, [_vp, _i]),
     "neo_hip_upols_timing": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
+    "neo_hip_upols_timing_detail": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
+    "neo_hip_upols_step_times": (_i, [_vp, ctypes.POINTER(ctypes.c_double), _i64, ctypes.POINTER(_i64)]),
+    "neo_hip_upols_level_plan": (_i, [_i] + [ctypes.POINTER(_i)] * 6),
     "neo_hip_upols_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
     "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),

@@ -54,6 +54,20 @@ def num_partitions(length: int, block: int) -> int:
     return p.value
 
 
+def level_plan(partitions: int) -> dict:
+    """The streaming level plan of a convolver with `partitions` partitions
+    (neo_hip_upols_level_plan; no device needed): the block step takes [0, a0), Toeplitz
+    level l a window of T[l] blocks over the band [a[l], b[l]), and nseg far segments of
+    128 partitions from 256."""
+    L = _native.load()
+    a0, nl, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    T, a, b = (ctypes.c_int * 3)(), (ctypes.c_int * 3)(), (ctypes.c_int * 3)()
+    _native.check(L.neo_hip_upols_level_plan(int(partitions), ctypes.byref(a0), ctypes.byref(nl), T, a, b,
+                                             ctypes.byref(ns)))
+    n = nl.value
+    return {"a0": a0.value, "T": list(T[:n]), "a": list(a[:n]), "b": list(b[:n]), "nseg": ns.value}
+
+
 def uniform_partition(impulse_response, block_size: int, device: int = 0) -> np.ndarray:
     """[C][L] float32 -> [C][P][B+1] complex64: rfft_2B of each zero-padded B-sample partition."""
     ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
@@ -89,15 +103,27 @@ class UpolsConvolver:
     (output block t corresponds to input block t, overlap_save.hpp:84-112).
     """
 
-    def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols"):
+    OPTION_DEFAULTS = {"fused": -1, "split_workgroups": 0, "batch_blocks": 0, "batch_bins": 0, "levels": -1}
+
+    def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols",
+                 options: dict | None = None):
+        """`options` (neo_hip_upols_create_ex): explicit code-path choices instead of the
+        shape-based defaults — fused (-1 auto / 0 / 1), split_workgroups (0 auto),
+        batch_blocks (0 auto / 2..32), batch_bins (0 auto / 1 / 2), levels (-1 auto / 0 / 1).
+        Every choice gives the same results up to float summation order."""
         lib = _native.load()
         h = ctypes.c_void_p()
-        creators = {"upols": lib.neo_hip_upols_create, "upola": lib.neo_hip_upola_create,
-                    "upola_v2": lib.neo_hip_upola2_create}
-        if method not in creators:
+        methods = {"upols": 0, "upola": 1, "upola_v2": 2}
+        if method not in methods:
             raise ValueError(f"method must be 'upols', 'upola' or 'upola_v2', got {method!r}")
-        create = creators[method]
-        _native.check(create(int(channels), int(block_size), int(partitions), int(device), ctypes.byref(h)))
+        opts = dict(self.OPTION_DEFAULTS)
+        for k, v in (options or {}).items():
+            if k not in opts:
+                raise ValueError(f"unknown convolver option {k!r}")
+            opts[k] = int(v)
+        o = _native.UpolsOpts(**opts)
+        _native.check(lib.neo_hip_upols_create_ex(int(channels), int(block_size), int(partitions), int(device),
+                                                  methods[method], ctypes.byref(o), ctypes.byref(h)))
         self._h = h
         self.channels, self.block_size, self.partitions, self.device = channels, block_size, partitions, device
         self.method = method
@@ -206,12 +232,12 @@ class UpolsConvolver:
         return t.value, s.value
 
     def set_ahead(self, enable: bool) -> None:
-        """Streaming lookahead for single-block steps (neo_hip_upols_set_ahead)."""
+        """Streaming levels for single-block steps (neo_hip_upols_set_ahead)."""
         _native.check(_native.load().neo_hip_upols_set_ahead(self._h, int(bool(enable))))
 
     def ahead_info(self):
-        """(lookahead enabled, block position in the current window, window length T,
-        splits of the window pass)."""
+        """(streaming levels enabled, block position in the current far window, longest
+        window, number of levels)."""
         v = [ctypes.c_int() for _ in range(4)]
         _native.check(_native.load().neo_hip_upols_get_ahead(self._h, *[ctypes.byref(x) for x in v]))
         return bool(v[0].value), v[1].value, v[2].value, v[3].value
@@ -224,10 +250,26 @@ class UpolsConvolver:
         _native.check(_native.load().neo_hip_upols_set_timing(self._h, int(every) if enable else 0))
 
     def timing(self):
-        """(accumulated MAC-kernel ms, launches) since the last call."""
+        """(accumulated ms, timed launch groups) since the last call: the MAC kernel of
+        plain / batched steps, the whole step of streaming-level steps."""
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _native.check(_native.load().neo_hip_upols_timing(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+    def timing_detail(self):
+        """Per part [(ms, count)] * 4 since the last call (neo_hip_upols_timing_detail):
+        streaming steps 0 = block step, 1 = Toeplitz level slices, 2 = far slice,
+        3 = whole step; plain / batched steps 0 = MAC kernel."""
+        ms, n = (ctypes.c_double * 4)(), (ctypes.c_int64 * 4)()
+        _native.check(_native.load().neo_hip_upols_timing_detail(self._h, ms, n))
+        return [(ms[k], n[k]) for k in range(4)]
+
+    def step_times(self, cap: int = 1 << 16):
+        """Duration (ms) of every timed launch group since the last drain, in order (a
+        streaming step: first to last event of the step)."""
+        buf, n = (ctypes.c_double * cap)(), ctypes.c_int64()
+        _native.check(_native.load().neo_hip_upols_step_times(self._h, buf, cap, ctypes.byref(n)))
+        return list(buf[: min(n.value, cap)])
 
     @property
     def splits(self) -> int:
@@ -303,16 +345,18 @@ class upola_convolver_v2(upols_convolver):
         return samples
 
 
-def dense_convolve(signal, impulse_response, block_size: int, device: int = 0, method: str = "upols") -> np.ndarray:
+def dense_convolve(signal, impulse_response, block_size: int, device: int = 0, method: str = "upols",
+                   options: dict | None = None) -> np.ndarray:
     """dense_convolve<upols_convolver | upola_convolver> (DenseConvolution.hpp:39-70): normalize
-    the IR matrix, partition it, run every block (tail zero-padded), output truncated to N."""
+    the IR matrix, partition it, run every block (tail zero-padded), output truncated to N.
+    `options`: UpolsConvolver code-path choices (same results)."""
     sig = np.ascontiguousarray(np.atleast_2d(np.asarray(signal, dtype=np.float32)))
     ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
     C, N = sig.shape
     if ir.shape[0] != C:
         raise ValueError("signal and impulse response channel counts differ")
     P = num_partitions(ir.shape[1], block_size)
-    conv = UpolsConvolver(C, block_size, P, device, method=method)
+    conv = UpolsConvolver(C, block_size, P, device, method=method, options=options)
     conv.set_impulse(ir, normalize=True)
     nb = -(-N // block_size)
     # whole signal in chunks of <= 2^26 samples: one upload, batched passes (T blocks per

@@ -1,0 +1,159 @@
+"""The streaming level schedule (neo-dsp_amd/csrc/upols_levels.hip), restated in float64
+numpy and checked against the direct block-axis convolution — no GPU needed.
+
+Per bin the convolver output is Y[t] = sum_p H[p] X[t - p]
+(uniform_partitioned_convolver.hpp:47-65; fdl_index.hpp:23-36: partition p meets FDL row
+t - p). The HIP path splits the partitions into the bands of neo_hip_upols_level_plan and
+computes each band's next window during the current one, a slice of the bins per step,
+from FDL rows that already exist. This test replays exactly that schedule — the ring
+positions the host passes (tw), the slice ranges, the double-buffered slabs, the far
+level's XF ring of row-pair spectra and its 256-point partition-axis transforms — on random
+spectra, with history before the levels start, ring wraparound and re-priming, and checks
+every output block. It pins the index arithmetic the kernels share with the host code; the
+kernels' arithmetic itself is pinned by the GPU parity tests against the oracle.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "neo-dsp_amd"))
+
+FT, FA, FN = 128, 256, 256  # far window, first far partition, transform length
+
+
+def plan(P):
+    import neo
+
+    try:
+        return neo.convolution.level_plan(P)
+    except OSError as e:  # pragma: no cover - library not built
+        pytest.skip(f"libneo_hip.so not loadable: {e}")
+
+
+class Sim:
+    """float64 replay of the level pipeline for one channel of K bins."""
+
+    def __init__(self, H, lp):
+        self.H, self.lp = H, lp
+        self.P, self.K = H.shape
+        self.R = self.P + 31
+        if lp["nseg"]:
+            self.R = max(self.R, 2 * FA)
+        self.ring = np.zeros((self.R, self.K), complex)
+        self.w = 0
+        self.n = -1
+        self.slab = [np.zeros((2, T, self.K), complex) for T in lp["T"]]
+        ns = lp["nseg"]
+        if ns:
+            self.M = ns
+            # segment spectra: s -> partitions [128 (s + 2), 128 (s + 3)), zero-padded to 256
+            seg = np.zeros((ns, FN, self.K), complex)
+            for s in range(ns):
+                lo = FT * (s + 2)
+                hi = min(self.P, lo + FT)
+                seg[s, : hi - lo] = H[lo:hi]
+            self.HF = np.fft.fft(seg, axis=1)
+            self.XF = np.zeros((ns, FN, self.K), complex)
+            self.ff = np.zeros((2, FT, self.K), complex)
+
+    def plain(self, x):
+        """One plain step (all partitions from the ring); the levels re-prime after it."""
+        self.ring[self.w] = x
+        y = (self.H * self.ring[(self.w - np.arange(self.P)) % self.R]).sum(0)
+        self.w = (self.w + 1) % self.R
+        self.n = -1
+        return y
+
+    def toep(self, l, tw, k0, k1, buf):
+        T, a, b = self.lp["T"][l], self.lp["a"][l], self.lp["b"][l]
+        ps = np.arange(a, b)
+        for j in range(T):
+            rows = (tw + j - ps) % self.R
+            self.slab[l][buf, j, k0:k1] = (self.H[a:b, k0:k1] * self.ring[rows, k0:k1]).sum(0)
+
+    def far(self, tw, wn, k0, k1, nfresh):
+        ns, M = self.lp["nseg"], self.M
+        acc = np.zeros((FN, k1 - k0), complex)
+        for s in range(ns):
+            slot = (wn - s - 1) % M
+            if s < nfresh:
+                rows = [(tw - (s + 3) * FT + i) % self.R for i in range(FN)]
+                self.XF[slot, :, k0:k1] = np.fft.fft(self.ring[rows, k0:k1], axis=0)
+            acc += self.XF[slot, :, k0:k1] * self.HF[s, :, k0:k1]
+        y = np.fft.ifft(acc, axis=0)
+        self.ff[wn & 1, :, k0:k1] = y[FT:]
+
+    def prime(self):
+        for l in range(len(self.lp["T"])):
+            self.toep(l, self.w, 0, self.K, 0)
+        if self.lp["nseg"]:
+            self.far(self.w, 0, 0, self.K, self.lp["nseg"])
+        self.n = 0
+
+    def step(self, x):
+        if self.n < 0:
+            self.prime()
+        n, lp, K, R = self.n, self.lp, self.K, self.R
+        # block step: level slabs of this block + partitions [0, a0)
+        self.ring[self.w] = x
+        y = (self.H[: lp["a0"]] * self.ring[(self.w - np.arange(lp["a0"])) % R]).sum(0)
+        for l, T in enumerate(lp["T"]):
+            y = y + self.slab[l][(n // T) & 1, n % T]
+        if lp["nseg"]:
+            y = y + self.ff[(n // FT) & 1, n % FT]
+        # slices of the next windows (the kernels use rows <= this block - 1 only: check it)
+        saved = self.ring[self.w].copy()
+        self.ring[self.w] = np.nan
+        for l, T in enumerate(lp["T"]):
+            st = n % T
+            k0, k1 = st * K // T, (st + 1) * K // T
+            if k1 > k0:
+                self.toep(l, (self.w - st + T) % R, k0, k1, ((n // T) + 1) & 1)
+        if lp["nseg"]:
+            st = n % FT
+            k0, k1 = st * K // FT, (st + 1) * K // FT
+            if k1 > k0:
+                self.far((self.w - st + FT) % R, n // FT + 1, k0, k1, 1)
+        self.ring[self.w] = saved
+        self.w = (self.w + 1) % R
+        self.n = n + 1
+        return y
+
+
+def test_level_plan_bands():
+    """Bands tile [0, P) exactly; every band [a, b) with window T starts at >= 2T."""
+    for P in [1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 255, 256, 257, 383, 384, 385, 938, 1875, 4000]:
+        lp = plan(P)
+        cover = [(0, lp["a0"])] + list(zip(lp["a"], lp["b"]))
+        if lp["nseg"]:
+            cover.append((FA, FA + FT * lp["nseg"]))
+            assert FA + FT * (lp["nseg"] - 1) < P <= FA + FT * lp["nseg"]
+        assert cover[0][0] == 0
+        for (lo, hi), (lo2, _) in zip(cover, cover[1:]):
+            assert hi == lo2, (P, cover)
+        assert min(cover[-1][1], P) == P or (lp["nseg"] and cover[-1][1] >= P)
+        for T, a in zip(lp["T"], lp["a"]):
+            assert a >= 2 * T
+
+
+@pytest.mark.parametrize("P", [5, 20, 40, 100, 257, 300, 700])
+def test_level_schedule_matches_direct(P):
+    lp = plan(P)
+    rng = np.random.default_rng(P)
+    K = 16
+    H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
+    sim = Sim(H, lp)
+    nb = max(3 * P, 2 * P + 300) if lp["nseg"] else 3 * P + 40
+    X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
+    worst = 0.0
+    for t in range(nb):
+        # plain steps first (history before the levels start), and again midway (re-prime)
+        y = sim.plain(X[t]) if (t < 37 or nb // 2 <= t < nb // 2 + 3) else sim.step(X[t])
+        m = min(P, t + 1)
+        ref = (H[:m] * X[t - np.arange(m)]).sum(0)
+        worst = max(worst, float(np.abs(y - ref).max() / (np.abs(ref).max() + 1e-300)))
+    assert worst < 1e-12, worst

@@ -40,17 +40,17 @@ def test_identity_ir(neo_gpu, oracle, B):
 @pytest.mark.parametrize("B,L,C,nb", [(512, 4096, 1, 40), (256, 2560, 2, 40), (128, 1000, 3, 30),
                                       (16, 100, 2, 20), (64, 64, 1, 10), (1024, 5000, 2, 12),
                                       (2048, 9000, 1, 6), (4096, 12000, 1, 5), (32, 7, 1, 8)])
-@pytest.mark.parametrize("fused", ["0", "1"])
-def test_random_ir_vs_oracle(neo_gpu, oracle, monkeypatch, B, L, C, nb, fused):
-    """Both step forms: MAC + finish launches, and one launch with the last-arriver tail
-    (the default below 64 MiB of filter + FDL)."""
-    monkeypatch.setenv("NEO_HIP_FUSED", fused)
+@pytest.mark.parametrize("fused", [0, 1])
+def test_random_ir_vs_oracle(neo_gpu, oracle, B, L, C, nb, fused):
+    """Both plain step forms for the single blocks after the batched passes: MAC + finish
+    launches, and one launch with the last-arriver tail (the default below 64 MiB of
+    filter + FDL)."""
     ir = np.stack([oracle.noise(20 + c, L) for c in range(C)])
     irn = oracle.normalize_impulse(ir)
     parts = oracle.uniform_partition(irn, B)
     sig = np.stack([oracle.noise(30 + c, B * nb) for c in range(C)])
     ref = oracle.dense_convolve(sig, parts)
-    got = neo_gpu.dense_convolve(sig, ir, B)
+    got = neo_gpu.dense_convolve(sig, ir, B, options={"fused": fused, "levels": 0})
     assert peak_err(got, ref) <= TOL
     assert np.abs(got - ref).max() <= 1e-5
 
@@ -214,53 +214,61 @@ def test_full_size_properties(neo_gpu, oracle, C, B, L):
         assert peak_err(ox[c].cpu().numpy(), ref[0]) <= TOL
 
 
-def test_full_size_far_field_default(neo_gpu, oracle):
-    """C4 shape (P = 1875 >= kFarAutoP) in lookahead mode with the environment default, i.e.
-    the two-level lookahead on: 300 blocks (three far windows, 14 segments each), two channels
-    checked against the oracle."""
+def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans):
+    """Default options (streaming levels on, far level on), device input, one block per
+    call as a real-time caller steps it, nb blocks: every level's windows repeat many times,
+    every far segment meets real FDL rows and the ring wraps. Channels `chans` against the
+    oracle's dense_convolve over the whole stream."""
     torch = pytest.importorskip("torch")
-    C, B, L, nb = 256, 256, 480000, 300
-    g = torch.Generator(device="cuda").manual_seed(77)
+    g = torch.Generator(device="cuda").manual_seed(seed)
     ir = (torch.rand((C, L), generator=g, device="cuda") * 2 - 1).contiguous()
     x = (torch.rand((C, B * nb), generator=g, device="cuda") * 2 - 1).contiguous()
-    conv = neo_gpu.UpolsConvolver(C, B, neo_gpu.num_partitions(L, B))
+    P = neo_gpu.num_partitions(L, B)
+    conv = neo_gpu.UpolsConvolver(C, B, P)
+    assert conv.ahead_info()[0]  # streaming levels are the default here
     conv.set_impulse(ir, normalize=True)
-    conv.set_batch(False)
-    conv.set_ahead(True)
+    conv.set_batch(False)  # one block per pass
     xh = x.cpu().numpy()
     conv.process_blocks(x)
     torch.cuda.synchronize()
     irh = oracle.normalize_impulse(ir.cpu().numpy())
-    for c in (0, C - 1):
+    for c in chans:
         ref = oracle.dense_convolve(xh[c:c + 1], oracle.uniform_partition(irh[c:c + 1], B))
-        assert peak_err(x[c].cpu().numpy(), ref[0]) <= TOL
+        assert peak_err(x[c].cpu().numpy(), ref[0]) <= TOL, c
+        # the last far window alone (steady state, ring wrapped many times)
+        assert peak_err(x[c, -128 * B:].cpu().numpy(), ref[0, -128 * B:]) <= TOL, c
+
+
+def test_full_size_c5_shard_steady_state(neo_gpu, oracle):
+    """The headline path at its own shape (configs[4] per-GPU shard: 256 ch, B = 512,
+    L = 480000, P = 938, ring 969): 1152 blocks (9 far windows), channels 0, 127, 255."""
+    _full_size_streaming(neo_gpu, oracle, 256, 512, 480000, 1152, 77, (0, 127, 255))
+
+
+def test_full_size_c4_steady_state(neo_gpu, oracle):
+    """configs[3] (256 ch, B = 256, L = 480000, P = 1875, 13 far segments): 2176 blocks
+    (17 far windows, the ring of 1906 rows wraps), channels 0 and 255."""
+    _full_size_streaming(neo_gpu, oracle, 256, 256, 480000, 2176, 78, (0, 255))
 
 
 def test_multirow_splits_with_wraparound(neo_gpu, oracle):
     """More blocks than partitions and several partitions per split (every split carries
-    nonzero FDL rows, ring wraps), forced via NEO_HIP_SPLIT_WGS read at create time."""
-    import os
-
+    nonzero FDL rows, ring wraps), plain MAC + finish steps with forced split targets."""
     B, L, C, nb = 128, 50 * 128, 2, 130  # P = 50
     ir = np.stack([oracle.noise(700 + c, L) for c in range(C)])
     sig = np.stack([oracle.noise(710 + c, B * nb) for c in range(C)])
     ref = oracle.dense_convolve(sig, oracle.uniform_partition(oracle.normalize_impulse(ir), B))
-    for target in ("6", "1", "64"):
-        os.environ["NEO_HIP_SPLIT_WGS"] = target
-        os.environ["NEO_HIP_FUSED"] = "0"  # the MAC + finish form (>= 8 rows per split)
-        try:
-            P = neo_gpu.num_partitions(L, B)
-            conv = neo_gpu.UpolsConvolver(C, B, P)
-            conv.set_impulse(ir)
-            out = np.empty_like(sig)
-            for t in range(nb):
-                blk = np.ascontiguousarray(sig[:, t * B:(t + 1) * B])
-                conv(blk)
-                out[:, t * B:(t + 1) * B] = blk
-        finally:
-            del os.environ["NEO_HIP_SPLIT_WGS"], os.environ["NEO_HIP_FUSED"]
+    for target in (6, 1, 64):
+        P = neo_gpu.num_partitions(L, B)
+        conv = neo_gpu.UpolsConvolver(C, B, P, options={"split_workgroups": target, "fused": 0, "levels": 0})
+        conv.set_impulse(ir)
+        out = np.empty_like(sig)
+        for t in range(nb):
+            blk = np.ascontiguousarray(sig[:, t * B:(t + 1) * B])
+            conv(blk)
+            out[:, t * B:(t + 1) * B] = blk
         # S = ceil(P / ceil(P / min(ceil(t/C), ceil(P/8), 64)))
-        assert conv.splits == {"6": 3, "1": 1, "64": 7}[target]
+        assert conv.splits == {6: 3, 1: 1, 64: 7}[target]
         assert peak_err(out, ref) <= TOL, (target, conv.splits)
 
 
@@ -309,21 +317,16 @@ def test_upola_equals_upols(neo_gpu, oracle):
 
 
 def test_fused_step_matches_two_launch(neo_gpu, oracle):
-    """NEO_HIP_FUSED=1 (last-arriver tail in one launch) equals the default two-launch step."""
-    import os as _os
-
+    """The one-launch plain step (last-arriver tail) equals the two-launch step."""
     B, L, C, nb = 256, 60 * 256, 3, 70
     ir = np.stack([oracle.noise(160 + c, L) for c in range(C)])
     sig = np.stack([oracle.noise(170 + c, B * nb) for c in range(C)])
     outs = []
-    for fused in ("0", "1"):
+    for fused in (0, 1):
         for method in ("upols", "upola"):
-            _os.environ["NEO_HIP_FUSED"] = fused
-            _os.environ["NEO_HIP_SPLIT_WGS"] = "12"  # 4 splits per channel
-            try:
-                outs.append((fused, method, neo_gpu.dense_convolve(sig, ir, B, method=method)))
-            finally:
-                del _os.environ["NEO_HIP_FUSED"], _os.environ["NEO_HIP_SPLIT_WGS"]
+            # 4 splits per channel; the single blocks after the batched passes take the plain step
+            opts = {"fused": fused, "split_workgroups": 12, "levels": 0}
+            outs.append((fused, method, neo_gpu.dense_convolve(sig, ir, B, method=method, options=opts)))
     ref = {m: oracle.dense_convolve(sig, oracle.uniform_partition(oracle.normalize_impulse(ir), B), method=m)
            for m in ("upols", "upola")}
     for fused, method, out in outs:
@@ -475,13 +478,11 @@ def test_batched_mixed_with_single_blocks(neo_gpu, oracle):
 
 
 @pytest.mark.parametrize("T", [2, 4, 8, 16, 32])
-@pytest.mark.parametrize("nbins", ["1", "2"])
-def test_every_batch_size(neo_gpu, oracle, monkeypatch, T, nbins):
+@pytest.mark.parametrize("nbins", [1, 2])
+def test_every_batch_size(neo_gpu, oracle, T, nbins):
     """Each compiled batch size (and the smaller ones used for leftovers) against the oracle,
     with 1 or 2 bins per lane-vector."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("NEO_HIP_BATCH_T", str(T))
-    monkeypatch.setenv("NEO_HIP_BATCH_NB", nbins)
     B, L, C = 256, 9000, 2
     nb = 2 * T + 3
     ir = np.stack([oracle.noise(270 + c, L) for c in range(C)])
@@ -489,9 +490,10 @@ def test_every_batch_size(neo_gpu, oracle, monkeypatch, T, nbins):
     sig = np.stack([oracle.noise(280 + c, B * nb) for c in range(C)])
     for method in ("upols", "upola"):
         ref = oracle.dense_convolve(sig, parts, method=method)
-        conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
+        conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method,
+                                      options={"batch_blocks": T, "batch_bins": nbins})
         conv.filter(parts)
-        assert conv.batch_info()[0] == min(T, 32 // int(nbins))  # accumulator cap at B = 256
+        assert conv.batch_info()[0] == min(T, 32 // nbins)  # accumulator cap at B = 256
         t = torch.from_numpy(sig).cuda()
         conv.process_blocks(t)
         torch.cuda.synchronize()
@@ -546,22 +548,17 @@ def test_host_staging_growth_keeps_batch_buffers(neo_gpu, oracle):
         assert peak_err(out, ref) <= TOL, method
 
 
-# ------------------------------------------------ streaming lookahead (k_batch_mac ahead + k_upols_ahead)
-@pytest.mark.parametrize("method", ["upols", "upola"])
-@pytest.mark.parametrize("B,L,C,nb", [(512, 20000, 3, 75), (256, 2560, 2, 70), (16, 100, 2, 40), (64, 64, 1, 37),
-                                      (1024, 30000, 2, 33), (4096, 12000, 1, 9), (128, 128 * 40, 2, 100)])
-@pytest.mark.parametrize("akern", ["1", "2"])
-def test_ahead_steps_vs_oracle(neo_gpu, oracle, monkeypatch, method, B, L, C, nb, akern):
-    """Single-block steps with lookahead: one batched pass per T-block window (p > j for
-    block j), the window's own partitions per step; P < T, P = 1 and ring wraparound.
-    akern: the per-block kernel (1 = k_upols_ahead, 2 = k_upols_ahead2, B <= 1024)."""
+# ------------------------------------------------ streaming levels (upols_levels.hip)
+def _stream(neo_gpu, oracle, method, B, P, C, nb, seed):
+    """Single-block steps with the streaming levels against the oracle's dense_convolve."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("NEO_HIP_AHEAD_KERNEL", akern)
-    ir = np.stack([oracle.noise(320 + c, L) for c in range(C)])
+    L = B * (P - 1) + B // 2 + 1
+    ir = np.stack([oracle.noise(seed + c, L) for c in range(C)])
     parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
-    sig = np.stack([oracle.noise(330 + c, B * nb) for c in range(C)])
+    assert parts.shape[1] == P
+    sig = np.stack([oracle.noise(seed + 10 + c, B * nb) for c in range(C)])
     ref = oracle.dense_convolve(sig, parts, method=method)
-    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
+    conv = neo_gpu.UpolsConvolver(C, B, P, method=method)
     conv.filter(parts)
     conv.set_batch(False)
     conv.set_ahead(True)
@@ -569,41 +566,40 @@ def test_ahead_steps_vs_oracle(neo_gpu, oracle, monkeypatch, method, B, L, C, nb
     t = torch.from_numpy(sig).cuda()
     conv.process_blocks(t)
     torch.cuda.synchronize()
-    assert conv.ahead_info()[1] == nb % conv.ahead_info()[2]
-    assert peak_err(t.cpu().numpy(), ref) <= TOL
+    assert conv.ahead_info()[1] == nb % 128
+    return peak_err(t.cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("method", ["upols", "upola"])
-@pytest.mark.parametrize("B,P,C,nb", [(256, 300, 2, 420), (512, 200, 2, 300), (32, 700, 1, 900), (64, 129, 2, 300),
-                                      (128, 256, 1, 520)])
-def test_far_field_steps_vs_oracle(neo_gpu, oracle, monkeypatch, method, B, P, C, nb):
-    """Two-level lookahead (NEO_HIP_FAR=1, upols_far.hip): partitions >= 128 by a 256-point
-    transform along the partition axis once per 128 blocks, the level-1 pass over partitions
-    < 128. Several far windows, ring wraparound, P just above 128, a last segment of one
-    partition, the packed DC/Nyquist bin; OLS and OLA."""
-    torch = pytest.importorskip("torch")
-    monkeypatch.setenv("NEO_HIP_FAR", "1")
-    L = B * (P - 1) + B // 2 + 1
-    ir = np.stack([oracle.noise(520 + c, L) for c in range(C)])
-    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
-    assert parts.shape[1] == P
-    sig = np.stack([oracle.noise(530 + c, B * nb) for c in range(C)])
-    ref = oracle.dense_convolve(sig, parts, method=method)
-    conv = neo_gpu.UpolsConvolver(C, B, P, method=method)
-    conv.filter(parts)
-    conv.set_batch(False)
-    conv.set_ahead(True)
-    t = torch.from_numpy(sig).cuda()
-    conv.process_blocks(t)
-    torch.cuda.synchronize()
-    assert peak_err(t.cpu().numpy(), ref) <= TOL
+@pytest.mark.parametrize("B,P,C,nb", [(512, 40, 3, 75), (256, 10, 2, 70), (16, 7, 2, 40), (64, 1, 1, 37),
+                                      (1024, 30, 2, 33), (128, 40, 2, 100), (32, 2, 1, 20)])
+def test_level_steps_small_filters(neo_gpu, oracle, method, B, P, C, nb):
+    """P below the far level: the block step alone (P <= 16) and the Toeplitz levels, every
+    block size the block step is built for, P = 1, ring wraparound; OLS and OLA."""
+    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 320) <= TOL
 
 
-def test_far_field_mixed_and_refilter(neo_gpu, oracle, monkeypatch):
-    """Far field across batched passes, lookahead toggles at arbitrary blocks and a filter
-    change: the far window restarts at the next lookahead window."""
+@pytest.mark.parametrize("P", [16, 17, 32, 33, 64, 65, 255, 256, 257, 384, 385, 513])
+def test_level_band_edges(neo_gpu, oracle, P):
+    """Every band edge of the level plan (block step / 8 / 16 / 32-block Toeplitz levels /
+    far segments, a last far segment of one partition): B = 32, past the ring length."""
+    assert _stream(neo_gpu, oracle, "upols", 32, P, 2, max(2 * P + 140, 300), 400 + P) <= TOL
+
+
+@pytest.mark.parametrize("method", ["upols", "upola"])
+@pytest.mark.parametrize("B,P,C,nb", [(256, 300, 2, 420), (32, 700, 1, 900), (64, 400, 2, 700), (16, 1000, 1, 1200),
+                                      (1024, 270, 1, 300), (128, 600, 3, 800)])
+def test_far_level_steps_vs_oracle(neo_gpu, oracle, method, B, P, C, nb):
+    """The far level (partitions >= 256 by 256-point transforms along the partition axis,
+    its next window computed during the current one): several far windows, ring wraparound,
+    the packed DC / Nyquist bin, several sub-units per 16-column unit; OLS and OLA."""
+    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 520) <= TOL
+
+
+def test_far_field_mixed_and_refilter(neo_gpu, oracle):
+    """Streaming levels across batched passes, toggles at arbitrary blocks and a filter
+    change: the levels re-prime at the next streaming step."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("NEO_HIP_FAR", "1")
     B, P, C = 256, 290, 2
     L = B * P
     irs = [np.stack([oracle.noise(540 + 7 * k + c, L) for c in range(C)]) for k in range(2)]
@@ -629,60 +625,32 @@ def test_far_field_mixed_and_refilter(neo_gpu, oracle, monkeypatch):
         assert peak_err(out, ref) <= TOL, k
 
 
-@pytest.mark.parametrize("B", [256, 512])
-@pytest.mark.parametrize("direct", ["0", "1"])
-@pytest.mark.parametrize("head", ["partitioned", "arbitrary"])
-def test_ahead_direct_head(neo_gpu, oracle, monkeypatch, B, direct, head):
-    """Direct-head block step (k_upols_ahead3, OLS): partition 0 as a B-tap time-domain
-    convolution when its head comes from a zero-padded partition; an arbitrary head
-    spectrum (second half of irfft(H0) not zero) keeps the transform path. Both must match
-    the reference restatement, which takes any spectra. NEO_HIP_AHEAD_DIRECT=1 forces the
-    direct head at B = 512 too (off by default there: no gain in a same-box A/B)."""
+def test_levels_before_any_filter(neo_gpu):
+    """Streaming steps on a fresh handle with a far level and no filter set (H is zero):
+    silence, no fault (the far buffers are allocated and primed on the first step)."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("NEO_HIP_AHEAD_DIRECT", direct)
-    C, L, nb = 2, 40 * B, 70
-    ir = np.stack([oracle.noise(370 + c, L) for c in range(C)])
-    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
-    if head == "arbitrary":
-        rng = np.random.default_rng(5)
-        noise = (rng.standard_normal((C, B + 1)) + 1j * rng.standard_normal((C, B + 1))).astype(np.complex64)
-        parts[:, 0] += 0.05 * noise
-    sig = np.stack([oracle.noise(380 + c, B * nb) for c in range(C)])
-    ref = oracle.dense_convolve(sig, parts)
-    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1])
-    conv.filter(parts)
+    conv = neo_gpu.UpolsConvolver(2, 128, 600)
     conv.set_batch(False)
-    conv.set_ahead(True)
-    t = torch.from_numpy(sig).cuda()
-    conv.process_blocks(t)
+    assert conv.ahead_info()[0]
+    x = torch.rand((2, 128 * 140), device="cuda")
+    conv.process_blocks(x)
     torch.cuda.synchronize()
-    assert peak_err(t.cpu().numpy(), ref) <= TOL
+    assert torch.count_nonzero(x).item() == 0
 
 
-@pytest.mark.parametrize("method", ["upols", "upola"])
-@pytest.mark.parametrize("B", [256, 512])
-@pytest.mark.parametrize("subw", ["8", "16"])
-@pytest.mark.parametrize("slab_nt", ["0", "1"])
-def test_ahead_subwindow_lengths(neo_gpu, oracle, monkeypatch, method, B, subw, slab_nt):
-    """Lookahead sub-windows of 8 and 16 blocks (one or three sub-window passes per window;
-    block steps walk up to 7 / 15 row pairs), slabs stored with either cache policy, over
-    three windows with ring wraparound."""
+def test_level_timing_detail(neo_gpu):
+    """timing_detail(): block step, Toeplitz slices, far slice and whole step per timed step."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("NEO_HIP_SUBWINDOW", subw)
-    monkeypatch.setenv("NEO_HIP_SLAB_NT", slab_nt)
-    C, L, nb = 2, 45 * B, 100
-    ir = np.stack([oracle.noise(390 + c, L) for c in range(C)])
-    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
-    sig = np.stack([oracle.noise(395 + c, B * nb) for c in range(C)])
-    ref = oracle.dense_convolve(sig, parts, method=method)
-    conv = neo_gpu.UpolsConvolver(C, B, parts.shape[1], method=method)
-    conv.filter(parts)
+    conv = neo_gpu.UpolsConvolver(4, 256, 300)
     conv.set_batch(False)
-    conv.set_ahead(True)
-    t = torch.from_numpy(sig).cuda()
-    conv.process_blocks(t)
-    torch.cuda.synchronize()
-    assert peak_err(t.cpu().numpy(), ref) <= TOL
+    x = torch.zeros((4, 256 * 12), device="cuda")
+    conv.set_timing(True, every=3)
+    conv.process_blocks(x)
+    conv.set_timing(False)
+    parts = conv.timing_detail()
+    assert [n for _, n in parts] == [4, 4, 4, 4]  # steps 0, 3, 6, 9
+    assert all(ms > 0 for ms, _ in parts)
+    assert parts[3][0] >= max(ms for ms, _ in parts[:3]) - 1e-6
 
 
 def test_ahead_mixed_paths(neo_gpu, oracle):
@@ -733,8 +701,16 @@ def test_ahead_defaults_and_errors(neo_gpu):
     big = neo_gpu.UpolsConvolver(64, 512, 300)  # filter + FDL 157 MB: HBM-bound step
     assert big.ahead_info()[0]
     assert neo_gpu.UpolsConvolver(1, 512, 188).ahead_info()[0]  # C3
-    small = neo_gpu.UpolsConvolver(1, 128, 20)  # P < 2T: the plain step
+    small = neo_gpu.UpolsConvolver(1, 128, 20)  # P < 64: the plain step
     assert not small.ahead_info()[0]
+    huge = neo_gpu.UpolsConvolver(1, 2048, 100)  # the block step is built for B <= 1024
+    assert not huge.ahead_info()[0]
+    with pytest.raises(RuntimeError):
+        huge.set_ahead(True)
+    with pytest.raises(ValueError):
+        neo_gpu.UpolsConvolver(1, 128, 20, options={"nope": 1})
+    with pytest.raises(RuntimeError):
+        neo_gpu.UpolsConvolver(1, 128, 20, options={"batch_blocks": 3})
     v2 = neo_gpu.UpolsConvolver(2, 128, 4, method="upola_v2")
     assert not v2.ahead_info()[0]
     with pytest.raises(RuntimeError):
