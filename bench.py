@@ -145,11 +145,6 @@ def load_pmc_traffic(workload: str, kernel: str = ""):
     return None
 
 
-def timing_stride(steps: int) -> int:
-    """Time every n-th step of the timed region: >= 12 samples, at most every 16th."""
-    return max(1, min(16, steps // 12))
-
-
 def cpu_baseline_upols(C, B, L, threads):
     """The oracle's restatement of dense_convolve<upols_convolver> (kind "port") on a
     bounded sample of the same workload, on this box's host cores."""
@@ -237,18 +232,21 @@ class Feed:
 
 def algorithmic_bytes(C, B, P, plan):
     """Algorithmic bytes per streaming step, per part:
-    block step: in + previous block read + write + out (4 x 4B) + FDL row write and H0 (2 x 8B)
-                + a0 - 1 filter/FDL row pairs (16B each) + one slab per level (8B)
+    block step: window (previous block + this block), previous-block write, output (4 x 4B),
+                FDL row write, H0 and the rest spectrum (3 x 8B)
+    rest role:  a0 - 1 filter/FDL row pairs (16B each) + one slab per level (8B) + the
+                rest spectrum write (8B)
     Toeplitz level l (window T, band [a, b)), C*B/T columns per step: per column b - a filter
                 rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
     far level, C*B/128 columns per step: per column 256 FDL rows, 256 stored + nseg - 1 older
                 row-pair spectra, nseg segment spectra (256 f each) and 128 far-field entries."""
     nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
-    block = C * B * (16 + 16 + 16 * (plan["a0"] - 1) + 8 + 8 * nlev)
+    block = C * B * (16 + 24)
+    rest = C * B * (16 * (plan["a0"] - 1) + 8 * nlev + 8)
     toep = sum(C * B / T * 8 * (2 * (b - a) + 2 * T - 1) for T, a, b in zip(plan["T"], plan["a"], plan["b"]))
     ns = plan["nseg"]
     far = C * B / 128 * 8 * (256 * (2 * ns + 1) + 128) if ns else 0.0
-    return block, toep, far
+    return block, rest, toep, far
 
 
 def oracle_parity(x, y, feed, irh, B, chans, K=4, threads=16):
@@ -296,7 +294,6 @@ def run_upols(args, world, rank, local):
     y = torch.empty_like(x)
     stream = torch.cuda.current_stream(dev).cuda_stream
     feed = Feed(conv, x, y, nx, B, stream)
-    stride = timing_stride(args.steps)
 
     def warm():
         t_warm = time.perf_counter()
@@ -306,28 +303,35 @@ def run_upols(args, world, rank, local):
             feed.run(64)
             torch.cuda.synchronize()
 
-    def timed_steps():
-        """args.steps single-block steps; per-part kernel time from HIP events the C-ABI
-        records on the launch stream around every `stride`-th step."""
+    def timed_region():
+        """args.steps single-block steps, nothing else in the timed region."""
         barrier(world)
         torch.cuda.synchronize()
-        conv.timing_detail()  # drain
-        conv.set_timing(True, every=stride)
         t0 = time.perf_counter()
         feed.run(args.steps)
         torch.cuda.synchronize()
         barrier(world)
         t1 = time.perf_counter()
+        assert torch.isfinite(y).all().item()
+        return max_over_ranks(t1 - t0, world)
+
+    def instrumented():
+        """max(steps, 64) more steps with HIP events the C-ABI records on the launch stream
+        around every part of every step: the per-part kernel times."""
+        conv.timing_detail()  # drain
+        conv.set_timing(True, every=1)
+        feed.run(max(args.steps, 64))
+        torch.cuda.synchronize()
         conv.set_timing(False)
         det = [(ms / n if n else None) for ms, n in conv.timing_detail()]
-        assert torch.isfinite(y).all().item()
-        return max_over_ranks(t1 - t0, world), [max_over_ranks(d, world) if d is not None else None for d in det]
+        return [max_over_ranks(d, world) if d is not None else None for d in det]
 
     samples = world * C * B * args.steps
     # the plain single-block step: one pass over filter + FDL per block (k_upols_step)
     conv.set_ahead(False)
     warm()
-    el_plain, det_plain = timed_steps()
+    el_plain = timed_region()
+    det_plain = instrumented()
     bytes_plain = C * (16 * P * B + 20 * B)  # filter + FDL stream (packed bins) + FDL row write + in/prev
     gbs_plain = bytes_plain / (det_plain[0] * 1e-3) / 1e9
     plain = {"value": samples / el_plain / 1e6, "ms_per_step": el_plain * 1e3 / args.steps,
@@ -337,7 +341,7 @@ def run_upols(args, world, rank, local):
     if levels:
         conv.set_ahead(True)
     warm()
-    elapsed, det = timed_steps()
+    elapsed = timed_region()
     parity = None
     if irh is not None:
         irn = None
@@ -349,6 +353,7 @@ def run_upols(args, world, rank, local):
                   "channels": sorted({0, C // 2, C - 1}), "blocks": 4,
                   "what": "last 4 blocks of the timed region vs oracle dense_convolve over their input history "
                           "(peak-normalized; bar 1e-5)"}
+    det = instrumented()
     # per-step latency: every step of a separate 256-step run bracketed by events (GPU time of the
     # step, first to last event), the distribution a per-block real-time caller sees
     conv.step_times()
@@ -363,19 +368,18 @@ def run_upols(args, world, rank, local):
                "note": "GPU time per step (HIP events around every step, which add their own records)"}
 
     if levels:
-        bs, tp, fr = algorithmic_bytes(C, B, P, plan)
+        bs, rs, tp, fr = algorithmic_bytes(C, B, P, plan)
         parts = [("block step k_upols_lvl<%d>" % B, det[0], bs),
-                 ("Toeplitz level slices k_lvl_toep (T = %s)" % "/".join(map(str, plan["T"])), det[1], tp),
-                 ("far slice k_lvf_slice (%d segments)" % plan["nseg"], det[2], fr)]
+                 ("slices k_lvl_slices (rest spectrum; Toeplitz T = %s; far %d segments)"
+                  % ("/".join(map(str, plan["T"])), plan["nseg"]), det[1], rs + tp + fr)]
         step_ms = det[3]
         kernels = []
         for name, ms, by in parts:
-            if not by:
-                continue
             gbs = by / (ms * 1e-3) / 1e9
             kernels.append({"kernel": name, "ms_per_step": ms, "share_of_step": ms / step_ms,
                             "algorithmic_bytes_per_step": by, "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS,
-                            "traffic": load_pmc_traffic(args.workload, name.split()[-2] if "(" in name else name)})
+                            "traffic": load_pmc_traffic(args.workload, name.split()[1])})
+        kernels[1]["bytes_by_role"] = {"rest": rs, "toeplitz": tp, "far": fr}
         dom = max(kernels, key=lambda k: k["ms_per_step"])
         step_bytes = bs + tp + fr
         roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",

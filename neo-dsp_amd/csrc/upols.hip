@@ -857,7 +857,7 @@ static int drain_events(upols_t* h)
             h->part_ms[k] += t;
             ++h->part_n[k];
         }
-        if (e.n == 4) {
+        if (e.n >= 3) {
             h->part_ms[3] += tot;
             ++h->part_n[3];
         }

@@ -17,17 +17,16 @@ constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read 
 // each: 168 MiB 17.8 us/step, 216 MiB 18.3, 126 MiB 18.1)
 constexpr double kBatchCacheBudgetBytes = 168.0 * 1024 * 1024;
 // streaming levels (upols_levels.hip)
-constexpr int kLvA0 = 16;    // partitions of the block step itself
-constexpr int kLvMax = 4;    // Toeplitz levels + far
+constexpr int kLvA0 = 4;     // partitions of the block step and its rest spectrum
+constexpr int kLvToep = 5;   // Toeplitz levels
 constexpr int kFarT = 128;   // far level: blocks per window (256-point partition-axis transform)
 constexpr int kFarA = 256;   // far level: first partition (2 kFarT)
-constexpr int kFarSPG = 2;   // far level: segments per sub-unit workgroup
 constexpr int kFarRing = 2 * kFarA;  // far level: FDL ring rows needed (a slice reads back 383 blocks)
 
 struct level_plan {
     int a0 = 1;                      // the block step takes partitions [0, a0)
     int n = 0;                       // Toeplitz levels
-    int T[3] = {}, a[3] = {}, b[3] = {};  // window (blocks) and partition band [a, b) per level
+    int T[kLvToep] = {}, a[kLvToep] = {}, b[kLvToep] = {};  // window (blocks) and partition band [a, b) per level
     int nseg = 0;                    // far segments of kFarT partitions from kFarA (0: no far level)
 };
 }  // namespace neo_hip
@@ -56,16 +55,13 @@ struct neo_hip_upols {
     neo_hip::level_plan lv;
     int64_t lv_n = -1;              // blocks since the levels were primed (-1: prime at the next step)
     bool lv_ready = false;          // level buffers allocated
-    neo_hip::cf* lv_slab[3] = {};   // Toeplitz level slabs [2][C][T][B]
+    neo_hip::cf* lv_slab[neo_hip::kLvToep] = {};  // Toeplitz level slabs [2][C][T][B]
+    neo_hip::cf* lv_rest = nullptr; // the next block's spectrum without partition 0 [C][B]
     neo_hip::cf* fv_hf = nullptr;   // far segment spectra [C][nseg][256][B]
-    neo_hip::cf* fv_hf0 = nullptr;  // far bin 0 second coefficient [C][nseg][256]
     neo_hip::cf* fv_xf = nullptr;   // far FDL row-pair spectra, ring of nseg slots [C][nseg][256][B]
-    neo_hip::cf* fv_xf0m = nullptr; // bin 0 conj(Z[-f]) of each slot [C][nseg][256]
     neo_hip::cf* fv_ff = nullptr;   // far field [2][C][128][B]
-    neo_hip::cf* fv_part = nullptr; // far sub-unit partial spectra of one slice
-    int* fv_cnt = nullptr;          // far sub-unit arrival counters of one slice
     neo_hip::cf* fv_tw = nullptr;   // 256-point twiddles
-    int fv_nsub = 1;                // far sub-units per unit
+    neo_hip::cf* fv_acc = nullptr;  // far phase-1 sums of two slices [2][units][256][16]
     bool fv_dirty = true;           // far segment spectra to recompute (filter changed)
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)

@@ -5,25 +5,27 @@
 //   Y[t][k] = sum_{p < P} H[p][k] X[t - p][k]       (uniform_partitioned_convolver.hpp:47-65;
 //                                                   fdl_index.hpp:23-36: partition p meets FDL row t - p)
 // The partitions are cut into bands by level:
-//   level 0   p in [0, 16)        the block step itself (its own FDL row for p = 0, rows t-15..t-1)
-//   level 1   p in [16, 32)       T = 8-block windows
-//   level 2   p in [32, 64)       T = 16
-//   level 3   p in [64, 256)      T = 32
+//   p = 0                         the block step itself (its own FDL row)
+//   p in [1, 4)                   the next block's "rest" spectrum, one step ahead
+//   Toeplitz  [4, 8) [8, 16) [16, 32) [32, 64) [64, 256): windows of 2, 4, 8, 16, 32 blocks
 //   far       p in [256, P)       T = 128, by a 256-point transform along the partition axis
 // A level with window T covers band [2T, b): for the blocks t_W + j (j < T) of a window its
 // rows t_W + j - p are at most t_W - T - 1, so the whole window's contribution can be computed
-// during the PREVIOUS window, 1/T of it per block step (1/T of the bins of every channel),
-// into a slab per block of the window (double-buffered). A block step then only adds its
-// slabs and the 15 newest partitions: every step does the same work, there is no window
-// pass, and no step waits for one (the lookahead of round 1 ran a pass over the filter at the
-// start of every 32-block window and a 0.63 ms far pass every 128 blocks).
+// during the PREVIOUS window, 1/T of it per step (a slice of the columns of every channel),
+// into a slab per block of the window (double-buffered); the slices run one step ahead, so a
+// window's slabs are complete one step before its first block. After every block step one
+// more launch (k_lvl_slices) runs the slices and sums, for the NEXT block, its partitions
+// 1..15 (their rows exist already) and its level slabs into one "rest" spectrum; the block
+// step itself is then the window r2c, rest + H0 X and the c2r. Every step does the same work
+// and no step waits for a window pass (round 1 ran a pass over the filter at the start of
+// every 32-block window and a 0.63 ms far pass every 128 blocks).
 //
 // Levels 1-3 are direct Toeplitz MACs (k_lvl_toep); the far level is, per bin, a sum over
 // segments q >= 2 of 128 partitions of DFT256(S_q) . DFT256(h_q) with S_q the 256 FDL rows
 // t_W - (q+1) 128 ... t_W - (q-1) 128 - 1 (outputs 128..255 of the circular convolution are
 // the window's 128 blocks, no wrap reaches them). S_{q+1} of window W+1 is S_q of window W, so
 // each window transforms ONE new row pair per bin (segment 2) and keeps the spectra in a ring
-// of NSEG slots (XF); the rest is a stream of XF . HF products (k_lvf_slice).
+// of NSEG slots (XF); the rest is a stream of XF . HF products (far_role).
 #include "upols_device.hpp"
 #include "upols_handle.hpp"
 
@@ -38,8 +40,9 @@ void plan_levels(int P, level_plan& lp)
 {
     lp = level_plan{};
     lp.a0 = std::min(P, kLvA0);
-    static constexpr int T[3] = {8, 16, 32}, A[3] = {16, 32, 64}, Bd[3] = {32, 64, kFarA};
-    for (int l = 0; l < 3; ++l) {
+    static constexpr int T[kLvToep] = {2, 4, 8, 16, 32}, A[kLvToep] = {4, 8, 16, 32, 64},
+                         Bd[kLvToep] = {8, 16, 32, 64, kFarA};
+    for (int l = 0; l < kLvToep; ++l) {
         if (P <= A[l]) break;
         lp.T[lp.n] = T[l];
         lp.a[lp.n] = A[l];
@@ -50,132 +53,448 @@ void plan_levels(int P, level_plan& lp)
 }
 
 // ---------------------------------------------------------------------------------------
-// Toeplitz level slice: for the 16-column units [u0, u1) (unit u = channel u / gpc, columns
-// 16 (u % gpc) ...), the T slabs of the window starting at ring row tw:
-//   slab[c][j][k] = sum_{p = a}^{b-1} H[c][p][k] X[c][(tw + j - p) mod R][k],  j < T.
-// Lanes: 16 columns x NPG partition groups of NPL partitions; a lane loads its NPL filter
-// rows and the NPL + T - 1 FDL rows they meet, MACs in registers, and the groups are summed
-// (shuffles in the wave, LDS across waves). 256 lanes = 256 / (16 NPG) units per workgroup.
-template<int T, int NPL, int NPG>
-__global__ __launch_bounds__(256) void k_lvl_toep(const cf* __restrict__ H, const cf* __restrict__ fdl,
-                                                  cf* __restrict__ slab, int a, int b, int tw, int ring, int u0,
-                                                  int u1, int gpc, int C, int B, int64_t cstride, int64_t pstride)
+// device helpers
+
+constexpr int kFN = 2 * kFarT;  // far level: partition-axis transform length
+
+// 256-point transforms of NC columns held by lanes (a, cp), a < 16, cp < NC: on entry
+// v[n2] = x[a + 16 n2], on exit v[k1] = X[16 k1 + a] (16-point DFTs in registers, twiddle,
+// LDS transpose, 16-point DFTs). Every lane of the workgroup calls it (barriers inside);
+// lanes with active = false only take part in the barriers.
+template<int DIR, int NC>
+__device__ __forceinline__ void col_fft(cf (&v)[16], cf* lds, const cf* tw, int a, int cp, bool active)
 {
-    static_assert(NPG >= 4 && NPG <= 16 && T % 4 == 0, "toeplitz slice geometry");
-    constexpr int UPW = 256 / (16 * NPG), WPU = NPG / 4, NX = NPL + T - 1;
-    __shared__ cf red[WPU > 1 ? UPW * (WPU - 1) * T * 16 : 1];
-    const int t = threadIdx.x, col = t & 15, pg = (t >> 4) % NPG, us = t / (16 * NPG);
-    const int wu = pg >> 2, q4 = pg & 3;  // wave of the unit, group within the wave
-    const int u = u0 + int(blockIdx.x) * UPW + us;
-    const bool live = u < u1;
-    const int uc = live ? u : u1 - 1;
-    const int c = uc / gpc, k = (uc - c * gpc) * 16 + col;
-    const int pa = a + pg * NPL;
-    const cf* Hc = H + int64_t(c) * cstride + k;
-    const cf* Xc = fdl + int64_t(c) * cstride + k;
-    cf acc[T];
+    if (active) {
+        dft<16, DIR>(v);
 #pragma unroll
-    for (int j = 0; j < T; ++j) acc[j] = cf{0.f, 0.f};
-    if (live && pa < b) {
+        for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], twiddle<kFN, DIR>(tw, a * k));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) lds[(k * 16 + a) * NC + cp] = v[k];
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+        for (int n = 0; n < 16; ++n) v[n] = lds[(a * 16 + n) * NC + cp];
+    }
+    __syncthreads();
+    if (active) dft<16, DIR>(v);
+}
+
+// packed complex MAC: acc = (re, im) += h x as (hr, hr)(xr, xi) + (-hi, hi)(xi, xr), two
+// v_pk_fma_f32; the packed bin 0 (DC, Nyquist: two real products) takes (hr, hi)(xr, xi)
+struct pk_coef {
+    f2v h1, h2;
+    __device__ __forceinline__ pk_coef(cf h, bool bin0)
+    {
+        const float s = bin0 ? 0.f : h.y;
+        h1 = f2v{h.x, bin0 ? h.y : h.x};
+        h2 = f2v{-s, s};
+    }
+    __device__ __forceinline__ void mac(f2v& acc, cf x) const
+    {
+        const f2v xv = {x.x, x.y};
+        acc = __builtin_elementwise_fma(h1, xv, acc);
+        acc = __builtin_elementwise_fma(h2, xv.yx, acc);
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// The per-step slices kernel: one launch after every block step, workgroups by role.
+//   rest      the next block's spectrum without partition 0: its partitions 1 .. a0 - 1
+//             (rows up to this block's) plus the level slabs of the next block
+//   Toeplitz  1/T of the next window of each Toeplitz level (a slice of its columns)
+//   far       1/128 of the next far window (a slice of its 8-column units)
+// Every role reads FDL rows up to this step's block only; the block step of the next call
+// then needs nothing but its window, this spectrum and H0.
+struct toep_arg {
+    cf* slab;           // the target window's slabs [C][T][B]
+    int T, a, b;        // window, band [a, b)
+    int tw;             // ring row of the window's first block
+    int u0, u1, nwg;    // units (16 columns x one of JH block halves) of this slice, workgroups
+};
+
+struct slice_args {
+    const cf* H;
+    cf* fdl;
+    int ring, C, B;
+    int64_t cstride, pstride;
+    // rest role
+    cf* rest;           // [C][B]
+    int nrest, wr, a0;  // workgroups; ring row of the newest FDL row (block t); block step partitions
+    int nsl;
+    const cf* sl[kLvToep];  // slab of block t + 1 per level, channel 0
+    int64_t scs[kLvToep];   // channel strides
+    // Toeplitz roles
+    int ntp;
+    toep_arg tp[kLvToep];
+    // far level (16-column units), common
+    int M, nseg, fnfresh;
+    const cf* hf;
+    cf* xf;
+    const cf* twf;
+    // far phase 1: stored-segment MAC (16 workgroups per unit) and fresh transforms (1 per unit)
+    int f1nwg, f1u0, f1tw, f1wn;
+    cf* f1acc;  // [units][256 f][16]
+    // far phase 2 (the slice phase 1 did one step earlier): fresh products, sum, inverse transform
+    int f2nwg, f2u0, f2wn;
+    const cf* f2acc;
+    cf* f2ff;   // the target far window [C][128][B]
+};
+
+constexpr int kSliceLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange, twiddles
+
+// rest[c][k] for block t + 1 = sum_{p=1}^{a0-1} H[p] X[t + 1 - p] + the Toeplitz slabs of block t + 1
+__device__ __forceinline__ void rest_role(const slice_args& a, int bid)
+{
+    const int t = threadIdx.x, Q = a.B / 2;  // float4 (2 bins) per row
+    const int lpc = Q < 256 ? Q : 256, cpw = 256 / lpc, gq = Q / lpc;
+    const int c = (bid / gq) * cpw + t / lpc, q = (bid % gq) * lpc + t % lpc;
+    if (c >= a.C) return;
+    const int64_t crow = int64_t(c) * a.cstride, ps4 = a.pstride / 2;
+    const float4* H4 = reinterpret_cast<const float4*>(a.H + crow);
+    const float4* F4 = reinterpret_cast<const float4*>(a.fdl + crow);
+    float4 sum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int l = 0; l < kLvToep; ++l) {
+        if (l < a.nsl) {
+            const float4 r = reinterpret_cast<const float4*>(a.sl[l] + int64_t(c) * a.scs[l])[q];
+            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+        }
+    }
+    constexpr int KC = 8;  // row pairs in flight
+    acc4 a0v = {0.f, 0.f, 0.f, 0.f}, a1v = a0v;
+    for (int pb = 1; pb < a.a0; pb += KC) {
+        float4 hv[KC], xv[KC];
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+            const int p = pb + k;
+            if (p < a.a0) {
+                const int r = a.wr + 1 - p < 0 ? a.wr + 1 - p + a.ring : a.wr + 1 - p;
+                hv[k] = H4[int64_t(p) * ps4 + q];
+                xv[k] = F4[int64_t(r) * ps4 + q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+            if (pb + k < a.a0) mac2(a0v, a1v, hv[k], xv[k]);
+    }
+    const cf b0 = finish(a0v, q == 0), b1 = finish(a1v, false);
+    reinterpret_cast<float4*>(a.rest + int64_t(c) * a.B)[q] =
+        make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
+}
+
+// Toeplitz level: for the units [u0, u1) (unit u = (channel, 16 columns, block half jh)),
+//   slab[c][j][k] = sum_{p = a}^{b-1} H[c][p][k] X[c][(tw + j - p) mod R][k],  j in half jh.
+// Lanes: 16 columns x NPG partition groups of NPL partitions; a lane loads its NPL filter
+// rows and the NPL + T/JH - 1 FDL rows they meet and MACs in registers (packed FMA); the
+// groups are summed (shuffles in the wave, LDS across waves). NPG = 1: a lane takes the
+// whole band of its column.
+template<int T, int NPL, int NPG, int JH>
+__device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
+{
+    static_assert((NPG == 1 || NPG == 4 || NPG == 8 || NPG == 16) && T % JH == 0, "toeplitz slice geometry");
+    constexpr int TJ = T / JH, LPU = 16 * NPG, UPW = 256 / LPU, WPU = NPG < 4 ? 1 : NPG / 4, NX = NPL + TJ - 1;
+    f2v* red = reinterpret_cast<f2v*>(smem);  // [UPW][WPU - 1][TJ][16]
+    const int t = threadIdx.x, col = t & 15, pg = (t >> 4) % NPG, us = t / LPU;
+    const int wu = pg >> 2, q4 = pg & 3;  // wave of the unit, group within the wave
+    const int gpc = sa.B / 16;
+    // two block halves of the same columns read the same filter and most of the same FDL rows:
+    // their workgroups run on one XCD (workgroups go round-robin over the 8 XCDs) so the second
+    // read hits its L2 -- within every 16 workgroups, XCD x takes the unit pair 2 x, 2 x + 1
+    int wb = bid;
+    if constexpr (JH == 2 && UPW == 1) {
+        if (bid < ta.nwg / 16 * 16) {
+            const int r = bid & 15;
+            wb = (bid & ~15) + (r & 7) * 2 + (r >> 3);
+        }
+    }
+    const int u = ta.u0 + wb * UPW + us;
+    const bool live = u < ta.u1;
+    const int uc = live ? u : ta.u1 - 1;
+    const int jh = uc % JH, cg = uc / JH, c = cg / gpc, k = (cg - c * gpc) * 16 + col;
+    const int j0 = jh * TJ, pa = ta.a + pg * NPL;
+    const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
+    const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
+    f2v acc[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[j] = f2v(0.f);
+    if (live && pa < ta.b) {
         cf xr[NX], hm[NPL];
-        // xr[i] = X[tw + T - 1 - pa - i]: partition pa + m meets block j at i = T - 1 - j + m
+        // xr[i] = X[tw + j0 + TJ - 1 - pa - i]: partition pa + m meets block j0 + jj at i = TJ - 1 - jj + m
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            int r = tw + T - 1 - pa - i;
-            r = r < 0 ? r + ring : r;
-            xr[i] = ld_nt(Xc + int64_t(r) * pstride);
+            int r = ta.tw + j0 + TJ - 1 - pa - i;
+            r = r < 0 ? r + sa.ring : r;
+            xr[i] = ld_nt(Xc + int64_t(r) * sa.pstride);
         }
 #pragma unroll
-        for (int m = 0; m < NPL; ++m) hm[m] = pa + m < b ? ld_nt(Hc + int64_t(pa + m) * pstride) : cf{0.f, 0.f};
-        // packed bin 0 = {DC, Nyquist}: two real products (hr xr, hi xi) instead of the complex one
-        const bool z = k == 0;
+        for (int m = 0; m < NPL; ++m) hm[m] = pa + m < ta.b ? ld_nt(Hc + int64_t(pa + m) * sa.pstride) : cf{0.f, 0.f};
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
-            const cf h = hm[m];
-            const float hn = z ? 0.f : -h.y, ha = z ? h.y : h.x, hb = z ? 0.f : h.y;
+            const pk_coef h(hm[m], k == 0);
 #pragma unroll
-            for (int j = 0; j < T; ++j) {
-                const cf x = xr[T - 1 - j + m];
-                acc[j].x = fmaf(h.x, x.x, fmaf(hn, x.y, acc[j].x));
-                acc[j].y = fmaf(ha, x.y, fmaf(hb, x.x, acc[j].y));
-            }
+            for (int jj = 0; jj < TJ; ++jj) h.mac(acc[jj], xr[TJ - 1 - jj + m]);
         }
     }
-    // the 4 groups of a wave (lanes 16 apart)
+    if constexpr (NPG >= 4) {  // the 4 groups of a wave (lanes 16 apart)
 #pragma unroll
-    for (int j = 0; j < T; ++j) {
-        acc[j].x += __shfl_xor(acc[j].x, 16);
-        acc[j].y += __shfl_xor(acc[j].y, 16);
-        acc[j].x += __shfl_xor(acc[j].x, 32);
-        acc[j].y += __shfl_xor(acc[j].y, 32);
+        for (int j = 0; j < TJ; ++j) {
+            acc[j].x += __shfl_xor(acc[j].x, 16);
+            acc[j].y += __shfl_xor(acc[j].y, 16);
+            acc[j].x += __shfl_xor(acc[j].x, 32);
+            acc[j].y += __shfl_xor(acc[j].y, 32);
+        }
     }
-    // every lane of a wave now holds its wave's sum; lane group q4 owns blocks j = 4 i + q4
+    // every lane of a wave now holds its wave's sum; the lanes of group 0 carry it on (a
+    // per-lane choice of blocks would index the accumulators at run time: scratch)
     if constexpr (WPU > 1) {
-        if (wu > 0) {
+        if (wu > 0 && q4 == 0) {
 #pragma unroll
-            for (int i = 0; i < T / 4; ++i) {
-                cf v = acc[4 * i];
-                v = q4 == 1 ? acc[4 * i + 1] : v;
-                v = q4 == 2 ? acc[4 * i + 2] : v;
-                v = q4 == 3 ? acc[4 * i + 3] : v;
-                red[((us * (WPU - 1) + wu - 1) * T + 4 * i + q4) * 16 + col] = v;
-            }
+            for (int j = 0; j < TJ; ++j) red[((us * (WPU - 1) + wu - 1) * TJ + j) * 16 + col] = acc[j];
         }
         __syncthreads();
     }
-    if (wu == 0 && live) {
-        cf* o = slab + (int64_t(c) * T) * B + k;
+    if (wu == 0 && q4 == 0 && live) {
+        cf* o = ta.slab + (int64_t(c) * T + j0) * sa.B + k;
 #pragma unroll
-        for (int i = 0; i < T / 4; ++i) {
-            cf v = acc[4 * i];
-            v = q4 == 1 ? acc[4 * i + 1] : v;
-            v = q4 == 2 ? acc[4 * i + 2] : v;
-            v = q4 == 3 ? acc[4 * i + 3] : v;
+        for (int j = 0; j < TJ; ++j) {
+            f2v v = acc[j];
             if constexpr (WPU > 1) {
 #pragma unroll
-                for (int w = 1; w < WPU; ++w) {
-                    const cf r = red[((us * (WPU - 1) + w - 1) * T + 4 * i + q4) * 16 + col];
-                    v.x += r.x;
-                    v.y += r.y;
-                }
+                for (int w = 1; w < WPU; ++w) v += red[((us * (WPU - 1) + w - 1) * TJ + j) * 16 + col];
             }
-            o[int64_t(4 * i + q4) * B] = v;
+            o[int64_t(j) * sa.B] = cf{v.x, v.y};
         }
     }
-    (void)C;
 }
 
-// ---------------------------------------------------------------------------------------
-// far level
-constexpr int kFN = 2 * kFarT;  // partition-axis transform length
+// Far level, for 16-column units (unit = channel c, columns 16 g ...): the far field of window
+// wn (first block at ring row tw), ff[c][j][k], j < 128:
+//   FF[j] = IDFT256( sum_s XF_s . HF_s )[128 + j] / 256,   s = 0 .. nseg - 1 (segment q = s + 2)
+// XF_s = DFT256 of the FDL rows tw - (s + 3) 128 ... + 255 (the row pair of segment s), stored
+// in slot (wn - s - 1) mod M. Segments s < fnfresh are transformed from the FDL (s = 0 in
+// steady state, all when the pipeline is primed), the others were stored by earlier windows.
+// Two phases, one step apart (the kernel boundary between them is the only synchronization:
+// an agent-scope release per workgroup costs an L2 write-back across the XCDs):
+//   phase 1  16 workgroups per unit MAC the stored segments for 16 f each, one (f, column) per
+//            lane with every load of the lane in flight at once, into acc[unit][f][col]; one
+//            more transforms the fresh row pairs and stores them to their slots
+//   phase 2  one workgroup per unit: acc + the fresh segments' products, the inverse transform
+// Packed bin 0 holds two real sequences (DC and Nyquist): its spectra are stored packed the
+// real-FFT way, W[f] = X_dc[f] (f <= 128) and W[256 - f] = X_ny[f] (0 < f < 128), with
+// W[0] = (X_dc[0], X_ny[0]) and W[128] = (X_dc[128], X_ny[128]) real pairs (k_lvf_filter
+// packs the segment spectra the same way): the MAC is the same complex product except two
+// real products at f = 0 and 128, and one unpack before the inverse transform restores
+// Y = Y_dc + i Y_ny.
+constexpr int kFarParts = 17;  // phase-1 workgroups per far unit
 
-// 256-point transform of the column held by lanes (a, cp): on entry v[n2] = x[a + 16 n2], on
-// exit v[k1] = X[16 k1 + a] (16-point DFTs in registers, twiddle, LDS transpose, 16-point DFTs)
-template<int DIR>
-__device__ __forceinline__ void col_fft(cf (&v)[16], cf* lds, const cf* tw, int a, int cp)
+// Z = DFT(x_dc + i x_ny) -> packed W (real-FFT packing of X_dc, X_ny) at f, from Z[f], Z[-f]
+__device__ __forceinline__ cf pack_bin0(cf zf, cf zm, int f)
 {
-    dft<16, DIR>(v);
+    if (f == 0 || f == kFN / 2) return zf;  // (Re, Im) = (X_dc, X_ny), both real here
+    if (f < kFN / 2) return cscale(cadd(zf, cconj(zm)), 0.5f);  // X_dc[f]
+    const cf d = csub(zm, cconj(zf));                            // f > 128: X_ny[256 - f] = (Z[-f] - conj Z[f]) / 2i
+    return cf{0.5f * d.y, -0.5f * d.x};
+}
+
+// packed W of bin 0 -> Y = Y_dc + i Y_ny at f, from W[f], W[-f]
+__device__ __forceinline__ cf unpack_bin0(cf wf, cf wm, int f)
+{
+    if (f == 0 || f == kFN / 2) return wf;
+    // f < 128: Y_dc[f] + i Y_ny[f] = W[f] + i W[256 - f]; f > 128: conj(W[256 - f]) + i conj(W[f])
+    const cf dc = f < kFN / 2 ? wf : cconj(wm);
+    const cf ny = f < kFN / 2 ? wm : cconj(wf);
+    return cf{dc.x - ny.y, dc.y + ny.x};
+}
+
+// bin 0 (column 0, lanes cp == 0) of a spectrum held with v[i] at f = FOFF(i): pack or unpack
+// through LDS z; every lane calls (barrier inside)
+template<bool PACK, class F>
+__device__ __forceinline__ void bin0_exchange(cf (&v)[16], cf* z, int cp, F foff)
+{
+    if (cp == 0) {
 #pragma unroll
-    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], twiddle<kFN, DIR>(tw, a * k));
-#pragma unroll
-    for (int k = 0; k < 16; ++k) lds[(k * 16 + a) * 16 + cp] = v[k];
+        for (int i = 0; i < 16; ++i) z[foff(i)] = v[i];
+    }
     __syncthreads();
+    if (cp == 0) {
 #pragma unroll
-    for (int n = 0; n < 16; ++n) v[n] = lds[(a * 16 + n) * 16 + cp];
-    __syncthreads();
-    dft<16, DIR>(v);
+        for (int i = 0; i < 16; ++i) {
+            const int f = foff(i);
+            const cf m = z[(kFN - f) & (kFN - 1)];
+            v[i] = PACK ? pack_bin0(v[i], m, f) : unpack_bin0(v[i], m, f);
+        }
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, int(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ cf buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    return __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 2 /* streaming */));
+}
+
+__device__ __forceinline__ void far1_role(const slice_args& sa, int bid, char* smem)
+{
+    cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
+    cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
+    cf* tws = z + kFN;                       // twiddles
+    const int t = threadIdx.x;
+    const int ul = bid / kFarParts, part = bid - ul * kFarParts;
+    const int gpc = sa.B / 16, u = sa.f1u0 + ul, c = u / gpc, g = u - c * gpc;
+    const bool unit0 = g == 0;  // uniform per workgroup: the unit holding packed bin 0
+    const int M = sa.M, nseg = sa.nseg;
+    auto slot = [&](int s) { return ((sa.f1wn - s - 1) % M + M) % M; };
+    const int64_t fs = sa.B;  // stride between f rows of a spectrum (complex)
+    const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));  // bytes per spectrum (a channel's span < 2 GiB)
+    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;       // first stored segment
+    // buffer loads: 32-bit lane offsets, segment / slot offsets in SGPRs
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
+    if (part < 16) {
+        // stored segments, lane (f, col)
+        const int col = t & 15, f = part * 16 + (t >> 4), k = g * 16 + col;
+        const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+        const int vo = int((int64_t(f) * fs + k) * int(sizeof(cf)));
+        const bool z0 = unit0 && col == 0 && (f & (kFN / 2 - 1)) == 0;  // packed bin 0 at f = 0, 128
+        f2v acc = f2v(0.f);
+        constexpr int NS = 12;  // segments per round (one round up to 13 segments)
+        for (int sb = s0; sb < nseg; sb += NS) {
+            cf xv[NS], hv[NS];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if (sb + i < nseg) {
+                    hv[i] = buf_ld(hres, vo, (sb + i) * spec);
+                    xv[i] = buf_ld(xres, vo, slot(sb + i) * spec);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if (sb + i < nseg) pk_coef(hv[i], z0).mac(acc, xv[i]);
+        }
+        sa.f1acc[(int64_t(ul) * kFN + f) * 16 + col] = cf{acc.x, acc.y};
+        return;
+    }
+    // fresh row pairs: lanes (a, cp) hold column cp's 256 values 16 per lane
+    const int a = t >> 4, cp = t & 15, k = g * 16 + cp;
+    tws[t] = sa.twf[t];
+    const __amdgpu_buffer_rsrc_t xres =
+        buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
+    for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
+        cf v[16];
+        // rows tw - (s + 3) 128 + a + 16 n2 (the ring holds >= kFarRing > 256 rows: one wrap at most)
+        int r0 = (sa.f1tw - (s + 3) * kFarT + a) % sa.ring;
+        r0 = r0 < 0 ? r0 + sa.ring : r0;
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) {
+            const int r = r0 + 16 * n2 >= sa.ring ? r0 + 16 * n2 - sa.ring : r0 + 16 * n2;
+            v[n2] = buf_ld(xres, int((int64_t(r) * sa.pstride + k) * int(sizeof(cf))), 0);
+        }
+        __syncthreads();  // twiddles; the previous segment's LDS use is done
+        col_fft<-1, 16>(v, lds, tws, a, cp, true);
+        if (unit0) bin0_exchange<true>(v, z, cp, [&](int i) { return 16 * i + a; });  // uniform per workgroup
+        cf* xs = sa.xf + (int64_t(c) * M + slot(s)) * kFN * fs + k;
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) xs[int64_t(16 * k1 + a) * fs] = v[k1];
+    }
+}
+
+__device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
+{
+    cf* lds = reinterpret_cast<cf*>(smem);
+    cf* z = lds + 16 * 16 * 16;
+    cf* tws = z + kFN;
+    const int t = threadIdx.x, a = t >> 4, cp = t & 15;
+    const int gpc = sa.B / 16, u = sa.f2u0 + bid, c = u / gpc, g = u - c * gpc, k = g * 16 + cp;
+    const bool unit0 = g == 0;
+    const int M = sa.M, nseg = sa.nseg;
+    auto slot = [&](int s) { return ((sa.f2wn - s - 1) % M + M) % M; };
+    const int64_t fs = sa.B;
+    const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));
+    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;
+    tws[t] = sa.twf[t];
+    // the stored segments' sum from phase 1 + the fresh segments' products; v[n2] at f = a + 16 n2
+    // (col_fft's input layout)
+    cf v[16];
+    const cf* ac = sa.f2acc + int64_t(bid) * kFN * 16;
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) v[n2] = ac[(a + 16 * n2) * 16 + cp];
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+    const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
+    for (int s = 0; s < s0; ++s) {  // uniform per workgroup
+        cf xv[16], hv[16];
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) {
+            const int so = int(16 * n2 * fs * int(sizeof(cf)));
+            hv[n2] = buf_ld(hres, vo, s * spec + so);
+            xv[n2] = buf_ld(xres, vo, slot(s) * spec + so);
+        }
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) {
+            f2v w = {v[n2].x, v[n2].y};
+            pk_coef(hv[n2], unit0 && cp == 0 && ((a + 16 * n2) & (kFN / 2 - 1)) == 0).mac(w, xv[n2]);
+            v[n2] = cf{w.x, w.y};
+        }
+    }
+    __syncthreads();  // twiddles
+    if (unit0) bin0_exchange<false>(v, z, cp, [&](int i) { return a + 16 * i; });  // uniform per workgroup
+    col_fft<1, 16>(v, lds, tws, a, cp, true);
+    constexpr float sc = 1.0f / kFN;
+    cf* o = sa.f2ff + int64_t(c) * kFarT * fs + k;
+#pragma unroll
+    for (int m = 8; m < 16; ++m) o[int64_t(16 * (m - 8) + a) * fs] = cscale(v[m], sc);  // n = 16 m + a >= 128
+}
+
+__global__ __launch_bounds__(256) void k_lvl_slices(slice_args a)
+{
+    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
+    int bid = int(blockIdx.x);
+#ifndef NEO_ROLES
+#define NEO_ROLES 15
+#endif
+    if (bid < a.nrest) {
+        if (NEO_ROLES & 1) rest_role(a, bid);
+        return;
+    }
+    bid -= a.nrest;
+#pragma unroll
+    for (int l = 0; l < kLvToep; ++l) {  // static indices: no copy of the argument block to scratch
+        if (l < a.ntp) {
+            const toep_arg ta = a.tp[l];  // by value: registers, not a scratch copy of the array
+            if (bid < ta.nwg) {  // geometry per window: toep_geom
+                if (ta.T == 2) {
+                    if (NEO_ROLES & 2) toep_role<2, 4, 1, 1>(a, ta, bid, smem);
+                } else if (ta.T == 4) {
+                    if (NEO_ROLES & 2) toep_role<4, 8, 1, 1>(a, ta, bid, smem);
+                } else if (ta.T == 8) {
+                    if (NEO_ROLES & 2) toep_role<8, 16, 1, 1>(a, ta, bid, smem);
+                } else if (ta.T == 16) {
+                    if (NEO_ROLES & 2) toep_role<16, 8, 4, 1>(a, ta, bid, smem);
+                } else {
+                    if (NEO_ROLES & 4) toep_role<32, 12, 16, 2>(a, ta, bid, smem);
+                }
+                return;
+            }
+            bid -= ta.nwg;
+        }
+    }
+    if (bid < a.f1nwg) {
+        if (NEO_ROLES & 8) far1_role(a, bid, smem);
+        return;
+    }
+    bid -= a.f1nwg;
+    if (bid < a.f2nwg && (NEO_ROLES & 8)) far2_role(a, bid, smem);
 }
 
 // Segment spectra (grid C x NSEG x B/16): hf[c][s][f][k] = DFT256 over r < 128 of
-// H[c][128 (s + 2) + r][k] (zero past P). Packed bin 0 holds two real sequences (DC and
-// Nyquist), so its partition-axis convolution is two real convolutions: with
-// Z = DFT(x_dc + i x_ny) and G = DFT(h_dc + i h_ny) the packed result's spectrum is
-// Z[f] A[f] + conj(Z[-f]) Bv[f], A = (Hdc + Hny) / 2, Bv = (Hdc - Hny) / 2,
-// Hdc = (G[f] + conj(G[-f])) / 2, Hny = (G[f] - conj(G[-f])) / 2i: A takes bin 0's slot,
-// hf0[c][s][f] = Bv.
+// H[c][128 (s + 2) + r][k] (zero past P); packed bin 0 (two real sequences, DC and Nyquist)
+// in the real-FFT packing of far_role (pack_bin0).
 __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf* __restrict__ hf,
-                                                    cf* __restrict__ hf0, const cf* __restrict__ twg, int B, int P,
-                                                    int nseg, int64_t cstride, int64_t pstride)
+                                                    const cf* __restrict__ twg, int B, int P, int nseg,
+                                                    int64_t cstride, int64_t pstride)
 {
     __shared__ cf lds[16 * 16 * 16];
     __shared__ cf z[kFN];
@@ -191,10 +510,8 @@ __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf
         const int r = a + 16 * n2, p = (s + 2) * kFarT + r;
         v[n2] = (r < kFarT && p < P) ? H[int64_t(c) * cstride + int64_t(p) * pstride + k] : cf{0.f, 0.f};
     }
-    col_fft<-1>(v, lds, tw, a, cp);
-    const bool b0 = g == 0;
-    cf* dst = hf + (int64_t(c) * nseg + s) * kFN * B + k;
-    if (b0) {  // uniform per workgroup
+    col_fft<-1, 16>(v, lds, tw, a, cp, true);
+    if (g == 0) {  // uniform per workgroup
         if (cp == 0) {
 #pragma unroll
             for (int k1 = 0; k1 < 16; ++k1) z[16 * k1 + a] = v[k1];
@@ -204,215 +521,61 @@ __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf
 #pragma unroll
             for (int k1 = 0; k1 < 16; ++k1) {
                 const int f = 16 * k1 + a;
-                const cf gf = v[k1], gm = cconj(z[(kFN - f) & (kFN - 1)]);
-                const cf hdc = cscale(cadd(gf, gm), 0.5f);
-                const cf d = cscale(csub(gf, gm), 0.5f);
-                const cf hny = {d.y, -d.x};  // d / i
-                v[k1] = cscale(cadd(hdc, hny), 0.5f);
-                hf0[(int64_t(c) * nseg + s) * kFN + f] = cscale(csub(hdc, hny), 0.5f);
+                v[k1] = pack_bin0(v[k1], z[(kFN - f) & (kFN - 1)], f);
             }
         }
     }
+    cf* dst = hf + (int64_t(c) * nseg + s) * kFN * B + k;
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) dst[int64_t(16 * k1 + a) * B] = v[k1];
 }
 
-// Far slice: for the 16-column units [u0, u0 + grid / nsub) the far field of window wn
-// (first block at ring row tw): ff[c][j][k], j < 128. Sub-unit sg of a unit takes segments
-// s = sg * SPG ... (segment s = q - 2); segments s < nfresh are transformed from the FDL rows
-// (s = 0 in steady state, all of them when the pipeline is primed) and their spectra stored
-// in XF slot (wn - s - 1) mod M, the others read from it. With nsub > 1 every sub-unit
-// publishes its partial spectrum and the last to arrive (agent-scope release / acquire on
-// the unit's counter) sums them in sub-unit order, so the result does not depend on arrival
-// order; it then runs the inverse transform and stores the window's 128 blocks.
-template<int SPG>
-__global__ __launch_bounds__(256) void k_lvf_slice(const cf* __restrict__ fdl, const cf* __restrict__ hf,
-                                                   const cf* __restrict__ hf0, cf* __restrict__ xf,
-                                                   cf* __restrict__ xf0m, cf* __restrict__ part,
-                                                   int* __restrict__ cnt, cf* __restrict__ ff,
-                                                   const cf* __restrict__ twg, int tw, int ring, int wn, int M,
-                                                   int nseg, int nfresh, int u0, int nsub, int gpc, int C, int B,
-                                                   int64_t cstride, int64_t pstride)
-{
-    __shared__ cf lds[16 * 16 * 16];
-    __shared__ cf z[SPG][kFN];
-    __shared__ cf tws[kFN];
-    __shared__ int last;
-    const int t = threadIdx.x, a = t >> 4, cp = t & 15;
-    const int ul = int(blockIdx.x) / nsub, sg = int(blockIdx.x) - ul * nsub;
-    const int u = u0 + ul, c = u / gpc, g = u - c * gpc, k = g * 16 + cp;
-    const bool b0 = g == 0;  // packed bin 0 lives in lane cp == 0 of these units
-    tws[t] = twg[t];
-    const int s0 = sg * SPG;
-    auto slot = [&](int s) { return ((wn - s - 1) % M + M) % M; };
-    const cf* X = fdl + int64_t(c) * cstride + k;
-    cf acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = cf{0.f, 0.f};
-    cf v[SPG][16], h[SPG][16];
-    // stored spectra and filter spectra of this sub-unit's segments, all loads issued up front
-#pragma unroll
-    for (int i = 0; i < SPG; ++i) {
-        const int s = s0 + i;
-        if (s < nseg) {
-            const cf* hs = hf + (int64_t(c) * nseg + s) * kFN * B + k;
-            const cf* xs = xf + (int64_t(c) * M + slot(s)) * kFN * B + k;
-#pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) {
-                h[i][k1] = ld_nt(hs + int64_t(16 * k1 + a) * B);
-                if (s >= nfresh) v[i][k1] = ld_nt(xs + int64_t(16 * k1 + a) * B);
-            }
-        }
-    }
-    __syncthreads();  // tws
-#pragma unroll
-    for (int i = 0; i < SPG; ++i) {
-        const int s = s0 + i;
-        if (s < nseg && s < nfresh) {  // uniform per workgroup
-            // S_q[n] = X[tw - (q + 1) 128 + n], q = s + 2
-            const int base = tw - (s + 3) * kFarT;
-#pragma unroll
-            for (int n2 = 0; n2 < 16; ++n2) {
-                int r = (base + a + 16 * n2) % ring;
-                r = r < 0 ? r + ring : r;
-                v[i][n2] = ld_nt(X + int64_t(r) * pstride);
-            }
-            col_fft<-1>(v[i], lds, tws, a, cp);
-            cf* xs = xf + (int64_t(c) * M + slot(s)) * kFN * B + k;
-#pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) xs[int64_t(16 * k1 + a) * B] = v[i][k1];
-            if (b0) {  // bin 0's conj(Z[-f]): kept in LDS for this launch, stored for later windows
-                if (cp == 0) {
-#pragma unroll
-                    for (int k1 = 0; k1 < 16; ++k1) z[i][16 * k1 + a] = v[i][k1];
-                }
-                __syncthreads();
-                if (cp == 0) {
-                    cf* zm = xf0m + (int64_t(c) * M + slot(s)) * kFN;
-#pragma unroll
-                    for (int k1 = 0; k1 < 16; ++k1) {
-                        const int f = 16 * k1 + a;
-                        zm[f] = cconj(z[i][(kFN - f) & (kFN - 1)]);
-                    }
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < SPG; ++i) {
-        if (s0 + i < nseg) {
-#pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) acc[k1] = cadd(acc[k1], cmul(v[i][k1], h[i][k1]));
-        }
-    }
-    if (b0 && cp == 0) {  // bin 0's second term conj(Z[-f]) Bv[f]
-#pragma unroll
-        for (int i = 0; i < SPG; ++i) {
-            const int s = s0 + i;
-            if (s < nseg) {
-                const cf* bv = hf0 + (int64_t(c) * nseg + s) * kFN;
-                const cf* zm = xf0m + (int64_t(c) * M + slot(s)) * kFN;
-#pragma unroll
-                for (int k1 = 0; k1 < 16; ++k1) {
-                    const int f = 16 * k1 + a;
-                    const cf mm = s < nfresh ? cconj(z[i][(kFN - f) & (kFN - 1)]) : zm[f];
-                    acc[k1] = cadd(acc[k1], cmul(mm, bv[f]));
-                }
-            }
-        }
-    }
-    if (nsub > 1) {
-        cf* pp = part + int64_t(ul * nsub + sg) * (kFN * 16);
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) pp[(16 * k1 + a) * 16 + cp] = acc[k1];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-        __syncthreads();
-        if (t == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int before = __hip_atomic_fetch_add(cnt + ul, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = before == nsub - 1;
-        }
-        __syncthreads();
-        if (!last) return;  // uniform per workgroup
-        if (t == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(cnt + ul, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        const cf* p0 = part + int64_t(ul * nsub) * (kFN * 16);
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) acc[k1] = p0[(16 * k1 + a) * 16 + cp];
-        for (int s2 = 1; s2 < nsub; ++s2) {
-            const cf* ps = p0 + int64_t(s2) * (kFN * 16);
-#pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) acc[k1] = cadd(acc[k1], ps[(16 * k1 + a) * 16 + cp]);
-        }
-    }
-    // inverse along f: acc[k1] sits at f = a + 16 k1, the layout col_fft takes
-    col_fft<1>(acc, lds, tws, a, cp);
-    constexpr float sc = 1.0f / kFN;
-    cf* o = ff + int64_t(c) * kFarT * B + k;
-#pragma unroll
-    for (int m = 8; m < 16; ++m) {  // n = 16 m + a >= 128: block j = n - 128
-        const int j = 16 * (m - 8) + a;
-        o[int64_t(j) * B] = cscale(acc[m], sc);
-    }
-    (void)C;
-}
-
 // ---------------------------------------------------------------------------------------
-// Block step (grid C, 64 + NG B/2 lanes): wave 0 loads the overlap window, stores this block
-// as the next call's previous block and runs the window transform (wave-synchronous Stockham);
-// NG groups of B/2 lanes meanwhile sum the level slabs of this block and MAC partitions
-// 1 .. a0 - 1 (rows w - p). After one barrier lane i of group 0 owns the mirror pair of bins
-// (i, B - i): r2c split, FDL row w, Y = partials + H0 X, c2r join; after a second, wave 0
-// runs the inverse transform and stores the block (OLS: window samples [B, 2B); OLA: first
-// half + overlap).
-struct lvl_in {
-    const cf* p[kLvMax];  // slab of this block for channel 0
-    int64_t cs[kLvMax];   // channel stride (complex)
-    int n;
-};
-
+// Block step (grid C, 64 + B/2 lanes): wave 0 loads the overlap window, stores this block
+// as the next call's previous block and runs the window transform (wave-synchronous
+// Stockham); meanwhile lane i of the other B/2 lanes loads the precomputed rest spectrum, the
+// block's far field and H0 of the mirror pair of bins (i, B - i). After one barrier those lanes run the r2c split,
+// insert FDL row w, form Y = rest + H0 X and the c2r join; after a second, wave 0 runs the
+// inverse transform and stores the block (OLS: window samples [B, 2B); OLA: first half +
+// overlap).
 template<int B>
 struct lstep_cfg {
-    static constexpr int Q = B / 2;                                  // float4 (2 bins) per row
-    static constexpr int NG = Q >= 768 ? 1 : (768 / Q > 6 ? 6 : 768 / Q);  // MAC groups
-    static constexpr int EW = B >= 512 ? B / 64 : 8;                 // transform elements per lane
-    static constexpr int TW = B / EW;                                // transform lanes (<= 64)
-    static constexpr int NT = 64 + NG * Q;                           // workgroup size
-    static constexpr int KC = 8;                                     // row pairs in flight per lane
+    static constexpr int Q = B / 2;                   // bin pairs
+    static constexpr int EW = B >= 512 ? B / 64 : 8;  // transform elements per lane
+    static constexpr int TW = B / EW;                 // transform lanes (<= 64)
+    static constexpr int NT = 64 + Q;                 // workgroup size
 };
 
 template<int B, bool OLA>
 __global__ __launch_bounds__(lstep_cfg<B>::NT) void k_upols_lvl(
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
-    const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ twg, int ring, int w, int a0,
-    int64_t cstride, int64_t pstride, lvl_in lv)
+    const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ twg, int w, int64_t cstride,
+    int64_t pstride, const cf* __restrict__ rest, const cf* __restrict__ far, int64_t fcs)
 {
     using K = upols_cfg<B>;
     using A = lstep_cfg<B>;
-    constexpr int Q = A::Q, NG = A::NG, EW = A::EW, TW = A::TW, KC = A::KC;
+    constexpr int EW = A::EW, TW = A::TW;
     static_assert(TW <= 64 && A::NT <= 1024 && EW % 2 == 0, "block step geometry");
     __shared__ __attribute__((aligned(16))) cf X[B];
-    __shared__ __attribute__((aligned(16))) float4 acc[NG][Q];
     __shared__ cf fft[K::LL];
     __shared__ cf tw[K::TW1 + K::TW2];
     const int tid = threadIdx.x, c = blockIdx.x;
     const int64_t crow = int64_t(c) * cstride;
     const float* in_c = in + int64_t(c) * ld_in;
     float* prev_c = prev + int64_t(c) * B;
-    const int64_t ps4 = pstride / 2;
-    const float4* H4 = reinterpret_cast<const float4*>(H + crow);
     const int i0 = tid - 64, k0 = i0, k1 = i0 == 0 ? B / 2 : B - i0;
-    cf h0a = {0.f, 0.f}, h0b = h0a;
-    if (tid >= 64 && tid < 64 + Q) {
+    cf h0a = {0.f, 0.f}, h0b = h0a, ra = h0a, rb = h0a;
+    if (tid >= 64) {
         h0a = H[crow + k0];
         h0b = H[crow + k1];
-    }
-    if (tid < 64) {  // wave 0: window r2c, previous block
+        ra = rest[int64_t(c) * B + k0];
+        rb = rest[int64_t(c) * B + k1];
+        if (far) {  // the far field of this block (not in rest: its window is finished by the
+                    // launch just before this step)
+            ra = cadd(ra, far[int64_t(c) * fcs + k0]);
+            rb = cadd(rb, far[int64_t(c) * fcs + k1]);
+        }
+    } else {  // wave 0: window r2c, previous block
         tw_regs<K::TW1 + K::TW2, 64> twr;
         twr.load(twg, tid);
         cf v[EW];
@@ -440,50 +603,17 @@ __global__ __launch_bounds__(lstep_cfg<B>::NT) void k_upols_lvl(
 #pragma unroll
             for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
         }
-    } else {  // MAC groups: level slabs + partitions 1 .. a0 - 1
-        const int u = tid - 64, g = u / Q, q = u - g * Q;
-        const float4* F4 = reinterpret_cast<const float4*>(fdl + crow);
-        float4 sum = {0.f, 0.f, 0.f, 0.f};
-        for (int l = g; l < lv.n; l += NG) {
-            const float4 r = reinterpret_cast<const float4*>(lv.p[l] + int64_t(c) * lv.cs[l])[q];
-            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
-        }
-        acc4 a0v = {0.f, 0.f, 0.f, 0.f}, a1v = a0v;
-        for (int pb = 1 + g; pb < a0; pb += NG * KC) {
-            float4 hv[KC], xv[KC];
-#pragma unroll
-            for (int kk = 0; kk < KC; ++kk) {
-                const int p = pb + kk * NG;
-                if (p < a0) {
-                    const int r = w - p < 0 ? w - p + ring : w - p;
-                    hv[kk] = H4[int64_t(p) * ps4 + q];
-                    xv[kk] = F4[int64_t(r) * ps4 + q];
-                }
-            }
-#pragma unroll
-            for (int kk = 0; kk < KC; ++kk)
-                if (pb + kk * NG < a0) mac2(a0v, a1v, hv[kk], xv[kk]);
-        }
-        const cf b0 = finish(a0v, q == 0), b1 = finish(a1v, false);
-        acc[g][q] = make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
     }
     __syncthreads();
-    if (tid >= 64 && tid < 64 + Q) {
-        // group 0, bin pair (k0, k1): r2c split of the window transform, FDL row w, Y = the
-        // groups' partial sums + H0 X, then the c2r join; w(B - k) = -conj(w(k))
+    if (tid >= 64) {
+        // bin pair (k0, k1): r2c split, FDL row w, Y = rest + H0 X, c2r join; w(B - k) = -conj(w(k))
         const cf wa = k0 == 0 ? cf{1.f, 0.f} : twiddle<2 * B, -1>(tw + K::TW1, k0);
         const cf wb = k0 == 0 ? cf{0.f, -1.f} : cf{-wa.x, wa.y};
         const cf xa = r2c_split_w<B>(fft, wa, k0), xb = r2c_split_w<B>(fft, wb, k1);
         cf* row = fdl + crow + int64_t(w) * pstride;
         row[k0] = xa;
         row[k1] = xb;
-        const cf* accb = reinterpret_cast<const cf*>(&acc[0][0]);  // acc[g] as B bins
-        cf ya = accb[k0], yb = accb[k1];
-#pragma unroll
-        for (int g = 1; g < NG; ++g) {
-            const cf ra = accb[g * B + k0], rb = accb[g * B + k1];
-            ya.x += ra.x; ya.y += ra.y; yb.x += rb.x; yb.y += rb.y;
-        }
+        cf ya = ra, yb = rb;
         if (k0 == 0) {  // packed {DC, Nyquist}: two real products
             ya.x += h0a.x * xa.x;
             ya.y += h0a.y * xa.y;
@@ -504,11 +634,7 @@ __global__ __launch_bounds__(lstep_cfg<B>::NT) void k_upols_lvl(
 // ---------------------------------------------------------------------------------------
 // host side
 
-int lvl_setup(upols_t* h)
-{
-    plan_levels(h->P, h->lv);
-    return NEO_HIP_OK;
-}
+static size_t far_units_per_slice(const upols_t* h) { return (size_t(h->C) * (h->B / 16) + kFarT - 1) / kFarT; }
 
 // device buffers of the level pipeline (allocated on the first streaming step), all or none
 static int lvl_buffers(upols_t* h)
@@ -529,33 +655,23 @@ static int lvl_buffers(upols_t* h)
         }
         return fail(NEO_HIP_ENOMEM, "level pipeline: allocation of %s (%zu bytes) failed", what, bytes);
     };
+    if (!alloc(reinterpret_cast<void**>(&h->lv_rest), C * B * sizeof(cf))) return undo("rest spectra", C * B * sizeof(cf));
     for (int l = 0; l < lp.n; ++l) {
         const size_t bytes = 2 * C * size_t(lp.T[l]) * B * sizeof(cf);
         if (!alloc(reinterpret_cast<void**>(&h->lv_slab[l]), bytes)) return undo("level slabs", bytes);
     }
     if (lp.nseg) {
-        const int M = lp.nseg, U = h->C * (h->B / 16);
-        const int upw = (U + kFarT - 1) / kFarT;  // units per steady-state slice
-        const int nsub = (lp.nseg + kFarSPG - 1) / kFarSPG;
         const size_t spec = C * size_t(lp.nseg) * kFN * B * sizeof(cf);
-        const size_t xfb = C * size_t(M) * kFN * B * sizeof(cf);
-        const size_t partb = size_t(upw) * nsub * kFN * 16 * sizeof(cf);
+        const size_t ffb = 2 * C * kFarT * B * sizeof(cf);
         if (!alloc(reinterpret_cast<void**>(&h->fv_hf), spec)) return undo("far segment spectra", spec);
-        if (!alloc(reinterpret_cast<void**>(&h->fv_hf0), C * lp.nseg * kFN * sizeof(cf)))
-            return undo("far bin-0 spectra", C * lp.nseg * kFN * sizeof(cf));
-        if (!alloc(reinterpret_cast<void**>(&h->fv_xf), xfb)) return undo("far FDL spectra", xfb);
-        if (!alloc(reinterpret_cast<void**>(&h->fv_xf0m), C * M * kFN * sizeof(cf)))
-            return undo("far bin-0 FDL spectra", C * M * kFN * sizeof(cf));
-        if (!alloc(reinterpret_cast<void**>(&h->fv_ff), 2 * C * kFarT * B * sizeof(cf)))
-            return undo("far field", 2 * C * kFarT * B * sizeof(cf));
-        if (!alloc(reinterpret_cast<void**>(&h->fv_part), partb)) return undo("far partials", partb);
-        if (!alloc(reinterpret_cast<void**>(&h->fv_cnt), size_t(upw) * sizeof(int)))
-            return undo("far counters", size_t(upw) * sizeof(int));
+        if (!alloc(reinterpret_cast<void**>(&h->fv_xf), spec)) return undo("far FDL spectra", spec);
+        if (!alloc(reinterpret_cast<void**>(&h->fv_ff), ffb)) return undo("far field", ffb);
         if (!alloc(reinterpret_cast<void**>(&h->fv_tw), kFN * sizeof(cf))) return undo("far twiddles", kFN * sizeof(cf));
+        const size_t accb = 2 * far_units_per_slice(h) * kFN * 16 * sizeof(cf);  // phase 1 -> 2, double-buffered
+        if (!alloc(reinterpret_cast<void**>(&h->fv_acc), accb)) return undo("far partial sums", accb);
         const auto t = make_twiddle_table(kFN);
-        NEO_HIP_CHECK(hipMemcpy(h->fv_tw, t.data(), kFN * sizeof(cf), hipMemcpyHostToDevice));
-        NEO_HIP_CHECK(hipMemset(h->fv_cnt, 0, size_t(upw) * sizeof(int)));
-        h->fv_nsub = nsub;
+        if (hipMemcpy(h->fv_tw, t.data(), kFN * sizeof(cf), hipMemcpyHostToDevice) != hipSuccess)
+            return undo("far twiddle upload", kFN * sizeof(cf));
         h->fv_dirty = true;
     }
     h->lv_ready = true;
@@ -568,12 +684,11 @@ void lvl_free(upols_t* h)
         (void)hipFree(p);
         p = nullptr;
     }
-    for (cf** p : {&h->fv_hf, &h->fv_hf0, &h->fv_xf, &h->fv_xf0m, &h->fv_ff, &h->fv_part, &h->fv_tw}) {
+    for (cf** p : {&h->lv_rest, &h->fv_hf, &h->fv_xf, &h->fv_ff, &h->fv_tw, &h->fv_acc}) {
         (void)hipFree(*p);
         *p = nullptr;
     }
-    (void)hipFree(h->fv_cnt);
-    h->fv_cnt = nullptr;
+
     h->lv_ready = false;
 }
 
@@ -584,124 +699,211 @@ void lvl_filter_changed(upols_t* h)
     h->lv_n = -1;
 }
 
-static int launch_toep(const upols_t* h, int l, int tw, int u0, int u1, int buf, hipStream_t s)
+static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) % R); }
+
+
+// far-level fields shared by both phases
+static void far_common(const upols_t* h, slice_args& a, int nfresh)
+{
+    a.M = h->lv.nseg;
+    a.nseg = h->lv.nseg;
+    a.fnfresh = nfresh;
+    a.hf = h->fv_hf;
+    a.xf = h->fv_xf;
+    a.twf = h->fv_tw;
+}
+
+// Toeplitz role geometry per window T (toep_role<T, NPL, NPG, JH> in k_lvl_slices)
+static void toep_geom(int T, int& JH, int& UPW)
+{
+    JH = T == 32 ? 2 : 1;
+    const int NPG = T <= 8 ? 1 : (T == 16 ? 4 : 16);
+    UPW = 256 / (16 * NPG);
+}
+
+// The slices launch of step n (block t at ring row w; n = -1: the step before the first,
+// part of priming): the rest spectrum of block t + 1 and slice (n + 1) mod T of window
+// (n + 1) / T + 1 of every level (the one-step lead leaves every window's slabs complete one
+// step before its first block, when the rest role reads them).
+static int launch_slices(upols_t* h, int64_t n, int w, hipStream_t s)
 {
     const level_plan& lp = h->lv;
-    const int T = lp.T[l], gpc = h->B / 16;
-    cf* slab = h->lv_slab[l] + size_t(buf) * h->C * T * h->B;
-#define NEO_TOEP(TT, NPL, NPG)                                                                                   \
-    {                                                                                                            \
-        constexpr int UPW = 256 / (16 * NPG);                                                                    \
-        const unsigned grid = unsigned((u1 - u0 + UPW - 1) / UPW);                                               \
-        hipLaunchKernelGGL((k_lvl_toep<TT, NPL, NPG>), dim3(grid), dim3(256), 0, s, h->H, h->fdl, slab, lp.a[l], \
-                           lp.b[l], tw, h->ring, u0, u1, gpc, h->C, h->B, h->cstride, h->pstride);               \
+    const int B = h->B, C = h->C, R = h->ring;
+    slice_args a{};
+    a.H = h->H;
+    a.fdl = h->fdl;
+    a.ring = R;
+    a.C = C;
+    a.B = B;
+    a.cstride = h->cstride;
+    a.pstride = h->pstride;
+    // rest role
+    const int64_t n1 = n + 1;
+    const int Q = B / 2, lpc = std::min(Q, 256), cpw = 256 / lpc, gq = Q / lpc;
+    a.rest = h->lv_rest;
+    a.nrest = (C + cpw - 1) / cpw * gq;
+    a.wr = w;
+    a.a0 = lp.a0;
+    for (int l = 0; l < lp.n; ++l) {
+        const int T = lp.T[l];
+        a.sl[a.nsl] = h->lv_slab[l] + ((n1 / T & 1) * C * T + n1 % T) * B;
+        a.scs[a.nsl++] = int64_t(T) * B;
     }
-    switch (T) {
-        case 8: NEO_TOEP(8, 4, 4) break;
-        case 16: NEO_TOEP(16, 4, 8) break;
-        case 32: NEO_TOEP(32, 12, 16) break;
-        default: return fail(NEO_HIP_EINVAL, "no Toeplitz level of %d blocks", T);
+    int total = a.nrest;
+    for (int l = 0; l < lp.n; ++l) {
+        const int T = lp.T[l];
+        int JH, UPW;
+        toep_geom(T, JH, UPW);
+        const int64_t U = int64_t(C) * (B / 16) * JH, st = n1 % T, W = n1 / T + 1;
+        toep_arg& ta = a.tp[a.ntp];
+        ta.u0 = int(st * U / T);
+        ta.u1 = int((st + 1) * U / T);
+        if (ta.u1 <= ta.u0) continue;
+        ta.slab = h->lv_slab[l] + (W & 1) * C * T * B;
+        ta.T = T;
+        ta.a = lp.a[l];
+        ta.b = lp.b[l];
+        ta.tw = ring_add(w, W * T - n, R);  // block t = t0 + n at row w; the window starts at t0 + W T
+        ta.nwg = (ta.u1 - ta.u0 + UPW - 1) / UPW;
+        total += ta.nwg;
+        ++a.ntp;
     }
-#undef NEO_TOEP
+    if (lp.nseg) {
+        far_common(h, a, 1);
+        const int64_t U = int64_t(C) * (B / 16);
+        const size_t accb = far_units_per_slice(h) * kFN * 16;
+        {  // phase 1: slice (n + 1) mod 128 of window (n + 1) / 128 + 1
+            const int64_t st = n1 % kFarT, W = n1 / kFarT + 1;
+            const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
+            a.f1u0 = u0;
+            a.f1nwg = (u1 - u0) * kFarParts;
+            a.f1tw = ring_add(w, W * kFarT - n, R);
+            a.f1wn = int(W);
+            a.f1acc = h->fv_acc + (n1 & 1) * accb;
+            total += a.f1nwg;
+        }
+        if (n >= 0) {  // phase 2: the slice phase 1 did at step n - 1
+            const int64_t st = n % kFarT, W = n / kFarT + 1;
+            const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
+            a.f2u0 = u0;
+            a.f2nwg = u1 - u0;
+            a.f2wn = int(W);
+            a.f2acc = h->fv_acc + (n & 1) * accb;
+            a.f2ff = h->fv_ff + (W & 1) * C * kFarT * B;
+            total += a.f2nwg;
+        }
+    }
+    hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(total)), dim3(256), 0, s, a);
     NEO_HIP_LAUNCH_CHECK();
     return NEO_HIP_OK;
 }
 
-static int launch_far(const upols_t* h, int tw, int wn, int u0, int u1, int nfresh, hipStream_t s)
-{
-    const level_plan& lp = h->lv;
-    const int nsub = h->fv_nsub;
-    cf* ff = h->fv_ff + size_t(wn & 1) * h->C * kFarT * h->B;
-    const unsigned grid = unsigned(u1 - u0) * unsigned(nsub);
-    hipLaunchKernelGGL((k_lvf_slice<kFarSPG>), dim3(grid), dim3(256), 0, s, h->fdl, h->fv_hf, h->fv_hf0, h->fv_xf,
-                       h->fv_xf0m, h->fv_part, h->fv_cnt, ff, h->fv_tw, tw, h->ring, wn, lp.nseg, lp.nseg, nfresh, u0,
-                       nsub, h->B / 16, h->C, h->B, h->cstride, h->pstride);
-    NEO_HIP_LAUNCH_CHECK();
-    return NEO_HIP_OK;
-}
-
-// First streaming step after a reset / filter change / batched pass: window 0 of every level
-// starts at this block; compute it whole (all units; the far level transforms every segment).
+// First streaming step after a reset / filter change / batched pass (block t0 at ring row w):
+// window 0 of every level, starting at t0, computed whole (all units; the far level
+// transforms every segment), then the slices launch of "step -1" (the rest spectrum of t0
+// and the first slice of every window 1).
 static int lvl_prime(upols_t* h, hipStream_t s)
 {
     const level_plan& lp = h->lv;
-    int rc;
+    const int B = h->B, C = h->C, w = h->wpos;
     if (lp.nseg && h->fv_dirty) {
-        const unsigned grid = unsigned(h->C) * unsigned(lp.nseg) * unsigned(h->B / 16);
-        hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->fv_hf, h->fv_hf0, h->fv_tw, h->B, h->P,
-                           lp.nseg, h->cstride, h->pstride);
+        const unsigned grid = unsigned(C) * unsigned(lp.nseg) * unsigned(B / 16);
+        hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->fv_hf, h->fv_tw, B, h->P, lp.nseg,
+                           h->cstride, h->pstride);
         NEO_HIP_LAUNCH_CHECK();
         h->fv_dirty = false;
     }
-    const int U = h->C * (h->B / 16);
-    for (int l = 0; l < lp.n; ++l)
-        if ((rc = launch_toep(h, l, h->wpos, 0, U, 0, s))) return rc;
-    if (lp.nseg) {
-        // in slices of the steady-state size (the partial buffer holds one slice)
+    slice_args a{};
+    a.H = h->H;
+    a.fdl = h->fdl;
+    a.ring = h->ring;
+    a.C = C;
+    a.B = B;
+    a.cstride = h->cstride;
+    a.pstride = h->pstride;
+    int total = 0;
+    for (int l = 0; l < lp.n; ++l) {
+        int JH, UPW;
+        toep_geom(lp.T[l], JH, UPW);
+        toep_arg& ta = a.tp[a.ntp++];
+        ta.slab = h->lv_slab[l];
+        ta.T = lp.T[l];
+        ta.a = lp.a[l];
+        ta.b = lp.b[l];
+        ta.tw = w;
+        ta.u0 = 0;
+        ta.u1 = C * (B / 16) * JH;
+        ta.nwg = (ta.u1 + UPW - 1) / UPW;
+        total += ta.nwg;
+    }
+    if (total) {
+        hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(total)), dim3(256), 0, s, a);
+        NEO_HIP_LAUNCH_CHECK();
+    }
+    if (lp.nseg) {  // far window 0, every segment transformed, in slices (the partial sums hold one)
+        slice_args f{};
+        f.H = h->H;
+        f.fdl = h->fdl;
+        f.ring = h->ring;
+        f.C = C;
+        f.B = B;
+        f.cstride = h->cstride;
+        f.pstride = h->pstride;
+        far_common(h, f, lp.nseg);
+        f.f1tw = w;
+        f.f1wn = 0;
+        f.f1acc = h->fv_acc;
+        f.f2wn = 0;
+        f.f2acc = h->fv_acc;
+        f.f2ff = h->fv_ff;
+        const int64_t U = int64_t(C) * (B / 16);
         for (int st = 0; st < kFarT; ++st) {
-            const int u0 = int(int64_t(st) * U / kFarT), u1 = int(int64_t(st + 1) * U / kFarT);
-            if (u1 > u0 && (rc = launch_far(h, h->wpos, 0, u0, u1, lp.nseg, s))) return rc;
+            const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
+            if (u1 <= u0) continue;
+            f.f1u0 = u0;
+            f.f1nwg = (u1 - u0) * kFarParts;
+            f.f2nwg = 0;
+            hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(f.f1nwg)), dim3(256), 0, s, f);
+            NEO_HIP_LAUNCH_CHECK();
+            f.f1nwg = 0;
+            f.f2u0 = u0;
+            f.f2nwg = u1 - u0;
+            hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(f.f2nwg)), dim3(256), 0, s, f);
+            NEO_HIP_LAUNCH_CHECK();
         }
     }
-    return NEO_HIP_OK;
+    return launch_slices(h, -1, ring_add(w, -1, h->ring), s);
 }
 
 int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
     int rc = lvl_buffers(h);
     if (rc) return rc;
-    const level_plan& lp = h->lv;
     if (h->lv_n < 0) {
         if ((rc = lvl_prime(h, s))) return rc;
         h->lv_n = 0;
     }
     const int64_t n = h->lv_n;
-    const int B = h->B, C = h->C, R = h->ring, U = C * (B / 16);
-    lvl_in li{};
-    for (int l = 0; l < lp.n; ++l) {
-        const int T = lp.T[l];
-        const int64_t buf = (n / T) & 1, j = n % T;
-        li.p[li.n] = h->lv_slab[l] + (buf * C * T + j) * B;
-        li.cs[li.n] = int64_t(T) * B;
-        ++li.n;
-    }
-    if (lp.nseg) {
-        const int64_t buf = (n / kFarT) & 1, j = n % kFarT;
-        li.p[li.n] = h->fv_ff + (buf * C * kFarT + j) * B;
-        li.cs[li.n] = int64_t(kFarT) * B;
-        ++li.n;
-    }
+    const int B = h->B, C = h->C, R = h->ring;
+    const cf* farp = h->lv.nseg ? h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B : nullptr;
+    const int64_t fcs = int64_t(kFarT) * B;
     upols_t::ev_group* ev = nullptr;
-    if ((rc = timing_begin(h, 4, &ev)) || (rc = timing_mark(ev, 0, s))) return rc;
+    if ((rc = timing_begin(h, 3, &ev)) || (rc = timing_mark(ev, 0, s))) return rc;
     if (h->ola) {
         NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                   (k_upols_lvl<BB, true>), dim3(unsigned(C)), dim3(lstep_cfg<BB>::NT), 0, s, in, ld_in,
-                                  out, ld_out, h->prev, h->H, h->fdl, h->tw, R, h->wpos, lp.a0, h->cstride, h->pstride, li))
+                                  out, ld_out, h->prev, h->H, h->fdl, h->tw, h->wpos, h->cstride, h->pstride, h->lv_rest,
+                                  farp, fcs))
     } else {
         NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
                                   (k_upols_lvl<BB, false>), dim3(unsigned(C)), dim3(lstep_cfg<BB>::NT), 0, s, in, ld_in,
-                                  out, ld_out, h->prev, h->H, h->fdl, h->tw, R, h->wpos, lp.a0, h->cstride, h->pstride, li))
+                                  out, ld_out, h->prev, h->H, h->fdl, h->tw, h->wpos, h->cstride, h->pstride, h->lv_rest,
+                                  farp, fcs))
     }
     NEO_HIP_LAUNCH_CHECK();
     if ((rc = timing_mark(ev, 1, s))) return rc;
-    // 1/T of the next window of every level (rows <= this block - 1 only)
-    for (int l = 0; l < lp.n; ++l) {
-        const int T = lp.T[l], st = int(n % T);
-        const int u0 = int(int64_t(st) * U / T), u1 = int(int64_t(st + 1) * U / T);
-        if (u1 <= u0) continue;
-        const int tw = ((h->wpos - st + T) % R + R) % R;
-        if ((rc = launch_toep(h, l, tw, u0, u1, int(((n / T) + 1) & 1), s))) return rc;
-    }
+    if ((rc = launch_slices(h, n, h->wpos, s))) return rc;
     if ((rc = timing_mark(ev, 2, s))) return rc;
-    if (lp.nseg) {
-        const int st = int(n % kFarT);
-        const int u0 = int(int64_t(st) * U / kFarT), u1 = int(int64_t(st + 1) * U / kFarT);
-        if (u1 > u0) {
-            const int tw = ((h->wpos - st + kFarT) % R + R) % R;
-            if ((rc = launch_far(h, tw, int(n / kFarT + 1), u0, u1, 1, s))) return rc;
-        }
-    }
-    if ((rc = timing_mark(ev, 3, s))) return rc;
     h->wpos = h->wpos + 1 >= R ? 0 : h->wpos + 1;
     h->lv_n = n + 1;
     return NEO_HIP_OK;

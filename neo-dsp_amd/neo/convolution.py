@@ -61,7 +61,7 @@ def level_plan(partitions: int) -> dict:
     128 partitions from 256."""
     L = _native.load()
     a0, nl, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    T, a, b = (ctypes.c_int * 3)(), (ctypes.c_int * 3)(), (ctypes.c_int * 3)()
+    T, a, b = (ctypes.c_int * 8)(), (ctypes.c_int * 8)(), (ctypes.c_int * 8)()
     _native.check(L.neo_hip_upols_level_plan(int(partitions), ctypes.byref(a0), ctypes.byref(nl), T, a, b,
                                              ctypes.byref(ns)))
     n = nl.value
@@ -258,8 +258,8 @@ class UpolsConvolver:
 
     def timing_detail(self):
         """Per part [(ms, count)] * 4 since the last call (neo_hip_upols_timing_detail):
-        streaming steps 0 = block step, 1 = Toeplitz level slices, 2 = far slice,
-        3 = whole step; plain / batched steps 0 = MAC kernel."""
+        streaming steps 0 = block step, 1 = the slices launch (rest spectrum, level
+        slices), 3 = whole step; plain / batched steps 0 = MAC kernel."""
         ms, n = (ctypes.c_double * 4)(), (ctypes.c_int64 * 4)()
         _native.check(_native.load().neo_hip_upols_timing_detail(self._h, ms, n))
         return [(ms[k], n[k]) for k in range(4)]

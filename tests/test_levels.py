@@ -4,10 +4,12 @@ numpy and checked against the direct block-axis convolution — no GPU needed.
 Per bin the convolver output is Y[t] = sum_p H[p] X[t - p]
 (uniform_partitioned_convolver.hpp:47-65; fdl_index.hpp:23-36: partition p meets FDL row
 t - p). The HIP path splits the partitions into the bands of neo_hip_upols_level_plan and
-computes each band's next window during the current one, a slice of the bins per step,
-from FDL rows that already exist. This test replays exactly that schedule — the ring
-positions the host passes (tw), the slice ranges, the double-buffered slabs, the far
-level's XF ring of row-pair spectra and its 256-point partition-axis transforms — on random
+computes each band's next window during the current one, a slice of the bins per step and
+one step ahead, from FDL rows that already exist; after each block step the same launch sums
+the next block's partitions 1..a0-1 and Toeplitz slabs into a "rest" spectrum, so the block
+step adds only the rest, its far-field entry and H0 X. This test replays exactly that schedule — the ring positions the host
+passes (tw), the slice ranges, the double-buffered slabs, the rest spectrum, the far level's
+XF ring of row-pair spectra and its 256-point partition-axis transforms — on random
 spectra, with history before the levels start, ring wraparound and re-priming, and checks
 every output block. It pins the index arithmetic the kernels share with the host code; the
 kernels' arithmetic itself is pinned by the GPU parity tests against the oracle.
@@ -47,6 +49,7 @@ class Sim:
         self.w = 0
         self.n = -1
         self.slab = [np.zeros((2, T, self.K), complex) for T in lp["T"]]
+        self.rest = np.zeros(self.K, complex)
         ns = lp["nseg"]
         if ns:
             self.M = ns
@@ -87,39 +90,51 @@ class Sim:
         y = np.fft.ifft(acc, axis=0)
         self.ff[wn & 1, :, k0:k1] = y[FT:]
 
+    def slices(self, n, w):
+        """The slices launch after the block step of step n (block at ring row w; n = -1:
+        the priming step before the first)."""
+        lp, K, R = self.lp, self.K, self.R
+        n1 = n + 1
+        rest = (self.H[1: lp["a0"]] * self.ring[(w + 1 - np.arange(1, lp["a0"])) % R]).sum(0)
+        for l, T in enumerate(lp["T"]):
+            rest = rest + self.slab[l][(n1 // T) & 1, n1 % T]
+        self.rest = rest
+        for l, T in enumerate(lp["T"]):
+            JH = 2 if T == 32 else 1
+            U = (K // 16) * JH if K >= 16 else K
+            st, W = n1 % T, n1 // T + 1
+            u0, u1 = st * U // T, (st + 1) * U // T
+            if u1 > u0:
+                k0, k1 = u0 * K // U, u1 * K // U
+                self.toep(l, (w + W * T - n) % R, k0, k1, W & 1)
+        if lp["nseg"]:
+            # phase 1 (transform, MAC) of slice (n + 1) mod 128 here; its phase 2 (inverse, the
+            # far-field store) one step later: the result only depends on phase 1's inputs
+            st, W = n1 % FT, n1 // FT + 1
+            k0, k1 = st * K // FT, (st + 1) * K // FT
+            if k1 > k0:
+                self.far((w + W * FT - n) % R, W, k0, k1, 1)
+
     def prime(self):
         for l in range(len(self.lp["T"])):
             self.toep(l, self.w, 0, self.K, 0)
         if self.lp["nseg"]:
             self.far(self.w, 0, 0, self.K, self.lp["nseg"])
+        self.slices(-1, (self.w - 1) % self.R)
         self.n = 0
 
     def step(self, x):
         if self.n < 0:
             self.prime()
-        n, lp, K, R = self.n, self.lp, self.K, self.R
-        # block step: level slabs of this block + partitions [0, a0)
+        n = self.n
+        # block step: the rest spectrum + the far field of the block + H0 X
         self.ring[self.w] = x
-        y = (self.H[: lp["a0"]] * self.ring[(self.w - np.arange(lp["a0"])) % R]).sum(0)
-        for l, T in enumerate(lp["T"]):
-            y = y + self.slab[l][(n // T) & 1, n % T]
-        if lp["nseg"]:
+        y = self.rest + self.H[0] * x
+        if self.lp["nseg"]:
             y = y + self.ff[(n // FT) & 1, n % FT]
-        # slices of the next windows (the kernels use rows <= this block - 1 only: check it)
-        saved = self.ring[self.w].copy()
-        self.ring[self.w] = np.nan
-        for l, T in enumerate(lp["T"]):
-            st = n % T
-            k0, k1 = st * K // T, (st + 1) * K // T
-            if k1 > k0:
-                self.toep(l, (self.w - st + T) % R, k0, k1, ((n // T) + 1) & 1)
-        if lp["nseg"]:
-            st = n % FT
-            k0, k1 = st * K // FT, (st + 1) * K // FT
-            if k1 > k0:
-                self.far((self.w - st + FT) % R, n // FT + 1, k0, k1, 1)
-        self.ring[self.w] = saved
-        self.w = (self.w + 1) % R
+        # slices (rows up to this block's; the newest one is needed by the rest only)
+        self.slices(n, self.w)
+        self.w = (self.w + 1) % self.R
         self.n = n + 1
         return y
 

@@ -579,10 +579,11 @@ def test_level_steps_small_filters(neo_gpu, oracle, method, B, P, C, nb):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 320) <= TOL
 
 
-@pytest.mark.parametrize("P", [16, 17, 32, 33, 64, 65, 255, 256, 257, 384, 385, 513])
+@pytest.mark.parametrize("P", [3, 4, 5, 8, 9, 16, 17, 32, 33, 64, 65, 255, 256, 257, 384, 385, 513])
 def test_level_band_edges(neo_gpu, oracle, P):
-    """Every band edge of the level plan (block step / 8 / 16 / 32-block Toeplitz levels /
-    far segments, a last far segment of one partition): B = 32, past the ring length."""
+    """Every band edge of the level plan (block step and rest / 2 / 4 / 8 / 16 / 32-block
+    Toeplitz levels / far segments, a last far segment of one partition): B = 32, past the
+    ring length."""
     assert _stream(neo_gpu, oracle, "upols", 32, P, 2, max(2 * P + 140, 300), 400 + P) <= TOL
 
 
@@ -639,7 +640,7 @@ def test_levels_before_any_filter(neo_gpu):
 
 
 def test_level_timing_detail(neo_gpu):
-    """timing_detail(): block step, Toeplitz slices, far slice and whole step per timed step."""
+    """timing_detail(): block step, slices launch and whole step per timed step."""
     torch = pytest.importorskip("torch")
     conv = neo_gpu.UpolsConvolver(4, 256, 300)
     conv.set_batch(False)
@@ -648,9 +649,9 @@ def test_level_timing_detail(neo_gpu):
     conv.process_blocks(x)
     conv.set_timing(False)
     parts = conv.timing_detail()
-    assert [n for _, n in parts] == [4, 4, 4, 4]  # steps 0, 3, 6, 9
-    assert all(ms > 0 for ms, _ in parts)
-    assert parts[3][0] >= max(ms for ms, _ in parts[:3]) - 1e-6
+    assert [n for _, n in parts] == [4, 4, 0, 4]  # steps 0, 3, 6, 9
+    assert parts[0][0] > 0 and parts[1][0] > 0
+    assert parts[3][0] >= parts[0][0] + parts[1][0] - 1e-6
 
 
 def test_ahead_mixed_paths(neo_gpu, oracle):
