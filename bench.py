@@ -146,24 +146,35 @@ def load_pmc_traffic(workload: str, kernel: str = ""):
 
 
 def cpu_baseline_upols(C, B, L, threads):
-    """The oracle's restatement of dense_convolve<upols_convolver> (kind "port") on a
-    bounded sample of the same workload, on this box's host cores."""
+    """The reference's SIMD CPU path (kind "port"): dense_convolve<upols_convolver> with the
+    xsimd interleaved FDL MAC of a -march=native build (multiply_add.hpp:196-223) restated in
+    oracle/neo_baseline.c, on bounded samples of the same workload on this box's host cores:
+    1 thread, and `threads` threads (the cores this job may use). `value` is the all-threads
+    figure. A reported baseline, not the target."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle as O
 
-    cs, nb = 64, 640  # 64 channels x 640 blocks ~ 15-20 CPU-seconds on the box's EPYC host
-    cs = min(cs, max(C, 1) * 64)
-    ir = np.stack([O.noise(8 + c, L) for c in range(cs)])
+    nb = 256
+    cs_all = max(threads, 1) * 4
+    ir = np.stack([O.noise(8 + c, L) for c in range(cs_all)])
     parts = O.uniform_partition(O.normalize_impulse(ir), B)
-    sig = np.stack([O.noise(7000 + c, B * nb) for c in range(cs)])
-    th = max(1, min(threads, cs))
-    t0 = time.perf_counter()
-    O.dense_convolve(sig, parts, threads=th)
-    dt = time.perf_counter() - t0
-    return {"value": cs * nb * B / dt / 1e6, "unit": "Msamples/s", "cores": th, "kind": "port",
-            "sample": f"{cs} ch x {nb} blocks of B={B}, L={L} (P={parts.shape[1]}), oracle dense_convolve "
-                      f"(c2c_dit2 r2c/c2r + scalar complex MAC), {th} threads, {dt:.2f} s wall"}
+    sig = np.stack([O.noise(7000 + c, B * nb) for c in range(cs_all)])
+
+    def run(cs, th):
+        t0 = time.perf_counter()
+        O.dense_convolve_simd(sig[:cs], parts[:cs], threads=th)
+        dt = time.perf_counter() - t0
+        return cs * nb * B / dt / 1e6, dt
+
+    v1, d1 = run(2, 1)
+    va, da = run(cs_all, threads)
+    lvl = O.simd_level()
+    return {"value": va, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "threads_1": v1, "threads_all": va, "simd": O.SIMD_NAMES[lvl],
+            "sample": f"B={B}, L={L} (P={parts.shape[1]}), {nb} blocks per channel: 2 channels on 1 thread "
+                      f"({d1:.2f} s), {cs_all} channels on {threads} threads ({da:.2f} s); dense_convolve with "
+                      f"the SIMD MAC ({O.SIMD_NAMES[lvl]}) over the oracle's c2c_dit2 r2c/c2r"}
 
 
 def cpu_baseline_fft(threads):
@@ -231,22 +242,20 @@ class Feed:
 
 
 def algorithmic_bytes(C, B, P, plan):
-    """Algorithmic bytes per streaming step, per part:
-    block step: window (previous block + this block), previous-block write, output (4 x 4B),
-                FDL row write, H0 and the rest spectrum (3 x 8B)
-    rest role:  a0 - 1 filter/FDL row pairs (16B each) + one slab per level (8B) + the
-                rest spectrum write (8B)
-    Toeplitz level l (window T, band [a, b)), C*B/T columns per step: per column b - a filter
-                rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
+    """Algorithmic bytes per streaming step of the step kernel k_lvl_step, by role:
+    block:     window (previous block + this block), previous-block write, output (4 x 4B per
+               sample), FDL row write and H0 (2 x 8B per bin), partitions 1 .. a0 - 1 (filter +
+               FDL row, 16B per bin each), one slab row per level and the far-field row (8B each)
+    Toeplitz level (window T, band [a, b)), C*B/T columns per step: per column b - a filter
+               rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
     far level, C*B/128 columns per step: per column 256 FDL rows, 256 stored + nseg - 1 older
-                row-pair spectra, nseg segment spectra (256 f each) and 128 far-field entries."""
+               row-pair spectra, nseg segment spectra (256 f each) and 128 far-field entries."""
     nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
-    block = C * B * (16 + 24)
-    rest = C * B * (16 * (plan["a0"] - 1) + 8 * nlev + 8)
+    block = C * B * (16 + 16 + 16 * (plan["a0"] - 1) + 8 * nlev)
     toep = sum(C * B / T * 8 * (2 * (b - a) + 2 * T - 1) for T, a, b in zip(plan["T"], plan["a"], plan["b"]))
     ns = plan["nseg"]
     far = C * B / 128 * 8 * (256 * (2 * ns + 1) + 128) if ns else 0.0
-    return block, rest, toep, far
+    return {"block": block, "toeplitz": toep, "far": far}
 
 
 def oracle_parity(x, y, feed, irh, B, chans, K=4, threads=16):
@@ -368,27 +377,21 @@ def run_upols(args, world, rank, local):
                "note": "GPU time per step (HIP events around every step, which add their own records)"}
 
     if levels:
-        bs, rs, tp, fr = algorithmic_bytes(C, B, P, plan)
-        parts = [("block step k_upols_lvl<%d>" % B, det[0], bs),
-                 ("slices k_lvl_slices (rest spectrum; Toeplitz T = %s; far %d segments)"
-                  % ("/".join(map(str, plan["T"])), plan["nseg"]), det[1], rs + tp + fr)]
-        step_ms = det[3]
-        kernels = []
-        for name, ms, by in parts:
-            gbs = by / (ms * 1e-3) / 1e9
-            kernels.append({"kernel": name, "ms_per_step": ms, "share_of_step": ms / step_ms,
-                            "algorithmic_bytes_per_step": by, "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS,
-                            "traffic": load_pmc_traffic(args.workload, name.split()[1])})
-        kernels[1]["bytes_by_role"] = {"rest": rs, "toeplitz": tp, "far": fr}
-        dom = max(kernels, key=lambda k: k["ms_per_step"])
-        step_bytes = bs + tp + fr
+        roles = algorithmic_bytes(C, B, P, plan)
+        step_ms = det[0]
+        by = sum(roles.values())
+        gbs = by / (step_ms * 1e-3) / 1e9
+        name = f"k_lvl_step<{B}>"
+        kernels = [{"kernel": name + " (block, Toeplitz T = %s, far %d segments)"
+                    % ("/".join(map(str, plan["T"])), plan["nseg"]),
+                    "ms_per_step": step_ms, "share_of_step": 1.0, "algorithmic_bytes_per_step": by,
+                    "bytes_by_role": roles, "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS,
+                    "traffic": load_pmc_traffic(args.workload, "k_lvl_step")}]
+        dom = kernels[0]
         roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
-                "kernel_avg_ms": dom["ms_per_step"], "steps_per_launch": 1,
-                "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_step"],
-                "step": {"ms": step_ms, "algorithmic_bytes": step_bytes,
-                         "achieved_gbs": step_bytes / (step_ms * 1e-3) / 1e9,
-                         "frac": step_bytes / (step_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+                "frac": dom["frac"], "traffic": dom["traffic"], "kernel": name,
+                "kernel_avg_ms": step_ms, "steps_per_launch": 1, "launches_per_step": 1,
+                "algorithmic_bytes_per_launch": by,
                 "kernels": kernels, "d2d_copy_gbs": copy_ceiling_gbs(dev)}
     else:
         roof = {"bound": "hbm", "achieved": gbs_plain, "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -142,12 +142,12 @@ NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in,
                                               int64_t ld_out, int64_t num_samples, int is_device, void* stream);
 NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
 /* Streaming levels for single-block steps (upols / upola; upols_levels.hip): the
- * partitions are cut into bands -- p = 0 in the block step; p in [1, 4) summed for the next
- * block one step ahead ("rest" spectrum); Toeplitz windows of 2 / 4 / 8 / 16 / 32 blocks for
- * [4, 8) / [8, 16) / [16, 32) / [32, 64) / [64, 256); a 128-block partition-axis transform
- * for [256, P) -- and every band's contribution to the blocks of its next window is computed
- * during the current window, a slice of the columns per block step, so every call does the
- * same work (two launches: the block step, then k_lvl_slices). Output is the same block by
+ * partitions are cut into bands -- p in [0, 4) MAC'd by the block itself; Toeplitz windows
+ * of 2 / 4 / 8 / 16 / 32 blocks for [4, 8) / [8, 16) / [16, 32) / [32, 64) / [64, 256); a
+ * 128-block partition-axis transform for [256, P) -- and every band's contribution to the
+ * blocks of its next window is computed during the current window, a slice of the columns
+ * per block step, so every call does the same work (ONE launch per block, k_lvl_step: the
+ * block and the slices side by side). Output is the same block by
  * block (summation order differs), latency stays one block. Default on from 64 partitions
  * (B <= 1024); v2 handles refuse it. Switching is allowed at any block boundary (the next
  * step computes the current windows whole). */
@@ -162,9 +162,8 @@ NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, 
  * bench.py): enable = n > 0 brackets every n-th launch group with events (0 = off).
  * timing() returns the summed ms of the bracketed part and the count of timed groups:
  * the MAC kernel of a plain or batched step, the whole step of a streaming-level step.
- * timing_detail() returns per part (ms[4], launches[4]): streaming steps 0 = block
- * step, 1 = the slices launch (rest spectrum, level slices), 3 = whole step; plain /
- * batched steps 0 = MAC kernel. Both drain the events. */
+ * timing_detail() returns per part (ms[4], launches[4]): streaming-level steps 0 = the
+ * step kernel; plain / batched steps 0 = MAC kernel. Both drain the events. */
 NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable);
 NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches);
 NEO_HIP_API int neo_hip_upols_timing_detail(neo_hip_upols* h, double* ms, int64_t* launches);

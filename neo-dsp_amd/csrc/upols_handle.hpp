@@ -56,7 +56,6 @@ struct neo_hip_upols {
     int64_t lv_n = -1;              // blocks since the levels were primed (-1: prime at the next step)
     bool lv_ready = false;          // level buffers allocated
     neo_hip::cf* lv_slab[neo_hip::kLvToep] = {};  // Toeplitz level slabs [2][C][T][B]
-    neo_hip::cf* lv_rest = nullptr; // the next block's spectrum without partition 0 [C][B]
     neo_hip::cf* fv_hf = nullptr;   // far segment spectra [C][nseg][256][B]
     neo_hip::cf* fv_xf = nullptr;   // far FDL row-pair spectra, ring of nseg slots [C][nseg][256][B]
     neo_hip::cf* fv_ff = nullptr;   // far field [2][C][128][B]

@@ -118,12 +118,20 @@ struct slice_args {
     cf* fdl;
     int ring, C, B;
     int64_t cstride, pstride;
-    // rest role
-    cf* rest;           // [C][B]
-    int nrest, wr, a0;  // workgroups; ring row of the newest FDL row (block t); block step partitions
+    // block role: this step's block, one workgroup per channel (nblk = 0 in priming launches)
+    int nblk;
+    const float* in;
+    int64_t ld_in;
+    float* out;
+    int64_t ld_out;
+    float* prev;
+    const cf* twg;
+    int w, a0;              // ring row of the block; partitions the block role MACs directly
     int nsl;
-    const cf* sl[kLvToep];  // slab of block t + 1 per level, channel 0
+    const cf* sl[kLvToep];  // slab row of this block per level, channel 0
     int64_t scs[kLvToep];   // channel strides
+    const cf* ff;           // far field row of this block, channel 0 (null: no far level)
+    int64_t fcs;
     // Toeplitz roles
     int ntp;
     toep_arg tp[kLvToep];
@@ -132,55 +140,164 @@ struct slice_args {
     const cf* hf;
     cf* xf;
     const cf* twf;
-    // far phase 1: stored-segment MAC (16 workgroups per unit) and fresh transforms (1 per unit)
-    int f1nwg, f1u0, f1tw, f1wn;
+    // far phase 1: stored-segment MAC (16 workgroups per unit)
+    int f1nwg, f1u0, f1wn, f1fpl;  // f rows per lane: 16 / f1fpl workgroups per unit
     cf* f1acc;  // [units][256 f][16]
-    // far phase 2 (the slice phase 1 did one step earlier): fresh products, sum, inverse transform
-    int f2nwg, f2u0, f2wn;
-    const cf* f2acc;
+    // far phase 2 (the slice phase 1 did one step earlier): the fresh row pairs' transforms
+    // (stored to their ring slots) and products, the sum, the inverse transform
+    int f2nwg, f2u0, f2tw, f2wn;
+    cf* f2acc;
     cf* f2ff;   // the target far window [C][128][B]
 };
 
 constexpr int kSliceLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange, twiddles
 
-// rest[c][k] for block t + 1 = sum_{p=1}^{a0-1} H[p] X[t + 1 - p] + the Toeplitz slabs of block t + 1
-__device__ __forceinline__ void rest_role(const slice_args& a, int bid)
+// Block role (lanes 0 .. B/2 - 1 of the workgroup, the others idle): lane i gathers, for the
+// mirror pair of bins (i, B - i), everything but partition 0 -- partitions 1 .. a0 - 1 (FDL
+// rows of the previous blocks), the level slabs and the far field of this block (their
+// windows finished in earlier launches) -- and loads H0; with those loads in flight wave 0
+// loads the overlap window, stores this block as the next call's previous block and runs the
+// window transform (wave-synchronous Stockham). After one barrier the pair lanes run the r2c
+// split, insert FDL row w, form Y = rest + H0 X and the c2r join; after a second, wave 0 runs
+// the inverse transform and stores the block (OLS: window samples [B, 2B); OLA: first half +
+// overlap).
+template<int B>
+struct lstep_cfg {
+    static constexpr int Q = B / 2;                   // bin pairs
+    static constexpr int EW = B >= 512 ? B / 64 : 8;  // transform elements per lane
+    static constexpr int TW = B / EW;                 // transform lanes (<= 64)
+    static constexpr int NT = Q > 64 ? Q : 64;        // lanes of the role
+    static constexpr int WG = NT > 256 ? NT : 256;    // workgroup size of the step kernel
+};
+
+// y += h x; the packed bin 0 ({DC, Nyquist}) takes two real products
+__device__ __forceinline__ void cmac(cf& y, cf h, cf x, bool bin0)
 {
-    const int t = threadIdx.x, Q = a.B / 2;  // float4 (2 bins) per row
-    const int lpc = Q < 256 ? Q : 256, cpw = 256 / lpc, gq = Q / lpc;
-    const int c = (bid / gq) * cpw + t / lpc, q = (bid % gq) * lpc + t % lpc;
-    if (c >= a.C) return;
-    const int64_t crow = int64_t(c) * a.cstride, ps4 = a.pstride / 2;
-    const float4* H4 = reinterpret_cast<const float4*>(a.H + crow);
-    const float4* F4 = reinterpret_cast<const float4*>(a.fdl + crow);
-    float4 sum = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int l = 0; l < kLvToep; ++l) {
-        if (l < a.nsl) {
-            const float4 r = reinterpret_cast<const float4*>(a.sl[l] + int64_t(c) * a.scs[l])[q];
-            sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
-        }
+    if (bin0) {
+        y.x = fmaf(h.x, x.x, y.x);
+        y.y = fmaf(h.y, x.y, y.y);
+    } else {
+        y.x = fmaf(h.x, x.x, fmaf(-h.y, x.y, y.x));
+        y.y = fmaf(h.x, x.y, fmaf(h.y, x.x, y.y));
     }
-    constexpr int KC = 8;  // row pairs in flight
-    acc4 a0v = {0.f, 0.f, 0.f, 0.f}, a1v = a0v;
-    for (int pb = 1; pb < a.a0; pb += KC) {
-        float4 hv[KC], xv[KC];
+}
+
+template<int B, bool OLA>
+__device__ __forceinline__ void block_role(const slice_args& a, int c, char* smem)
+{
+    using K = upols_cfg<B>;
+    using A = lstep_cfg<B>;
+    constexpr int EW = A::EW, TW = A::TW;
+    static_assert(TW <= 64 && A::NT <= 1024 && EW % 2 == 0, "block step geometry");
+    cf* X = reinterpret_cast<cf*>(smem);
+    cf* fft = X + B;
+    cf* tw = fft + K::LL;
+    const int tid = threadIdx.x;
+    const int64_t crow = int64_t(c) * a.cstride;
+    const float* in_c = a.in + int64_t(c) * a.ld_in;
+    float* prev_c = a.prev + int64_t(c) * B;
+    const int k0 = tid, k1 = tid == 0 ? B / 2 : B - tid;
+    const bool pair = tid < A::Q;
+    cf h0a = {0.f, 0.f}, h0b = h0a, ra = h0a, rb = h0a;
+    if (pair) {
+        h0a = a.H[crow + k0];
+        h0b = a.H[crow + k1];
+        cf ha[kLvA0 - 1], hb[kLvA0 - 1], xa[kLvA0 - 1], xb[kLvA0 - 1];
 #pragma unroll
-        for (int k = 0; k < KC; ++k) {
-            const int p = pb + k;
+        for (int p = 1; p < kLvA0; ++p) {
             if (p < a.a0) {
-                const int r = a.wr + 1 - p < 0 ? a.wr + 1 - p + a.ring : a.wr + 1 - p;
-                hv[k] = H4[int64_t(p) * ps4 + q];
-                xv[k] = F4[int64_t(r) * ps4 + q];
+                const int r = a.w - p < 0 ? a.w - p + a.ring : a.w - p;
+                ha[p - 1] = a.H[crow + int64_t(p) * a.pstride + k0];
+                hb[p - 1] = a.H[crow + int64_t(p) * a.pstride + k1];
+                xa[p - 1] = a.fdl[crow + int64_t(r) * a.pstride + k0];
+                xb[p - 1] = a.fdl[crow + int64_t(r) * a.pstride + k1];
             }
         }
 #pragma unroll
-        for (int k = 0; k < KC; ++k)
-            if (pb + k < a.a0) mac2(a0v, a1v, hv[k], xv[k]);
+        for (int l = 0; l < kLvToep; ++l) {
+            if (l < a.nsl) {
+                const cf* sr = a.sl[l] + int64_t(c) * a.scs[l];
+                ra = cadd(ra, sr[k0]);
+                rb = cadd(rb, sr[k1]);
+            }
+        }
+        if (a.ff) {
+            ra = cadd(ra, a.ff[int64_t(c) * a.fcs + k0]);
+            rb = cadd(rb, a.ff[int64_t(c) * a.fcs + k1]);
+        }
+#pragma unroll
+        for (int p = 1; p < kLvA0; ++p) {
+            if (p < a.a0) {
+                cmac(ra, ha[p - 1], xa[p - 1], k0 == 0);
+                cmac(rb, hb[p - 1], xb[p - 1], false);
+            }
+        }
     }
-    const cf b0 = finish(a0v, q == 0), b1 = finish(a1v, false);
-    reinterpret_cast<float4*>(a.rest + int64_t(c) * a.B)[q] =
-        make_float4(sum.x + b0.x, sum.y + b0.y, sum.z + b1.x, sum.w + b1.y);
+    if (tid < 64) {  // wave 0: window r2c, previous block
+        tw_regs<K::TW1 + K::TW2, 64> twr;
+        twr.load(a.twg, tid);
+        cf v[EW];
+        if (tid < TW) {
+            const cf* pz = reinterpret_cast<const cf*>(prev_c);
+            const cf* iz = reinterpret_cast<const cf*>(in_c);
+#pragma unroll
+            for (int m = 0; m < EW; ++m) {
+                const int n = tid + m * TW;
+                if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
+                else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+            }
+            if constexpr (!OLA) {
+                // the window's second half becomes the next call's first half, stored from
+                // registers; the lane read prev_c[n] in an earlier load of the same wave
+                cf* pw = reinterpret_cast<cf*>(prev_c);
+#pragma unroll
+                for (int m = EW / 2; m < EW; ++m) pw[tid + m * TW - B / 2] = v[m];
+            }
+        }
+        twr.store(tw, tid);
+        wave_sync();
+        stockham<B, EW, -1, 1, true>(v, fft, tw, tid, tid < TW);
+        if (tid < TW) {
+#pragma unroll
+            for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
+        }
+    }
+    __syncthreads();
+    if (pair) {
+        // bin pair (k0, k1): r2c split, FDL row w, Y = rest + H0 X, c2r join; w(B - k) = -conj(w(k))
+        const cf wa = k0 == 0 ? cf{1.f, 0.f} : twiddle<2 * B, -1>(tw + K::TW1, k0);
+        const cf wb = k0 == 0 ? cf{0.f, -1.f} : cf{-wa.x, wa.y};
+        const cf xa = r2c_split_w<B>(fft, wa, k0), xb = r2c_split_w<B>(fft, wb, k1);
+        cf* row = a.fdl + crow + int64_t(a.w) * a.pstride;
+        row[k0] = xa;
+        row[k1] = xb;
+        cf ya = ra, yb = rb;
+        cmac(ya, h0a, xa, k0 == 0);
+        cmac(yb, h0b, xb, false);
+        X[k0] = k0 == 0 ? c2r_join_w<B>(cf{ya.x, 0.f}, cf{ya.y, 0.f}, cf{1.f, 0.f}, 0)
+                        : c2r_join_w<B>(ya, yb, cf{wa.x, -wa.y}, k0);
+        X[k1] = c2r_join_w<B>(yb, k0 == 0 ? yb : ya, cf{wb.x, -wb.y}, k1);
+    }
+    __syncthreads();
+    if (tid < 64) c2r_tail<B, OLA, EW, true, true>(X, fft, tw, a.out + int64_t(c) * a.ld_out, prev_c, tid);
+}
+
+// buffer loads / stores: 32-bit lane offsets, uniform offsets in SGPRs (fewer VGPRs than
+// 64-bit addresses); offsets past the size read 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, int(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ cf buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    return __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 2 /* streaming */));
+}
+
+__device__ __forceinline__ void buf_st(cf v, __amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, 0);
 }
 
 // Toeplitz level: for the units [u0, u1) (unit u = (channel, 16 columns, block half jh)),
@@ -213,27 +330,59 @@ __device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& 
     const int uc = live ? u : ta.u1 - 1;
     const int jh = uc % JH, cg = uc / JH, c = cg / gpc, k = (cg - c * gpc) * 16 + col;
     const int j0 = jh * TJ, pa = ta.a + pg * NPL;
-    const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
-    const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
     f2v acc[TJ];
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[j] = f2v(0.f);
-    if (live && pa < ta.b) {
-        cf xr[NX], hm[NPL];
-        // xr[i] = X[tw + j0 + TJ - 1 - pa - i]: partition pa + m meets block j0 + jj at i = TJ - 1 - jj + m
+    if constexpr (UPW == 1) {
+        // one unit per workgroup: channel and block half are uniform, buffer loads with the
+        // row offsets in SGPRs; filter rows past the band read 0 (the buffer ends at b)
+        const int cu = __builtin_amdgcn_readfirstlane(c);
+        const int ps8 = int(sa.pstride * int(sizeof(cf)));
+        const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(cu) * sa.cstride, int64_t(ta.b) * ps8);
+        const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(cu) * sa.cstride, int64_t(sa.ring) * ps8);
+        if (live && pa < ta.b) {
+            cf xr[NX], hm[NPL];
+            // xr[i] = X[tw + j0 + TJ - 1 - pa - i] = row r0 + NX - 1 - i, r0 the lane's oldest
+            // row; rows from r0 + dw on wrap to the ring's start
+            int r0 = ta.tw + j0 + TJ - 1 - pa - (NX - 1);
+            r0 = r0 < 0 ? r0 + sa.ring : r0;
+            const int dw = sa.ring - r0;
+            const int v0 = r0 * ps8 + k * int(sizeof(cf)), vw = v0 - sa.ring * ps8;
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            int r = ta.tw + j0 + TJ - 1 - pa - i;
-            r = r < 0 ? r + sa.ring : r;
-            xr[i] = ld_nt(Xc + int64_t(r) * sa.pstride);
+            for (int i = 0; i < NX; ++i) {
+                const int d = NX - 1 - i;
+                xr[i] = buf_ld(xres, (d >= dw ? vw : v0) + d * ps8, 0);  // >= 0 either way
+            }
+            const int hv0 = pa * ps8 + k * int(sizeof(cf));
+#pragma unroll
+            for (int m = 0; m < NPL; ++m) hm[m] = buf_ld(hres, hv0, m * ps8);
+#pragma unroll
+            for (int m = 0; m < NPL; ++m) {
+                const pk_coef h(hm[m], k == 0);
+#pragma unroll
+                for (int jj = 0; jj < TJ; ++jj) h.mac(acc[jj], xr[TJ - 1 - jj + m]);
+            }
         }
+    } else {
+        const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
+        const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
+        if (live && pa < ta.b) {
+            cf xr[NX], hm[NPL];
+            // xr[i] = X[tw + j0 + TJ - 1 - pa - i]: partition pa + m meets block j0 + jj at i = TJ - 1 - jj + m
 #pragma unroll
-        for (int m = 0; m < NPL; ++m) hm[m] = pa + m < ta.b ? ld_nt(Hc + int64_t(pa + m) * sa.pstride) : cf{0.f, 0.f};
+            for (int i = 0; i < NX; ++i) {
+                int r = ta.tw + j0 + TJ - 1 - pa - i;
+                r = r < 0 ? r + sa.ring : r;
+                xr[i] = ld_nt(Xc + int64_t(r) * sa.pstride);
+            }
 #pragma unroll
-        for (int m = 0; m < NPL; ++m) {
-            const pk_coef h(hm[m], k == 0);
+            for (int m = 0; m < NPL; ++m) hm[m] = pa + m < ta.b ? ld_nt(Hc + int64_t(pa + m) * sa.pstride) : cf{0.f, 0.f};
 #pragma unroll
-            for (int jj = 0; jj < TJ; ++jj) h.mac(acc[jj], xr[TJ - 1 - jj + m]);
+            for (int m = 0; m < NPL; ++m) {
+                const pk_coef h(hm[m], k == 0);
+#pragma unroll
+                for (int jj = 0; jj < TJ; ++jj) h.mac(acc[jj], xr[TJ - 1 - jj + m]);
+            }
         }
     }
     if constexpr (NPG >= 4) {  // the 4 groups of a wave (lanes 16 apart)
@@ -277,16 +426,16 @@ __device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& 
 // Two phases, one step apart (the kernel boundary between them is the only synchronization:
 // an agent-scope release per workgroup costs an L2 write-back across the XCDs):
 //   phase 1  16 workgroups per unit MAC the stored segments for 16 f each, one (f, column) per
-//            lane with every load of the lane in flight at once, into acc[unit][f][col]; one
-//            more transforms the fresh row pairs and stores them to their slots
-//   phase 2  one workgroup per unit: acc + the fresh segments' products, the inverse transform
-// Packed bin 0 holds two real sequences (DC and Nyquist): its spectra are stored packed the
-// real-FFT way, W[f] = X_dc[f] (f <= 128) and W[256 - f] = X_ny[f] (0 < f < 128), with
-// W[0] = (X_dc[0], X_ny[0]) and W[128] = (X_dc[128], X_ny[128]) real pairs (k_lvf_filter
-// packs the segment spectra the same way): the MAC is the same complex product except two
-// real products at f = 0 and 128, and one unpack before the inverse transform restores
-// Y = Y_dc + i Y_ny.
-constexpr int kFarParts = 17;  // phase-1 workgroups per far unit
+//            lane with every load of the lane in flight at once, into acc[unit][f][col]
+//   phase 2  one workgroup per unit: the fresh row pairs' transforms (stored to their slots
+//            for later windows) and products, + acc, the inverse transform
+// Phase 2 reads FDL rows up to tw - 129, the last block before the window in progress, which
+// an earlier launch wrote. Packed bin 0 holds two real sequences (DC and Nyquist): its spectra are
+// stored packed the real-FFT way, W[f] = X_dc[f] (f <= 128) and W[256 - f] = X_ny[f]
+// (0 < f < 128), with W[0] = (X_dc[0], X_ny[0]) and W[128] = (X_dc[128], X_ny[128]) real pairs
+// (k_lvf_filter packs the segment spectra the same way): the MAC is the same complex product
+// except two real products at f = 0 and 128, and one unpack before the inverse transform
+// restores Y = Y_dc + i Y_ny.
 
 // Z = DFT(x_dc + i x_ny) -> packed W (real-FFT packing of X_dc, X_ny) at f, from Z[f], Z[-f]
 __device__ __forceinline__ cf pack_bin0(cf zf, cf zm, int f)
@@ -307,161 +456,171 @@ __device__ __forceinline__ cf unpack_bin0(cf wf, cf wm, int f)
     return cf{dc.x - ny.y, dc.y + ny.x};
 }
 
-// bin 0 (column 0, lanes cp == 0) of a spectrum held with v[i] at f = FOFF(i): pack or unpack
+// bin 0 (column 0, lanes cp == 0) of a spectrum held with v[i] at f = a + 16 i: pack or unpack
 // through LDS z; every lane calls (barrier inside)
-template<bool PACK, class F>
-__device__ __forceinline__ void bin0_exchange(cf (&v)[16], cf* z, int cp, F foff)
+template<bool PACK>
+__device__ __forceinline__ void bin0_exchange(cf (&v)[16], cf* z, int a, int cp)
 {
     if (cp == 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) z[foff(i)] = v[i];
+        for (int i = 0; i < 16; ++i) z[a + 16 * i] = v[i];
     }
     __syncthreads();
     if (cp == 0) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const int f = foff(i);
+            const int f = a + 16 * i;
             const cf m = z[(kFN - f) & (kFN - 1)];
             v[i] = PACK ? pack_bin0(v[i], m, f) : unpack_bin0(v[i], m, f);
         }
     }
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes)
+// phase 1, FPL f rows per lane (16 / FPL workgroups per unit; the host picks FPL so that one
+// round of NS = 16 / FPL segments covers the stored ones: every load of a lane in flight at once)
+template<int FPL>
+__device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
 {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, int(bytes), 0x00020000);
-}
-
-__device__ __forceinline__ cf buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff)
-{
-    return __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 2 /* streaming */));
-}
-
-__device__ __forceinline__ void far1_role(const slice_args& sa, int bid, char* smem)
-{
-    cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
-    cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
-    cf* tws = z + kFN;                       // twiddles
+    constexpr int PPU = 16 / FPL, NS = 16 / FPL;  // workgroups per unit, segments per round
     const int t = threadIdx.x;
-    const int ul = bid / kFarParts, part = bid - ul * kFarParts;
+    const int ul = bid / PPU, part = bid - ul * PPU;
     const int gpc = sa.B / 16, u = sa.f1u0 + ul, c = u / gpc, g = u - c * gpc;
-    const bool unit0 = g == 0;  // uniform per workgroup: the unit holding packed bin 0
     const int M = sa.M, nseg = sa.nseg;
     auto slot = [&](int s) { return ((sa.f1wn - s - 1) % M + M) % M; };
     const int64_t fs = sa.B;  // stride between f rows of a spectrum (complex)
     const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));  // bytes per spectrum (a channel's span < 2 GiB)
     const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;       // first stored segment
-    // buffer loads: 32-bit lane offsets, segment / slot offsets in SGPRs
+    // buffer loads: 32-bit lane offsets, segment / slot / f-row offsets in SGPRs; lane (f, col)
+    // holds f = 16 FPL part + (t >> 4) + 16 j, j < FPL
     const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
-    if (part < 16) {
-        // stored segments, lane (f, col)
-        const int col = t & 15, f = part * 16 + (t >> 4), k = g * 16 + col;
-        const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
-        const int vo = int((int64_t(f) * fs + k) * int(sizeof(cf)));
-        const bool z0 = unit0 && col == 0 && (f & (kFN / 2 - 1)) == 0;  // packed bin 0 at f = 0, 128
-        f2v acc = f2v(0.f);
-        constexpr int NS = 12;  // segments per round (one round up to 13 segments)
-        for (int sb = s0; sb < nseg; sb += NS) {
-            cf xv[NS], hv[NS];
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+    const int col = t & 15, f0 = part * 16 * FPL + (t >> 4), k = g * 16 + col;
+    const int vo = int((int64_t(f0) * fs + k) * int(sizeof(cf))), fo = int(16 * fs * int(sizeof(cf)));
+    f2v acc[FPL];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                if (sb + i < nseg) {
-                    hv[i] = buf_ld(hres, vo, (sb + i) * spec);
-                    xv[i] = buf_ld(xres, vo, slot(sb + i) * spec);
+    for (int j = 0; j < FPL; ++j) acc[j] = f2v(0.f);
+    for (int sb = s0; sb < nseg; sb += NS) {
+        cf xv[NS][FPL], hv[NS][FPL];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (sb + i < nseg) {
+#pragma unroll
+                for (int j = 0; j < FPL; ++j) {
+                    hv[i][j] = buf_ld(hres, vo, (sb + i) * spec + j * fo);
+                    xv[i][j] = buf_ld(xres, vo, slot(sb + i) * spec + j * fo);
                 }
             }
-#pragma unroll
-            for (int i = 0; i < NS; ++i)
-                if (sb + i < nseg) pk_coef(hv[i], z0).mac(acc, xv[i]);
         }
-        sa.f1acc[(int64_t(ul) * kFN + f) * 16 + col] = cf{acc.x, acc.y};
-        return;
-    }
-    // fresh row pairs: lanes (a, cp) hold column cp's 256 values 16 per lane
-    const int a = t >> 4, cp = t & 15, k = g * 16 + cp;
-    tws[t] = sa.twf[t];
-    const __amdgpu_buffer_rsrc_t xres =
-        buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
-    for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
-        cf v[16];
-        // rows tw - (s + 3) 128 + a + 16 n2 (the ring holds >= kFarRing > 256 rows: one wrap at most)
-        int r0 = (sa.f1tw - (s + 3) * kFarT + a) % sa.ring;
-        r0 = r0 < 0 ? r0 + sa.ring : r0;
 #pragma unroll
-        for (int n2 = 0; n2 < 16; ++n2) {
-            const int r = r0 + 16 * n2 >= sa.ring ? r0 + 16 * n2 - sa.ring : r0 + 16 * n2;
-            v[n2] = buf_ld(xres, int((int64_t(r) * sa.pstride + k) * int(sizeof(cf))), 0);
+        for (int i = 0; i < NS; ++i) {
+            if (sb + i < nseg) {
+#pragma unroll
+                for (int j = 0; j < FPL; ++j) {
+                    const bool z0 = g == 0 && col == 0 && ((f0 + 16 * j) & (kFN / 2 - 1)) == 0;  // packed bin 0, f = 0, 128
+                    pk_coef(hv[i][j], z0).mac(acc[j], xv[i][j]);
+                }
+            }
         }
-        __syncthreads();  // twiddles; the previous segment's LDS use is done
-        col_fft<-1, 16>(v, lds, tws, a, cp, true);
-        if (unit0) bin0_exchange<true>(v, z, cp, [&](int i) { return 16 * i + a; });  // uniform per workgroup
-        cf* xs = sa.xf + (int64_t(c) * M + slot(s)) * kFN * fs + k;
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) xs[int64_t(16 * k1 + a) * fs] = v[k1];
     }
+#pragma unroll
+    for (int j = 0; j < FPL; ++j) sa.f1acc[(int64_t(ul) * kFN + f0 + 16 * j) * 16 + col] = cf{acc[j].x, acc[j].y};
 }
 
 __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
 {
-    cf* lds = reinterpret_cast<cf*>(smem);
-    cf* z = lds + 16 * 16 * 16;
-    cf* tws = z + kFN;
+    cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
+    cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
+    cf* tws = z + kFN;                       // twiddles
     const int t = threadIdx.x, a = t >> 4, cp = t & 15;
     const int gpc = sa.B / 16, u = sa.f2u0 + bid, c = u / gpc, g = u - c * gpc, k = g * 16 + cp;
-    const bool unit0 = g == 0;
+    const bool unit0 = g == 0;  // uniform per workgroup: the unit holding packed bin 0
     const int M = sa.M, nseg = sa.nseg;
     auto slot = [&](int s) { return ((sa.f2wn - s - 1) % M + M) % M; };
     const int64_t fs = sa.B;
     const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));
     const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;
     tws[t] = sa.twf[t];
-    // the stored segments' sum from phase 1 + the fresh segments' products; v[n2] at f = a + 16 n2
-    // (col_fft's input layout)
-    cf v[16];
-    const cf* ac = sa.f2acc + int64_t(bid) * kFN * 16;
-#pragma unroll
-    for (int n2 = 0; n2 < 16; ++n2) v[n2] = ac[(a + 16 * n2) * 16 + cp];
     const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
+    const __amdgpu_buffer_rsrc_t fres =
+        buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
     const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
     const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
-    for (int s = 0; s < s0; ++s) {  // uniform per workgroup
-        cf xv[16], hv[16];
+    // v[i] at f = a + 16 i (col_fft's output and input layout): the stored segments' sum from
+    // phase 1 + the fresh segments' products, kept in acc between segments (priming: every
+    // segment is fresh) so that it is not live across a transform
+    cf v[16];
+    const __amdgpu_buffer_rsrc_t ares = buf_rsrc(sa.f2acc + int64_t(bid) * kFN * 16, kFN * 16 * int(sizeof(cf)));
+    const int ao = (a * 16 + cp) * int(sizeof(cf)), as = 16 * 16 * int(sizeof(cf));  // f = a + 16 i
+    for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
+        // fresh row pair: rows tw - (s + 3) 128 + a + 16 n (the ring holds >= kFarRing > 256
+        // rows: one wrap at most)
+        cf x[16];
+        int r0 = (sa.f2tw - (s + 3) * kFarT + a) % sa.ring;
+        r0 = r0 < 0 ? r0 + sa.ring : r0;
 #pragma unroll
-        for (int n2 = 0; n2 < 16; ++n2) {
-            const int so = int(16 * n2 * fs * int(sizeof(cf)));
-            hv[n2] = buf_ld(hres, vo, s * spec + so);
-            xv[n2] = buf_ld(xres, vo, slot(s) * spec + so);
+        for (int n = 0; n < 16; ++n) {
+            const int r = r0 + 16 * n >= sa.ring ? r0 + 16 * n - sa.ring : r0 + 16 * n;
+            x[n] = buf_ld(fres, int((int64_t(r) * sa.pstride + k) * int(sizeof(cf))), 0);
         }
+        __syncthreads();  // twiddles; the previous segment's LDS use is done
+        col_fft<-1, 16>(x, lds, tws, a, cp, true);
+        if (unit0) bin0_exchange<true>(x, z, a, cp);  // uniform per workgroup
+        cf hv[16];
 #pragma unroll
-        for (int n2 = 0; n2 < 16; ++n2) {
-            f2v w = {v[n2].x, v[n2].y};
-            pk_coef(hv[n2], unit0 && cp == 0 && ((a + 16 * n2) & (kFN / 2 - 1)) == 0).mac(w, xv[n2]);
-            v[n2] = cf{w.x, w.y};
+        for (int i = 0; i < 16; ++i) hv[i] = buf_ld(hres, vo, s * spec + int(16 * i * fs * int(sizeof(cf))));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = buf_ld(ares, ao, i * as);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            buf_st(x[i], xres, vo, slot(s) * spec + int(16 * i * fs * int(sizeof(cf))));
+            f2v w = {v[i].x, v[i].y};
+            pk_coef(hv[i], unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0).mac(w, x[i]);
+            v[i] = cf{w.x, w.y};
+        }
+        if (s + 1 < s0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) buf_st(v[i], ares, ao, i * as);
         }
     }
-    __syncthreads();  // twiddles
-    if (unit0) bin0_exchange<false>(v, z, cp, [&](int i) { return a + 16 * i; });  // uniform per workgroup
+    __syncthreads();  // twiddles; the bin-0 exchange of the last segment is done
+    if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
     col_fft<1, 16>(v, lds, tws, a, cp, true);
     constexpr float sc = 1.0f / kFN;
-    cf* o = sa.f2ff + int64_t(c) * kFarT * fs + k;
+    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f2ff + int64_t(c) * kFarT * fs, spec / 2);
 #pragma unroll
-    for (int m = 8; m < 16; ++m) o[int64_t(16 * (m - 8) + a) * fs] = cscale(v[m], sc);  // n = 16 m + a >= 128
+    for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128
+        buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
 }
 
-__global__ __launch_bounds__(256) void k_lvl_slices(slice_args a)
+// The step kernel (k_lvl_step): one launch per block, workgroups by role, the longest chains
+// first -- far phase 2, the block itself, the Toeplitz slices (largest window first), far
+// phase 1. No role reads what another role of the same launch writes: the block writes FDL
+// row w and reads its slabs / far field (finished in earlier launches); the slices read FDL
+// rows before the current window and write the next window's slabs / far field.
+#ifndef NEO_STEP_WPE
+#define NEO_STEP_WPE 3  // waves per SIMD the step kernel is compiled for (VGPR budget)
+#endif
+template<int B, bool OLA>
+__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(NEO_STEP_WPE))) void k_lvl_step(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
     int bid = int(blockIdx.x);
 #ifndef NEO_ROLES
-#define NEO_ROLES 15
+#define NEO_ROLES 31  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2
 #endif
-    if (bid < a.nrest) {
-        if (NEO_ROLES & 1) rest_role(a, bid);
+    if (bid < a.f2nwg) {
+        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2_role(a, bid, smem);
         return;
     }
-    bid -= a.nrest;
+    bid -= a.f2nwg;
+    if (bid < a.nblk) {
+        if (NEO_ROLES & 1) block_role<B, OLA>(a, bid, smem);
+        return;
+    }
+    bid -= a.nblk;
+    if (threadIdx.x >= 256) return;
 #pragma unroll
-    for (int l = 0; l < kLvToep; ++l) {  // static indices: no copy of the argument block to scratch
+    for (int l = kLvToep - 1; l >= 0; --l) {  // static indices: no copy of the argument block to scratch
         if (l < a.ntp) {
             const toep_arg ta = a.tp[l];  // by value: registers, not a scratch copy of the array
             if (bid < ta.nwg) {  // geometry per window: toep_geom
@@ -481,12 +640,11 @@ __global__ __launch_bounds__(256) void k_lvl_slices(slice_args a)
             bid -= ta.nwg;
         }
     }
-    if (bid < a.f1nwg) {
-        if (NEO_ROLES & 8) far1_role(a, bid, smem);
-        return;
+    if (bid < a.f1nwg && (NEO_ROLES & 8)) {
+        if (a.f1fpl == 4) far1_role<4>(a, bid);
+        else if (a.f1fpl == 2) far1_role<2>(a, bid);
+        else far1_role<1>(a, bid);
     }
-    bid -= a.f1nwg;
-    if (bid < a.f2nwg && (NEO_ROLES & 8)) far2_role(a, bid, smem);
 }
 
 // Segment spectra (grid C x NSEG x B/16): hf[c][s][f][k] = DFT256 over r < 128 of
@@ -531,108 +689,11 @@ __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf
 }
 
 // ---------------------------------------------------------------------------------------
-// Block step (grid C, 64 + B/2 lanes): wave 0 loads the overlap window, stores this block
-// as the next call's previous block and runs the window transform (wave-synchronous
-// Stockham); meanwhile lane i of the other B/2 lanes loads the precomputed rest spectrum, the
-// block's far field and H0 of the mirror pair of bins (i, B - i). After one barrier those lanes run the r2c split,
-// insert FDL row w, form Y = rest + H0 X and the c2r join; after a second, wave 0 runs the
-// inverse transform and stores the block (OLS: window samples [B, 2B); OLA: first half +
-// overlap).
-template<int B>
-struct lstep_cfg {
-    static constexpr int Q = B / 2;                   // bin pairs
-    static constexpr int EW = B >= 512 ? B / 64 : 8;  // transform elements per lane
-    static constexpr int TW = B / EW;                 // transform lanes (<= 64)
-    static constexpr int NT = 64 + Q;                 // workgroup size
-};
-
-template<int B, bool OLA>
-__global__ __launch_bounds__(lstep_cfg<B>::NT) void k_upols_lvl(
-    const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
-    const cf* __restrict__ H, cf* __restrict__ fdl, const cf* __restrict__ twg, int w, int64_t cstride,
-    int64_t pstride, const cf* __restrict__ rest, const cf* __restrict__ far, int64_t fcs)
-{
-    using K = upols_cfg<B>;
-    using A = lstep_cfg<B>;
-    constexpr int EW = A::EW, TW = A::TW;
-    static_assert(TW <= 64 && A::NT <= 1024 && EW % 2 == 0, "block step geometry");
-    __shared__ __attribute__((aligned(16))) cf X[B];
-    __shared__ cf fft[K::LL];
-    __shared__ cf tw[K::TW1 + K::TW2];
-    const int tid = threadIdx.x, c = blockIdx.x;
-    const int64_t crow = int64_t(c) * cstride;
-    const float* in_c = in + int64_t(c) * ld_in;
-    float* prev_c = prev + int64_t(c) * B;
-    const int i0 = tid - 64, k0 = i0, k1 = i0 == 0 ? B / 2 : B - i0;
-    cf h0a = {0.f, 0.f}, h0b = h0a, ra = h0a, rb = h0a;
-    if (tid >= 64) {
-        h0a = H[crow + k0];
-        h0b = H[crow + k1];
-        ra = rest[int64_t(c) * B + k0];
-        rb = rest[int64_t(c) * B + k1];
-        if (far) {  // the far field of this block (not in rest: its window is finished by the
-                    // launch just before this step)
-            ra = cadd(ra, far[int64_t(c) * fcs + k0]);
-            rb = cadd(rb, far[int64_t(c) * fcs + k1]);
-        }
-    } else {  // wave 0: window r2c, previous block
-        tw_regs<K::TW1 + K::TW2, 64> twr;
-        twr.load(twg, tid);
-        cf v[EW];
-        if (tid < TW) {
-            const cf* pz = reinterpret_cast<const cf*>(prev_c);
-            const cf* iz = reinterpret_cast<const cf*>(in_c);
-#pragma unroll
-            for (int m = 0; m < EW; ++m) {
-                const int n = tid + m * TW;
-                if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
-                else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
-            }
-            if constexpr (!OLA) {
-                // the window's second half becomes the next call's first half, stored from
-                // registers; the lane read prev_c[n] in an earlier load of the same wave
-                cf* pw = reinterpret_cast<cf*>(prev_c);
-#pragma unroll
-                for (int m = EW / 2; m < EW; ++m) pw[tid + m * TW - B / 2] = v[m];
-            }
-        }
-        twr.store(tw, tid);
-        wave_sync();
-        stockham<B, EW, -1, 1, true>(v, fft, tw, tid, tid < TW);
-        if (tid < TW) {
-#pragma unroll
-            for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
-        }
-    }
-    __syncthreads();
-    if (tid >= 64) {
-        // bin pair (k0, k1): r2c split, FDL row w, Y = rest + H0 X, c2r join; w(B - k) = -conj(w(k))
-        const cf wa = k0 == 0 ? cf{1.f, 0.f} : twiddle<2 * B, -1>(tw + K::TW1, k0);
-        const cf wb = k0 == 0 ? cf{0.f, -1.f} : cf{-wa.x, wa.y};
-        const cf xa = r2c_split_w<B>(fft, wa, k0), xb = r2c_split_w<B>(fft, wb, k1);
-        cf* row = fdl + crow + int64_t(w) * pstride;
-        row[k0] = xa;
-        row[k1] = xb;
-        cf ya = ra, yb = rb;
-        if (k0 == 0) {  // packed {DC, Nyquist}: two real products
-            ya.x += h0a.x * xa.x;
-            ya.y += h0a.y * xa.y;
-        } else {
-            ya.x += h0a.x * xa.x - h0a.y * xa.y;
-            ya.y += h0a.x * xa.y + h0a.y * xa.x;
-        }
-        yb.x += h0b.x * xb.x - h0b.y * xb.y;
-        yb.y += h0b.x * xb.y + h0b.y * xb.x;
-        X[k0] = k0 == 0 ? c2r_join_w<B>(cf{ya.x, 0.f}, cf{ya.y, 0.f}, cf{1.f, 0.f}, 0)
-                        : c2r_join_w<B>(ya, yb, cf{wa.x, -wa.y}, k0);
-        X[k1] = c2r_join_w<B>(yb, k0 == 0 ? yb : ya, cf{wb.x, -wb.y}, k1);
-    }
-    __syncthreads();
-    if (tid < 64) c2r_tail<B, OLA, EW, true, true>(X, fft, tw, out + int64_t(c) * ld_out, prev_c, tid);
-}
-
 // ---------------------------------------------------------------------------------------
 // host side
+
+// phase 1 f rows per lane: one load round covers the stored segments (far1_role)
+static int far1_fpl(const upols_t* h) { return h->lv.nseg - 1 <= 4 ? 4 : (h->lv.nseg - 1 <= 8 ? 2 : 1); }
 
 static size_t far_units_per_slice(const upols_t* h) { return (size_t(h->C) * (h->B / 16) + kFarT - 1) / kFarT; }
 
@@ -655,7 +716,6 @@ static int lvl_buffers(upols_t* h)
         }
         return fail(NEO_HIP_ENOMEM, "level pipeline: allocation of %s (%zu bytes) failed", what, bytes);
     };
-    if (!alloc(reinterpret_cast<void**>(&h->lv_rest), C * B * sizeof(cf))) return undo("rest spectra", C * B * sizeof(cf));
     for (int l = 0; l < lp.n; ++l) {
         const size_t bytes = 2 * C * size_t(lp.T[l]) * B * sizeof(cf);
         if (!alloc(reinterpret_cast<void**>(&h->lv_slab[l]), bytes)) return undo("level slabs", bytes);
@@ -684,11 +744,10 @@ void lvl_free(upols_t* h)
         (void)hipFree(p);
         p = nullptr;
     }
-    for (cf** p : {&h->lv_rest, &h->fv_hf, &h->fv_xf, &h->fv_ff, &h->fv_tw, &h->fv_acc}) {
+    for (cf** p : {&h->fv_hf, &h->fv_xf, &h->fv_ff, &h->fv_tw, &h->fv_acc}) {
         (void)hipFree(*p);
         *p = nullptr;
     }
-
     h->lv_ready = false;
 }
 
@@ -701,19 +760,7 @@ void lvl_filter_changed(upols_t* h)
 
 static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) % R); }
 
-
-// far-level fields shared by both phases
-static void far_common(const upols_t* h, slice_args& a, int nfresh)
-{
-    a.M = h->lv.nseg;
-    a.nseg = h->lv.nseg;
-    a.fnfresh = nfresh;
-    a.hf = h->fv_hf;
-    a.xf = h->fv_xf;
-    a.twf = h->fv_tw;
-}
-
-// Toeplitz role geometry per window T (toep_role<T, NPL, NPG, JH> in k_lvl_slices)
+// Toeplitz role geometry per window T (toep_role<T, NPL, NPG, JH> in k_lvl_step)
 static void toep_geom(int T, int& JH, int& UPW)
 {
     JH = T == 32 ? 2 : 1;
@@ -721,40 +768,88 @@ static void toep_geom(int T, int& JH, int& UPW)
     UPW = 256 / (16 * NPG);
 }
 
-// The slices launch of step n (block t at ring row w; n = -1: the step before the first,
-// part of priming): the rest spectrum of block t + 1 and slice (n + 1) mod T of window
-// (n + 1) / T + 1 of every level (the one-step lead leaves every window's slabs complete one
-// step before its first block, when the rest role reads them).
-static int launch_slices(upols_t* h, int64_t n, int w, hipStream_t s)
+static slice_args base_args(const upols_t* h)
 {
-    const level_plan& lp = h->lv;
-    const int B = h->B, C = h->C, R = h->ring;
     slice_args a{};
     a.H = h->H;
     a.fdl = h->fdl;
-    a.ring = R;
-    a.C = C;
-    a.B = B;
+    a.ring = h->ring;
+    a.C = h->C;
+    a.B = h->B;
     a.cstride = h->cstride;
     a.pstride = h->pstride;
-    // rest role
-    const int64_t n1 = n + 1;
-    const int Q = B / 2, lpc = std::min(Q, 256), cpw = 256 / lpc, gq = Q / lpc;
-    a.rest = h->lv_rest;
-    a.nrest = (C + cpw - 1) / cpw * gq;
-    a.wr = w;
+    if (h->lv.nseg) {
+        a.M = h->lv.nseg;
+        a.nseg = h->lv.nseg;
+        a.fnfresh = 1;
+        a.hf = h->fv_hf;
+        a.xf = h->fv_xf;
+        a.twf = h->fv_tw;
+    }
+    return a;
+}
+
+static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t s)
+{
+    const unsigned grid = unsigned(a.f2nwg + a.nblk + a.f1nwg) + [&] {
+        unsigned t = 0;
+        for (int l = 0; l < a.ntp; ++l) t += unsigned(a.tp[l].nwg);
+        return t;
+    }();
+    if (!grid) return NEO_HIP_OK;
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, true>), dim3(grid),
+                                                                             dim3(lstep_cfg<BB>::WG), 0, s, a))
+    } else {
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, false>), dim3(grid),
+                                                                             dim3(lstep_cfg<BB>::WG), 0, s, a))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    return NEO_HIP_OK;
+}
+
+// far phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1 (one step ahead of
+// its phase 2); block t0 + n is at ring row w
+static void far1_args(const upols_t* h, int64_t n, slice_args& a)
+{
+    const int64_t U = int64_t(h->C) * (h->B / 16), n1 = n + 1, st = n1 % kFarT, W = n1 / kFarT + 1;
+    const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
+    a.f1u0 = u0;
+    a.f1fpl = far1_fpl(h);
+    a.f1nwg = (u1 - u0) * (16 / a.f1fpl);
+    a.f1wn = int(W);
+    a.f1acc = h->fv_acc + (n1 & 1) * far_units_per_slice(h) * kFN * 16;
+}
+
+// The launch of step n >= 0 (block t0 + n at ring row w): the block and slice n mod T of
+// window n / T + 1 of every Toeplitz level (its rows end at the window in progress, so every
+// window's slabs are complete when its first block runs); far phase 2 of slice n mod 128 of
+// window n / 128 + 1 and phase 1 of the next slice.
+static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, float* out, int64_t ld_out,
+                       hipStream_t s)
+{
+    const level_plan& lp = h->lv;
+    const int B = h->B, C = h->C, R = h->ring, w = h->wpos;
+    slice_args a = base_args(h);
+    a.nblk = C;
+    a.in = in;
+    a.ld_in = ld_in;
+    a.out = out;
+    a.ld_out = ld_out;
+    a.prev = h->prev;
+    a.twg = h->tw;
+    a.w = w;
     a.a0 = lp.a0;
     for (int l = 0; l < lp.n; ++l) {
         const int T = lp.T[l];
-        a.sl[a.nsl] = h->lv_slab[l] + ((n1 / T & 1) * C * T + n1 % T) * B;
+        a.sl[a.nsl] = h->lv_slab[l] + ((n / T & 1) * C * T + n % T) * B;
         a.scs[a.nsl++] = int64_t(T) * B;
     }
-    int total = a.nrest;
     for (int l = 0; l < lp.n; ++l) {
         const int T = lp.T[l];
         int JH, UPW;
         toep_geom(T, JH, UPW);
-        const int64_t U = int64_t(C) * (B / 16) * JH, st = n1 % T, W = n1 / T + 1;
+        const int64_t U = int64_t(C) * (B / 16) * JH, st = n % T, W = n / T + 1;
         toep_arg& ta = a.tp[a.ntp];
         ta.u0 = int(st * U / T);
         ta.u1 = int((st + 1) * U / T);
@@ -763,45 +858,30 @@ static int launch_slices(upols_t* h, int64_t n, int w, hipStream_t s)
         ta.T = T;
         ta.a = lp.a[l];
         ta.b = lp.b[l];
-        ta.tw = ring_add(w, W * T - n, R);  // block t = t0 + n at row w; the window starts at t0 + W T
+        ta.tw = ring_add(w, W * T - n, R);  // block t0 + n at row w; the window starts at t0 + W T
         ta.nwg = (ta.u1 - ta.u0 + UPW - 1) / UPW;
-        total += ta.nwg;
         ++a.ntp;
     }
     if (lp.nseg) {
-        far_common(h, a, 1);
-        const int64_t U = int64_t(C) * (B / 16);
-        const size_t accb = far_units_per_slice(h) * kFN * 16;
-        {  // phase 1: slice (n + 1) mod 128 of window (n + 1) / 128 + 1
-            const int64_t st = n1 % kFarT, W = n1 / kFarT + 1;
-            const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
-            a.f1u0 = u0;
-            a.f1nwg = (u1 - u0) * kFarParts;
-            a.f1tw = ring_add(w, W * kFarT - n, R);
-            a.f1wn = int(W);
-            a.f1acc = h->fv_acc + (n1 & 1) * accb;
-            total += a.f1nwg;
-        }
-        if (n >= 0) {  // phase 2: the slice phase 1 did at step n - 1
-            const int64_t st = n % kFarT, W = n / kFarT + 1;
-            const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
-            a.f2u0 = u0;
-            a.f2nwg = u1 - u0;
-            a.f2wn = int(W);
-            a.f2acc = h->fv_acc + (n & 1) * accb;
-            a.f2ff = h->fv_ff + (W & 1) * C * kFarT * B;
-            total += a.f2nwg;
-        }
+        a.ff = h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B;
+        a.fcs = int64_t(kFarT) * B;
+        const int64_t U = int64_t(C) * (B / 16), st = n % kFarT, W = n / kFarT + 1;
+        const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
+        a.f2u0 = u0;
+        a.f2nwg = u1 - u0;
+        a.f2tw = ring_add(w, W * kFarT - n, R);
+        a.f2wn = int(W);
+        a.f2acc = h->fv_acc + (n & 1) * far_units_per_slice(h) * kFN * 16;
+        a.f2ff = h->fv_ff + (W & 1) * C * kFarT * B;
+        far1_args(h, n, a);
     }
-    hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(total)), dim3(256), 0, s, a);
-    NEO_HIP_LAUNCH_CHECK();
-    return NEO_HIP_OK;
+    return launch_step_kernel(h, a, s);
 }
 
 // First streaming step after a reset / filter change / batched pass (block t0 at ring row w):
 // window 0 of every level, starting at t0, computed whole (all units; the far level
-// transforms every segment), then the slices launch of "step -1" (the rest spectrum of t0
-// and the first slice of every window 1).
+// transforms every segment), then phase 1 of the far level's first slice of window 1 (the
+// launch of "step -1").
 static int lvl_prime(upols_t* h, hipStream_t s)
 {
     const level_plan& lp = h->lv;
@@ -813,15 +893,7 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         NEO_HIP_LAUNCH_CHECK();
         h->fv_dirty = false;
     }
-    slice_args a{};
-    a.H = h->H;
-    a.fdl = h->fdl;
-    a.ring = h->ring;
-    a.C = C;
-    a.B = B;
-    a.cstride = h->cstride;
-    a.pstride = h->pstride;
-    int total = 0;
+    slice_args a = base_args(h);
     for (int l = 0; l < lp.n; ++l) {
         int JH, UPW;
         toep_geom(lp.T[l], JH, UPW);
@@ -834,45 +906,35 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         ta.u0 = 0;
         ta.u1 = C * (B / 16) * JH;
         ta.nwg = (ta.u1 + UPW - 1) / UPW;
-        total += ta.nwg;
     }
-    if (total) {
-        hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(total)), dim3(256), 0, s, a);
-        NEO_HIP_LAUNCH_CHECK();
+    if (int rc = launch_step_kernel(h, a, s)) return rc;
+    if (!lp.nseg) return NEO_HIP_OK;
+    // far window 0, every segment transformed, in slices (the partial sums hold one)
+    slice_args f = base_args(h);
+    f.fnfresh = lp.nseg;
+    f.f1wn = 0;
+    f.f1acc = h->fv_acc;
+    f.f2tw = w;
+    f.f2wn = 0;
+    f.f2acc = h->fv_acc;
+    f.f2ff = h->fv_ff;
+    const int64_t U = int64_t(C) * (B / 16);
+    for (int st = 0; st < kFarT; ++st) {
+        const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
+        if (u1 <= u0) continue;
+        f.f1u0 = u0;
+        f.f1fpl = far1_fpl(h);
+        f.f1nwg = (u1 - u0) * (16 / f.f1fpl);  // zero partial sums (no stored segments)
+        f.f2nwg = 0;
+        if (int rc = launch_step_kernel(h, f, s)) return rc;
+        f.f1nwg = 0;
+        f.f2u0 = u0;
+        f.f2nwg = u1 - u0;
+        if (int rc = launch_step_kernel(h, f, s)) return rc;
     }
-    if (lp.nseg) {  // far window 0, every segment transformed, in slices (the partial sums hold one)
-        slice_args f{};
-        f.H = h->H;
-        f.fdl = h->fdl;
-        f.ring = h->ring;
-        f.C = C;
-        f.B = B;
-        f.cstride = h->cstride;
-        f.pstride = h->pstride;
-        far_common(h, f, lp.nseg);
-        f.f1tw = w;
-        f.f1wn = 0;
-        f.f1acc = h->fv_acc;
-        f.f2wn = 0;
-        f.f2acc = h->fv_acc;
-        f.f2ff = h->fv_ff;
-        const int64_t U = int64_t(C) * (B / 16);
-        for (int st = 0; st < kFarT; ++st) {
-            const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
-            if (u1 <= u0) continue;
-            f.f1u0 = u0;
-            f.f1nwg = (u1 - u0) * kFarParts;
-            f.f2nwg = 0;
-            hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(f.f1nwg)), dim3(256), 0, s, f);
-            NEO_HIP_LAUNCH_CHECK();
-            f.f1nwg = 0;
-            f.f2u0 = u0;
-            f.f2nwg = u1 - u0;
-            hipLaunchKernelGGL(k_lvl_slices, dim3(unsigned(f.f2nwg)), dim3(256), 0, s, f);
-            NEO_HIP_LAUNCH_CHECK();
-        }
-    }
-    return launch_slices(h, -1, ring_add(w, -1, h->ring), s);
+    slice_args p = base_args(h);
+    far1_args(h, -1, p);
+    return launch_step_kernel(h, p, s);
 }
 
 int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
@@ -884,27 +946,11 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
         h->lv_n = 0;
     }
     const int64_t n = h->lv_n;
-    const int B = h->B, C = h->C, R = h->ring;
-    const cf* farp = h->lv.nseg ? h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B : nullptr;
-    const int64_t fcs = int64_t(kFarT) * B;
     upols_t::ev_group* ev = nullptr;
-    if ((rc = timing_begin(h, 3, &ev)) || (rc = timing_mark(ev, 0, s))) return rc;
-    if (h->ola) {
-        NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
-                                  (k_upols_lvl<BB, true>), dim3(unsigned(C)), dim3(lstep_cfg<BB>::NT), 0, s, in, ld_in,
-                                  out, ld_out, h->prev, h->H, h->fdl, h->tw, h->wpos, h->cstride, h->pstride, h->lv_rest,
-                                  farp, fcs))
-    } else {
-        NEO_UPOLS_DISPATCH(B, if constexpr (BB <= 1024) hipLaunchKernelGGL(
-                                  (k_upols_lvl<BB, false>), dim3(unsigned(C)), dim3(lstep_cfg<BB>::NT), 0, s, in, ld_in,
-                                  out, ld_out, h->prev, h->H, h->fdl, h->tw, h->wpos, h->cstride, h->pstride, h->lv_rest,
-                                  farp, fcs))
-    }
-    NEO_HIP_LAUNCH_CHECK();
+    if ((rc = timing_begin(h, 2, &ev)) || (rc = timing_mark(ev, 0, s))) return rc;
+    if ((rc = launch_step(h, n, in, ld_in, out, ld_out, s))) return rc;
     if ((rc = timing_mark(ev, 1, s))) return rc;
-    if ((rc = launch_slices(h, n, h->wpos, s))) return rc;
-    if ((rc = timing_mark(ev, 2, s))) return rc;
-    h->wpos = h->wpos + 1 >= R ? 0 : h->wpos + 1;
+    h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
     h->lv_n = n + 1;
     return NEO_HIP_OK;
 }

@@ -258,8 +258,8 @@ class UpolsConvolver:
 
     def timing_detail(self):
         """Per part [(ms, count)] * 4 since the last call (neo_hip_upols_timing_detail):
-        streaming steps 0 = block step, 1 = the slices launch (rest spectrum, level
-        slices), 3 = whole step; plain / batched steps 0 = MAC kernel."""
+        streaming-level steps 0 = the step kernel (k_lvl_step: block and level slices);
+        plain / batched steps 0 = MAC kernel."""
         ms, n = (ctypes.c_double * 4)(), (ctypes.c_int64 * 4)()
         _native.check(_native.load().neo_hip_upols_timing_detail(self._h, ms, n))
         return [(ms[k], n[k]) for k in range(4)]

@@ -373,3 +373,44 @@ def stft(x: np.ndarray, frame: int, transform: int, overlap: int, window: np.nda
     if lib().oracle_stft(x, C, L, frame, transform, overlap, w, out):
         raise RuntimeError("oracle stft failed")
     return out.view(np.complex64).reshape(C, F, N // 2 + 1)
+
+
+# ---------------------------------------------------------------------------------------
+# cpu_baseline only (bench.py): the reference's SIMD MAC restated (neo_baseline.c), a separate
+# library so that liboracle.so stays the exact scalar oracle
+_BLIB = os.path.join(_HERE, "liboracle_simd.so")
+_blib = None
+SIMD_NAMES = {2: "avx512f (xsimd batch<complex<float>>, 16 complex per op, restated)",
+              1: "avx2+fma (xsimd batch<complex<float>>, 8 complex per op, restated)", 0: "scalar"}
+
+
+def baseline_lib():
+    global _blib
+    if _blib is None:
+        srcs = [os.path.join(_HERE, f) for f in ("neo_baseline.c", "neo_oracle.c", "neo_oracle_f64.c")]
+        if not os.path.exists(_BLIB) or os.path.getmtime(_BLIB) < max(os.path.getmtime(f) for f in srcs):
+            subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle_simd.so"])
+        L = ctypes.CDLL(_BLIB)
+        L.baseline_dense_convolve.argtypes = [_f32p, _f32p, _f32p, _sz, _sz, _sz, _sz, ctypes.c_int, ctypes.c_int]
+        L.baseline_simd_level.restype = ctypes.c_int
+        _blib = L
+    return _blib
+
+
+def simd_level() -> int:
+    """2 = AVX-512F, 1 = AVX2 + FMA, 0 = scalar: what the baseline's MAC uses on this host."""
+    return int(baseline_lib().baseline_simd_level())
+
+
+def dense_convolve_simd(signal: np.ndarray, partitions: np.ndarray, threads: int = 1, level: int = -1) -> np.ndarray:
+    """dense_convolve<upols_convolver> with the reference's SIMD interleaved MAC (timing
+    baseline; matches dense_convolve within float rounding, not bit for bit)."""
+    signal = np.ascontiguousarray(signal, dtype=np.float32)
+    C, N = signal.shape
+    _, P, bins = partitions.shape
+    out = np.empty_like(signal)
+    rc = baseline_lib().baseline_dense_convolve(signal, out, _cf(partitions).reshape(-1), C, N, P, bins - 1,
+                                                threads, level)
+    if rc:
+        raise RuntimeError("baseline dense_convolve failed")
+    return out

@@ -3,16 +3,18 @@ numpy and checked against the direct block-axis convolution — no GPU needed.
 
 Per bin the convolver output is Y[t] = sum_p H[p] X[t - p]
 (uniform_partitioned_convolver.hpp:47-65; fdl_index.hpp:23-36: partition p meets FDL row
-t - p). The HIP path splits the partitions into the bands of neo_hip_upols_level_plan and
-computes each band's next window during the current one, a slice of the bins per step and
-one step ahead, from FDL rows that already exist; after each block step the same launch sums
-the next block's partitions 1..a0-1 and Toeplitz slabs into a "rest" spectrum, so the block
-step adds only the rest, its far-field entry and H0 X. This test replays exactly that schedule — the ring positions the host
-passes (tw), the slice ranges, the double-buffered slabs, the rest spectrum, the far level's
-XF ring of row-pair spectra and its 256-point partition-axis transforms — on random
-spectra, with history before the levels start, ring wraparound and re-priming, and checks
-every output block. It pins the index arithmetic the kernels share with the host code; the
-kernels' arithmetic itself is pinned by the GPU parity tests against the oracle.
+t - p). The HIP path splits the partitions into the bands of neo_hip_upols_level_plan: the
+block itself takes partitions 0..a0-1, each Toeplitz level computes its next window during
+the current one (a slice of the bins per step, from FDL rows before the current window), and
+the far level does the same in two phases one step apart. All of it runs in ONE launch per
+step (k_lvl_step), so no role may read what another role of the same step writes. This test
+replays exactly that schedule — the ring positions the host passes (tw), the slice ranges,
+the double-buffered slabs, the far level's XF ring of row-pair spectra, its partial sums and
+256-point partition-axis transforms — on random spectra, with history before the levels
+start, ring wraparound and re-priming, running the roles of every step in a random order
+(with the block's FDL row written at a random point among them), and checks every output
+block. It pins the index arithmetic the kernels share with the host code; the kernels'
+arithmetic itself is pinned by the GPU parity tests against the oracle.
 """
 from __future__ import annotations
 
@@ -49,7 +51,7 @@ class Sim:
         self.w = 0
         self.n = -1
         self.slab = [np.zeros((2, T, self.K), complex) for T in lp["T"]]
-        self.rest = np.zeros(self.K, complex)
+        self.rng = np.random.default_rng(self.P)
         ns = lp["nseg"]
         if ns:
             self.M = ns
@@ -62,6 +64,7 @@ class Sim:
             self.HF = np.fft.fft(seg, axis=1)
             self.XF = np.zeros((ns, FN, self.K), complex)
             self.ff = np.zeros((2, FT, self.K), complex)
+            self.acc = np.zeros((2, FN, self.K), complex)
 
     def plain(self, x):
         """One plain step (all partitions from the ring); the levels re-prime after it."""
@@ -78,65 +81,86 @@ class Sim:
             rows = (tw + j - ps) % self.R
             self.slab[l][buf, j, k0:k1] = (self.H[a:b, k0:k1] * self.ring[rows, k0:k1]).sum(0)
 
-    def far(self, tw, wn, k0, k1, nfresh):
-        ns, M = self.lp["nseg"], self.M
+    def far1(self, wn, k0, k1, nfresh, buf):
+        """phase 1: the stored segments' products into the partial sums"""
         acc = np.zeros((FN, k1 - k0), complex)
-        for s in range(ns):
-            slot = (wn - s - 1) % M
-            if s < nfresh:
-                rows = [(tw - (s + 3) * FT + i) % self.R for i in range(FN)]
-                self.XF[slot, :, k0:k1] = np.fft.fft(self.ring[rows, k0:k1], axis=0)
+        for s in range(nfresh, self.lp["nseg"]):
+            slot = (wn - s - 1) % self.M
             acc += self.XF[slot, :, k0:k1] * self.HF[s, :, k0:k1]
-        y = np.fft.ifft(acc, axis=0)
-        self.ff[wn & 1, :, k0:k1] = y[FT:]
+        self.acc[buf, :, k0:k1] = acc
 
-    def slices(self, n, w):
-        """The slices launch after the block step of step n (block at ring row w; n = -1:
-        the priming step before the first)."""
-        lp, K, R = self.lp, self.K, self.R
+    def far2(self, tw, wn, k0, k1, nfresh, buf):
+        """phase 2: the fresh row pairs' transforms (stored to their slots) and products, the
+        inverse transform into the far field"""
+        acc = self.acc[buf, :, k0:k1].copy()
+        for s in range(min(nfresh, self.lp["nseg"])):
+            slot = (wn - s - 1) % self.M
+            rows = [(tw - (s + 3) * FT + i) % self.R for i in range(FN)]
+            self.XF[slot, :, k0:k1] = np.fft.fft(self.ring[rows, k0:k1], axis=0)
+            acc += self.XF[slot, :, k0:k1] * self.HF[s, :, k0:k1]
+        self.ff[wn & 1, :, k0:k1] = np.fft.ifft(acc, axis=0)[FT:]
+
+    def far1_slice(self, n, w):
+        """phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1"""
         n1 = n + 1
-        rest = (self.H[1: lp["a0"]] * self.ring[(w + 1 - np.arange(1, lp["a0"])) % R]).sum(0)
-        for l, T in enumerate(lp["T"]):
-            rest = rest + self.slab[l][(n1 // T) & 1, n1 % T]
-        self.rest = rest
+        st, W = n1 % FT, n1 // FT + 1
+        k0, k1 = st * self.K // FT, (st + 1) * self.K // FT
+        if k1 > k0:
+            self.far1(W, k0, k1, 1, n1 & 1)
+
+    def roles(self, n, w):
+        """the slice roles of step n (block at ring row w), as closures"""
+        lp, K, R = self.lp, self.K, self.R
+        out = []
         for l, T in enumerate(lp["T"]):
             JH = 2 if T == 32 else 1
             U = (K // 16) * JH if K >= 16 else K
-            st, W = n1 % T, n1 // T + 1
+            st, W = n % T, n // T + 1
             u0, u1 = st * U // T, (st + 1) * U // T
             if u1 > u0:
                 k0, k1 = u0 * K // U, u1 * K // U
-                self.toep(l, (w + W * T - n) % R, k0, k1, W & 1)
+                out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w + W * T - n) % R, k0, k1, W & 1))
         if lp["nseg"]:
-            # phase 1 (transform, MAC) of slice (n + 1) mod 128 here; its phase 2 (inverse, the
-            # far-field store) one step later: the result only depends on phase 1's inputs
-            st, W = n1 % FT, n1 // FT + 1
+            st, W = n % FT, n // FT + 1
             k0, k1 = st * K // FT, (st + 1) * K // FT
             if k1 > k0:
-                self.far((w + W * FT - n) % R, W, k0, k1, 1)
+                out.append(lambda: self.far2((w + W * FT - n) % R, W, k0, k1, 1, n & 1))
+            out.append(lambda: self.far1_slice(n, w))
+        return out
 
     def prime(self):
         for l in range(len(self.lp["T"])):
             self.toep(l, self.w, 0, self.K, 0)
         if self.lp["nseg"]:
-            self.far(self.w, 0, 0, self.K, self.lp["nseg"])
-        self.slices(-1, (self.w - 1) % self.R)
+            ns = self.lp["nseg"]
+            self.far1(0, 0, self.K, ns, 0)
+            self.far2(self.w, 0, 0, self.K, ns, 0)
+            self.far1_slice(-1, (self.w - 1) % self.R)
         self.n = 0
 
     def step(self, x):
         if self.n < 0:
             self.prime()
-        n = self.n
-        # block step: the rest spectrum + the far field of the block + H0 X
-        self.ring[self.w] = x
-        y = self.rest + self.H[0] * x
-        if self.lp["nseg"]:
-            y = y + self.ff[(n // FT) & 1, n % FT]
-        # slices (rows up to this block's; the newest one is needed by the rest only)
-        self.slices(n, self.w)
-        self.w = (self.w + 1) % self.R
+        n, lp, R, w = self.n, self.lp, self.R, self.w
+        y = [None]
+
+        def block_read():  # partitions 1..a0-1, the block's slabs and far field
+            r = (self.H[1: lp["a0"]] * self.ring[(w - np.arange(1, lp["a0"])) % R]).sum(0)
+            for l, T in enumerate(lp["T"]):
+                r = r + self.slab[l][(n // T) & 1, n % T]
+            if lp["nseg"]:
+                r = r + self.ff[(n // FT) & 1, n % FT]
+            y[0] = r + self.H[0] * x
+
+        def block_write():
+            self.ring[w] = x
+
+        jobs = self.roles(n, w) + [block_read, block_write]
+        for i in self.rng.permutation(len(jobs)):
+            jobs[i]()
+        self.w = (w + 1) % R
         self.n = n + 1
-        return y
+        return y[0]
 
 
 def test_level_plan_bands():

@@ -368,3 +368,22 @@ def test_stft_frames_and_values(oracle):
         seg = xs[f * 128:f * 128 + 256]
         truth.append(np.fft.rfft(np.pad(seg, (0, 256 - len(seg))) * w64))
     assert peak_err(S[0], np.stack(truth)) < 1e-6
+
+
+@pytest.mark.parametrize("level", [0, 1, 2])
+@pytest.mark.parametrize("B,L", [(64, 3000), (512, 20000), (32, 700)])
+def test_simd_baseline_matches_oracle(oracle, level, B, L):
+    """bench.py's cpu_baseline (the reference's xsimd MAC restated, neo_baseline.c) computes the
+    same dense_convolve as the oracle: bit-exact on the scalar path, within float rounding on
+    the SIMD ones (vector tails: B + 1 bins). Levels above the host's
+    ISA fall back to the best available."""
+    C = 3
+    ir = np.stack([oracle.noise(20 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    sig = np.stack([oracle.noise(40 + c, B * 9 + B // 3) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts, threads=2)
+    got = oracle.dense_convolve_simd(sig, parts, threads=2, level=level)
+    if level == 0:
+        assert np.array_equal(got, ref)
+    else:
+        assert peak_err(got, ref) < 1e-6

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Diagnostic builds of libneo_hip.so with only some roles of the slices kernel (k_lvl_slices)
-# enabled (NEO_ROLES bit mask: 1 rest, 2 Toeplitz 8/16, 4 Toeplitz 32, 8 far), for timing the
+# Diagnostic builds of libneo_hip.so with only some roles of the step kernel (k_lvl_step)
+# enabled (NEO_ROLES bit mask: 1 block, 2 Toeplitz T <= 16, 4 Toeplitz 32, 8 far phase 1, 16 far phase 2), for timing the
 # roles apart on the GPU (results of a partial build are wrong): tools/ab/<mask>/libneo_hip.so
 set -e
 cd "$(dirname "$0")/../neo-dsp_amd"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC FETCH_SIZE / WRITE_SIZE of k_lvl_slices for role-masked builds (separate passes)
+# PMC FETCH_SIZE / WRITE_SIZE of k_lvl_step for role-masked builds (separate passes)
 set -o pipefail
 R0=$(pwd); O=$R0/gpurun_out
 cd /tmp && export TMPDIR=/tmp
@@ -10,8 +10,7 @@ for R in "$@"; do
     f=$(find $O/pmcr_${R}_$C -name "*counter_collection.csv" | head -1)
     python3 -c "
 import csv
-v=[float(r['Counter_Value']) for r in csv.DictReader(open('$f')) if 'k_lvl_slices' in r['Kernel_Name']]
-w=[float(r['Counter_Value']) for r in csv.DictReader(open('$f')) if 'k_upols_lvl' in r['Kernel_Name']]
-print('$R $C slices %.1f MB (n=%d)  block %.1f MB' % (sum(v)/len(v)*1024/1e6, len(v), sum(w)/max(1,len(w))*1024/1e6))"
+v=[float(r['Counter_Value']) for r in csv.DictReader(open('$f')) if 'k_lvl_step' in r['Kernel_Name']]
+print('$R $C step %.1f MB (n=%d)' % (sum(v)/len(v)*1024/1e6, len(v)))"
   done
 done
