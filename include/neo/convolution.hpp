@@ -205,6 +205,62 @@ private:
     detail::upols_ptr _h;
 };
 
+namespace detail {
+struct upols_multi_deleter {
+    void operator()(neo_hip_upols_multi* m) const noexcept { neo_hip_upols_multi_destroy(m); }
+};
+}  // namespace detail
+
+/// upols_multichannel over several devices of one node (neo_hip_upols_multi_*): channel
+/// shard i = [C i / n, C (i + 1) / n) on devices[i] (a device may repeat), no collective
+/// (channels are independent, DenseConvolution.hpp:35,50-67); every call runs the shards
+/// concurrently. Results equal one upols_multichannel over all channels bit for bit.
+struct upols_multidevice {
+    upols_multidevice(std::size_t channels, std::size_t block_size, std::size_t partitions,
+                      std::vector<int> const& devices, method m = method::upols)
+        : _C{channels}, _B{block_size}, _P{partitions}
+    {
+        int const mi = m == method::upols ? 0 : m == method::upola ? 1 : -1;
+        if (mi < 0) throw std::invalid_argument{"neo_hip: multidevice convolver supports method::upols and method::upola"};
+        neo_hip_upols_multi* h = nullptr;
+        neo::hip::check(neo_hip_upols_multi_create(int(channels), int(block_size), int(partitions), devices.data(),
+                                                   int(devices.size()), mi, nullptr, &h));
+        _h.reset(h);
+    }
+
+    /// filter [C][P][B+1] complex<float>, contiguous host memory; resets state
+    auto filter(std::complex<float> const* partitions) -> void
+    {
+        neo::hip::check(neo_hip_upols_multi_set_filter(_h.get(), partitions));
+    }
+    /// normalize_impulse over all channels (optional) + uniform_partition of ir [C][length]
+    auto impulse(float const* ir, std::size_t length, bool normalize = true) -> void
+    {
+        neo::hip::check(neo_hip_upols_multi_set_impulse(_h.get(), ir, std::int64_t(length), normalize ? 1 : 0));
+    }
+    /// num_samples (whole blocks) per channel, in place, io [C][num_samples] host memory
+    auto process(float* io, std::size_t num_samples) -> void
+    {
+        auto const n = std::int64_t(num_samples);
+        neo::hip::check(neo_hip_upols_multi_process_samples(_h.get(), io, n, io, n, n));
+    }
+    auto reset() -> void { neo::hip::check(neo_hip_upols_multi_reset(_h.get())); }
+    [[nodiscard]] auto shards() const -> int
+    {
+        int n = 0;
+        neo::hip::check(neo_hip_upols_multi_shards(_h.get(), &n));
+        return n;
+    }
+
+    [[nodiscard]] auto channels() const noexcept { return _C; }
+    [[nodiscard]] auto block_size() const noexcept { return _B; }
+    [[nodiscard]] auto partitions() const noexcept { return _P; }
+
+private:
+    std::size_t _C, _B, _P;
+    std::unique_ptr<neo_hip_upols_multi, detail::upols_multi_deleter> _h;
+};
+
 /// Single-channel drop-in for upols_convolver<complex<float>> (uniform_partitioned_convolver.hpp:13-65)
 /// and, with M = method::upola, upola_convolver: default-constructible; filter([P][B+1])
 /// (re)initializes everything; operator()(block[B]) in place.

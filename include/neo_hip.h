@@ -158,6 +158,33 @@ NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* pha
  * Toeplitz level l < nlevels has a window of T[l] blocks and the band [a[l], b[l]);
  * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries). */
 NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, int* T, int* a, int* b, int* nseg);
+/* -- Multichannel convolver over several devices ------------------------------
+ * C channels cut into n contiguous shards, shard i = channels [C i / n, C (i + 1) / n) on
+ * devices[i] (a device may repeat), each a neo_hip_upols handle of its own (own stream).
+ * The reference steps all channels of a plugin instance in one loop
+ * (extra/plugin/src/dsp/DenseConvolution.hpp:35,50-67); channels never interact, so there is
+ * no collective: every call below fans out to the shards concurrently (one host thread per
+ * shard) and returns when all are done. Shard results are bit for bit those of one handle
+ * over all channels. method / opts as neo_hip_upols_create_ex. */
+typedef struct neo_hip_upols_multi neo_hip_upols_multi;
+NEO_HIP_API int neo_hip_upols_multi_create(int channels, int block, int partitions, const int* devices, int ndevices,
+                                           int method, const neo_hip_upols_opts* opts, neo_hip_upols_multi** m);
+NEO_HIP_API int neo_hip_upols_multi_destroy(neo_hip_upols_multi* m);
+NEO_HIP_API int neo_hip_upols_multi_shards(neo_hip_upols_multi* m, int* nshards);
+/* shard i: its handle (for device-resident I/O with neo_hip_upols_process_device /
+ * process_blocks on that device), device, first channel and channel count */
+NEO_HIP_API int neo_hip_upols_multi_shard(neo_hip_upols_multi* m, int i, neo_hip_upols** h, int* device,
+                                          int* first_channel, int* channels);
+/* filter [C][P][B+1] complex, host memory; resets all state */
+NEO_HIP_API int neo_hip_upols_multi_set_filter(neo_hip_upols_multi* m, const void* filter);
+/* ir [C][length] float, host memory; normalize: one factor over all C channels
+ * (normalize_impulse.hpp:21-30), as a single handle would */
+NEO_HIP_API int neo_hip_upols_multi_set_impulse(neo_hip_upols_multi* m, const float* ir, int64_t length, int normalize);
+/* num_samples per channel (channel c at in + c*ld_in / out + c*ld_out, in == out allowed),
+ * host memory, synchronous; block rules as neo_hip_upols_process_samples */
+NEO_HIP_API int neo_hip_upols_multi_process_samples(neo_hip_upols_multi* m, const float* in, int64_t ld_in, float* out,
+                                                    int64_t ld_out, int64_t num_samples);
+NEO_HIP_API int neo_hip_upols_multi_reset(neo_hip_upols_multi* m);
 /* Kernel timing with HIP events recorded on the launch stream (for the roofline in
  * bench.py): enable = n > 0 brackets every n-th launch group with events (0 = off).
  * timing() returns the summed ms of the bracketed part and the count of timed groups:

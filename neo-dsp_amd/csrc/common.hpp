@@ -48,7 +48,10 @@ struct device_guard {
     {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         if (dev >= 0 && dev != prev) {
-            if (hipSetDevice(dev) != hipSuccess) rc = fail(NEO_HIP_ENODEV, "hipSetDevice(%d) failed", dev);
+            if (hipSetDevice(dev) != hipSuccess) {
+                (void)hipGetLastError();  // not sticky: a later launch check must not see it
+                rc = fail(NEO_HIP_ENODEV, "hipSetDevice(%d) failed", dev);
+            }
         }
     }
     ~device_guard()

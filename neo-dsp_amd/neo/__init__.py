@@ -7,7 +7,7 @@ is libneo_hip.so (include/neo_hip.h). Put `<repo>/neo-dsp_amd` on sys.path.
 from . import _native
 from . import convolution
 from . import fft
-from .convolution import (UpolsConvolver, convolve, dense_convolve, direct_convolve, fft_convolve, normalize_impulse,
+from .convolution import (UpolsConvolver, UpolsMultiConvolver, convolve, dense_convolve, direct_convolve, fft_convolve, normalize_impulse,
                           num_partitions, split_upola_convolver, split_upols_convolver, uniform_partition,
                           upola_convolver, upola_convolver_v2, upols_convolver)
 
@@ -17,6 +17,7 @@ __all__ = [
     "fft",
     "convolution",
     "UpolsConvolver",
+    "UpolsMultiConvolver",
     "upols_convolver",
     "split_upols_convolver",
     "upola_convolver",

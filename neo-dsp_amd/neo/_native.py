@@ -61,6 +61,14 @@ SIGNATURES = {
     "neo_hip_upols_step_times": (_i, [_vp, ctypes.POINTER(ctypes.c_double), _i64, ctypes.POINTER(_i64)]),
     "neo_hip_upols_level_plan": (_i, [_i] + [ctypes.POINTER(_i)] * 6),
     "neo_hip_upols_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "neo_hip_upols_multi_create": (_i, [_i, _i, _i, _vp, _i, _i, _vp, ctypes.POINTER(_vp)]),
+    "neo_hip_upols_multi_destroy": (_i, [_vp]),
+    "neo_hip_upols_multi_shards": (_i, [_vp, ctypes.POINTER(_i)]),
+    "neo_hip_upols_multi_shard": (_i, [_vp, _i, ctypes.POINTER(_vp)] + [ctypes.POINTER(_i)] * 3),
+    "neo_hip_upols_multi_set_filter": (_i, [_vp, _vp]),
+    "neo_hip_upols_multi_set_impulse": (_i, [_vp, _vp, _i64, _i]),
+    "neo_hip_upols_multi_process_samples": (_i, [_vp, _vp, _i64, _vp, _i64, _i64]),
+    "neo_hip_upols_multi_reset": (_i, [_vp]),
     "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
     "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),
     "neo_hip_normalize_impulse": (_i, [_vp, _i, _i64, _i, _i]),

@@ -289,6 +289,85 @@ class UpolsConvolver:
             pass
 
 
+class UpolsMultiConvolver:
+    """C channels sharded over several devices of one node (neo_hip_upols_multi_*): shard i
+    = channels [C i / n, C (i + 1) / n) on devices[i] (a device may repeat), one handle and
+    stream each, no collective (the reference steps all channels in one loop,
+    DenseConvolution.hpp:35,50-67). Host I/O; every call runs the shards concurrently and
+    returns when all are done. Results equal one UpolsConvolver over all channels bit for
+    bit."""
+
+    def __init__(self, channels: int, block_size: int, partitions: int, devices, method: str = "upols",
+                 options: dict | None = None):
+        lib = _native.load()
+        methods = {"upols": 0, "upola": 1, "upola_v2": 2}
+        if method not in methods:
+            raise ValueError(f"method must be 'upols', 'upola' or 'upola_v2', got {method!r}")
+        opts = dict(UpolsConvolver.OPTION_DEFAULTS)
+        for k, v in (options or {}).items():
+            if k not in opts:
+                raise ValueError(f"unknown convolver option {k!r}")
+            opts[k] = int(v)
+        o = _native.UpolsOpts(**opts)
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        h = ctypes.c_void_p()
+        _native.check(lib.neo_hip_upols_multi_create(int(channels), int(block_size), int(partitions), devs,
+                                                     len(devices), methods[method], ctypes.byref(o), ctypes.byref(h)))
+        self._h = h
+        self.channels, self.block_size, self.partitions = channels, block_size, partitions
+        self.devices = list(devices)
+
+    def shards(self):
+        """[(device, first_channel, channels)] per shard"""
+        lib = _native.load()
+        n = ctypes.c_int()
+        _native.check(lib.neo_hip_upols_multi_shards(self._h, ctypes.byref(n)))
+        out = []
+        for i in range(n.value):
+            d, c0, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            _native.check(lib.neo_hip_upols_multi_shard(self._h, i, None, ctypes.byref(d), ctypes.byref(c0),
+                                                        ctypes.byref(nc)))
+            out.append((d.value, c0.value, nc.value))
+        return out
+
+    def filter(self, partitions) -> None:
+        H = np.ascontiguousarray(partitions, dtype=np.complex64)
+        if H.shape != (self.channels, self.partitions, self.block_size + 1):
+            raise ValueError(f"filter shape {H.shape} != {(self.channels, self.partitions, self.block_size + 1)}")
+        _native.check(_native.load().neo_hip_upols_multi_set_filter(self._h, _ptr(H)))
+
+    def set_impulse(self, impulse_response, normalize: bool = True) -> None:
+        ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
+        if ir.shape[0] != self.channels:
+            raise ValueError("impulse channel count mismatch")
+        _native.check(_native.load().neo_hip_upols_multi_set_impulse(self._h, _ptr(ir), ir.shape[1], int(normalize)))
+
+    def process(self, samples) -> np.ndarray:
+        """[C][n] float32 host samples (n a multiple of the block except for upola_v2) ->
+        [C][n] output; the shards run concurrently."""
+        x = np.ascontiguousarray(samples, dtype=np.float32)
+        if x.ndim != 2 or x.shape[0] != self.channels:
+            raise ValueError(f"samples must be [{self.channels}][n]")
+        y = np.empty_like(x)
+        n = x.shape[1]
+        _native.check(_native.load().neo_hip_upols_multi_process_samples(self._h, _ptr(x), n, _ptr(y), n, n))
+        return y
+
+    def reset(self) -> None:
+        _native.check(_native.load().neo_hip_upols_multi_reset(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _native.load().neo_hip_upols_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class upols_convolver:
     """Single-channel drop-in for upols_convolver<complex<float>>: default-constructible,
     filter([P][B+1]) then __call__(block[B]) in place."""

@@ -185,6 +185,28 @@ static void test_dense_convolve_vs_oracle()
     REQUIRE(hd / hp <= 1e-5);
 }
 
+// upols_multidevice on the box's device listed twice equals upols_multichannel bit for bit
+static void test_multidevice_equals_multichannel()
+{
+    std::size_t const C = 5, B = 128, L = 128 * 40, N = B * 20;
+    std::vector<float> ir(C * L), sig(C * N);
+    for (std::size_t c = 0; c < C; ++c) {
+        auto a = rnoise(300 + c, L), b = rnoise(400 + c, N);
+        std::copy(a.begin(), a.end(), ir.begin() + c * L);
+        std::copy(b.begin(), b.end(), sig.begin() + c * N);
+    }
+    auto const P = neo::convolution::num_partitions(L, B);
+    neo::convolution::upols_multidevice md{C, B, P, std::vector<int>{0, 0}};
+    neo::convolution::upols_multichannel one{C, B, P};
+    REQUIRE(md.shards() == 2);
+    md.impulse(ir.data(), L);
+    one.impulse(ir.data(), L);
+    auto a = sig, b = sig;
+    md.process(a.data(), N);
+    one.process(b.data(), N);
+    REQUIRE(a == b);
+}
+
 static void test_upola_v2_pieces_vs_oracle()
 {
     // overlap_add_convolver::operator() with sub-block calls, against the restatement
@@ -348,6 +370,7 @@ int main()
     test_uniform_partition_shapes();
     test_one_shot_convolve();
     test_upola_v2_pieces_vs_oracle();
+    test_multidevice_equals_multichannel();
     test_double_precision();
     test_stft();
     std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);

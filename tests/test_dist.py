@@ -87,3 +87,69 @@ def test_shard_ranges():
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             sizes = [b - a for a, b in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _hip_worker(rank, world, port, q, C, B, L, nb):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path[:0] = [REPO, os.path.join(REPO, "neo-dsp_amd"), os.path.join(REPO, "oracle")]
+    import bench
+    import neo
+    import oracle as O
+    import torch
+    import torch.distributed as dist
+
+    try:
+        w, r, local = bench.dist_setup(None)
+        lo, hi = bench.shard(C, w, r)
+        dev = bench.device_for(local)
+        ir = np.stack([O.noise(60 + c, L) for c in range(C)])
+        irn = neo.normalize_impulse(ir, device=dev)  # one factor over all channels, then shard
+        P = neo.num_partitions(L, B)
+        conv = neo.UpolsConvolver(hi - lo, B, P, device=dev)
+        conv.set_impulse(irn[lo:hi], normalize=False)
+        conv.set_batch(False)  # streaming steps (levels from 64 partitions)
+        sig = np.stack([O.noise(70 + c, B * nb) for c in range(C)])[lo:hi]
+        t = torch.from_numpy(np.ascontiguousarray(sig)).to(f"cuda:{dev}")
+        conv.process_blocks(t)
+        torch.cuda.synchronize(dev)
+        bench.barrier(w)
+        q.put((rank, lo, hi, t.cpu().numpy()))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((rank, "error", repr(e), None))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gloo_world2_hip_shards_equal_unsharded():
+    """Two gloo ranks (both on the box's device 0 when only one is visible) each run the HIP
+    convolver on their bench.shard channel range, streaming steps through the level
+    pipeline; the assembled output equals one unsharded HIP run bit for bit."""
+    sys.path[:0] = [REPO, os.path.join(REPO, "neo-dsp_amd"), os.path.join(REPO, "oracle")]
+    C, B, L, nb = 5, 128, 128 * 300, 40
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hip_worker, args=(r, world, port, q, C, B, L, nb)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r
+    res.sort(key=lambda r: r[0])
+    sharded = np.concatenate([r[3] for r in res])
+    import neo
+    import oracle as O
+    import torch
+
+    ir = np.stack([O.noise(60 + c, L) for c in range(C)])
+    conv = neo.UpolsConvolver(C, B, neo.num_partitions(L, B))
+    conv.set_impulse(ir, normalize=True)
+    conv.set_batch(False)
+    t = torch.from_numpy(np.stack([O.noise(70 + c, B * nb) for c in range(C)])).cuda()
+    conv.process_blocks(t)
+    torch.cuda.synchronize()
+    assert np.array_equal(sharded, t.cpu().numpy())

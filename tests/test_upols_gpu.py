@@ -716,3 +716,37 @@ def test_ahead_defaults_and_errors(neo_gpu):
     with pytest.raises(RuntimeError):
         v2.set_ahead(True)
     v2.set_ahead(False)
+
+
+@pytest.mark.parametrize("devices,C,method", [([0, 0], 6, "upols"), ([0, 0, 0], 7, "upols"), ([0, 0], 5, "upola")])
+def test_multi_device_shards(neo_gpu, oracle, devices, C, method):
+    """neo_hip_upols_multi_*: C channels sharded over a device list (here the box's one
+    device, repeated: shards of 3 / 2-2-3 / 2-3 channels on their own handles and streams).
+    Bit for bit the unsharded handle on the same calls (set_impulse normalization over all
+    channels, 90 blocks in one call, a reset, 5 more), and within tolerance of the oracle."""
+    B, L, nb = 128, 128 * 70, 90
+    P = neo_gpu.num_partitions(L, B)
+    ir = np.stack([oracle.noise(500 + c, L) for c in range(C)])
+    sig = np.stack([oracle.noise(600 + c, B * nb) for c in range(C)])
+    multi = neo_gpu.UpolsMultiConvolver(C, B, P, devices, method=method)
+    assert [s[1:] for s in multi.shards()] == [(C * i // len(devices), C * (i + 1) // len(devices) - C * i // len(devices))
+                                               for i in range(len(devices))]
+    one = neo_gpu.UpolsConvolver(C, B, P, method=method)
+    multi.set_impulse(ir, normalize=True)
+    one.set_impulse(ir, normalize=True)
+    got = multi.process(sig)
+    ref = one.process(sig.copy())
+    assert np.array_equal(got, ref)
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    assert peak_err(got, oracle.dense_convolve(sig, parts, method=method)) < TOL
+    multi.reset()
+    one.reset()
+    tail = sig[:, :5 * B].copy()
+    assert np.array_equal(multi.process(tail), one.process(tail.copy()))
+
+
+def test_multi_device_errors(neo_gpu):
+    with pytest.raises(neo_gpu._native.NeoHipError):
+        neo_gpu.UpolsMultiConvolver(2, 128, 10, [0, 0, 0])  # more shards than channels
+    with pytest.raises(neo_gpu._native.NeoHipError):
+        neo_gpu.UpolsMultiConvolver(4, 128, 10, [0, 1 << 20])  # no such device
