@@ -7,6 +7,8 @@ both in KiB, and on gfx950 FETCH_SIZE counts exactly half the bytes of a wide
 Usage:
   python tools/pmc_summary.py <tag>      every pass of tools/gpu_pmc.sh <tag>, algorithmic
                                          bytes taken from the same round's bench lines
+                                         (gpurun_out/bench_<w>_<tag>.json); the summaries carry
+                                         bench.code_tag() so bench.py uses them only for this code
   python tools/pmc_summary.py <tag> <pmc-dir-workload> <kernel-substring> <alg-bytes> [label]
 """
 import csv
@@ -19,12 +21,21 @@ OUT = os.path.join(REPO, "gpurun_out")
 
 
 def mean_counter(path, kernel):
-    vals = []
+    """mean counter value over the kernel's dispatches with its most common grid (the
+    steady-state launches: priming launches of the step kernel have other grids)"""
+    rows = []
     with open(path) as f:
         for row in csv.DictReader(f):
             if kernel in row["Kernel_Name"]:
-                vals.append(float(row["Counter_Value"]))
-    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+                rows.append((row["Grid_Size"], float(row["Counter_Value"])))
+    if not rows:
+        return None, 0
+    grids = {}
+    for g, _ in rows:
+        grids[g] = grids.get(g, 0) + 1
+    g = max(grids, key=grids.get)
+    vals = [v for gg, v in rows if gg == g]
+    return sum(vals) / len(vals), len(vals)
 
 
 def summarize(tag, workload, kernel, alg, label=None):
@@ -35,7 +46,10 @@ def summarize(tag, workload, kernel, alg, label=None):
         print(f"{label}: no dispatches of {kernel!r}", file=sys.stderr)
         return None
     hbm = 2 * fetch * 1024 + write * 1024
-    res = {"workload": label, "kernel": kernel, "tag": tag, "dispatches": [nf, nw],
+    sys.path.insert(0, REPO)
+    import bench
+
+    res = {"workload": label, "kernel": kernel, "tag": tag, "code_tag": bench.code_tag(), "dispatches": [nf, nw],
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": hbm / alg,
            "method": "separate rocprofv3 --pmc passes; 2*FETCH_SIZE (gfx950 16-B stream calibration) + WRITE_SIZE"}
@@ -58,15 +72,13 @@ def main():
         return
     for w in ("c5", "c4"):
         b = bench_line(tag, w)
-        # the window pass only (T = 32), not the lookahead's sub-window passes (T = 8)
-        summarize(tag, w, f"k_batch_mac<{b['config']['block']}, 32", b["roofline"]["algorithmic_bytes_per_launch"], w)
+        r = b["roofline"]
+        summarize(tag, w, "k_lvl_step", r["algorithmic_bytes_per_launch"], w)
         summarize(tag, w, "k_upols_step", b["per_block_step"]["algorithmic_bytes_per_launch"], w + "_plain")
+        if b.get("offline"):
+            summarize(tag, w, "k_batch_mac", b["offline"]["algorithmic_bytes_per_launch"], w + "_offline")
     b = bench_line(tag, "c2")
     summarize(tag, "c2", "k_c2c_lds<4096", b["roofline"]["algorithmic_bytes_per_launch"], "c2")
-    b = bench_line(tag, "c5")
-    if b.get("offline"):
-        summarize(tag, "c5o", f"k_batch_mac<{b['config']['block']}, 32", b["offline"]["algorithmic_bytes_per_launch"],
-                  "c5_offline")
 
 
 if __name__ == "__main__":
