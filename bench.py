@@ -314,15 +314,22 @@ def run_upols(args, world, rank, local):
             feed.run(64)
             torch.cuda.synchronize()
 
-    def timed_region():
-        """args.steps single-block steps, nothing else in the timed region."""
+    gpu_ms = {}
+
+    def timed_region(tag):
+        """args.steps single-block steps, nothing else in the timed region; HIP events on the
+        launch stream around them give the GPU time per step (gpu_ms[tag])."""
         barrier(world)
         torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e0.record()
         feed.run(args.steps)
+        e1.record()
         torch.cuda.synchronize()
         barrier(world)
         t1 = time.perf_counter()
+        gpu_ms[tag] = max_over_ranks(e0.elapsed_time(e1) / args.steps, world)
         assert torch.isfinite(y).all().item()
         return max_over_ranks(t1 - t0, world)
 
@@ -341,7 +348,7 @@ def run_upols(args, world, rank, local):
     # the plain single-block step: one pass over filter + FDL per block (k_upols_step)
     conv.set_ahead(False)
     warm()
-    el_plain = timed_region()
+    el_plain = timed_region("plain")
     det_plain = instrumented()
     bytes_plain = C * (16 * P * B + 20 * B)  # filter + FDL stream (packed bins) + FDL row write + in/prev
     gbs_plain = bytes_plain / (det_plain[0] * 1e-3) / 1e9
@@ -352,7 +359,7 @@ def run_upols(args, world, rank, local):
     if levels:
         conv.set_ahead(True)
     warm()
-    elapsed = timed_region()
+    elapsed = timed_region("levels")
     parity = None
     if irh is not None:
         irn = None
@@ -380,7 +387,7 @@ def run_upols(args, world, rank, local):
 
     if levels:
         roles = algorithmic_bytes(C, B, P, plan)
-        step_ms = det[0]
+        step_ms = gpu_ms["levels"]  # one launch per step: events around the timed steps
         by = sum(roles.values())
         gbs = by / (step_ms * 1e-3) / 1e9
         name = f"k_lvl_step<{B}>"
@@ -391,8 +398,11 @@ def run_upols(args, world, rank, local):
                     "traffic": load_pmc_traffic(args.workload, "k_lvl_step")}]
         dom = kernels[0]
         roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": dom["frac"], "traffic": dom["traffic"], "kernel": name,
+                "frac": dom["frac"], "traffic": dom["traffic"],
+                "traffic_over_algorithmic": dom["traffic"] / by if dom["traffic"] else None, "kernel": name,
                 "kernel_avg_ms": step_ms, "steps_per_launch": 1, "launches_per_step": 1,
+                "timing": "HIP events on the launch stream around the timed steps (one launch per step); "
+                          "with events around every step: %.4f ms" % det[0],
                 "algorithmic_bytes_per_launch": by,
                 "kernels": kernels, "d2d_copy_gbs": copy_ceiling_gbs(dev)}
     else:

@@ -592,6 +592,35 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
         buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
 }
 
+#ifndef NEO_ROLES
+#define NEO_ROLES 31  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2
+#endif
+
+// Toeplitz level L of the step kernel (window T = 2 << L, geometry as toep_geom): runs the
+// role and returns true if workgroup bid is one of its slice's, else moves bid past them.
+template<int L>
+__device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* smem)
+{
+    if (L >= a.ntp) return false;
+    const toep_arg ta = a.tp[L];  // static index, by value: registers, not a scratch copy
+    if (bid >= ta.nwg) {
+        bid -= ta.nwg;
+        return false;
+    }
+    if constexpr (L == 0) {
+        if (NEO_ROLES & 2) toep_role<2, 4, 1, 1>(a, ta, bid, smem);
+    } else if constexpr (L == 1) {
+        if (NEO_ROLES & 2) toep_role<4, 8, 1, 1>(a, ta, bid, smem);
+    } else if constexpr (L == 2) {
+        if (NEO_ROLES & 2) toep_role<8, 16, 1, 1>(a, ta, bid, smem);
+    } else if constexpr (L == 3) {
+        if (NEO_ROLES & 2) toep_role<16, 8, 4, 1>(a, ta, bid, smem);
+    } else {
+        if (NEO_ROLES & 4) toep_role<32, 12, 16, 2>(a, ta, bid, smem);
+    }
+    return true;
+}
+
 // The step kernel (k_lvl_step): one launch per block, workgroups by role, the longest chains
 // first -- far phase 2, the block itself, the Toeplitz slices (largest window first), far
 // phase 1. No role reads what another role of the same launch writes: the block writes FDL
@@ -605,9 +634,6 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
     int bid = int(blockIdx.x);
-#ifndef NEO_ROLES
-#define NEO_ROLES 31  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2
-#endif
     if (bid < a.f2nwg) {
         if ((NEO_ROLES & 16) && threadIdx.x < 256) far2_role(a, bid, smem);
         return;
@@ -619,27 +645,10 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
     }
     bid -= a.nblk;
     if (threadIdx.x >= 256) return;
-#pragma unroll
-    for (int l = kLvToep - 1; l >= 0; --l) {  // static indices: no copy of the argument block to scratch
-        if (l < a.ntp) {
-            const toep_arg ta = a.tp[l];  // by value: registers, not a scratch copy of the array
-            if (bid < ta.nwg) {  // geometry per window: toep_geom
-                if (ta.T == 2) {
-                    if (NEO_ROLES & 2) toep_role<2, 4, 1, 1>(a, ta, bid, smem);
-                } else if (ta.T == 4) {
-                    if (NEO_ROLES & 2) toep_role<4, 8, 1, 1>(a, ta, bid, smem);
-                } else if (ta.T == 8) {
-                    if (NEO_ROLES & 2) toep_role<8, 16, 1, 1>(a, ta, bid, smem);
-                } else if (ta.T == 16) {
-                    if (NEO_ROLES & 2) toep_role<16, 8, 4, 1>(a, ta, bid, smem);
-                } else {
-                    if (NEO_ROLES & 4) toep_role<32, 12, 16, 2>(a, ta, bid, smem);
-                }
-                return;
-            }
-            bid -= ta.nwg;
-        }
-    }
+    // level l has window T = 2 << l (plan_levels), one code copy per level; largest first
+    if (toep_level<4>(a, bid, smem) || toep_level<3>(a, bid, smem) || toep_level<2>(a, bid, smem) ||
+        toep_level<1>(a, bid, smem) || toep_level<0>(a, bid, smem))
+        return;
     if (bid < a.f1nwg && (NEO_ROLES & 8)) {
         if (a.f1fpl == 4) far1_role<4>(a, bid);
         else if (a.f1fpl == 2) far1_role<2>(a, bid);
@@ -850,17 +859,16 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
         int JH, UPW;
         toep_geom(T, JH, UPW);
         const int64_t U = int64_t(C) * (B / 16) * JH, st = n % T, W = n / T + 1;
-        toep_arg& ta = a.tp[a.ntp];
+        toep_arg& ta = a.tp[l];  // slot l = level l (the kernel dispatches on it), empty slices allowed
         ta.u0 = int(st * U / T);
         ta.u1 = int((st + 1) * U / T);
-        if (ta.u1 <= ta.u0) continue;
         ta.slab = h->lv_slab[l] + (W & 1) * C * T * B;
         ta.T = T;
         ta.a = lp.a[l];
         ta.b = lp.b[l];
         ta.tw = ring_add(w, W * T - n, R);  // block t0 + n at row w; the window starts at t0 + W T
-        ta.nwg = (ta.u1 - ta.u0 + UPW - 1) / UPW;
-        ++a.ntp;
+        ta.nwg = ta.u1 > ta.u0 ? (ta.u1 - ta.u0 + UPW - 1) / UPW : 0;
+        a.ntp = l + 1;
     }
     if (lp.nseg) {
         a.ff = h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B;
