@@ -153,7 +153,7 @@ NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
  * step computes the current windows whole). */
 NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable);
 /* enabled, block position in the current far window, longest window, number of levels */
-NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* phase, int* window, int* splits);
+NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* phase, int* window, int* levels);
 /* The level plan for `partitions` (no device needed): the block step takes [0, a0);
  * Toeplitz level l < nlevels has a window of T[l] blocks and the band [a[l], b[l]);
  * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries). */
