@@ -17,8 +17,9 @@ constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read 
 // each: 168 MiB 17.8 us/step, 216 MiB 18.3, 126 MiB 18.1)
 constexpr double kBatchCacheBudgetBytes = 168.0 * 1024 * 1024;
 // streaming levels (upols_levels.hip)
-constexpr int kLvA0 = 4;     // partitions of the block step and its rest spectrum
-constexpr int kLvToep = 5;   // Toeplitz levels
+constexpr int kLvA0 = 8;     // partitions the block itself MACs (p < kLvA0)
+constexpr int kLvToep = 4;   // Toeplitz levels (level l: window kLvT0 << l)
+constexpr int kLvT0 = 4;
 constexpr int kFarT = 128;   // far level: blocks per window (256-point partition-axis transform)
 constexpr int kFarA = 256;   // far level: first partition (2 kFarT)
 constexpr int kFarRing = 2 * kFarA;  // far level: FDL ring rows needed (a slice reads back 383 blocks)

@@ -1,31 +1,27 @@
 // upols_levels.hip — the streaming UPOLS step (one block per call) with the same work in
-// every step: time-distributed partition levels.
+// every step: time-distributed partition levels, all in ONE launch per block.
 //
 // Per bin k the convolver output is a convolution along the block axis
 //   Y[t][k] = sum_{p < P} H[p][k] X[t - p][k]       (uniform_partitioned_convolver.hpp:47-65;
 //                                                   fdl_index.hpp:23-36: partition p meets FDL row t - p)
-// The partitions are cut into bands by level:
-//   p = 0                         the block step itself (its own FDL row)
-//   p in [1, 4)                   the next block's "rest" spectrum, one step ahead
-//   Toeplitz  [4, 8) [8, 16) [16, 32) [32, 64) [64, 256): windows of 2, 4, 8, 16, 32 blocks
+// The partitions are cut into bands (plan_levels):
+//   p in [0, 8)                   the block itself (its own FDL row and 7 older ones)
+//   Toeplitz  [8, 16) [16, 32) [32, 64) [64, 256): windows of T = 4, 8, 16, 32 blocks
 //   far       p in [256, P)       T = 128, by a 256-point transform along the partition axis
-// A level with window T covers band [2T, b): for the blocks t_W + j (j < T) of a window its
-// rows t_W + j - p are at most t_W - T - 1, so the whole window's contribution can be computed
-// during the PREVIOUS window, 1/T of it per step (a slice of the columns of every channel),
-// into a slab per block of the window (double-buffered); the slices run one step ahead, so a
-// window's slabs are complete one step before its first block. After every block step one
-// more launch (k_lvl_slices) runs the slices and sums, for the NEXT block, its partitions
-// 1..15 (their rows exist already) and its level slabs into one "rest" spectrum; the block
-// step itself is then the window r2c, rest + H0 X and the c2r. Every step does the same work
-// and no step waits for a window pass (round 1 ran a pass over the filter at the start of
-// every 32-block window and a 0.63 ms far pass every 128 blocks).
+// A level with window T covers a band starting at 2T: for the blocks t_W + j (j < T) of a
+// window its rows t_W + j - p are at most t_W - T - 1, so the whole window's contribution can
+// be computed during the PREVIOUS window, 1/T of it per step (a slice of the columns of every
+// channel), into a slab per block of the window (double-buffered). The step kernel
+// (k_lvl_step) runs the block and those slices side by side; no role reads what another role
+// of the same launch writes (see k_lvl_step). Round 1 instead ran a pass over the filter at
+// the start of every 32-block window and a 0.63 ms far pass every 128 blocks.
 //
-// Levels 1-3 are direct Toeplitz MACs (k_lvl_toep); the far level is, per bin, a sum over
-// segments q >= 2 of 128 partitions of DFT256(S_q) . DFT256(h_q) with S_q the 256 FDL rows
-// t_W - (q+1) 128 ... t_W - (q-1) 128 - 1 (outputs 128..255 of the circular convolution are
-// the window's 128 blocks, no wrap reaches them). S_{q+1} of window W+1 is S_q of window W, so
-// each window transforms ONE new row pair per bin (segment 2) and keeps the spectra in a ring
-// of NSEG slots (XF); the rest is a stream of XF . HF products (far_role).
+// The far level is, per bin, a sum over segments q >= 2 of 128 partitions of
+// DFT256(S_q) . DFT256(h_q) with S_q the 256 FDL rows t_W - (q+1) 128 ... t_W - (q-1) 128 - 1
+// (outputs 128..255 of the circular convolution are the window's 128 blocks, no wrap reaches
+// them). S_{q+1} of window W+1 is S_q of window W, so each window transforms ONE new row
+// pair per bin (segment 2) and keeps the spectra in a ring of NSEG slots (XF); the rest is a
+// stream of XF . HF products (far1_role / far2_role).
 #include "upols_device.hpp"
 #include "upols_handle.hpp"
 
@@ -40,8 +36,7 @@ void plan_levels(int P, level_plan& lp)
 {
     lp = level_plan{};
     lp.a0 = std::min(P, kLvA0);
-    static constexpr int T[kLvToep] = {2, 4, 8, 16, 32}, A[kLvToep] = {4, 8, 16, 32, 64},
-                         Bd[kLvToep] = {8, 16, 32, 64, kFarA};
+    static constexpr int T[kLvToep] = {4, 8, 16, 32}, A[kLvToep] = {8, 16, 32, 64}, Bd[kLvToep] = {16, 32, 64, kFarA};
     for (int l = 0; l < kLvToep; ++l) {
         if (P <= A[l]) break;
         lp.T[lp.n] = T[l];
@@ -300,6 +295,23 @@ __device__ __forceinline__ void buf_st(cf v, __amdgpu_buffer_rsrc_t r, int voff,
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, 0);
 }
 
+// v + v of the lane D = 16 / 32 apart (v_permlane16_swap / v_permlane32_swap, gfx950): the
+// swap of v with itself leaves v and its partner in the two halves of the pair, whose sum is
+// the same float sum in every lane as v + __shfl_xor(v, D)
+template<int D>
+__device__ __forceinline__ float xor_sum(float v)
+{
+    const unsigned u = __float_as_uint(v);
+    if constexpr (D == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    } else {
+        static_assert(D == 32, "lane distance 16 or 32");
+        const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+}
+
 // Toeplitz level: for the units [u0, u1) (unit u = (channel, 16 columns, block half jh)),
 //   slab[c][j][k] = sum_{p = a}^{b-1} H[c][p][k] X[c][(tw + j - p) mod R][k],  j in half jh.
 // Lanes: 16 columns x NPG partition groups of NPL partitions; a lane loads its NPL filter
@@ -385,13 +397,13 @@ __device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& 
             }
         }
     }
-    if constexpr (NPG >= 4) {  // the 4 groups of a wave (lanes 16 apart)
+    if constexpr (NPG >= 4) {  // the 4 groups of a wave (lanes 16 apart): VALU lane swaps, no LDS
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-            acc[j].x += __shfl_xor(acc[j].x, 16);
-            acc[j].y += __shfl_xor(acc[j].y, 16);
-            acc[j].x += __shfl_xor(acc[j].x, 32);
-            acc[j].y += __shfl_xor(acc[j].y, 32);
+            acc[j].x = xor_sum<16>(acc[j].x);
+            acc[j].y = xor_sum<16>(acc[j].y);
+            acc[j].x = xor_sum<32>(acc[j].x);
+            acc[j].y = xor_sum<32>(acc[j].y);
         }
     }
     // every lane of a wave now holds its wave's sum; the lanes of group 0 carry it on (a
@@ -596,7 +608,7 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
 #define NEO_ROLES 31  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2
 #endif
 
-// Toeplitz level L of the step kernel (window T = 2 << L, geometry as toep_geom): runs the
+// Toeplitz level L of the step kernel (window T = kLvT0 << L, geometry as toep_geom): runs the
 // role and returns true if workgroup bid is one of its slice's, else moves bid past them.
 template<int L>
 __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* smem)
@@ -607,13 +619,12 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
         bid -= ta.nwg;
         return false;
     }
+    static_assert(kLvT0 == 4 && kLvToep == 4, "level slots: windows 4, 8, 16, 32");
     if constexpr (L == 0) {
-        if (NEO_ROLES & 2) toep_role<2, 4, 1, 1>(a, ta, bid, smem);
-    } else if constexpr (L == 1) {
         if (NEO_ROLES & 2) toep_role<4, 8, 1, 1>(a, ta, bid, smem);
-    } else if constexpr (L == 2) {
+    } else if constexpr (L == 1) {
         if (NEO_ROLES & 2) toep_role<8, 16, 1, 1>(a, ta, bid, smem);
-    } else if constexpr (L == 3) {
+    } else if constexpr (L == 2) {
         if (NEO_ROLES & 2) toep_role<16, 8, 4, 1>(a, ta, bid, smem);
     } else {
         if (NEO_ROLES & 4) toep_role<32, 12, 16, 2>(a, ta, bid, smem);
@@ -645,9 +656,9 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
     }
     bid -= a.nblk;
     if (threadIdx.x >= 256) return;
-    // level l has window T = 2 << l (plan_levels), one code copy per level; largest first
-    if (toep_level<4>(a, bid, smem) || toep_level<3>(a, bid, smem) || toep_level<2>(a, bid, smem) ||
-        toep_level<1>(a, bid, smem) || toep_level<0>(a, bid, smem))
+    // level l has window T = kLvT0 << l (plan_levels), one code copy per level; largest first
+    if (toep_level<3>(a, bid, smem) || toep_level<2>(a, bid, smem) || toep_level<1>(a, bid, smem) ||
+        toep_level<0>(a, bid, smem))
         return;
     if (bid < a.f1nwg && (NEO_ROLES & 8)) {
         if (a.f1fpl == 4) far1_role<4>(a, bid);
