@@ -145,7 +145,12 @@ struct slice_args {
     cf* f2ff;   // the target far window [C][128][B]
 };
 
-constexpr int kSliceLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange, twiddles
+// the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
+// they meet, 16 columns each, column-major with padded strides
+constexpr int kT32Band = 192, kT32Rows = kT32Band + 31, kT32HS = kT32Band + 2, kT32XS = kT32Rows + 2;
+constexpr int kFarLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));      // far roles: transposes, bin-0 exchange, twiddles
+constexpr int kT32Lds = 16 * (kT32HS + kT32XS) * int(sizeof(cf));         // 53760 B: three workgroups per CU
+constexpr int kSliceLds = kFarLds > kT32Lds ? kFarLds : kT32Lds;
 
 // Block role (lanes 0 .. B/2 - 1 of the workgroup, the others idle): lane i gathers, for the
 // mirror pair of bins (i, B - i), everything but partition 0 -- partitions 1 .. a0 - 1 (FDL
@@ -429,6 +434,117 @@ __device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& 
     }
 }
 
+// Toeplitz level T = 32 through LDS: one workgroup per 16-column unit and the whole window,
+//   slab[c][j][k] = sum_{p = a}^{b-1} H[c][p][k] X[c][(tw + j - p) mod R][k],  j < 32.
+// The band's filter rows and the FDL rows they meet (b - a and b - a + 31 rows of 16 columns:
+// the unit's distinct data, loaded once, coalesced) go to LDS column-major; lane (col, q)
+// then owns outputs 2q and 2q + 1 of its column and walks the band from the oldest row with
+// one filter value and one new FDL value per partition (the other FDL value slides over from
+// the previous partition): every product is its own, no cross-lane reduction.
+__device__ __forceinline__ void cmac_pk(f2v& acc, cf h, cf x)
+{
+    const f2v xv = {x.x, x.y};
+    acc = __builtin_elementwise_fma(f2v{h.x, h.x}, xv, acc);
+    acc = __builtin_elementwise_fma(f2v{-h.y, h.y}, xv.yx, acc);
+}
+
+// partitions m = m1 - 1 down to m0 (p = a + m): output j0 + o (o < 4) meets FDL value
+// i = j0 + o + nb - 1 - m, so each partition brings one new FDL value (the other three slide
+// over); 8 partitions per chunk with all their LDS reads issued first
+template<bool BIN0>
+__device__ __forceinline__ void t32_walk(const cf* hc, const cf* xc, int nb, int j0, int m0, int m1, bool z0,
+                                         f2v (&acc)[4])
+{
+    constexpr int K = 8;
+    const int ib = j0 + nb - 1;  // i of output j0 at m = 0
+    cf xw[4];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) xw[o + 1] = xc[ib - (m1 - 1) + o];  // the window's first three, shifted in below
+    int m = m1 - 1;
+    auto one = [&](cf h, cf xn) {
+#pragma unroll
+        for (int o = 0; o < 3; ++o) xw[o] = xw[o + 1];
+        xw[3] = xn;
+        if constexpr (BIN0) {
+            const pk_coef hk(h, z0);
+#pragma unroll
+            for (int o = 0; o < 4; ++o) hk.mac(acc[o], xw[o]);
+        } else {
+#pragma unroll
+            for (int o = 0; o < 4; ++o) cmac_pk(acc[o], h, xw[o]);
+        }
+    };
+    for (; m - (K - 1) >= m0; m -= K) {
+        cf h[K], x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            h[i] = hc[m - i];
+            x[i] = xc[ib - (m - i) + 3];
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) one(h[i], x[i]);
+    }
+    for (; m >= m0; --m) one(hc[m], xc[ib - m + 3]);
+}
+
+__device__ __forceinline__ void toep32_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
+{
+    constexpr int T = 32, NH = (kT32Band + 15) / 16, NXL = (kT32Rows + 15) / 16;
+    cf* hs = reinterpret_cast<cf*>(smem);  // hs[col][m] = H[p = a + m]
+    cf* xs = hs + 16 * kT32HS;             // xs[col][i] = X[row tw - (b - 1) + i]
+    const int t = threadIdx.x, col = t & 15, q = t >> 4;
+    const int u = ta.u0 + bid, gpc = sa.B / 16;
+    const int c = __builtin_amdgcn_readfirstlane(u / gpc), g = __builtin_amdgcn_readfirstlane(u - (u / gpc) * gpc);
+    const int k = g * 16 + col, nb = ta.b - ta.a, nx = nb + T - 1;
+    const int ps8 = int(sa.pstride * int(sizeof(cf))), R = sa.ring;
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(c) * sa.cstride, int64_t(ta.b) * ps8);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(R) * ps8);
+    int rb = ta.tw - (ta.b - 1);  // the oldest row (b - 1 < 256 < R: one wrap at most)
+    rb = rb < 0 ? rb + R : rb;
+    cf hv[NH], xv[NXL];  // every load of the lane in flight, then the LDS writes
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        const int m = q + 16 * i;
+        if (m < nb) hv[i] = buf_ld(hres, (ta.a + m) * ps8 + k * int(sizeof(cf)), 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NXL; ++i) {
+        const int r = q + 16 * i;
+        if (r < nx) {
+            const int rr = rb + r >= R ? rb + r - R : rb + r;
+            xv[i] = buf_ld(xres, rr * ps8 + k * int(sizeof(cf)), 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NH; ++i)
+        if (q + 16 * i < nb) hs[col * kT32HS + q + 16 * i] = hv[i];
+#pragma unroll
+    for (int i = 0; i < NXL; ++i)
+        if (q + 16 * i < nx) xs[col * kT32XS + q + 16 * i] = xv[i];
+    __syncthreads();
+    // lane (col, q8, half): outputs 4 q8 .. 4 q8 + 3, partitions of its half of the band
+    const int q8 = q & 7, half = q >> 3, j0 = 4 * q8, nh = (nb + 1) / 2;
+    const int m0 = half ? nh : 0, m1 = half ? nb : nh;
+    f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
+    if (g == 0) t32_walk<true>(hs + col * kT32HS, xs + col * kT32XS, nb, j0, m0, m1, col == 0, acc);  // uniform
+    else t32_walk<false>(hs + col * kT32HS, xs + col * kT32XS, nb, j0, m0, m1, false, acc);
+    __syncthreads();  // the filter tile is free: the halves meet there
+    f2v* red = reinterpret_cast<f2v*>(smem);  // [128][4]
+    if (half) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) red[(t - 128) * 4 + o] = acc[o];
+    }
+    __syncthreads();
+    if (!half) {
+        cf* o = ta.slab + (int64_t(c) * T + j0) * sa.B + k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f2v v = acc[i] + red[t * 4 + i];
+            o[int64_t(i) * sa.B] = cf{v.x, v.y};
+        }
+    }
+}
+
 // Far level, for 16-column units (unit = channel c, columns 16 g ...): the far field of window
 // wn (first block at ring row tw), ff[c][j][k], j < 128:
 //   FF[j] = IDFT256( sum_s XF_s . HF_s )[128 + j] / 256,   s = 0 .. nseg - 1 (segment q = s + 2)
@@ -627,7 +743,7 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
     } else if constexpr (L == 2) {
         if (NEO_ROLES & 2) toep_role<16, 8, 4, 1>(a, ta, bid, smem);
     } else {
-        if (NEO_ROLES & 4) toep_role<32, 12, 16, 2>(a, ta, bid, smem);
+        if (NEO_ROLES & 4) toep32_role(a, ta, bid, smem);
     }
     return true;
 }
@@ -783,9 +899,9 @@ static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) 
 // Toeplitz role geometry per window T (toep_role<T, NPL, NPG, JH> in k_lvl_step)
 static void toep_geom(int T, int& JH, int& UPW)
 {
-    JH = T == 32 ? 2 : 1;
-    const int NPG = T <= 8 ? 1 : (T == 16 ? 4 : 16);
-    UPW = 256 / (16 * NPG);
+    JH = 1;
+    const int NPG = T <= 8 ? 1 : (T == 16 ? 4 : 16);  // T = 32: one unit per workgroup (toep32_role)
+    UPW = T == 32 ? 1 : 256 / (16 * NPG);
 }
 
 static slice_args base_args(const upols_t* h)

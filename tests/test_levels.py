@@ -113,8 +113,7 @@ class Sim:
         lp, K, R = self.lp, self.K, self.R
         out = []
         for l, T in enumerate(lp["T"]):
-            JH = 2 if T == 32 else 1
-            U = (K // 16) * JH if K >= 16 else K
+            U = K // 16 if K >= 16 else K  # 16-column units (toep_geom: one window part each)
             st, W = n % T, n // T + 1
             u0, u1 = st * U // T, (st + 1) * U // T
             if u1 > u0:
