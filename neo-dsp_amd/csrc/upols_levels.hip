@@ -147,7 +147,7 @@ struct slice_args {
 
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
 // they meet, 16 columns each, column-major with padded strides
-constexpr int kT32Band = 192, kT32Rows = kT32Band + 31, kT32HS = kT32Band + 2, kT32XS = kT32Rows + 2;
+constexpr int kT32Band = 192, kT32Rows = kT32Band + 31, kT32HS = kT32Band + 2, kT32XS = kT32Rows + 3;  // even strides
 constexpr int kFarLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));      // far roles: transposes, bin-0 exchange, twiddles
 constexpr int kT32Lds = 16 * (kT32HS + kT32XS) * int(sizeof(cf));         // 53760 B: three workgroups per CU
 constexpr int kSliceLds = kFarLds > kT32Lds ? kFarLds : kT32Lds;
@@ -448,43 +448,50 @@ __device__ __forceinline__ void cmac_pk(f2v& acc, cf h, cf x)
     acc = __builtin_elementwise_fma(f2v{-h.y, h.y}, xv.yx, acc);
 }
 
-// partitions m = m1 - 1 down to m0 (p = a + m): output j0 + o (o < 4) meets FDL value
-// i = j0 + o + nb - 1 - m, so each partition brings one new FDL value (the other three slide
-// over); 8 partitions per chunk with all their LDS reads issued first
 template<bool BIN0>
-__device__ __forceinline__ void t32_walk(const cf* hc, const cf* xc, int nb, int j0, int m0, int m1, bool z0,
-                                         f2v (&acc)[4])
+__device__ __forceinline__ void t32_step(f2v (&acc)[4], cf (&xw)[4], cf h, cf xn, bool z0)
 {
-    constexpr int K = 8;
-    const int ib = j0 + nb - 1;  // i of output j0 at m = 0
+    xw[3] = xw[2];
+    xw[2] = xw[1];
+    xw[1] = xw[0];
+    xw[0] = xn;
+    if constexpr (BIN0) {
+        const pk_coef hk(h, z0);
+#pragma unroll
+        for (int o = 0; o < 4; ++o) hk.mac(acc[o], xw[o]);
+    } else {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) cmac_pk(acc[o], h, xw[o]);
+    }
+}
+
+// partitions m = m0 .. m1 - 1 (p = a + m, m0 even): output j0 + o (o < 4) meets FDL value
+// i = ib - m + o (ib = j0 + nb - 1), so each partition brings one new value, xc[ib - m], and
+// the other three slide over. Partition pairs (m, m + 1) come as one 16-B LDS read of the
+// filter column and one of the FDL column (xc is offset so that xc + ib - m - 1 is 16-B
+// aligned), four pairs per chunk with all their reads issued first.
+template<bool BIN0>
+__device__ __forceinline__ void t32_walk(const cf* hc, const cf* xc, int ib, int m0, int m1, bool z0, f2v (&acc)[4])
+{
+    constexpr int KP = 4;
     cf xw[4];
 #pragma unroll
-    for (int o = 0; o < 3; ++o) xw[o + 1] = xc[ib - (m1 - 1) + o];  // the window's first three, shifted in below
-    int m = m1 - 1;
-    auto one = [&](cf h, cf xn) {
+    for (int o = 0; o < 3; ++o) xw[o] = xc[ib - m0 + 1 + o];
+    int m = m0;
+    for (; m + 2 * KP <= m1; m += 2 * KP) {
+        float4 h2[KP], x2[KP];
 #pragma unroll
-        for (int o = 0; o < 3; ++o) xw[o] = xw[o + 1];
-        xw[3] = xn;
-        if constexpr (BIN0) {
-            const pk_coef hk(h, z0);
-#pragma unroll
-            for (int o = 0; o < 4; ++o) hk.mac(acc[o], xw[o]);
-        } else {
-#pragma unroll
-            for (int o = 0; o < 4; ++o) cmac_pk(acc[o], h, xw[o]);
-        }
-    };
-    for (; m - (K - 1) >= m0; m -= K) {
-        cf h[K], x[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            h[i] = hc[m - i];
-            x[i] = xc[ib - (m - i) + 3];
+        for (int i = 0; i < KP; ++i) {
+            h2[i] = *reinterpret_cast<const float4*>(hc + m + 2 * i);
+            x2[i] = *reinterpret_cast<const float4*>(xc + ib - (m + 2 * i) - 1);
         }
 #pragma unroll
-        for (int i = 0; i < K; ++i) one(h[i], x[i]);
+        for (int i = 0; i < KP; ++i) {
+            t32_step<BIN0>(acc, xw, cf{h2[i].x, h2[i].y}, cf{x2[i].z, x2[i].w}, z0);
+            t32_step<BIN0>(acc, xw, cf{h2[i].z, h2[i].w}, cf{x2[i].x, x2[i].y}, z0);
+        }
     }
-    for (; m >= m0; --m) one(hc[m], xc[ib - m + 3]);
+    for (; m < m1; ++m) t32_step<BIN0>(acc, xw, hc[m], xc[ib - m], z0);
 }
 
 __device__ __forceinline__ void toep32_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
@@ -518,16 +525,19 @@ __device__ __forceinline__ void toep32_role(const slice_args& sa, const toep_arg
 #pragma unroll
     for (int i = 0; i < NH; ++i)
         if (q + 16 * i < nb) hs[col * kT32HS + q + 16 * i] = hv[i];
+    const int odd = nb & 1;  // FDL column shift: keeps the pair reads 16-B aligned (t32_walk)
 #pragma unroll
     for (int i = 0; i < NXL; ++i)
-        if (q + 16 * i < nx) xs[col * kT32XS + q + 16 * i] = xv[i];
+        if (q + 16 * i < nx) xs[col * kT32XS + odd + q + 16 * i] = xv[i];
     __syncthreads();
     // lane (col, q8, half): outputs 4 q8 .. 4 q8 + 3, partitions of its half of the band
-    const int q8 = q & 7, half = q >> 3, j0 = 4 * q8, nh = (nb + 1) / 2;
-    const int m0 = half ? nh : 0, m1 = half ? nb : nh;
+    const int q8 = q & 7, half = q >> 3, j0 = 4 * q8, nh = ((nb + 1) / 2 + 1) & ~1;
+    const int m0 = half ? nh : 0, m1 = half ? nb : (nh < nb ? nh : nb);
     f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
-    if (g == 0) t32_walk<true>(hs + col * kT32HS, xs + col * kT32XS, nb, j0, m0, m1, col == 0, acc);  // uniform
-    else t32_walk<false>(hs + col * kT32HS, xs + col * kT32XS, nb, j0, m0, m1, false, acc);
+    const cf* hc = hs + col * kT32HS;
+    const cf* xc = xs + col * kT32XS + odd;
+    if (g == 0) t32_walk<true>(hc, xc, j0 + nb - 1, m0, m1, col == 0, acc);  // uniform branch
+    else t32_walk<false>(hc, xc, j0 + nb - 1, m0, m1, false, acc);
     __syncthreads();  // the filter tile is free: the halves meet there
     f2v* red = reinterpret_cast<f2v*>(smem);  // [128][4]
     if (half) {
