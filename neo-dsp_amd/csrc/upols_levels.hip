@@ -147,9 +147,9 @@ struct slice_args {
 
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
 // they meet, 16 columns each, column-major with padded strides
-constexpr int kT32Band = 192, kT32Rows = kT32Band + 31, kT32HS = kT32Band + 2, kT32XS = kT32Rows + 3;  // even strides
-constexpr int kFarLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));      // far roles: transposes, bin-0 exchange, twiddles
-constexpr int kT32Lds = 16 * (kT32HS + kT32XS) * int(sizeof(cf));         // 53760 B: three workgroups per CU
+constexpr int kT32Band = 192;                                       // [64, 256)
+constexpr int kFarLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange, twiddles
+constexpr int kT32Lds = 16 * ((kT32Band + 2) + (kT32Band + 34)) * int(sizeof(cf));  // toep_tile<32, 192>: 53760 B, 3 workgroups per CU
 constexpr int kSliceLds = kFarLds > kT32Lds ? kFarLds : kT32Lds;
 
 // Block role (lanes 0 .. B/2 - 1 of the workgroup, the others idle): lane i gathers, for the
@@ -434,13 +434,9 @@ __device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& 
     }
 }
 
-// Toeplitz level T = 32 through LDS: one workgroup per 16-column unit and the whole window,
-//   slab[c][j][k] = sum_{p = a}^{b-1} H[c][p][k] X[c][(tw + j - p) mod R][k],  j < 32.
-// The band's filter rows and the FDL rows they meet (b - a and b - a + 31 rows of 16 columns:
-// the unit's distinct data, loaded once, coalesced) go to LDS column-major; lane (col, q)
-// then owns outputs 2q and 2q + 1 of its column and walks the band from the oldest row with
-// one filter value and one new FDL value per partition (the other FDL value slides over from
-// the previous partition): every product is its own, no cross-lane reduction.
+// Toeplitz levels: slab[c][j][k] = sum_{p = a}^{b-1} H[c][p][k] X[c][(tw + j - p) mod R][k],
+// j < T, for the next window (toep_lds_role below). Complex MAC in two packed FMAs, the
+// splat / swap / sign folded into operand modifiers: acc += (hr, hr)(xr, xi) + (-hi, hi)(xi, xr).
 __device__ __forceinline__ void cmac_pk(f2v& acc, cf h, cf x)
 {
     const f2v xv = {x.x, x.y};
@@ -494,62 +490,95 @@ __device__ __forceinline__ void t32_walk(const cf* hc, const cf* xc, int ib, int
     for (; m < m1; ++m) t32_step<BIN0>(acc, xw, hc[m], xc[ib - m], z0);
 }
 
-__device__ __forceinline__ void toep32_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
+// Toeplitz level with window T through LDS, for every level (band [a, b), b - a <= NB):
+// 32 / T units of 16 columns per workgroup, each with the whole window. A unit's filter rows
+// and the FDL rows they meet (b - a and b - a + T - 1 rows of 16 columns: its distinct data,
+// loaded once, coalesced) go to an LDS tile, column-major; lane (col, q4, half) then owns
+// outputs 4 q4 .. 4 q4 + 3 of its column over half of the band (t32_walk), and the halves
+// meet through LDS.
+template<int T, int NB>
+struct toep_tile {
+    static constexpr int UPW = 32 / T, LPU = 256 / UPW, NQ = LPU / 16, QUADS = T / 4;  // two halves of QUADS
+    static constexpr int HS = NB + 2, XS = NB + T + 2;  // even column strides (16-B aligned pair reads)
+    static constexpr int NH = (NB + NQ - 1) / NQ, NXL = (NB + T - 1 + NQ - 1) / NQ;
+    static constexpr int LDS = UPW * 16 * (HS + XS) * int(sizeof(cf));
+    static_assert(NQ == 2 * QUADS, "two halves of the band per unit");
+};
+
+template<int T, int NB>
+__device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
 {
-    constexpr int T = 32, NH = (kT32Band + 15) / 16, NXL = (kT32Rows + 15) / 16;
-    cf* hs = reinterpret_cast<cf*>(smem);  // hs[col][m] = H[p = a + m]
-    cf* xs = hs + 16 * kT32HS;             // xs[col][i] = X[row tw - (b - 1) + i]
-    const int t = threadIdx.x, col = t & 15, q = t >> 4;
-    const int u = ta.u0 + bid, gpc = sa.B / 16;
-    const int c = __builtin_amdgcn_readfirstlane(u / gpc), g = __builtin_amdgcn_readfirstlane(u - (u / gpc) * gpc);
-    const int k = g * 16 + col, nb = ta.b - ta.a, nx = nb + T - 1;
-    const int ps8 = int(sa.pstride * int(sizeof(cf))), R = sa.ring;
-    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(c) * sa.cstride, int64_t(ta.b) * ps8);
-    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(R) * ps8);
+    using G = toep_tile<T, NB>;
+    const int t = threadIdx.x, us = t / G::LPU, lt = t % G::LPU, col = lt & 15, q = lt >> 4;
+    cf* hs = reinterpret_cast<cf*>(smem) + us * 16 * (G::HS + G::XS);  // hs[col][m] = H[p = a + m]
+    cf* xs = hs + 16 * G::HS;                                          // xs[col][i] = X[row tw - (b - 1) + i]
+    const int u = ta.u0 + bid * G::UPW + us, gpc = sa.B / 16;
+    const bool live = u < ta.u1;
+    const int uc = live ? u : ta.u1 - 1, c = uc / gpc, g = uc - c * gpc;
+    const int k = g * 16 + col, nb = ta.b - ta.a, nx = nb + T - 1, R = sa.ring;
     int rb = ta.tw - (ta.b - 1);  // the oldest row (b - 1 < 256 < R: one wrap at most)
     rb = rb < 0 ? rb + R : rb;
-    cf hv[NH], xv[NXL];  // every load of the lane in flight, then the LDS writes
+    cf hv[G::NH], xv[G::NXL];  // every load of the lane in flight, then the LDS writes
+    if constexpr (G::UPW == 1) {  // channel uniform: buffer loads, row offsets in SGPRs
+        const int cu = __builtin_amdgcn_readfirstlane(c), ps8 = int(sa.pstride * int(sizeof(cf)));
+        const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(cu) * sa.cstride, int64_t(ta.b) * ps8);
+        const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(cu) * sa.cstride, int64_t(R) * ps8);
 #pragma unroll
-    for (int i = 0; i < NH; ++i) {
-        const int m = q + 16 * i;
-        if (m < nb) hv[i] = buf_ld(hres, (ta.a + m) * ps8 + k * int(sizeof(cf)), 0);
-    }
+        for (int i = 0; i < G::NH; ++i) {
+            const int m = q + G::NQ * i;
+            if (m < nb) hv[i] = buf_ld(hres, (ta.a + m) * ps8 + k * int(sizeof(cf)), 0);
+        }
 #pragma unroll
-    for (int i = 0; i < NXL; ++i) {
-        const int r = q + 16 * i;
-        if (r < nx) {
-            const int rr = rb + r >= R ? rb + r - R : rb + r;
-            xv[i] = buf_ld(xres, rr * ps8 + k * int(sizeof(cf)), 0);
+        for (int i = 0; i < G::NXL; ++i) {
+            const int r = q + G::NQ * i;
+            if (r < nx) xv[i] = buf_ld(xres, (rb + r >= R ? rb + r - R : rb + r) * ps8 + k * int(sizeof(cf)), 0);
+        }
+    } else {
+        const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
+        const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
+#pragma unroll
+        for (int i = 0; i < G::NH; ++i) {
+            const int m = q + G::NQ * i;
+            if (live && m < nb) hv[i] = ld_nt(Hc + int64_t(ta.a + m) * sa.pstride);
+        }
+#pragma unroll
+        for (int i = 0; i < G::NXL; ++i) {
+            const int r = q + G::NQ * i;
+            if (live && r < nx) xv[i] = ld_nt(Xc + int64_t(rb + r >= R ? rb + r - R : rb + r) * sa.pstride);
         }
     }
-#pragma unroll
-    for (int i = 0; i < NH; ++i)
-        if (q + 16 * i < nb) hs[col * kT32HS + q + 16 * i] = hv[i];
     const int odd = nb & 1;  // FDL column shift: keeps the pair reads 16-B aligned (t32_walk)
+    if (live) {
 #pragma unroll
-    for (int i = 0; i < NXL; ++i)
-        if (q + 16 * i < nx) xs[col * kT32XS + odd + q + 16 * i] = xv[i];
-    __syncthreads();
-    // lane (col, q8, half): outputs 4 q8 .. 4 q8 + 3, partitions of its half of the band
-    const int q8 = q & 7, half = q >> 3, j0 = 4 * q8, nh = ((nb + 1) / 2 + 1) & ~1;
-    const int m0 = half ? nh : 0, m1 = half ? nb : (nh < nb ? nh : nb);
-    f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
-    const cf* hc = hs + col * kT32HS;
-    const cf* xc = xs + col * kT32XS + odd;
-    if (g == 0) t32_walk<true>(hc, xc, j0 + nb - 1, m0, m1, col == 0, acc);  // uniform branch
-    else t32_walk<false>(hc, xc, j0 + nb - 1, m0, m1, false, acc);
-    __syncthreads();  // the filter tile is free: the halves meet there
-    f2v* red = reinterpret_cast<f2v*>(smem);  // [128][4]
-    if (half) {
+        for (int i = 0; i < G::NH; ++i)
+            if (q + G::NQ * i < nb) hs[col * G::HS + q + G::NQ * i] = hv[i];
 #pragma unroll
-        for (int o = 0; o < 4; ++o) red[(t - 128) * 4 + o] = acc[o];
+        for (int i = 0; i < G::NXL; ++i)
+            if (q + G::NQ * i < nx) xs[col * G::XS + odd + q + G::NQ * i] = xv[i];
     }
     __syncthreads();
-    if (!half) {
+    const int half = q >= G::QUADS, j0 = 4 * (q - half * G::QUADS), nh = ((nb + 1) / 2 + 1) & ~1;
+    const int m0 = half ? nh : 0, m1 = half ? nb : (nh < nb ? nh : nb);
+    f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
+    const cf* hc = hs + col * G::HS;
+    const cf* xc = xs + col * G::XS + odd;
+    if (live) {
+        if (g == 0) t32_walk<true>(hc, xc, j0 + nb - 1, m0, m1, col == 0, acc);  // uniform per unit
+        else t32_walk<false>(hc, xc, j0 + nb - 1, m0, m1, false, acc);
+    }
+    __syncthreads();  // the tiles are free: the halves meet there
+    f2v* red = reinterpret_cast<f2v*>(smem);  // [units][LPU / 2][4]
+    const int hl = lt - half * (G::LPU / 2);
+    if (half) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) red[(us * (G::LPU / 2) + hl) * 4 + o] = acc[o];
+    }
+    __syncthreads();
+    if (!half && live) {
         cf* o = ta.slab + (int64_t(c) * T + j0) * sa.B + k;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const f2v v = acc[i] + red[t * 4 + i];
+            const f2v v = acc[i] + red[(us * (G::LPU / 2) + hl) * 4 + i];
             o[int64_t(i) * sa.B] = cf{v.x, v.y};
         }
     }
@@ -745,15 +774,15 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
         bid -= ta.nwg;
         return false;
     }
-    static_assert(kLvT0 == 4 && kLvToep == 4, "level slots: windows 4, 8, 16, 32");
-    if constexpr (L == 0) {
+    static_assert(kLvT0 == 4 && kLvToep == 4, "level slots: windows 4, 8, 16, 32 (bands 2T, 2T, 2T, 6T)");
+    if constexpr (L == 0) {  // T = 4, 8: a lane takes its column's whole band in registers
         if (NEO_ROLES & 2) toep_role<4, 8, 1, 1>(a, ta, bid, smem);
     } else if constexpr (L == 1) {
         if (NEO_ROLES & 2) toep_role<8, 16, 1, 1>(a, ta, bid, smem);
     } else if constexpr (L == 2) {
-        if (NEO_ROLES & 2) toep_role<16, 8, 4, 1>(a, ta, bid, smem);
+        if (NEO_ROLES & 2) toep_lds_role<16, 32>(a, ta, bid, smem);
     } else {
-        if (NEO_ROLES & 4) toep32_role(a, ta, bid, smem);
+        if (NEO_ROLES & 4) toep_lds_role<32, kT32Band>(a, ta, bid, smem);
     }
     return true;
 }
@@ -910,8 +939,7 @@ static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) 
 static void toep_geom(int T, int& JH, int& UPW)
 {
     JH = 1;
-    const int NPG = T <= 8 ? 1 : (T == 16 ? 4 : 16);  // T = 32: one unit per workgroup (toep32_role)
-    UPW = T == 32 ? 1 : 256 / (16 * NPG);
+    UPW = T <= 8 ? 16 : 32 / T;  // toep_role<T, 2T, 1, 1>: 16 units per workgroup; toep_tile: 32 / T
 }
 
 static slice_args base_args(const upols_t* h)
