@@ -419,6 +419,7 @@ def run_upols(args, world, rank, local):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
+        "gpu_ms_per_step": gpu_ms.get("levels" if levels else "plain"),  # HIP events around the same steps
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
