@@ -103,6 +103,8 @@ typedef struct neo_hip_upols_opts {
     int batch_blocks;     /* batched passes: 0 auto (32), else blocks per pass (power of two, 2..32) */
     int batch_bins;       /* batched passes: 0 auto (1), else bins per lane vector (1 or 2) */
     int levels;           /* single-block steps: -1 auto (streaming levels from 64 partitions), 0 plain step, 1 levels */
+    int far_level;        /* streaming levels, partitions >= 256: -1 auto (= 1), 0 a 128-block Toeplitz level (more
+                             VALU / LDS work, fewer bytes), 1 the 128-block partition-axis transform level */
 } neo_hip_upols_opts;
 NEO_HIP_API int neo_hip_upols_create_ex(int channels, int block, int partitions, int device, int method,
                                         const neo_hip_upols_opts* opts, neo_hip_upols** h);
@@ -142,9 +144,10 @@ NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in,
                                               int64_t ld_out, int64_t num_samples, int is_device, void* stream);
 NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h);
 /* Streaming levels for single-block steps (upols / upola; upols_levels.hip): the
- * partitions are cut into bands -- p in [0, 4) MAC'd by the block itself; Toeplitz windows
- * of 2 / 4 / 8 / 16 / 32 blocks for [4, 8) / [8, 16) / [16, 32) / [32, 64) / [64, 256); a
- * 128-block partition-axis transform for [256, P) -- and every band's contribution to the
+ * partitions are cut into bands -- p in [0, 8) MAC'd by the block itself; Toeplitz windows
+ * of 4 / 8 / 16 / 32 blocks for [8, 16) / [16, 32) / [32, 64) / [64, 256); for [256, P) a
+ * 128-block partition-axis transform (or, by neo_hip_upols_opts.far_level, a Toeplitz window
+ * of 128 blocks) -- and every band's contribution to the
  * blocks of its next window is computed during the current window, a slice of the columns
  * per block step, so every call does the same work (ONE launch per block, k_lvl_step: the
  * block and the slices side by side). Output is the same block by
@@ -156,7 +159,8 @@ NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable);
 NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* phase, int* window, int* levels);
 /* The level plan for `partitions` (no device needed): the block step takes [0, a0);
  * Toeplitz level l < nlevels has a window of T[l] blocks and the band [a[l], b[l]);
- * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries). */
+ * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries); the automatic
+ * choice of far_level. */
 NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, int* T, int* a, int* b, int* nseg);
 /* -- Multichannel convolver over several devices ------------------------------
  * C channels cut into n contiguous shards, shard i = channels [C i / n, C (i + 1) / n) on

@@ -521,8 +521,9 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
                      const neo_hip_upols_opts* opt, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
-    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1};
-    if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.split_workgroups < 0 ||
+    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1};
+    if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.far_level < -1 || o.far_level > 1 ||
+        o.split_workgroups < 0 ||
         (o.batch_blocks && (o.batch_blocks < 2 || o.batch_blocks > kMaxBatch || (o.batch_blocks & (o.batch_blocks - 1)))) ||
         o.batch_bins < 0 || o.batch_bins > 2)
         return fail(NEO_HIP_EINVAL, "invalid convolver options");
@@ -538,7 +539,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->B = block;
     h->P = partitions;
     h->ring = partitions + kMaxBatch - 1;
-    plan_levels(partitions, h->lv);
+    plan_levels(partitions, h->lv, o.far_level);
     if (h->lv.nseg) h->ring = std::max(h->ring, kFarRing);  // far slices read 383 blocks back
     h->ola = ola || v2;
     h->v2 = v2;

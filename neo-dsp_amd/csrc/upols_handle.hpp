@@ -18,8 +18,10 @@ constexpr double kCacheBudgetBytes = 216.0 * 1024 * 1024;  // filter bytes read 
 constexpr double kBatchCacheBudgetBytes = 168.0 * 1024 * 1024;
 // streaming levels (upols_levels.hip)
 constexpr int kLvA0 = 8;     // partitions the block itself MACs (p < kLvA0)
-constexpr int kLvToep = 4;   // Toeplitz levels (level l: window kLvT0 << l)
+constexpr int kLvToep = 5;   // Toeplitz level slots: l < 4 window kLvT0 << l; slot 4 the big level
 constexpr int kLvT0 = 4;
+constexpr int kBigT = 128;   // big Toeplitz level: window, band [2 kBigT, P) instead of the far level (opt-in:
+                             // 26.9 vs 19.2 us per C5 step, its 89 M complex MACs per step are VALU / LDS bound)
 constexpr int kFarT = 128;   // far level: blocks per window (256-point partition-axis transform)
 constexpr int kFarA = 256;   // far level: first partition (2 kFarT)
 constexpr int kFarRing = 2 * kFarA;  // far level: FDL ring rows needed (a slice reads back 383 blocks)
@@ -161,7 +163,8 @@ inline int timing_mark(upols_t::ev_group* g, int i, hipStream_t s)
 // upols_levels.hip: one streaming block step (level slabs + the newest partitions) and 1/T
 // of every level's next window; the level plan; buffers; filter-change hook
 int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
-void plan_levels(int P, level_plan& lp);
+// far: -1 auto (= 1), 0 the big Toeplitz level, 1 the far level
+void plan_levels(int P, level_plan& lp, int far = -1);
 void lvl_free(upols_t* h);
 void lvl_filter_changed(upols_t* h);
 // upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device

@@ -32,19 +32,27 @@ namespace neo_hip {
 
 // ---------------------------------------------------------------------------------------
 // level plan (host; also exported for the CPU schedule test, neo_hip_upols_level_plan)
-void plan_levels(int P, level_plan& lp)
+void plan_levels(int P, level_plan& lp, int far)
 {
     lp = level_plan{};
     lp.a0 = std::min(P, kLvA0);
-    static constexpr int T[kLvToep] = {4, 8, 16, 32}, A[kLvToep] = {8, 16, 32, 64}, Bd[kLvToep] = {16, 32, 64, kFarA};
-    for (int l = 0; l < kLvToep; ++l) {
+    static constexpr int T[4] = {4, 8, 16, 32}, A[4] = {8, 16, 32, 64}, Bd[4] = {16, 32, 64, kFarA};
+    for (int l = 0; l < 4; ++l) {
         if (P <= A[l]) break;
         lp.T[lp.n] = T[l];
         lp.a[lp.n] = A[l];
         lp.b[lp.n] = std::min(P, Bd[l]);
         ++lp.n;
     }
-    lp.nseg = P > kFarA ? (P - kFarA + kFarT - 1) / kFarT : 0;
+    if (P <= kFarA) return;
+    if (far != 0) {
+        lp.nseg = (P - kFarA + kFarT - 1) / kFarT;
+    } else {  // [256, P) by the big Toeplitz level (slot 4)
+        lp.T[lp.n] = kBigT;
+        lp.a[lp.n] = 2 * kBigT;
+        lp.b[lp.n] = P;
+        ++lp.n;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -584,6 +592,85 @@ __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_a
     }
 }
 
+// The big Toeplitz level (window kBigT = 128, band [256, P), instead of the far level when
+// neo_hip_upols_opts.far_level = 0): per 16-column unit, kBigJH parts of kBigJP = 16 outputs, one
+// workgroup each (the parts of a column group on one XCD: they share filter rows and most
+// FDL rows through its L2). The band goes through an LDS tile in chunks of kBigNC
+// partitions; lane (col, quad, quarter) owns 4 outputs of the part over a quarter of each
+// chunk (t32_walk), and the quarters meet through LDS at the end.
+constexpr int kBigJH = 8, kBigJP = kBigT / kBigJH, kBigNC = 192;
+constexpr int kBigHS = kBigNC + 2, kBigXS = kBigNC + kBigJP + 2;  // even column strides
+static_assert(16 * (kBigHS + kBigXS) * int(sizeof(cf)) <= kSliceLds, "big level tile");
+
+__device__ __forceinline__ void toep_big_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
+{
+    constexpr int NH = kBigNC / 16, NXL = (kBigNC + kBigJP - 1 + 15) / 16;
+    cf* hs = reinterpret_cast<cf*>(smem);  // hs[col][m] = H[p = a + mc + m]
+    cf* xs = hs + 16 * kBigHS;             // xs[col][i] = X[the chunk's oldest row + i]
+    const int t = threadIdx.x, col = t & 15, qq = t >> 4, quad = qq & 3, quarter = qq >> 2;
+    int wb = bid;  // within every 64 workgroups, XCD x (= blockIdx mod 8) takes the 8 parts of column groups x, x + 8, ...
+    if (bid < ta.nwg / 64 * 64) {
+        const int r = bid & 63;
+        wb = (bid & ~63) + (r & 7) * 8 + (r >> 3);
+    }
+    const int u = ta.u0 + wb, jp = u % kBigJH, cg = u / kBigJH, gpc = sa.B / 16;
+    const int c = __builtin_amdgcn_readfirstlane(cg / gpc), g = __builtin_amdgcn_readfirstlane(cg - (cg / gpc) * gpc);
+    const int k = g * 16 + col, nb = ta.b - ta.a, R = sa.ring, jpart = jp * kBigJP;
+    const int ps8 = int(sa.pstride * int(sizeof(cf)));
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(c) * sa.cstride, int64_t(ta.b) * ps8);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(R) * ps8);
+    f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
+    for (int mc = 0; mc < nb; mc += kBigNC) {  // uniform per workgroup
+        const int nc = nb - mc < kBigNC ? nb - mc : kBigNC, nx = nc + kBigJP - 1;
+        // the chunk's oldest FDL row: tw + jpart - (a + mc + nc - 1), at most P + 127 < R + 128 rows back
+        int rb = (ta.tw + jpart - (ta.a + mc + nc - 1)) % R;
+        rb = rb < 0 ? rb + R : rb;
+        cf hv[NH], xv[NXL];
+#pragma unroll
+        for (int i = 0; i < NH; ++i) {
+            const int m = qq + 16 * i;
+            if (m < nc) hv[i] = buf_ld(hres, (ta.a + mc + m) * ps8 + k * int(sizeof(cf)), 0);
+        }
+#pragma unroll
+        for (int i = 0; i < NXL; ++i) {
+            const int r = qq + 16 * i;
+            if (r < nx) xv[i] = buf_ld(xres, (rb + r >= R ? rb + r - R : rb + r) * ps8 + k * int(sizeof(cf)), 0);
+        }
+        if (mc) __syncthreads();  // the previous chunk's walk is done with the tile
+        const int odd = nc & 1;   // FDL column shift: keeps the pair reads 16-B aligned (t32_walk)
+#pragma unroll
+        for (int i = 0; i < NH; ++i)
+            if (qq + 16 * i < nc) hs[col * kBigHS + qq + 16 * i] = hv[i];
+#pragma unroll
+        for (int i = 0; i < NXL; ++i)
+            if (qq + 16 * i < nx) xs[col * kBigXS + odd + qq + 16 * i] = xv[i];
+        __syncthreads();
+        const int nq = ((nc + 3) / 4 + 1) & ~1, m0 = quarter * nq, m1 = m0 + nq < nc ? m0 + nq : nc;
+        if (m0 < m1) {
+            const cf* hc = hs + col * kBigHS;
+            const cf* xc = xs + col * kBigXS + odd;
+            if (g == 0) t32_walk<true>(hc, xc, nc - 1 + 4 * quad, m0, m1, col == 0, acc);  // uniform branch
+            else t32_walk<false>(hc, xc, nc - 1 + 4 * quad, m0, m1, false, acc);
+        }
+    }
+    __syncthreads();  // the tile is free: the quarters meet there
+    f2v* red = reinterpret_cast<f2v*>(smem);  // [3][64][4]
+    const int ql = t & 63;                    // (col, quad)
+    if (quarter) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) red[((quarter - 1) * 64 + ql) * 4 + o] = acc[o];
+    }
+    __syncthreads();
+    if (!quarter) {
+        cf* o = ta.slab + (int64_t(c) * kBigT + jpart + 4 * quad) * sa.B + k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f2v v = acc[i] + red[ql * 4 + i] + red[(64 + ql) * 4 + i] + red[(128 + ql) * 4 + i];
+            o[int64_t(i) * sa.B] = cf{v.x, v.y};
+        }
+    }
+}
+
 // Far level, for 16-column units (unit = channel c, columns 16 g ...): the far field of window
 // wn (first block at ring row tw), ff[c][j][k], j < 128:
 //   FF[j] = IDFT256( sum_s XF_s . HF_s )[128 + j] / 256,   s = 0 .. nseg - 1 (segment q = s + 2)
@@ -774,15 +861,17 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
         bid -= ta.nwg;
         return false;
     }
-    static_assert(kLvT0 == 4 && kLvToep == 4, "level slots: windows 4, 8, 16, 32 (bands 2T, 2T, 2T, 6T)");
+    static_assert(kLvT0 == 4 && kLvToep == 5, "level slots: windows 4, 8, 16, 32 (bands 2T, 2T, 2T, 6T), 128");
     if constexpr (L == 0) {  // T = 4, 8: a lane takes its column's whole band in registers
         if (NEO_ROLES & 2) toep_role<4, 8, 1, 1>(a, ta, bid, smem);
     } else if constexpr (L == 1) {
         if (NEO_ROLES & 2) toep_role<8, 16, 1, 1>(a, ta, bid, smem);
     } else if constexpr (L == 2) {
         if (NEO_ROLES & 2) toep_lds_role<16, 32>(a, ta, bid, smem);
-    } else {
+    } else if constexpr (L == 3) {
         if (NEO_ROLES & 4) toep_lds_role<32, kT32Band>(a, ta, bid, smem);
+    } else {
+        if (NEO_ROLES & 4) toep_big_role(a, ta, bid, smem);
     }
     return true;
 }
@@ -812,8 +901,8 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
     bid -= a.nblk;
     if (threadIdx.x >= 256) return;
     // level l has window T = kLvT0 << l (plan_levels), one code copy per level; largest first
-    if (toep_level<3>(a, bid, smem) || toep_level<2>(a, bid, smem) || toep_level<1>(a, bid, smem) ||
-        toep_level<0>(a, bid, smem))
+    if (toep_level<4>(a, bid, smem) || toep_level<3>(a, bid, smem) || toep_level<2>(a, bid, smem) ||
+        toep_level<1>(a, bid, smem) || toep_level<0>(a, bid, smem))
         return;
     if (bid < a.f1nwg && (NEO_ROLES & 8)) {
         if (a.f1fpl == 4) far1_role<4>(a, bid);
@@ -938,8 +1027,8 @@ static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) 
 // Toeplitz role geometry per window T (toep_role<T, NPL, NPG, JH> in k_lvl_step)
 static void toep_geom(int T, int& JH, int& UPW)
 {
-    JH = 1;
-    UPW = T <= 8 ? 16 : 32 / T;  // toep_role<T, 2T, 1, 1>: 16 units per workgroup; toep_tile: 32 / T
+    JH = T == kBigT ? kBigJH : 1;  // the big level: parts of kBigJP outputs (toep_big_role)
+    UPW = T <= 8 ? 16 : (T <= 32 ? 32 / T : 1);  // toep_role<T, 2T, 1, 1>: 16 units; toep_tile: 32 / T
 }
 
 static slice_args base_args(const upols_t* h)

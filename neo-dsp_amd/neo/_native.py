@@ -25,7 +25,7 @@ F64 = 16  # OR into the kind: complex128 / float64 plans
 class UpolsOpts(ctypes.Structure):
     """neo_hip_upols_opts (include/neo_hip.h)."""
     _fields_ = [("fused", ctypes.c_int), ("split_workgroups", ctypes.c_int), ("batch_blocks", ctypes.c_int),
-                ("batch_bins", ctypes.c_int), ("levels", ctypes.c_int)]
+                ("batch_bins", ctypes.c_int), ("levels", ctypes.c_int), ("far_level", ctypes.c_int)]
 
 
 # every symbol declared in include/neo_hip.h: (name, restype, argtypes)

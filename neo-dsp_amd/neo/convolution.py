@@ -103,13 +103,15 @@ class UpolsConvolver:
     (output block t corresponds to input block t, overlap_save.hpp:84-112).
     """
 
-    OPTION_DEFAULTS = {"fused": -1, "split_workgroups": 0, "batch_blocks": 0, "batch_bins": 0, "levels": -1}
+    OPTION_DEFAULTS = {"fused": -1, "split_workgroups": 0, "batch_blocks": 0, "batch_bins": 0, "levels": -1,
+                       "far_level": -1}
 
     def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols",
                  options: dict | None = None):
         """`options` (neo_hip_upols_create_ex): explicit code-path choices instead of the
         shape-based defaults — fused (-1 auto / 0 / 1), split_workgroups (0 auto),
-        batch_blocks (0 auto / 2..32), batch_bins (0 auto / 1 / 2), levels (-1 auto / 0 / 1).
+        batch_blocks (0 auto / 2..32), batch_bins (0 auto / 1 / 2), levels (-1 auto / 0 / 1),
+        far_level (-1 auto / 0 Toeplitz window of 128 blocks / 1 partition-axis transform, for p >= 256).
         Every choice gives the same results up to float summation order."""
         lib = _native.load()
         h = ctypes.c_void_p()

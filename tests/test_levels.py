@@ -178,7 +178,7 @@ def test_level_plan_bands():
             assert a >= 2 * T
 
 
-@pytest.mark.parametrize("P", [5, 20, 40, 100, 257, 300, 700])
+@pytest.mark.parametrize("P", [5, 20, 40, 100, 257, 300, 700, 1100])
 def test_level_schedule_matches_direct(P):
     lp = plan(P)
     rng = np.random.default_rng(P)
@@ -190,6 +190,29 @@ def test_level_schedule_matches_direct(P):
     worst = 0.0
     for t in range(nb):
         # plain steps first (history before the levels start), and again midway (re-prime)
+        y = sim.plain(X[t]) if (t < 37 or nb // 2 <= t < nb // 2 + 3) else sim.step(X[t])
+        m = min(P, t + 1)
+        ref = (H[:m] * X[t - np.arange(m)]).sum(0)
+        worst = max(worst, float(np.abs(y - ref).max() / (np.abs(ref).max() + 1e-300)))
+    assert worst < 1e-12, worst
+
+
+@pytest.mark.parametrize("P", [300, 700])
+def test_level_schedule_big_level(P):
+    """The same schedule with [256, P) as the 128-block Toeplitz level instead of the far
+    level (neo_hip_upols_opts.far_level = 0)."""
+    lp = dict(plan(P))
+    assert lp["nseg"]
+    lp["T"], lp["a"], lp["b"] = list(lp["T"]) + [128], list(lp["a"]) + [256], list(lp["b"]) + [P]
+    lp["nseg"] = 0
+    rng = np.random.default_rng(P + 1)
+    K = 16
+    H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
+    sim = Sim(H, lp)
+    nb = 3 * P + 40
+    X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
+    worst = 0.0
+    for t in range(nb):
         y = sim.plain(X[t]) if (t < 37 or nb // 2 <= t < nb // 2 + 3) else sim.step(X[t])
         m = min(P, t + 1)
         ref = (H[:m] * X[t - np.arange(m)]).sum(0)

@@ -549,7 +549,7 @@ def test_host_staging_growth_keeps_batch_buffers(neo_gpu, oracle):
 
 
 # ------------------------------------------------ streaming levels (upols_levels.hip)
-def _stream(neo_gpu, oracle, method, B, P, C, nb, seed):
+def _stream(neo_gpu, oracle, method, B, P, C, nb, seed, options=None):
     """Single-block steps with the streaming levels against the oracle's dense_convolve."""
     torch = pytest.importorskip("torch")
     L = B * (P - 1) + B // 2 + 1
@@ -558,7 +558,7 @@ def _stream(neo_gpu, oracle, method, B, P, C, nb, seed):
     assert parts.shape[1] == P
     sig = np.stack([oracle.noise(seed + 10 + c, B * nb) for c in range(C)])
     ref = oracle.dense_convolve(sig, parts, method=method)
-    conv = neo_gpu.UpolsConvolver(C, B, P, method=method)
+    conv = neo_gpu.UpolsConvolver(C, B, P, method=method, options=options)
     conv.filter(parts)
     conv.set_batch(False)
     conv.set_ahead(True)
@@ -579,25 +579,29 @@ def test_level_steps_small_filters(neo_gpu, oracle, method, B, P, C, nb):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 320) <= TOL
 
 
-@pytest.mark.parametrize("P", [3, 4, 5, 8, 9, 16, 17, 32, 33, 64, 65, 255, 256, 257, 384, 385, 513])
-def test_level_band_edges(neo_gpu, oracle, P):
-    """Every band edge of the level plan (block step and rest / 2 / 4 / 8 / 16 / 32-block
-    Toeplitz levels / far segments, a last far segment of one partition): B = 32, past the
-    ring length."""
-    assert _stream(neo_gpu, oracle, "upols", 32, P, 2, max(2 * P + 140, 300), 400 + P) <= TOL
+@pytest.mark.parametrize("P,far", [(p, -1) for p in (3, 8, 9, 16, 17, 32, 33, 64, 65, 255, 256, 257, 448, 449, 450)] +
+                         [(p, 1) for p in (257, 384, 385, 513)])
+def test_level_band_edges(neo_gpu, oracle, P, far):
+    """Every band edge of the level plan (the block's own partitions / 4 / 8 / 16 / 32-block
+    Toeplitz levels / the 128-block level and its 192-partition LDS chunks / far segments, a
+    last far segment of one partition): B = 32, past the ring length."""
+    assert _stream(neo_gpu, oracle, "upols", 32, P, 2, max(2 * P + 140, 300), 400 + P, {"far_level": far}) <= TOL
 
 
+@pytest.mark.parametrize("far", [0, 1])
 @pytest.mark.parametrize("method", ["upols", "upola"])
 @pytest.mark.parametrize("B,P,C,nb", [(256, 300, 2, 420), (32, 700, 1, 900), (64, 400, 2, 700), (16, 1000, 1, 1200),
                                       (1024, 270, 1, 300), (128, 600, 3, 800)])
-def test_far_level_steps_vs_oracle(neo_gpu, oracle, method, B, P, C, nb):
-    """The far level (partitions >= 256 by 256-point transforms along the partition axis,
-    its next window computed during the current one): several far windows, ring wraparound,
-    the packed DC / Nyquist bin, several sub-units per 16-column unit; OLS and OLA."""
-    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 520) <= TOL
+def test_far_level_steps_vs_oracle(neo_gpu, oracle, method, B, P, C, nb, far):
+    """Partitions >= 256, both forms: the 128-block Toeplitz level (far = 0) and the far
+    level (far = 1: 256-point transforms along the partition axis), each computing its next
+    window during the current one: several windows, ring wraparound, the packed DC / Nyquist
+    bin, several sub-units per 16-column unit; OLS and OLA."""
+    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 520, {"far_level": far}) <= TOL
 
 
-def test_far_field_mixed_and_refilter(neo_gpu, oracle):
+@pytest.mark.parametrize("far", [0, 1])
+def test_far_field_mixed_and_refilter(neo_gpu, oracle, far):
     """Streaming levels across batched passes, toggles at arbitrary blocks and a filter
     change: the levels re-prime at the next streaming step."""
     torch = pytest.importorskip("torch")
@@ -605,7 +609,7 @@ def test_far_field_mixed_and_refilter(neo_gpu, oracle):
     L = B * P
     irs = [np.stack([oracle.noise(540 + 7 * k + c, L) for c in range(C)]) for k in range(2)]
     parts = [oracle.uniform_partition(oracle.normalize_impulse(ir), B) for ir in irs]
-    conv = neo_gpu.UpolsConvolver(C, B, P)
+    conv = neo_gpu.UpolsConvolver(C, B, P, options={"far_level": far})
     for k in range(2):
         nb = 480
         sig = np.stack([oracle.noise(560 + 3 * k + c, B * nb) for c in range(C)])
@@ -626,11 +630,13 @@ def test_far_field_mixed_and_refilter(neo_gpu, oracle):
         assert peak_err(out, ref) <= TOL, k
 
 
-def test_levels_before_any_filter(neo_gpu):
-    """Streaming steps on a fresh handle with a far level and no filter set (H is zero):
-    silence, no fault (the far buffers are allocated and primed on the first step)."""
+@pytest.mark.parametrize("far", [0, 1])
+def test_levels_before_any_filter(neo_gpu, far):
+    """Streaming steps on a fresh handle with a far level (or the 128-block level) and no
+    filter set (H is zero): silence, no fault (the level buffers are allocated and primed on
+    the first step)."""
     torch = pytest.importorskip("torch")
-    conv = neo_gpu.UpolsConvolver(2, 128, 600)
+    conv = neo_gpu.UpolsConvolver(2, 128, 600, options={"far_level": far})
     conv.set_batch(False)
     assert conv.ahead_info()[0]
     x = torch.rand((2, 128 * 140), device="cuda")
