@@ -957,7 +957,13 @@ __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf
 // host side
 
 // phase 1 f rows per lane: one load round covers the stored segments (far1_role)
-static int far1_fpl(const upols_t* h) { return h->lv.nseg - 1 <= 4 ? 4 : (h->lv.nseg - 1 <= 8 ? 2 : 1); }
+static int far1_fpl(const upols_t* h)
+{
+#ifdef NEO_FAR_FPL  // diagnostic builds
+    return NEO_FAR_FPL;
+#endif
+    return h->lv.nseg - 1 <= 4 ? 4 : (h->lv.nseg - 1 <= 8 ? 2 : 1);
+}
 
 static size_t far_units_per_slice(const upols_t* h) { return (size_t(h->C) * (h->B / 16) + kFarT - 1) / kFarT; }
 
