@@ -281,6 +281,20 @@ def oracle_parity(x, y, feed, irh, B, chans, K=4, threads=16):
     return worst
 
 
+def spin_wait(local: int) -> None:
+    """hipDeviceScheduleSpin on this process's device: a real-time caller waits for each
+    block by spinning (HIP's auto mode yields on a host with more cores than contexts, which
+    adds tens of microseconds of wake-up to every wait). torch's HIP runtime is already
+    loaded, so the soname resolves to it."""
+    import ctypes
+
+    if os.environ.get("NEO_BENCH_SPIN", "1") != "1":
+        return
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipSetDevice(ctypes.c_int(local))
+    hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+
+
 def run_upols(args, world, rank, local):
     import numpy as np
     import torch
@@ -288,6 +302,7 @@ def run_upols(args, world, rank, local):
 
     C, B, L = WORKLOADS[args.workload]
     local = device_for(local)
+    spin_wait(local)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     P = neo.num_partitions(L, B)
@@ -303,7 +318,10 @@ def run_upols(args, world, rank, local):
     nx = P + 192  # cyclic input: covers the parity check's history window (P + 5 blocks)
     x = torch.rand((C, nx * B), generator=g, device=dev).mul_(2).sub_(1)
     y = torch.empty_like(x)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # a stream of its own (not the null stream): the steps and the events around them
+    sobj = torch.cuda.Stream(dev) if os.environ.get("NEO_BENCH_NULL_STREAM") != "1" else torch.cuda.current_stream(dev)
+    stream = sobj.cuda_stream
+    torch.cuda.synchronize(dev)  # x, y and the filter were made on the default stream
     feed = Feed(conv, x, y, nx, B, stream)
 
     def warm():
@@ -317,20 +335,27 @@ def run_upols(args, world, rank, local):
     gpu_ms = {}
 
     def timed_region(tag):
-        """args.steps single-block steps, nothing else in the timed region; HIP events on the
-        launch stream around them give the GPU time per step (gpu_ms[tag])."""
+        """args.steps single-block steps, nothing else in the timed region (wall clock); then
+        the same number of steps again with HIP events on the launch stream around them: the
+        GPU time per step (gpu_ms[tag]) and the host's enqueue time."""
         barrier(world)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        e0.record()
         feed.run(args.steps)
-        e1.record()
         torch.cuda.synchronize()
         barrier(world)
         t1 = time.perf_counter()
-        gpu_ms[tag] = max_over_ranks(e0.elapsed_time(e1) / args.steps, world)
         assert torch.isfinite(y).all().item()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        e0.record(sobj)
+        feed.run(args.steps)
+        e1.record(sobj)
+        t3 = time.perf_counter()
+        torch.cuda.synchronize()
+        gpu_ms[tag] = max_over_ranks(e0.elapsed_time(e1) / args.steps, world)
+        gpu_ms[tag + "_host_launch_ms"] = (t3 - t2) * 1e3
         return max_over_ranks(t1 - t0, world)
 
     def instrumented():
@@ -420,6 +445,7 @@ def run_upols(args, world, rank, local):
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "gpu_ms_per_step": gpu_ms.get("levels" if levels else "plain"),  # HIP events around the same steps
+        "host_launch_ms": gpu_ms.get(("levels" if levels else "plain") + "_host_launch_ms"),  # t0 -> all steps enqueued
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
