@@ -241,14 +241,15 @@ def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans):
 
 def test_full_size_c5_shard_steady_state(neo_gpu, oracle):
     """The headline path at its own shape (configs[4] per-GPU shard: 256 ch, B = 512,
-    L = 480000, P = 938, ring 969): 1152 blocks (9 far windows), channels 0, 127, 255."""
+    L = 480000, P = 938, 6 far segments, ring 969): 1152 blocks (9 far windows), channels 0,
+    127, 255."""
     _full_size_streaming(neo_gpu, oracle, 256, 512, 480000, 1152, 77, (0, 127, 255))
 
 
 def test_full_size_c4_steady_state(neo_gpu, oracle):
     """configs[3] (256 ch, B = 256, L = 480000, P = 1875, 13 far segments): 2176 blocks
-    (17 far windows, the ring of 1906 rows wraps), channels 0 and 255."""
-    _full_size_streaming(neo_gpu, oracle, 256, 256, 480000, 2176, 78, (0, 255))
+    (17 far windows, the ring of 1906 rows wraps), channels 0, 127 and 255."""
+    _full_size_streaming(neo_gpu, oracle, 256, 256, 480000, 2176, 78, (0, 127, 255))
 
 
 def test_multirow_splits_with_wraparound(neo_gpu, oracle):
