@@ -144,7 +144,7 @@ struct slice_args {
     cf* xf;
     const cf* twf;
     // far phase 1: stored-segment MAC (16 workgroups per unit)
-    int f1nwg, f1u0, f1wn, f1fpl;  // f rows per lane: 16 / f1fpl workgroups per unit
+    int f1nwg, f1u0, f1nu, f1wn, f1fpl;  // slice units [f1u0, f1u0 + f1nu); f rows per lane
     cf* f1acc;  // [units][256 f][16]
     // far phase 2 (the slice phase 1 did one step earlier): the fresh row pairs' transforms
     // (stored to their ring slots) and products, the sum, the inverse transform
@@ -730,26 +730,29 @@ __device__ __forceinline__ void bin0_exchange(cf (&v)[16], cf* z, int a, int cp)
     }
 }
 
-// phase 1, FPL f rows per lane (16 / FPL workgroups per unit; the host picks FPL so that one
-// round of NS = 16 / FPL segments covers the stored ones: every load of a lane in flight at once)
+// phase 1, FPL f rows per lane: a workgroup takes kF1UG units side by side (64 columns:
+// every wave-load reads 512 contiguous bytes of one f row) and 4 FPL f rows of them, so
+// kFN / (4 FPL) workgroups per unit group; the host picks FPL so that one round of NS =
+// 16 / FPL segments covers the stored ones (every load of a lane in flight at once)
+constexpr int kF1UG = 4;
+
 template<int FPL>
 __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
 {
-    constexpr int PPU = 16 / FPL, NS = 16 / FPL;  // workgroups per unit, segments per round
-    const int t = threadIdx.x;
-    const int ul = bid / PPU, part = bid - ul * PPU;
-    const int gpc = sa.B / 16, u = sa.f1u0 + ul, c = u / gpc, g = u - c * gpc;
+    constexpr int FR = 4 * FPL, PPG = kFN / FR, NS = 16 / FPL;  // f rows per workgroup, workgroups per group, segments per round
+    const int t = threadIdx.x, cl = t & 63, fq = t >> 6;
+    const int grp = bid / PPG, part = bid - grp * PPG;
+    const int ul = grp * kF1UG + (cl >> 4);  // the lane's unit within the slice
+    if (ul >= sa.f1nu) return;              // a partial last group (no barriers in this role)
+    const int gpc = sa.B / 16, u = sa.f1u0 + ul, c = u / gpc, g = u - c * gpc, col = cl & 15, k = g * 16 + col;
     const int M = sa.M, nseg = sa.nseg;
     auto slot = [&](int s) { return ((sa.f1wn - s - 1) % M + M) % M; };
-    const int64_t fs = sa.B;  // stride between f rows of a spectrum (complex)
-    const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));  // bytes per spectrum (a channel's span < 2 GiB)
-    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;       // first stored segment
-    // buffer loads: 32-bit lane offsets, segment / slot / f-row offsets in SGPRs; lane (f, col)
-    // holds f = 16 FPL part + (t >> 4) + 16 j, j < FPL
-    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
-    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
-    const int col = t & 15, f0 = part * 16 * FPL + (t >> 4), k = g * 16 + col;
-    const int vo = int((int64_t(f0) * fs + k) * int(sizeof(cf))), fo = int(16 * fs * int(sizeof(cf)));
+    const int64_t fs = sa.B;
+    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;  // first stored segment
+    const int f0 = part * FR + fq;                          // f = f0 + 4 j
+    const cf* hc = sa.hf + int64_t(c) * nseg * kFN * fs + int64_t(f0) * fs + k;
+    const cf* xc = sa.xf + int64_t(c) * M * kFN * fs + int64_t(f0) * fs + k;
+    const int64_t sp = int64_t(kFN) * fs;  // one spectrum
     f2v acc[FPL];
 #pragma unroll
     for (int j = 0; j < FPL; ++j) acc[j] = f2v(0.f);
@@ -758,10 +761,12 @@ __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             if (sb + i < nseg) {
+                const cf* hs = hc + (sb + i) * sp;
+                const cf* xs = xc + slot(sb + i) * sp;
 #pragma unroll
                 for (int j = 0; j < FPL; ++j) {
-                    hv[i][j] = buf_ld(hres, vo, (sb + i) * spec + j * fo);
-                    xv[i][j] = buf_ld(xres, vo, slot(sb + i) * spec + j * fo);
+                    hv[i][j] = ld_nt(hs + 4 * j * fs);
+                    xv[i][j] = ld_nt(xs + 4 * j * fs);
                 }
             }
         }
@@ -770,14 +775,14 @@ __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
             if (sb + i < nseg) {
 #pragma unroll
                 for (int j = 0; j < FPL; ++j) {
-                    const bool z0 = g == 0 && col == 0 && ((f0 + 16 * j) & (kFN / 2 - 1)) == 0;  // packed bin 0, f = 0, 128
+                    const bool z0 = g == 0 && col == 0 && ((f0 + 4 * j) & (kFN / 2 - 1)) == 0;  // packed bin 0, f = 0, 128
                     pk_coef(hv[i][j], z0).mac(acc[j], xv[i][j]);
                 }
             }
         }
     }
 #pragma unroll
-    for (int j = 0; j < FPL; ++j) sa.f1acc[(int64_t(ul) * kFN + f0 + 16 * j) * 16 + col] = cf{acc[j].x, acc[j].y};
+    for (int j = 0; j < FPL; ++j) sa.f1acc[(int64_t(ul) * kFN + f0 + 4 * j) * 16 + col] = cf{acc[j].x, acc[j].y};
 }
 
 __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
@@ -1085,7 +1090,8 @@ static void far1_args(const upols_t* h, int64_t n, slice_args& a)
     const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
     a.f1u0 = u0;
     a.f1fpl = far1_fpl(h);
-    a.f1nwg = (u1 - u0) * (16 / a.f1fpl);
+    a.f1nu = u1 - u0;
+    a.f1nwg = (u1 - u0 + kF1UG - 1) / kF1UG * (kFN / (4 * a.f1fpl));
     a.f1wn = int(W);
     a.f1acc = h->fv_acc + (n1 & 1) * far_units_per_slice(h) * kFN * 16;
 }
@@ -1192,7 +1198,8 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         if (u1 <= u0) continue;
         f.f1u0 = u0;
         f.f1fpl = far1_fpl(h);
-        f.f1nwg = (u1 - u0) * (16 / f.f1fpl);  // zero partial sums (no stored segments)
+        f.f1nu = u1 - u0;
+        f.f1nwg = (u1 - u0 + kF1UG - 1) / kF1UG * (kFN / (4 * f.f1fpl));  // zero partial sums (no stored segments)
         f.f2nwg = 0;
         if (int rc = launch_step_kernel(h, f, s)) return rc;
         f.f1nwg = 0;
