@@ -207,10 +207,27 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
     const int k0 = tid, k1 = tid == 0 ? B / 2 : B - tid;
     const bool pair = tid < A::Q;
     cf h0a = {0.f, 0.f}, h0b = h0a, ra = h0a, rb = h0a;
-    if (pair) {
+    // wave 0 issues its window loads first: its transform waits for them only, not for the
+    // bin-pair loads it issues next (loads return in order)
+    tw_regs<K::TW1 + K::TW2, 64> twr;
+    cf v[EW];
+    if (tid < 64) {
+        twr.load(a.twg, tid);
+        if (tid < TW) {
+            const cf* pz = reinterpret_cast<const cf*>(prev_c);
+            const cf* iz = reinterpret_cast<const cf*>(in_c);
+#pragma unroll
+            for (int m = 0; m < EW; ++m) {
+                const int n = tid + m * TW;
+                if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
+                else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+            }
+        }
+    }
+    cf ha[kLvA0 - 1], hb[kLvA0 - 1], xa[kLvA0 - 1], xb[kLvA0 - 1], sla[kLvToep + 1], slb[kLvToep + 1];
+    if (pair) {  // loads only; the sums follow the transform
         h0a = a.H[crow + k0];
         h0b = a.H[crow + k1];
-        cf ha[kLvA0 - 1], hb[kLvA0 - 1], xa[kLvA0 - 1], xb[kLvA0 - 1];
 #pragma unroll
         for (int p = 1; p < kLvA0; ++p) {
             if (p < a.a0) {
@@ -225,36 +242,18 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
         for (int l = 0; l < kLvToep; ++l) {
             if (l < a.nsl) {
                 const cf* sr = a.sl[l] + int64_t(c) * a.scs[l];
-                ra = cadd(ra, sr[k0]);
-                rb = cadd(rb, sr[k1]);
+                sla[l] = sr[k0];
+                slb[l] = sr[k1];
             }
         }
         if (a.ff) {
-            ra = cadd(ra, a.ff[int64_t(c) * a.fcs + k0]);
-            rb = cadd(rb, a.ff[int64_t(c) * a.fcs + k1]);
-        }
-#pragma unroll
-        for (int p = 1; p < kLvA0; ++p) {
-            if (p < a.a0) {
-                cmac(ra, ha[p - 1], xa[p - 1], k0 == 0);
-                cmac(rb, hb[p - 1], xb[p - 1], false);
-            }
+            sla[kLvToep] = a.ff[int64_t(c) * a.fcs + k0];
+            slb[kLvToep] = a.ff[int64_t(c) * a.fcs + k1];
         }
     }
-    if (tid < 64) {  // wave 0: window r2c, previous block
-        tw_regs<K::TW1 + K::TW2, 64> twr;
-        twr.load(a.twg, tid);
-        cf v[EW];
-        if (tid < TW) {
-            const cf* pz = reinterpret_cast<const cf*>(prev_c);
-            const cf* iz = reinterpret_cast<const cf*>(in_c);
-#pragma unroll
-            for (int m = 0; m < EW; ++m) {
-                const int n = tid + m * TW;
-                if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
-                else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
-            }
-            if constexpr (!OLA) {
+    if (tid < 64) {  // wave 0: previous block, window r2c
+        if constexpr (!OLA) {
+            if (tid < TW) {
                 // the window's second half becomes the next call's first half, stored from
                 // registers; the lane read prev_c[n] in an earlier load of the same wave
                 cf* pw = reinterpret_cast<cf*>(prev_c);
@@ -268,6 +267,26 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
         if (tid < TW) {
 #pragma unroll
             for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
+        }
+    }
+    if (pair) {
+#pragma unroll
+        for (int l = 0; l < kLvToep; ++l) {
+            if (l < a.nsl) {
+                ra = cadd(ra, sla[l]);
+                rb = cadd(rb, slb[l]);
+            }
+        }
+        if (a.ff) {
+            ra = cadd(ra, sla[kLvToep]);
+            rb = cadd(rb, slb[kLvToep]);
+        }
+#pragma unroll
+        for (int p = 1; p < kLvA0; ++p) {
+            if (p < a.a0) {
+                cmac(ra, ha[p - 1], xa[p - 1], k0 == 0);
+                cmac(rb, hb[p - 1], xb[p - 1], false);
+            }
         }
     }
     __syncthreads();
