@@ -113,7 +113,8 @@ struct toep_arg {
     cf* slab;           // the target window's slabs [C][T][B]
     int T, a, b;        // window, band [a, b)
     int tw;             // ring row of the window's first block
-    int u0, u1, nwg;    // units (16 columns x one of JH block halves) of this slice, workgroups
+    int u0, u1, nwg;    // units (16 columns x one of JH window parts) of this slice, workgroups
+    int jh;             // window parts per column group (toep_geom)
 };
 
 struct slice_args {
@@ -523,27 +524,31 @@ __device__ __forceinline__ void t32_walk(const cf* hc, const cf* xc, int ib, int
 // loaded once, coalesced) go to an LDS tile, column-major; lane (col, q4, half) then owns
 // outputs 4 q4 .. 4 q4 + 3 of its column over half of the band (t32_walk), and the halves
 // meet through LDS.
-template<int T, int NB>
+template<int T, int NB, int JH>
 struct toep_tile {
-    static constexpr int UPW = 32 / T, LPU = 256 / UPW, NQ = LPU / 16, QUADS = T / 4;  // two halves of QUADS
-    static constexpr int HS = NB + 2, XS = NB + T + 2;  // even column strides (16-B aligned pair reads)
-    static constexpr int NH = (NB + NQ - 1) / NQ, NXL = (NB + T - 1 + NQ - 1) / NQ;
+    static constexpr int UPW = 32 / T, LPU = 256 / UPW, NQ = LPU / 16;  // units per workgroup, lanes per unit
+    static constexpr int TP = T / JH, QUADS = TP / 4, NG = NQ / QUADS;  // outputs per unit, lanes per column, band groups
+    static constexpr int HS = NB + 2, XS = NB + TP + 2;                 // even column strides (16-B aligned pair reads)
+    static constexpr int NH = (NB + NQ - 1) / NQ, NXL = (NB + TP - 1 + NQ - 1) / NQ;
     static constexpr int LDS = UPW * 16 * (HS + XS) * int(sizeof(cf));
-    static_assert(NQ == 2 * QUADS, "two halves of the band per unit");
+    static_assert(NG >= 2 && NQ % QUADS == 0 && TP % 4 == 0, "toeplitz tile geometry");
 };
 
-template<int T, int NB>
+// unit u = (column group u / JH, window part u mod JH of T / JH outputs); JH = 2 where a step
+// has few units (one channel: the part halves the longest chain of the step)
+template<int T, int NB, int JH>
 __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
 {
-    using G = toep_tile<T, NB>;
+    using G = toep_tile<T, NB, JH>;
+    static_assert(G::LDS <= kSliceLds, "toeplitz tile");
     const int t = threadIdx.x, us = t / G::LPU, lt = t % G::LPU, col = lt & 15, q = lt >> 4;
     cf* hs = reinterpret_cast<cf*>(smem) + us * 16 * (G::HS + G::XS);  // hs[col][m] = H[p = a + m]
-    cf* xs = hs + 16 * G::HS;                                          // xs[col][i] = X[row tw - (b - 1) + i]
+    cf* xs = hs + 16 * G::HS;                                          // xs[col][i] = X[the oldest row + i]
     const int u = ta.u0 + bid * G::UPW + us, gpc = sa.B / 16;
     const bool live = u < ta.u1;
-    const int uc = live ? u : ta.u1 - 1, c = uc / gpc, g = uc - c * gpc;
-    const int k = g * 16 + col, nb = ta.b - ta.a, nx = nb + T - 1, R = sa.ring;
-    int rb = ta.tw - (ta.b - 1);  // the oldest row (b - 1 < 256 < R: one wrap at most)
+    const int uc = live ? u : ta.u1 - 1, jp = uc % JH, cg = uc / JH, c = cg / gpc, g = cg - c * gpc;
+    const int k = g * 16 + col, nb = ta.b - ta.a, nx = nb + G::TP - 1, R = sa.ring, jpart = jp * G::TP;
+    int rb = ta.tw + jpart - (ta.b - 1);  // the oldest row (b - 1 < 256 < R: one wrap at most)
     rb = rb < 0 ? rb + R : rb;
     cf hv[G::NH], xv[G::NXL];  // every load of the lane in flight, then the LDS writes
     if constexpr (G::UPW == 1) {  // channel uniform: buffer loads, row offsets in SGPRs
@@ -584,28 +589,32 @@ __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_a
             if (q + G::NQ * i < nx) xs[col * G::XS + odd + q + G::NQ * i] = xv[i];
     }
     __syncthreads();
-    const int half = q >= G::QUADS, j0 = 4 * (q - half * G::QUADS), nh = ((nb + 1) / 2 + 1) & ~1;
-    const int m0 = half ? nh : 0, m1 = half ? nb : (nh < nb ? nh : nb);
+    // lane (col, quad, group): outputs 4 quad .. 4 quad + 3 of the part, partitions of band group
+    const int grp = q / G::QUADS, j0 = 4 * (q - grp * G::QUADS), nq = ((nb + G::NG - 1) / G::NG + 1) & ~1;
+    const int m0 = grp * nq < nb ? grp * nq : nb, m1 = m0 + nq < nb ? m0 + nq : nb;
     f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
     const cf* hc = hs + col * G::HS;
     const cf* xc = xs + col * G::XS + odd;
-    if (live) {
+    if (live && m0 < m1) {
         if (g == 0) t32_walk<true>(hc, xc, j0 + nb - 1, m0, m1, col == 0, acc);  // uniform per unit
         else t32_walk<false>(hc, xc, j0 + nb - 1, m0, m1, false, acc);
     }
-    __syncthreads();  // the tiles are free: the halves meet there
-    f2v* red = reinterpret_cast<f2v*>(smem);  // [units][LPU / 2][4]
-    const int hl = lt - half * (G::LPU / 2);
-    if (half) {
+    __syncthreads();  // the tiles are free: the band groups meet there
+    constexpr int LG = 16 * G::QUADS;          // lanes per band group
+    f2v* red = reinterpret_cast<f2v*>(smem);  // [units][NG - 1][LG][4]
+    const int lg = lt - grp * LG;
+    if (grp) {
 #pragma unroll
-        for (int o = 0; o < 4; ++o) red[(us * (G::LPU / 2) + hl) * 4 + o] = acc[o];
+        for (int o = 0; o < 4; ++o) red[((us * (G::NG - 1) + grp - 1) * LG + lg) * 4 + o] = acc[o];
     }
     __syncthreads();
-    if (!half && live) {
-        cf* o = ta.slab + (int64_t(c) * T + j0) * sa.B + k;
+    if (!grp && live) {
+        cf* o = ta.slab + (int64_t(c) * T + jpart + j0) * sa.B + k;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const f2v v = acc[i] + red[(us * (G::LPU / 2) + hl) * 4 + i];
+            f2v v = acc[i];
+#pragma unroll
+            for (int r = 1; r < G::NG; ++r) v += red[((us * (G::NG - 1) + r - 1) * LG + lg) * 4 + i];
             o[int64_t(i) * sa.B] = cf{v.x, v.y};
         }
     }
@@ -891,9 +900,12 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
     } else if constexpr (L == 1) {
         if (NEO_ROLES & 2) toep_role<8, 16, 1, 1>(a, ta, bid, smem);
     } else if constexpr (L == 2) {
-        if (NEO_ROLES & 2) toep_lds_role<16, 32>(a, ta, bid, smem);
+        if (NEO_ROLES & 2) toep_lds_role<16, 32, 1>(a, ta, bid, smem);
     } else if constexpr (L == 3) {
-        if (NEO_ROLES & 4) toep_lds_role<32, kT32Band>(a, ta, bid, smem);
+        if (NEO_ROLES & 4) {
+            if (ta.jh == 2) toep_lds_role<32, kT32Band, 2>(a, ta, bid, smem);  // uniform per launch
+            else toep_lds_role<32, kT32Band, 1>(a, ta, bid, smem);
+        }
     } else {
         if (NEO_ROLES & 4) toep_big_role(a, ta, bid, smem);
     }
@@ -1054,10 +1066,12 @@ void lvl_filter_changed(upols_t* h)
 
 static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) % R); }
 
-// Toeplitz role geometry per window T (toep_role<T, NPL, NPG, JH> in k_lvl_step)
-static void toep_geom(int T, int& JH, int& UPW)
+// Toeplitz role geometry per window T (k_lvl_step's level roles): window parts per column
+// group and units per workgroup. T = 32 splits its window in two where a step has fewer than
+// 8 of its units (few channels: the part halves the step's longest chain).
+static void toep_geom(const upols_t* h, int T, int& JH, int& UPW)
 {
-    JH = T == kBigT ? kBigJH : 1;  // the big level: parts of kBigJP outputs (toep_big_role)
+    JH = T == kBigT ? kBigJH : (T == 32 && h->C * (h->B / 16) < 8 * 32 ? 2 : 1);
     UPW = T <= 8 ? 16 : (T <= 32 ? 32 / T : 1);  // toep_role<T, 2T, 1, 1>: 16 units; toep_tile: 32 / T
 }
 
@@ -1142,7 +1156,7 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
     for (int l = 0; l < lp.n; ++l) {
         const int T = lp.T[l];
         int JH, UPW;
-        toep_geom(T, JH, UPW);
+        toep_geom(h, T, JH, UPW);
         const int64_t U = int64_t(C) * (B / 16) * JH, st = n % T, W = n / T + 1;
         toep_arg& ta = a.tp[l];  // slot l = level l (the kernel dispatches on it), empty slices allowed
         ta.u0 = int(st * U / T);
@@ -1153,6 +1167,7 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
         ta.b = lp.b[l];
         ta.tw = ring_add(w, W * T - n, R);  // block t0 + n at row w; the window starts at t0 + W T
         ta.nwg = ta.u1 > ta.u0 ? (ta.u1 - ta.u0 + UPW - 1) / UPW : 0;
+        ta.jh = JH;
         a.ntp = l + 1;
     }
     if (lp.nseg) {
@@ -1189,8 +1204,9 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     slice_args a = base_args(h);
     for (int l = 0; l < lp.n; ++l) {
         int JH, UPW;
-        toep_geom(lp.T[l], JH, UPW);
+        toep_geom(h, lp.T[l], JH, UPW);
         toep_arg& ta = a.tp[a.ntp++];
+        ta.jh = JH;
         ta.slab = h->lv_slab[l];
         ta.T = lp.T[l];
         ta.a = lp.a[l];
