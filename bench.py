@@ -48,6 +48,7 @@ WORKLOADS = {
     "c5": (256, 512, 480000),  # headline: 2048 ch / 8 GPUs, B=512, IR 10 s @ 48 kHz
     "c4": (256, 256, 480000),  # 256 ch, B=256, IR 10 s @ 48 kHz
     "c3": (1, 512, 96000),     # 1 ch, B=512, IR 2 s @ 48 kHz
+    "c5full": (2048, 512, 480000),  # the metric's whole 2048-channel configuration on one GPU
 }
 
 
