@@ -2,11 +2,13 @@
 """bench.py — MI355X throughput of neo's UPOLS convolver (and FFT) hot path.
 
 Headline (BASELINE.json metric "Msamples/sec UPOLS convolver (block=512,
-IR=10s@48k); achieved HBM GB/s"): configs[4], the 2048-channel UPOLS sharded by
-channel across GPUs — 256 channels per GPU, B = 512, L = 480000 taps (P = 938).
-At N = 1 that is one GPU's shard; at N GPUs, N x 256 channels (weak scaling; the
-channels are independent, so there is no collective on the data path — torch
-.distributed (gloo) only carries the timing barrier and the max-over-ranks).
+IR=10s@48k); achieved HBM GB/s"): configs[4], the 2048-channel UPOLS, B = 512,
+L = 480000 taps (P = 938). The whole configuration fits one MI355X (~45 GB of filter,
+FDL and level buffers of 288 GB), so at N = 1 the workload is all 2048 channels on one
+GPU (`--workload c5full`, the default); at N GPUs, N x 2048 channels, 2048 per GPU
+(weak scaling; the channels are independent, so there is no collective on the data path
+— torch.distributed (gloo) only carries the timing barrier and the max-over-ranks).
+`--workload c5` is the 256-channel per-GPU shard of configs[4] split over 8 GPUs.
 
 A "step" = one block of B samples through the whole convolver for every channel,
 inputs already resident in HBM, one block per call as a real-time caller runs it
@@ -21,7 +23,7 @@ distribution, `parity` the last timed blocks against the oracle, `per_block_step
 plain one-pass-per-block step and `offline` the batched form (blocks up front), both
 timed in the same run; `c2_fft` the 4096 x 65536 batched FFT.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c4|c3|c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5full|c5|c4|c3|c2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 """
@@ -45,10 +47,10 @@ WARM_SECONDS = 0.25
 
 WORKLOADS = {
     # name: (channels per GPU, block, taps)
-    "c5": (256, 512, 480000),  # headline: 2048 ch / 8 GPUs, B=512, IR 10 s @ 48 kHz
+    "c5full": (2048, 512, 480000),  # headline: the metric's whole 2048-channel configuration per GPU
+    "c5": (256, 512, 480000),  # one GPU's shard of 2048 ch / 8 GPUs, B=512, IR 10 s @ 48 kHz
     "c4": (256, 256, 480000),  # 256 ch, B=256, IR 10 s @ 48 kHz
     "c3": (1, 512, 96000),     # 1 ch, B=512, IR 2 s @ 48 kHz
-    "c5full": (2048, 512, 480000),  # the metric's whole 2048-channel configuration on one GPU
 }
 
 
@@ -57,7 +59,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS) + ["c2"])
+    ap.add_argument("--workload", default="c5full", choices=sorted(WORKLOADS) + ["c2"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ahead", action="store_true", help="headline = the plain one-pass-per-block step")
     ap.add_argument("--no-offline", action="store_true", help="skip the batched (blocks up front) line")

@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 TAG=${1:-r2}
 cd /tmp && export TMPDIR=/tmp
-for W in c5 c4 c2; do
+for W in c5full c5 c4 c2; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${W}_${C}_$TAG -o run -- \
       python3 $R/bench.py --workload $W --steps 32 --warmup 2 --no-cpu-baseline --no-parity --no-fft \

@@ -70,13 +70,17 @@ def main():
     if len(sys.argv) > 2:
         summarize(tag, sys.argv[2], sys.argv[3], float(sys.argv[4]), sys.argv[5] if len(sys.argv) > 5 else None)
         return
-    for w in ("c5", "c4"):
+    for w in ("c5full", "c5", "c4"):
+        if not os.path.exists(os.path.join(OUT, f"pmc_{w}_FETCH_SIZE_{tag}")):
+            continue
         b = bench_line(tag, w)
         r = b["roofline"]
         summarize(tag, w, "k_lvl_step", r["algorithmic_bytes_per_launch"], w)
         summarize(tag, w, "k_upols_step", b["per_block_step"]["algorithmic_bytes_per_launch"], w + "_plain")
         if b.get("offline"):
             summarize(tag, w, "k_batch_mac", b["offline"]["algorithmic_bytes_per_launch"], w + "_offline")
+    if not os.path.exists(os.path.join(OUT, f"pmc_c2_FETCH_SIZE_{tag}")):
+        return
     b = bench_line(tag, "c2")
     summarize(tag, "c2", "k_c2c_lds<4096", b["roofline"]["algorithmic_bytes_per_launch"], "c2")
 
