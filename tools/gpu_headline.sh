@@ -27,7 +27,7 @@ echo pmc-ok && \
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 5 --no-fft > $O/bench_${W}_n2_$T.json 2> $O/bench_${W}_n2_$T.err && \
 echo n2-ok
-echo "headline exit=$?"; [ -f $O/bench_${W}_n2_$T.json ] || exit 1
+st=$?; echo "headline exit=$st"; [ $st -eq 0 ] || exit $st
 # role-masked builds (tools/build_roles.sh) at the headline workload, if built
 if [ -d tools/ab/1 ]; then
   W=$W timeout -k 10 900 bash tools/gpu_prof_roles.sh full 1 2 4 8 16 30 29 27 23 15 > $O/roles_${W}_$T.log 2>&1
