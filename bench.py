@@ -253,13 +253,16 @@ def algorithmic_bytes(C, B, P, plan):
                FDL row, 16B per bin each), one slab row per level and the far-field row (8B each)
     Toeplitz level (window T, band [a, b)), C*B/T columns per step: per column b - a filter
                rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
-    far level, C*B/128 columns per step: per column 256 FDL rows, 256 stored + nseg - 1 older
-               row-pair spectra, nseg segment spectra (256 f each) and 128 far-field entries."""
+    far level, C*B/128 columns per step: per column 256 FDL rows, the new row-pair spectrum
+               (256 f) stored, its segment spectrum and 128 far-field entries; phase 1 takes two
+               windows per pass over the nseg - 1 older row-pair and segment spectra (half per
+               window), and phase 2 segment 1 of every other window (2 x 256 f, half per window):
+               256 (nseg + 3) + 128 values per window for nseg >= 2 (256 x 3 + 128 for nseg 1)."""
     nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
     block = C * B * (16 + 16 + 16 * (plan["a0"] - 1) + 8 * nlev)
     toep = sum(C * B / T * 8 * (2 * (b - a) + 2 * T - 1) for T, a, b in zip(plan["T"], plan["a"], plan["b"]))
     ns = plan["nseg"]
-    far = C * B / 128 * 8 * (256 * (2 * ns + 1) + 128) if ns else 0.0
+    far = C * B / 128 * 8 * (256 * (ns + 3 if ns >= 2 else 3) + 128) if ns else 0.0
     return {"block": block, "toeplitz": toep, "far": far}
 
 

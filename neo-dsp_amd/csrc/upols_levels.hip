@@ -144,14 +144,18 @@ struct slice_args {
     const cf* hf;
     cf* xf;
     const cf* twf;
-    // far phase 1: stored-segment MAC (16 workgroups per unit)
-    int f1nwg, f1u0, f1nu, f1wn, f1fpl;  // slice units [f1u0, f1u0 + f1nu); f rows per lane
-    cf* f1acc;  // [units][256 f][16]
+    int fU;     // units (16 columns) of all channels
+    // far phase 1: stored-segment MAC, groups of kF1UG units; in pair mode a group takes two
+    // windows at once (far1_role)
+    int f1nwg, f1u0, f1u1, f1wn, f1fpl;  // slice units [f1u0, f1u1); target window; f rows per lane
+    int f1g0, f1gs, f1mode, f1par;       // first group, group step; 0 single, 1 pairs, 2 pairs + single; pair parity
+    cf* f1acc;  // partial sums [2 (window parity)][fU][256 f][16]
     // far phase 2 (the slice phase 1 did one step earlier): the fresh row pairs' transforms
     // (stored to their ring slots) and products, the sum, the inverse transform
     int f2nwg, f2u0, f2tw, f2wn;
-    cf* f2acc;
-    cf* f2ff;   // the target far window [C][128][B]
+    int f2pairs;  // units of the other parity take segment 1 here (second window of their pair)
+    cf* f2acc;    // as f1acc
+    cf* f2ff;     // the target far window [C][128][B]
 };
 
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
@@ -761,29 +765,35 @@ __device__ __forceinline__ void bin0_exchange(cf (&v)[16], cf* z, int a, int cp)
 // phase 1, FPL f rows per lane: a workgroup takes kF1UG units side by side (64 columns:
 // every wave-load reads 512 contiguous bytes of one f row) and 4 FPL f rows of them, so
 // kFN / (4 FPL) workgroups per unit group; the host picks FPL so that one round of NS =
-// 16 / FPL segments covers the stored ones (every load of a lane in flight at once)
+// 16 / FPL segments covers the stored ones (every load of a lane in flight at once).
+// Window pairs: the stored segments of window wn are s = 1 .. nseg - 1 (XF slot wn - s - 1),
+// those of window wn + 1 are s = 2 .. nseg - 1 (slot wn - s: the same slots, one segment on) --
+// so a group of parity f1par takes BOTH windows in one pass over its spectra (each XF and HF
+// value read once for two products) and the groups of the other parity take the next pair
+// one window later: half the phase-1 reads. Segment 1 of the second window (slot wn - 1, not
+// stored until this window's phase 2) is phase 2's, one window later (f2pairs).
 constexpr int kF1UG = 4;
 
-template<int FPL>
-__device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
+template<int FPL, bool PAIR>
+__device__ __forceinline__ void far1_mac(const slice_args& sa, int u, int f0, int col)
 {
-    constexpr int FR = 4 * FPL, PPG = kFN / FR, NS = 16 / FPL;  // f rows per workgroup, workgroups per group, segments per round
-    const int t = threadIdx.x, cl = t & 63, fq = t >> 6;
-    const int grp = bid / PPG, part = bid - grp * PPG;
-    const int ul = grp * kF1UG + (cl >> 4);  // the lane's unit within the slice
-    if (ul >= sa.f1nu) return;              // a partial last group (no barriers in this role)
-    const int gpc = sa.B / 16, u = sa.f1u0 + ul, c = u / gpc, g = u - c * gpc, col = cl & 15, k = g * 16 + col;
-    const int M = sa.M, nseg = sa.nseg;
-    auto slot = [&](int s) { return ((sa.f1wn - s - 1) % M + M) % M; };
-    const int64_t fs = sa.B;
-    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;  // first stored segment
-    const int f0 = part * FR + fq;                          // f = f0 + 4 j
-    const cf* hc = sa.hf + int64_t(c) * nseg * kFN * fs + int64_t(f0) * fs + k;
-    const cf* xc = sa.xf + int64_t(c) * M * kFN * fs + int64_t(f0) * fs + k;
-    const int64_t sp = int64_t(kFN) * fs;  // one spectrum
-    f2v acc[FPL];
+    constexpr int NS = 16 / FPL;  // segments per round
+    const int gpc = sa.B / 16, c = u / gpc, g = u - c * gpc, k = g * 16 + col;
+    const int M = sa.M, nseg = sa.nseg, wn = sa.f1wn;
+    auto slot = [&](int s) { return ((wn - s - 1) % M + M) % M; };
+    const int64_t fs = sa.B, sp = int64_t(kFN) * fs;  // one spectrum
+    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;  // first stored segment (1 in pair mode)
+    const cf* hc = sa.hf + int64_t(c) * nseg * sp + int64_t(f0) * fs + k;
+    const cf* xc = sa.xf + int64_t(c) * M * sp + int64_t(f0) * fs + k;
+    f2v acc[FPL], acc2[FPL];  // window wn; PAIR: window wn + 1
+    cf xp[FPL];               // PAIR: the previous segment's spectra (last of the previous round)
+    bool z0[FPL];             // packed bin 0, f = 0 and 128
 #pragma unroll
-    for (int j = 0; j < FPL; ++j) acc[j] = f2v(0.f);
+    for (int j = 0; j < FPL; ++j) {
+        acc[j] = f2v(0.f);
+        acc2[j] = f2v(0.f);
+        z0[j] = g == 0 && col == 0 && ((f0 + 4 * j) & (kFN / 2 - 1)) == 0;
+    }
     for (int sb = s0; sb < nseg; sb += NS) {
         cf xv[NS][FPL], hv[NS][FPL];
 #pragma unroll
@@ -803,14 +813,41 @@ __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
             if (sb + i < nseg) {
 #pragma unroll
                 for (int j = 0; j < FPL; ++j) {
-                    const bool z0 = g == 0 && col == 0 && ((f0 + 4 * j) & (kFN / 2 - 1)) == 0;  // packed bin 0, f = 0, 128
-                    pk_coef(hv[i][j], z0).mac(acc[j], xv[i][j]);
+                    const pk_coef h(hv[i][j], z0[j]);
+                    h.mac(acc[j], xv[i][j]);
+                    if constexpr (PAIR) {
+                        if (sb + i > s0) h.mac(acc2[j], i ? xv[i - 1][j] : xp[j]);
+                    }
                 }
             }
         }
-    }
+        if constexpr (PAIR) {
 #pragma unroll
-    for (int j = 0; j < FPL; ++j) sa.f1acc[(int64_t(ul) * kFN + f0 + 4 * j) * 16 + col] = cf{acc[j].x, acc[j].y};
+            for (int j = 0; j < FPL; ++j) xp[j] = xv[NS - 1][j];  // read only if the next round runs
+        }
+    }
+    cf* o = sa.f1acc + (int64_t((wn & 1) * sa.fU + u) * kFN + f0) * 16 + col;
+#pragma unroll
+    for (int j = 0; j < FPL; ++j) o[4 * j * 16] = cf{acc[j].x, acc[j].y};
+    if constexpr (PAIR) {
+        cf* o2 = sa.f1acc + (int64_t(((wn + 1) & 1) * sa.fU + u) * kFN + f0) * 16 + col;
+#pragma unroll
+        for (int j = 0; j < FPL; ++j) o2[4 * j * 16] = cf{acc2[j].x, acc2[j].y};
+    }
+}
+
+template<int FPL>
+__device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
+{
+    constexpr int FR = 4 * FPL, PPG = kFN / FR;  // f rows per workgroup, workgroups per group
+    const int t = threadIdx.x, cl = t & 63, fq = t >> 6;
+    const int grp = bid / PPG, part = bid - grp * PPG;
+    const int g4 = sa.f1g0 + grp * sa.f1gs;  // the group (global index; uniform per workgroup)
+    const int u = g4 * kF1UG + (cl >> 4);    // the lane's unit
+    if (u < sa.f1u0 || u >= sa.f1u1) return;  // groups straddle slices (no barriers in this role)
+    const int f0 = part * FR + fq;            // f = f0 + 4 j
+    if (sa.f1mode != 0 && (g4 & 1) == sa.f1par) far1_mac<FPL, true>(sa, u, f0, cl & 15);
+    else far1_mac<FPL, false>(sa, u, f0, cl & 15);
 }
 
 __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
@@ -836,7 +873,8 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
     // phase 1 + the fresh segments' products, kept in acc between segments (priming: every
     // segment is fresh) so that it is not live across a transform
     cf v[16];
-    const __amdgpu_buffer_rsrc_t ares = buf_rsrc(sa.f2acc + int64_t(bid) * kFN * 16, kFN * 16 * int(sizeof(cf)));
+    const __amdgpu_buffer_rsrc_t ares =
+        buf_rsrc(sa.f2acc + int64_t((sa.f2wn & 1) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
     const int ao = (a * 16 + cp) * int(sizeof(cf)), as = 16 * 16 * int(sizeof(cf));  // f = a + 16 i
     for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
         // fresh row pair: rows tw - (s + 3) 128 + a + 16 n (the ring holds >= kFarRing > 256
@@ -867,6 +905,22 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
         if (s + 1 < s0) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) buf_st(v[i], ares, ao, i * as);
+        }
+    }
+    if (sa.f2pairs && ((u / kF1UG) & 1) != (sa.f2wn & 1)) {  // uniform per workgroup
+        // the second window of this unit's phase-1 pair: segment 1 (slot f2wn - 2, stored by the
+        // previous window's phase 2) was not there when the pair ran
+        cf hv[16], xv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            hv[i] = buf_ld(hres, vo, spec + int(16 * i * fs * int(sizeof(cf))));
+            xv[i] = buf_ld(xres, vo, slot(1) * spec + int(16 * i * fs * int(sizeof(cf))));
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            f2v w = {v[i].x, v[i].y};
+            pk_coef(hv[i], unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0).mac(w, xv[i]);
+            v[i] = cf{w.x, w.y};
         }
     }
     __syncthreads();  // twiddles; the bin-0 exchange of the last segment is done
@@ -1001,7 +1055,25 @@ static int far1_fpl(const upols_t* h)
     return h->lv.nseg - 1 <= 4 ? 4 : (h->lv.nseg - 1 <= 8 ? 2 : 1);
 }
 
-static size_t far_units_per_slice(const upols_t* h) { return (size_t(h->C) * (h->B / 16) + kFarT - 1) / kFarT; }
+static int64_t far_units(const upols_t* h) { return int64_t(h->C) * (h->B / 16); }
+
+// far phase 1 over the slice units [u0, u1): mode 0 one window per group, 1 only the groups of
+// parity par (two windows each), 2 every group, those of parity par with two windows
+static void far1_range(const upols_t* h, slice_args& a, int u0, int u1, int mode, int par)
+{
+    a.f1u0 = u0;
+    a.f1u1 = u1;
+    a.f1fpl = far1_fpl(h);
+    a.f1mode = mode;
+    a.f1par = par;
+    a.f1nwg = 0;
+    if (u1 <= u0) return;
+    const int ga = u0 / kF1UG, gb = (u1 - 1) / kF1UG;  // groups holding slice units
+    a.f1g0 = mode == 1 ? ga + ((ga & 1) != par) : ga;
+    a.f1gs = mode == 1 ? 2 : 1;
+    const int ng = a.f1g0 > gb ? 0 : (gb - a.f1g0) / a.f1gs + 1;
+    a.f1nwg = ng * (kFN / (4 * a.f1fpl));
+}
 
 // device buffers of the level pipeline (allocated on the first streaming step), all or none
 static int lvl_buffers(upols_t* h)
@@ -1033,7 +1105,7 @@ static int lvl_buffers(upols_t* h)
         if (!alloc(reinterpret_cast<void**>(&h->fv_xf), spec)) return undo("far FDL spectra", spec);
         if (!alloc(reinterpret_cast<void**>(&h->fv_ff), ffb)) return undo("far field", ffb);
         if (!alloc(reinterpret_cast<void**>(&h->fv_tw), kFN * sizeof(cf))) return undo("far twiddles", kFN * sizeof(cf));
-        const size_t accb = 2 * far_units_per_slice(h) * kFN * 16 * sizeof(cf);  // phase 1 -> 2, double-buffered
+        const size_t accb = 2 * size_t(far_units(h)) * kFN * 16 * sizeof(cf);  // phase 1 -> 2, per window parity
         if (!alloc(reinterpret_cast<void**>(&h->fv_acc), accb)) return undo("far partial sums", accb);
         const auto t = make_twiddle_table(kFN);
         if (hipMemcpy(h->fv_tw, t.data(), kFN * sizeof(cf), hipMemcpyHostToDevice) != hipSuccess)
@@ -1089,6 +1161,9 @@ static slice_args base_args(const upols_t* h)
         a.M = h->lv.nseg;
         a.nseg = h->lv.nseg;
         a.fnfresh = 1;
+        a.fU = int(far_units(h));
+        a.f1acc = h->fv_acc;
+        a.f2acc = h->fv_acc;
         a.hf = h->fv_hf;
         a.xf = h->fv_xf;
         a.twf = h->fv_tw;
@@ -1115,18 +1190,15 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t
     return NEO_HIP_OK;
 }
 
-// far phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1 (one step ahead of
-// its phase 2); block t0 + n is at ring row w
+// far phase 1 of step n: slice (n + 1) mod 128 of window W = (n + 1) / 128 + 1 (one step ahead
+// of its phase 2), the groups of parity W mod 2 for the windows W and W + 1 (far1_mac); in
+// window 1, the first after priming, the other groups for window 1 alone
 static void far1_args(const upols_t* h, int64_t n, slice_args& a)
 {
-    const int64_t U = int64_t(h->C) * (h->B / 16), n1 = n + 1, st = n1 % kFarT, W = n1 / kFarT + 1;
-    const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
-    a.f1u0 = u0;
-    a.f1fpl = far1_fpl(h);
-    a.f1nu = u1 - u0;
-    a.f1nwg = (u1 - u0 + kF1UG - 1) / kF1UG * (kFN / (4 * a.f1fpl));
+    const int64_t U = far_units(h), n1 = n + 1, st = n1 % kFarT, W = n1 / kFarT + 1;
     a.f1wn = int(W);
-    a.f1acc = h->fv_acc + (n1 & 1) * far_units_per_slice(h) * kFN * 16;
+    far1_range(h, a, int(st * U / kFarT), int((st + 1) * U / kFarT), h->lv.nseg < 2 ? 0 : (W == 1 ? 2 : 1),
+               int(W & 1));
 }
 
 // The launch of step n >= 0 (block t0 + n at ring row w): the block and slice n mod T of
@@ -1179,7 +1251,7 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
         a.f2nwg = u1 - u0;
         a.f2tw = ring_add(w, W * kFarT - n, R);
         a.f2wn = int(W);
-        a.f2acc = h->fv_acc + (n & 1) * far_units_per_slice(h) * kFN * 16;
+        a.f2pairs = lp.nseg >= 2 && W >= 2;
         a.f2ff = h->fv_ff + (W & 1) * C * kFarT * B;
         far1_args(h, n, a);
     }
@@ -1222,19 +1294,14 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     slice_args f = base_args(h);
     f.fnfresh = lp.nseg;
     f.f1wn = 0;
-    f.f1acc = h->fv_acc;
     f.f2tw = w;
     f.f2wn = 0;
-    f.f2acc = h->fv_acc;
     f.f2ff = h->fv_ff;
     const int64_t U = int64_t(C) * (B / 16);
     for (int st = 0; st < kFarT; ++st) {
         const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
         if (u1 <= u0) continue;
-        f.f1u0 = u0;
-        f.f1fpl = far1_fpl(h);
-        f.f1nu = u1 - u0;
-        f.f1nwg = (u1 - u0 + kF1UG - 1) / kF1UG * (kFN / (4 * f.f1fpl));  // zero partial sums (no stored segments)
+        far1_range(h, f, u0, u1, 0, 0);  // zero partial sums (no stored segments)
         f.f2nwg = 0;
         if (int rc = launch_step_kernel(h, f, s)) return rc;
         f.f1nwg = 0;

@@ -9,7 +9,7 @@ the current one (a slice of the bins per step, from FDL rows before the current 
 the far level does the same in two phases one step apart. All of it runs in ONE launch per
 step (k_lvl_step), so no role may read what another role of the same step writes. This test
 replays exactly that schedule — the ring positions the host passes (tw), the slice ranges,
-the double-buffered slabs, the far level's XF ring of row-pair spectra, its partial sums and
+the double-buffered slabs, the far level's XF ring of row-pair spectra, its partial sums (phase 1 in window pairs) and
 256-point partition-axis transforms — on random spectra, with history before the levels
 start, ring wraparound and re-priming, running the roles of every step in a random order
 (with the block's FDL row written at a random point among them), and checks every output
@@ -41,8 +41,8 @@ def plan(P):
 class Sim:
     """float64 replay of the level pipeline for one channel of K bins."""
 
-    def __init__(self, H, lp):
-        self.H, self.lp = H, lp
+    def __init__(self, H, lp, G=4):
+        self.H, self.lp, self.G = H, lp, G
         self.P, self.K = H.shape
         self.R = self.P + 31
         if lp["nseg"]:
@@ -81,32 +81,52 @@ class Sim:
             rows = (tw + j - ps) % self.R
             self.slab[l][buf, j, k0:k1] = (self.H[a:b, k0:k1] * self.ring[rows, k0:k1]).sum(0)
 
-    def far1(self, wn, k0, k1, nfresh, buf):
-        """phase 1: the stored segments' products into the partial sums"""
-        acc = np.zeros((FN, k1 - k0), complex)
-        for s in range(nfresh, self.lp["nseg"]):
-            slot = (wn - s - 1) % self.M
-            acc += self.XF[slot, :, k0:k1] * self.HF[s, :, k0:k1]
-        self.acc[buf, :, k0:k1] = acc
+    def half(self, k):
+        """phase-1 pair parity of column k (the kernels: 16-column unit u, group u // 4)"""
+        return (k // self.G) & 1
 
-    def far2(self, tw, wn, k0, k1, nfresh, buf):
-        """phase 2: the fresh row pairs' transforms (stored to their slots) and products, the
-        inverse transform into the far field"""
-        acc = self.acc[buf, :, k0:k1].copy()
+    def far1(self, wn, k0, k1, nfresh, mode=0, par=0):
+        """phase 1: the stored segments' products into the partial sums of window wn; mode 1:
+        only the columns of parity par, each for windows wn AND wn + 1 (segments s >= 2 of
+        wn + 1 use the slots of s - 1 of wn); mode 2: those, and the others for wn alone"""
+        ns = self.lp["nseg"]
+        for k in range(k0, k1):
+            pair = mode != 0 and self.half(k) == par
+            if mode == 1 and not pair:
+                continue
+            acc = np.zeros(FN, complex)
+            for s in range(min(nfresh, ns), ns):
+                acc += self.XF[(wn - s - 1) % self.M, :, k] * self.HF[s, :, k]
+            self.acc[wn & 1, :, k] = acc
+            if pair:
+                acc2 = np.zeros(FN, complex)
+                for s in range(2, ns):
+                    acc2 += self.XF[(wn - s) % self.M, :, k] * self.HF[s, :, k]
+                self.acc[(wn + 1) & 1, :, k] = acc2
+
+    def far2(self, tw, wn, k0, k1, nfresh, pairs=False):
+        """phase 2: the fresh row pairs' transforms (stored to their slots) and products, segment
+        1 for the second window of a phase-1 pair, the inverse transform into the far field"""
+        acc = self.acc[wn & 1, :, k0:k1].copy()
         for s in range(min(nfresh, self.lp["nseg"])):
             slot = (wn - s - 1) % self.M
             rows = [(tw - (s + 3) * FT + i) % self.R for i in range(FN)]
             self.XF[slot, :, k0:k1] = np.fft.fft(self.ring[rows, k0:k1], axis=0)
             acc += self.XF[slot, :, k0:k1] * self.HF[s, :, k0:k1]
+        if pairs:
+            for k in range(k0, k1):
+                if self.half(k) != (wn & 1):
+                    acc[:, k - k0] += self.XF[(wn - 2) % self.M, :, k] * self.HF[1, :, k]
         self.ff[wn & 1, :, k0:k1] = np.fft.ifft(acc, axis=0)[FT:]
 
     def far1_slice(self, n, w):
-        """phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1"""
+        """phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1, paired"""
         n1 = n + 1
         st, W = n1 % FT, n1 // FT + 1
         k0, k1 = st * self.K // FT, (st + 1) * self.K // FT
         if k1 > k0:
-            self.far1(W, k0, k1, 1, n1 & 1)
+            mode = 0 if self.lp["nseg"] < 2 else (2 if W == 1 else 1)
+            self.far1(W, k0, k1, 1, mode, W & 1)
 
     def roles(self, n, w):
         """the slice roles of step n (block at ring row w), as closures"""
@@ -123,7 +143,7 @@ class Sim:
             st, W = n % FT, n // FT + 1
             k0, k1 = st * K // FT, (st + 1) * K // FT
             if k1 > k0:
-                out.append(lambda: self.far2((w + W * FT - n) % R, W, k0, k1, 1, n & 1))
+                out.append(lambda: self.far2((w + W * FT - n) % R, W, k0, k1, 1, lp["nseg"] >= 2 and W >= 2))
             out.append(lambda: self.far1_slice(n, w))
         return out
 
@@ -132,8 +152,8 @@ class Sim:
             self.toep(l, self.w, 0, self.K, 0)
         if self.lp["nseg"]:
             ns = self.lp["nseg"]
-            self.far1(0, 0, self.K, ns, 0)
-            self.far2(self.w, 0, 0, self.K, ns, 0)
+            self.far1(0, 0, self.K, ns)
+            self.far2(self.w, 0, 0, self.K, ns)
             self.far1_slice(-1, (self.w - 1) % self.R)
         self.n = 0
 
