@@ -19,6 +19,7 @@ timeout -k 10 300 python bench.py --workload c4 --steps 128 --no-cpu-baseline --
 timeout -k 10 300 python bench.py --workload c3 --steps 256 --no-cpu-baseline --no-fft > $O/bench_c3_$TAG.json 2> $O/bench_c3_$TAG.err && \
 timeout -k 10 300 python bench.py --workload c5 --host-io --steps 200 > $O/bench_c5_hostio_$TAG.json 2> $O/bench_c5_hostio_$TAG.err && \
 cd /tmp && export TMPDIR=/tmp && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5full_$TAG -o run -- python3 $R/bench.py --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5full_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$TAG -o run -- python3 $R/bench.py --workload c5 --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2_$TAG -o run -- python3 $R/bench.py --workload c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_c2_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- python3 $R/bench.py --workload c4 --steps 128 --no-cpu-baseline --no-parity --no-fft > $O/prof_c4_$TAG.log 2>&1 && \
