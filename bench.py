@@ -246,6 +246,18 @@ class Feed:
             n -= k
 
 
+def far_group(nseg: int, units: int) -> int:
+    """Windows per far phase-1 pass, as upols_levels.hip far_group: round(sqrt(2 (nseg - 1)))
+    clamped to [2, 4] from 32768 16-column units (C * B / 16) on, else 2 (1 below two segments)."""
+    import math
+
+    if nseg < 2:
+        return 1
+    if units < 32768:
+        return 2
+    return min(4, max(2, int(math.floor(math.sqrt(2.0 * (nseg - 1)) + 0.5))))
+
+
 def algorithmic_bytes(C, B, P, plan):
     """Algorithmic bytes per streaming step of the step kernel k_lvl_step, by role:
     block:     window (previous block + this block), previous-block write, output (4 x 4B per
@@ -254,15 +266,17 @@ def algorithmic_bytes(C, B, P, plan):
     Toeplitz level (window T, band [a, b)), C*B/T columns per step: per column b - a filter
                rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
     far level, C*B/128 columns per step: per column 256 FDL rows, the new row-pair spectrum
-               (256 f) stored, its segment spectrum and 128 far-field entries; phase 1 takes two
-               windows per pass over the nseg - 1 older row-pair and segment spectra (half per
-               window), and phase 2 segment 1 of every other window (2 x 256 f, half per window):
-               256 (nseg + 3) + 128 values per window for nseg >= 2 (256 x 3 + 128 for nseg 1)."""
+               (256 f) stored, its segment spectrum and 128 far-field entries; phase 1 takes K
+               windows per pass over the nseg - 1 older row-pair and segment spectra (1/K per
+               window), and phase 2 segments 1 .. j of window j of a group (K - 1 spectrum pairs
+               per window on average): 256 (3 + 2 (nseg - 1) / K + K - 1) + 128 values per
+               window, K = far_group(nseg, units) (upols_levels.hip)."""
     nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
     block = C * B * (16 + 16 + 16 * (plan["a0"] - 1) + 8 * nlev)
     toep = sum(C * B / T * 8 * (2 * (b - a) + 2 * T - 1) for T, a, b in zip(plan["T"], plan["a"], plan["b"]))
     ns = plan["nseg"]
-    far = C * B / 128 * 8 * (256 * (ns + 3 if ns >= 2 else 3) + 128) if ns else 0.0
+    K = far_group(ns, C * B // 16)
+    far = C * B / 128 * 8 * (256 * (3 + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
     return {"block": block, "toeplitz": toep, "far": far}
 
 

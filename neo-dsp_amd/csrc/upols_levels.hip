@@ -26,6 +26,7 @@
 #include "upols_handle.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 namespace neo_hip {
@@ -148,12 +149,13 @@ struct slice_args {
     // far phase 1: stored-segment MAC, groups of kF1UG units; in pair mode a group takes two
     // windows at once (far1_role)
     int f1nwg, f1u0, f1u1, f1wn, f1fpl;  // slice units [f1u0, f1u1); target window; f rows per lane
-    int f1g0, f1gs, f1mode, f1par;       // first group, group step; 0 single, 1 pairs, 2 pairs + single; pair parity
-    cf* f1acc;  // partial sums [2 (window parity)][fU][256 f][16]
+    int fK;                              // windows per phase-1 pass (1: one window per pass)
+    int f1g0, f1gs, f1mode, f1cls;       // first group, group step; 0 single, 1 the class's groups, 2 every group; class
+    cf* f1acc;  // partial sums [fK (window mod fK)][fU][256 f][16]
     // far phase 2 (the slice phase 1 did one step earlier): the fresh row pairs' transforms
     // (stored to their ring slots) and products, the sum, the inverse transform
     int f2nwg, f2u0, f2tw, f2wn;
-    int f2pairs;  // units of the other parity take segment 1 here (second window of their pair)
+    int f2grp;    // phase-1 window groups on: a unit in window j of its group takes segments 1..j here
     cf* f2acc;    // as f1acc
     cf* f2ff;     // the target far window [C][128][B]
 };
@@ -766,32 +768,40 @@ __device__ __forceinline__ void bin0_exchange(cf (&v)[16], cf* z, int a, int cp)
 // every wave-load reads 512 contiguous bytes of one f row) and 4 FPL f rows of them, so
 // kFN / (4 FPL) workgroups per unit group; the host picks FPL so that one round of NS =
 // 16 / FPL segments covers the stored ones (every load of a lane in flight at once).
-// Window pairs: the stored segments of window wn are s = 1 .. nseg - 1 (XF slot wn - s - 1),
-// those of window wn + 1 are s = 2 .. nseg - 1 (slot wn - s: the same slots, one segment on) --
-// so a group of parity f1par takes BOTH windows in one pass over its spectra (each XF and HF
-// value read once for two products) and the groups of the other parity take the next pair
-// one window later: half the phase-1 reads. Segment 1 of the second window (slot wn - 1, not
-// stored until this window's phase 2) is phase 2's, one window later (f2pairs).
+// Window groups: the stored segments of window wn are s = 1 .. nseg - 1 (XF slot wn - s - 1),
+// those of window wn + j are s = j + 1 .. nseg - 1 (slot wn + j - s - 1: the same slots, j
+// segments on) -- so a unit group of class c = (group index) mod K takes K windows in one pass
+// over its spectra (each XF and HF value read once for up to K products) when wn = c mod K, and
+// the other classes take theirs in the other windows: 1/K of the phase-1 reads. Segments 1 .. j
+// of window wn + j (slots not yet stored when the pass runs: phase 2 of windows wn .. wn + j - 1
+// writes them) are phase 2's, in that window (f2grp). K ~ sqrt(2 (nseg - 1)) (far_group) balances
+// the two: 2 (nseg - 1) / K + K - 1 spectra per window and column instead of 2 (nseg - 1).
 constexpr int kF1UG = 4;
+constexpr int kFarKMax = 4;
 
-template<int FPL, bool PAIR>
+// first window >= 1 whose phase-1 pass a unit group of class c starts (earlier windows after
+// priming: one window per pass)
+__host__ __device__ __forceinline__ int far_first(int c, int K) { return 1 + ((c - 1) % K + K) % K; }
+
+template<int FPL, int K>
 __device__ __forceinline__ void far1_mac(const slice_args& sa, int u, int f0, int col)
 {
     constexpr int NS = 16 / FPL;  // segments per round
+    static_assert(NS >= K - 1 || K == 1, "history of the previous round");
     const int gpc = sa.B / 16, c = u / gpc, g = u - c * gpc, k = g * 16 + col;
     const int M = sa.M, nseg = sa.nseg, wn = sa.f1wn;
     auto slot = [&](int s) { return ((wn - s - 1) % M + M) % M; };
     const int64_t fs = sa.B, sp = int64_t(kFN) * fs;  // one spectrum
-    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;  // first stored segment (1 in pair mode)
+    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;  // first stored segment (1 when K > 1)
     const cf* hc = sa.hf + int64_t(c) * nseg * sp + int64_t(f0) * fs + k;
     const cf* xc = sa.xf + int64_t(c) * M * sp + int64_t(f0) * fs + k;
-    f2v acc[FPL], acc2[FPL];  // window wn; PAIR: window wn + 1
-    cf xp[FPL];               // PAIR: the previous segment's spectra (last of the previous round)
-    bool z0[FPL];             // packed bin 0, f = 0 and 128
+    f2v acc[K][FPL];             // window wn + j
+    cf xp[K > 1 ? K - 1 : 1][FPL];  // xp[d]: segment sb - 1 - d's spectra (the previous rounds)
+    bool z0[FPL];                // packed bin 0, f = 0 and 128
 #pragma unroll
     for (int j = 0; j < FPL; ++j) {
-        acc[j] = f2v(0.f);
-        acc2[j] = f2v(0.f);
+#pragma unroll
+        for (int w = 0; w < K; ++w) acc[w][j] = f2v(0.f);
         z0[j] = g == 0 && col == 0 && ((f0 + 4 * j) & (kFN / 2 - 1)) == 0;
     }
     for (int sb = s0; sb < nseg; sb += NS) {
@@ -814,25 +824,24 @@ __device__ __forceinline__ void far1_mac(const slice_args& sa, int u, int f0, in
 #pragma unroll
                 for (int j = 0; j < FPL; ++j) {
                     const pk_coef h(hv[i][j], z0[j]);
-                    h.mac(acc[j], xv[i][j]);
-                    if constexpr (PAIR) {
-                        if (sb + i > s0) h.mac(acc2[j], i ? xv[i - 1][j] : xp[j]);
-                    }
+#pragma unroll
+                    for (int w = 0; w < K; ++w)  // window wn + w: segment sb + i meets slot of sb + i - w
+                        if (sb + i - w >= s0) h.mac(acc[w][j], i >= w ? xv[i - w][j] : xp[w - i - 1][j]);
                 }
             }
         }
-        if constexpr (PAIR) {
+        if constexpr (K > 1) {
 #pragma unroll
-            for (int j = 0; j < FPL; ++j) xp[j] = xv[NS - 1][j];  // read only if the next round runs
+            for (int d = 0; d < K - 1; ++d)
+#pragma unroll
+                for (int j = 0; j < FPL; ++j) xp[d][j] = xv[NS - 1 - d][j];  // read only if the next round runs
         }
     }
-    cf* o = sa.f1acc + (int64_t((wn & 1) * sa.fU + u) * kFN + f0) * 16 + col;
 #pragma unroll
-    for (int j = 0; j < FPL; ++j) o[4 * j * 16] = cf{acc[j].x, acc[j].y};
-    if constexpr (PAIR) {
-        cf* o2 = sa.f1acc + (int64_t(((wn + 1) & 1) * sa.fU + u) * kFN + f0) * 16 + col;
+    for (int w = 0; w < K; ++w) {
+        cf* o = sa.f1acc + (int64_t(((wn + w) % sa.fK) * sa.fU + u) * kFN + f0) * 16 + col;
 #pragma unroll
-        for (int j = 0; j < FPL; ++j) o2[4 * j * 16] = cf{acc2[j].x, acc2[j].y};
+        for (int j = 0; j < FPL; ++j) o[4 * j * 16] = cf{acc[w][j].x, acc[w][j].y};
     }
 }
 
@@ -846,8 +855,14 @@ __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
     const int u = g4 * kF1UG + (cl >> 4);    // the lane's unit
     if (u < sa.f1u0 || u >= sa.f1u1) return;  // groups straddle slices (no barriers in this role)
     const int f0 = part * FR + fq;            // f = f0 + 4 j
-    if (sa.f1mode != 0 && (g4 & 1) == sa.f1par) far1_mac<FPL, true>(sa, u, f0, cl & 15);
-    else far1_mac<FPL, false>(sa, u, f0, cl & 15);
+    const int K = sa.fK, cls = sa.f1mode ? g4 % K : 0;
+    if (sa.f1mode == 0 || (cls != sa.f1cls && far_first(cls, K) > sa.f1wn)) {
+        far1_mac<FPL, 1>(sa, u, f0, cl & 15);  // one window (priming, or the class has not started)
+    } else if (cls == sa.f1cls) {
+        if (K == 2) far1_mac<FPL, 2>(sa, u, f0, cl & 15);
+        else if (K == 3) far1_mac<FPL, 3>(sa, u, f0, cl & 15);
+        else far1_mac<FPL, kFarKMax>(sa, u, f0, cl & 15);
+    }
 }
 
 __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
@@ -874,7 +889,7 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
     // segment is fresh) so that it is not live across a transform
     cf v[16];
     const __amdgpu_buffer_rsrc_t ares =
-        buf_rsrc(sa.f2acc + int64_t((sa.f2wn & 1) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
+        buf_rsrc(sa.f2acc + int64_t((sa.f2wn % sa.fK) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
     const int ao = (a * 16 + cp) * int(sizeof(cf)), as = 16 * 16 * int(sizeof(cf));  // f = a + 16 i
     for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
         // fresh row pair: rows tw - (s + 3) 128 + a + 16 n (the ring holds >= kFarRing > 256
@@ -907,20 +922,24 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
             for (int i = 0; i < 16; ++i) buf_st(v[i], ares, ao, i * as);
         }
     }
-    if (sa.f2pairs && ((u / kF1UG) & 1) != (sa.f2wn & 1)) {  // uniform per workgroup
-        // the second window of this unit's phase-1 pair: segment 1 (slot f2wn - 2, stored by the
-        // previous window's phase 2) was not there when the pair ran
-        cf hv[16], xv[16];
+    if (sa.f2grp) {  // uniform per workgroup
+        // window j of this unit's phase-1 group: segments 1 .. j (slots f2wn - 2 .. f2wn - j - 1,
+        // stored by the group's earlier windows' phase 2) were not there when the pass ran
+        const int K = sa.fK, cls = (u / kF1UG) % K, first = far_first(cls, K);
+        const int jw = sa.f2wn >= first ? (sa.f2wn - cls) % K : 0;
+        for (int s1 = 1; s1 <= jw && s1 < nseg; ++s1) {
+            cf hv[16], xv[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            hv[i] = buf_ld(hres, vo, spec + int(16 * i * fs * int(sizeof(cf))));
-            xv[i] = buf_ld(xres, vo, slot(1) * spec + int(16 * i * fs * int(sizeof(cf))));
-        }
+            for (int i = 0; i < 16; ++i) {
+                hv[i] = buf_ld(hres, vo, s1 * spec + int(16 * i * fs * int(sizeof(cf))));
+                xv[i] = buf_ld(xres, vo, slot(s1) * spec + int(16 * i * fs * int(sizeof(cf))));
+            }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            f2v w = {v[i].x, v[i].y};
-            pk_coef(hv[i], unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0).mac(w, xv[i]);
-            v[i] = cf{w.x, w.y};
+            for (int i = 0; i < 16; ++i) {
+                f2v w = {v[i].x, v[i].y};
+                pk_coef(hv[i], unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0).mac(w, xv[i]);
+                v[i] = cf{w.x, w.y};
+            }
         }
     }
     __syncthreads();  // twiddles; the bin-0 exchange of the last segment is done
@@ -1057,20 +1076,37 @@ static int far1_fpl(const upols_t* h)
 
 static int64_t far_units(const upols_t* h) { return int64_t(h->C) * (h->B / 16); }
 
-// far phase 1 over the slice units [u0, u1): mode 0 one window per group, 1 only the groups of
-// parity par (two windows each), 2 every group, those of parity par with two windows
-static void far1_range(const upols_t* h, slice_args& a, int u0, int u1, int mode, int par)
+// windows per far phase-1 pass (far1_mac): K ~ sqrt(2 (nseg - 1)) minimizes the spectra read per
+// window and column, 2 (nseg - 1) / K + K - 1; but phase 2 takes up to K - 1 extra segments in
+// its one-workgroup-per-unit chain, which bounds the step where a step has few far units
+// (measured: K = 3 / 4 instead of 2 at 64 / 32 units per step, C5 / C4: 13 % / 25 % slower; at
+// 512, the 2048-channel headline: 3 % faster), so K = 2 below kFarGroupUnits units
+constexpr int64_t kFarGroupUnits = 32768;  // 256 units per step
+
+static int far_group(const upols_t* h)
 {
+    const int ns = h->lv.nseg;
+    if (ns < 2) return 1;
+    if (int64_t(h->C) * (h->B / 16) < kFarGroupUnits) return 2;
+    const int K = int(std::lround(std::sqrt(2.0 * (ns - 1))));
+    return std::min(kFarKMax, std::max(2, K));
+}
+
+// far phase 1 over the slice units [u0, u1): mode 0 one window per group, 1 only the groups of
+// class cls (K windows each), 2 every group (class cls: K windows; classes not started: one)
+static void far1_range(const upols_t* h, slice_args& a, int u0, int u1, int mode, int cls)
+{
+    const int K = far_group(h);
     a.f1u0 = u0;
     a.f1u1 = u1;
     a.f1fpl = far1_fpl(h);
     a.f1mode = mode;
-    a.f1par = par;
+    a.f1cls = cls;
     a.f1nwg = 0;
     if (u1 <= u0) return;
     const int ga = u0 / kF1UG, gb = (u1 - 1) / kF1UG;  // groups holding slice units
-    a.f1g0 = mode == 1 ? ga + ((ga & 1) != par) : ga;
-    a.f1gs = mode == 1 ? 2 : 1;
+    a.f1g0 = mode == 1 ? ga + ((cls - ga % K) % K + K) % K : ga;
+    a.f1gs = mode == 1 ? K : 1;
     const int ng = a.f1g0 > gb ? 0 : (gb - a.f1g0) / a.f1gs + 1;
     a.f1nwg = ng * (kFN / (4 * a.f1fpl));
 }
@@ -1105,7 +1141,7 @@ static int lvl_buffers(upols_t* h)
         if (!alloc(reinterpret_cast<void**>(&h->fv_xf), spec)) return undo("far FDL spectra", spec);
         if (!alloc(reinterpret_cast<void**>(&h->fv_ff), ffb)) return undo("far field", ffb);
         if (!alloc(reinterpret_cast<void**>(&h->fv_tw), kFN * sizeof(cf))) return undo("far twiddles", kFN * sizeof(cf));
-        const size_t accb = 2 * size_t(far_units(h)) * kFN * 16 * sizeof(cf);  // phase 1 -> 2, per window parity
+        const size_t accb = size_t(far_group(h)) * size_t(far_units(h)) * kFN * 16 * sizeof(cf);  // phase 1 -> 2
         if (!alloc(reinterpret_cast<void**>(&h->fv_acc), accb)) return undo("far partial sums", accb);
         const auto t = make_twiddle_table(kFN);
         if (hipMemcpy(h->fv_tw, t.data(), kFN * sizeof(cf), hipMemcpyHostToDevice) != hipSuccess)
@@ -1162,6 +1198,7 @@ static slice_args base_args(const upols_t* h)
         a.nseg = h->lv.nseg;
         a.fnfresh = 1;
         a.fU = int(far_units(h));
+        a.fK = far_group(h);
         a.f1acc = h->fv_acc;
         a.f2acc = h->fv_acc;
         a.hf = h->fv_hf;
@@ -1191,14 +1228,14 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t
 }
 
 // far phase 1 of step n: slice (n + 1) mod 128 of window W = (n + 1) / 128 + 1 (one step ahead
-// of its phase 2), the groups of parity W mod 2 for the windows W and W + 1 (far1_mac); in
-// window 1, the first after priming, the other groups for window 1 alone
+// of its phase 2), the unit groups of class W mod K for the windows W .. W + K - 1 (far1_mac); in
+// the first windows after priming (W < K) the classes that have not started, for window W alone
 static void far1_args(const upols_t* h, int64_t n, slice_args& a)
 {
     const int64_t U = far_units(h), n1 = n + 1, st = n1 % kFarT, W = n1 / kFarT + 1;
+    const int K = far_group(h);
     a.f1wn = int(W);
-    far1_range(h, a, int(st * U / kFarT), int((st + 1) * U / kFarT), h->lv.nseg < 2 ? 0 : (W == 1 ? 2 : 1),
-               int(W & 1));
+    far1_range(h, a, int(st * U / kFarT), int((st + 1) * U / kFarT), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
 }
 
 // The launch of step n >= 0 (block t0 + n at ring row w): the block and slice n mod T of
@@ -1251,7 +1288,7 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
         a.f2nwg = u1 - u0;
         a.f2tw = ring_add(w, W * kFarT - n, R);
         a.f2wn = int(W);
-        a.f2pairs = lp.nseg >= 2 && W >= 2;
+        a.f2grp = far_group(h) > 1;
         a.f2ff = h->fv_ff + (W & 1) * C * kFarT * B;
         far1_args(h, n, a);
     }

@@ -41,8 +41,11 @@ def plan(P):
 class Sim:
     """float64 replay of the level pipeline for one channel of K bins."""
 
-    def __init__(self, H, lp, G=4):
+    def __init__(self, H, lp, G=4, Kw=None):
         self.H, self.lp, self.G = H, lp, G
+        ns = lp["nseg"]
+        # windows per phase-1 pass (upols_levels.hip far_group), or a forced value
+        self.Kw = Kw or (1 if ns < 2 else min(4, max(2, int(np.floor(np.sqrt(2.0 * (ns - 1)) + 0.5)))))
         self.P, self.K = H.shape
         self.R = self.P + 31
         if lp["nseg"]:
@@ -64,7 +67,7 @@ class Sim:
             self.HF = np.fft.fft(seg, axis=1)
             self.XF = np.zeros((ns, FN, self.K), complex)
             self.ff = np.zeros((2, FT, self.K), complex)
-            self.acc = np.zeros((2, FN, self.K), complex)
+            self.acc = np.zeros((self.Kw, FN, self.K), complex)
 
     def plain(self, x):
         """One plain step (all partitions from the ring); the levels re-prime after it."""
@@ -81,52 +84,60 @@ class Sim:
             rows = (tw + j - ps) % self.R
             self.slab[l][buf, j, k0:k1] = (self.H[a:b, k0:k1] * self.ring[rows, k0:k1]).sum(0)
 
-    def half(self, k):
-        """phase-1 pair parity of column k (the kernels: 16-column unit u, group u // 4)"""
-        return (k // self.G) & 1
+    def cls(self, k):
+        """phase-1 class of column k (the kernels: 16-column unit u, group u // 4, class mod K)"""
+        return (k // self.G) % self.Kw
 
-    def far1(self, wn, k0, k1, nfresh, mode=0, par=0):
+    def first(self, c):
+        """first window >= 1 whose phase-1 pass a class starts (far_first)"""
+        return 1 + ((c - 1) % self.Kw)
+
+    def far1(self, wn, k0, k1, nfresh, mode=0, cls=0):
         """phase 1: the stored segments' products into the partial sums of window wn; mode 1:
-        only the columns of parity par, each for windows wn AND wn + 1 (segments s >= 2 of
-        wn + 1 use the slots of s - 1 of wn); mode 2: those, and the others for wn alone"""
-        ns = self.lp["nseg"]
+        the columns of class cls, each for the windows wn .. wn + K - 1 (segments s >= j + 1 of
+        wn + j use the slots of s - j of wn); mode 2: those, and the classes that have not
+        started for wn alone"""
+        ns, K = self.lp["nseg"], self.Kw
         for k in range(k0, k1):
-            pair = mode != 0 and self.half(k) == par
-            if mode == 1 and not pair:
-                continue
-            acc = np.zeros(FN, complex)
-            for s in range(min(nfresh, ns), ns):
-                acc += self.XF[(wn - s - 1) % self.M, :, k] * self.HF[s, :, k]
-            self.acc[wn & 1, :, k] = acc
-            if pair:
-                acc2 = np.zeros(FN, complex)
-                for s in range(2, ns):
-                    acc2 += self.XF[(wn - s) % self.M, :, k] * self.HF[s, :, k]
-                self.acc[(wn + 1) & 1, :, k] = acc2
+            c = self.cls(k) if mode else 0
+            if mode and c != cls:
+                if self.first(c) <= wn:
+                    continue  # inside a group started earlier
+                nw = 1
+            else:
+                nw = K if mode else 1
+            for j in range(nw):
+                acc = np.zeros(FN, complex)
+                for s in range(max(min(nfresh, ns), j + 1), ns):
+                    acc += self.XF[(wn - (s - j) - 1) % self.M, :, k] * self.HF[s, :, k]
+                self.acc[(wn + j) % K, :, k] = acc
 
-    def far2(self, tw, wn, k0, k1, nfresh, pairs=False):
-        """phase 2: the fresh row pairs' transforms (stored to their slots) and products, segment
-        1 for the second window of a phase-1 pair, the inverse transform into the far field"""
-        acc = self.acc[wn & 1, :, k0:k1].copy()
-        for s in range(min(nfresh, self.lp["nseg"])):
+    def far2(self, tw, wn, k0, k1, nfresh, grp=False):
+        """phase 2: the fresh row pairs' transforms (stored to their slots) and products,
+        segments 1 .. j for window j of a phase-1 group, the inverse transform into the far field"""
+        ns, K = self.lp["nseg"], self.Kw
+        acc = self.acc[wn % K, :, k0:k1].copy()
+        for s in range(min(nfresh, ns)):
             slot = (wn - s - 1) % self.M
             rows = [(tw - (s + 3) * FT + i) % self.R for i in range(FN)]
             self.XF[slot, :, k0:k1] = np.fft.fft(self.ring[rows, k0:k1], axis=0)
             acc += self.XF[slot, :, k0:k1] * self.HF[s, :, k0:k1]
-        if pairs:
+        if grp:
             for k in range(k0, k1):
-                if self.half(k) != (wn & 1):
-                    acc[:, k - k0] += self.XF[(wn - 2) % self.M, :, k] * self.HF[1, :, k]
+                c = self.cls(k)
+                j = (wn - c) % K if wn >= self.first(c) else 0
+                for s in range(1, min(j, ns - 1) + 1):
+                    acc[:, k - k0] += self.XF[(wn - s - 1) % self.M, :, k] * self.HF[s, :, k]
         self.ff[wn & 1, :, k0:k1] = np.fft.ifft(acc, axis=0)[FT:]
 
     def far1_slice(self, n, w):
-        """phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1, paired"""
+        """phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1, in groups"""
         n1 = n + 1
         st, W = n1 % FT, n1 // FT + 1
         k0, k1 = st * self.K // FT, (st + 1) * self.K // FT
         if k1 > k0:
-            mode = 0 if self.lp["nseg"] < 2 else (2 if W == 1 else 1)
-            self.far1(W, k0, k1, 1, mode, W & 1)
+            K = self.Kw
+            self.far1(W, k0, k1, 1, 0 if K == 1 else (2 if W < K else 1), W % K)
 
     def roles(self, n, w):
         """the slice roles of step n (block at ring row w), as closures"""
@@ -143,7 +154,7 @@ class Sim:
             st, W = n % FT, n // FT + 1
             k0, k1 = st * K // FT, (st + 1) * K // FT
             if k1 > k0:
-                out.append(lambda: self.far2((w + W * FT - n) % R, W, k0, k1, 1, lp["nseg"] >= 2 and W >= 2))
+                out.append(lambda: self.far2((w + W * FT - n) % R, W, k0, k1, 1, self.Kw > 1))
             out.append(lambda: self.far1_slice(n, w))
         return out
 
@@ -230,6 +241,26 @@ def test_level_schedule_big_level(P):
     H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
     sim = Sim(H, lp)
     nb = 3 * P + 40
+    X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
+    worst = 0.0
+    for t in range(nb):
+        y = sim.plain(X[t]) if (t < 37 or nb // 2 <= t < nb // 2 + 3) else sim.step(X[t])
+        m = min(P, t + 1)
+        ref = (H[:m] * X[t - np.arange(m)]).sum(0)
+        worst = max(worst, float(np.abs(y - ref).max() / (np.abs(ref).max() + 1e-300)))
+    assert worst < 1e-12, worst
+
+
+@pytest.mark.parametrize("P,Kw", [(700, 2), (700, 4), (1100, 3), (1100, 4), (450, 3)])
+def test_level_schedule_window_groups(P, Kw):
+    """The far level's phase 1 over groups of Kw windows (far_group picks one per nseg; every
+    group size must give the same outputs), across re-priming."""
+    lp = plan(P)
+    rng = np.random.default_rng(P + Kw)
+    K = 32
+    H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
+    sim = Sim(H, lp, Kw=Kw)
+    nb = 2 * P + 700
     X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
     worst = 0.0
     for t in range(nb):
