@@ -783,9 +783,7 @@ constexpr int kFarKMax = 4;
 // priming: one window per pass)
 __host__ __device__ __forceinline__ int far_first(int c, int K) { return 1 + ((c - 1) % K + K) % K; }
 
-// K windows in this pass; KM the handle's window-group size (partial-sum slots) at compile
-// time, 0: sa.fK
-template<int FPL, int K, int KM>
+template<int FPL, int K>
 __device__ __forceinline__ void far1_mac(const slice_args& sa, int u, int f0, int col)
 {
     constexpr int NS = 16 / FPL;  // segments per round
@@ -841,13 +839,13 @@ __device__ __forceinline__ void far1_mac(const slice_args& sa, int u, int f0, in
     }
 #pragma unroll
     for (int w = 0; w < K; ++w) {
-        cf* o = sa.f1acc + (int64_t(((wn + w) % (KM ? KM : sa.fK)) * sa.fU + u) * kFN + f0) * 16 + col;
+        cf* o = sa.f1acc + (int64_t(((wn + w) % sa.fK) * sa.fU + u) * kFN + f0) * 16 + col;
 #pragma unroll
         for (int j = 0; j < FPL; ++j) o[4 * j * 16] = cf{acc[w][j].x, acc[w][j].y};
     }
 }
 
-template<int FPL, int KF>
+template<int FPL>
 __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
 {
     constexpr int FR = 4 * FPL, PPG = kFN / FR;  // f rows per workgroup, workgroups per group
@@ -857,23 +855,18 @@ __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
     const int u = g4 * kF1UG + (cl >> 4);    // the lane's unit
     if (u < sa.f1u0 || u >= sa.f1u1) return;  // groups straddle slices (no barriers in this role)
     const int f0 = part * FR + fq;            // f = f0 + 4 j
-    const int K = KF ? KF : sa.fK, cls = sa.f1mode ? g4 % K : 0;
+    const int K = sa.fK, cls = sa.f1mode ? g4 % K : 0;
     if (sa.f1mode == 0 || (cls != sa.f1cls && far_first(cls, K) > sa.f1wn)) {
-        far1_mac<FPL, 1, KF>(sa, u, f0, cl & 15);  // one window (priming, or the class has not started)
+        far1_mac<FPL, 1>(sa, u, f0, cl & 15);  // one window (priming, or the class has not started)
     } else if (cls == sa.f1cls) {
-        if constexpr (KF == 2) {
-            far1_mac<FPL, 2, 2>(sa, u, f0, cl & 15);
-        } else {
-            if (K == 3) far1_mac<FPL, 3, KF>(sa, u, f0, cl & 15);
-            else far1_mac<FPL, kFarKMax, KF>(sa, u, f0, cl & 15);
-        }
+        if (K == 2) far1_mac<FPL, 2>(sa, u, f0, cl & 15);
+        else if (K == 3) far1_mac<FPL, 3>(sa, u, f0, cl & 15);
+        else far1_mac<FPL, kFarKMax>(sa, u, f0, cl & 15);
     }
 }
 
-template<int KF>
 __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
 {
-    const int KW = KF ? KF : sa.fK;  // window-group size
     cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
     cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
     cf* tws = z + kFN;                       // twiddles
@@ -896,7 +889,7 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
     // segment is fresh) so that it is not live across a transform
     cf v[16];
     const __amdgpu_buffer_rsrc_t ares =
-        buf_rsrc(sa.f2acc + int64_t((sa.f2wn % KW) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
+        buf_rsrc(sa.f2acc + int64_t((sa.f2wn % sa.fK) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
     const int ao = (a * 16 + cp) * int(sizeof(cf)), as = 16 * 16 * int(sizeof(cf));  // f = a + 16 i
     for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
         // fresh row pair: rows tw - (s + 3) 128 + a + 16 n (the ring holds >= kFarRing > 256
@@ -932,7 +925,7 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
     if (sa.f2grp) {  // uniform per workgroup
         // window j of this unit's phase-1 group: segments 1 .. j (slots f2wn - 2 .. f2wn - j - 1,
         // stored by the group's earlier windows' phase 2) were not there when the pass ran
-        const int K = KW, cls = (u / kF1UG) % K, first = far_first(cls, K);
+        const int K = sa.fK, cls = (u / kF1UG) % K, first = far_first(cls, K);
         const int jw = sa.f2wn >= first ? (sa.f2wn - cls) % K : 0;
         for (int s1 = 1; s1 <= jw && s1 < nseg; ++s1) {
             cf hv[16], xv[16];
@@ -1000,15 +993,13 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
 #ifndef NEO_STEP_WPE
 #define NEO_STEP_WPE 3  // waves per SIMD the step kernel is compiled for (VGPR budget)
 #endif
-// KF: the far level's window-group size at compile time (2, pairs: the code every shape below
-// kFarGroupUnits runs), or 0: sa.fK (far_group)
-template<int B, bool OLA, int KF>
+template<int B, bool OLA>
 __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(NEO_STEP_WPE))) void k_lvl_step(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
     int bid = int(blockIdx.x);
     if (bid < a.f2nwg) {
-        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2_role<KF>(a, bid, smem);
+        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2_role(a, bid, smem);
         return;
     }
     bid -= a.f2nwg;
@@ -1023,9 +1014,9 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
         toep_level<1>(a, bid, smem) || toep_level<0>(a, bid, smem))
         return;
     if (bid < a.f1nwg && (NEO_ROLES & 8)) {
-        if (a.f1fpl == 4) far1_role<4, KF>(a, bid);
-        else if (a.f1fpl == 2) far1_role<2, KF>(a, bid);
-        else far1_role<1, KF>(a, bid);
+        if (a.f1fpl == 4) far1_role<4>(a, bid);
+        else if (a.f1fpl == 2) far1_role<2>(a, bid);
+        else far1_role<1>(a, bid);
     }
 }
 
@@ -1150,7 +1141,7 @@ static int lvl_buffers(upols_t* h)
         if (!alloc(reinterpret_cast<void**>(&h->fv_xf), spec)) return undo("far FDL spectra", spec);
         if (!alloc(reinterpret_cast<void**>(&h->fv_ff), ffb)) return undo("far field", ffb);
         if (!alloc(reinterpret_cast<void**>(&h->fv_tw), kFN * sizeof(cf))) return undo("far twiddles", kFN * sizeof(cf));
-        const size_t accb = size_t(std::max(2, far_group(h))) * size_t(far_units(h)) * kFN * 16 * sizeof(cf);  // phase 1 -> 2
+        const size_t accb = size_t(far_group(h)) * size_t(far_units(h)) * kFN * 16 * sizeof(cf);  // phase 1 -> 2
         if (!alloc(reinterpret_cast<void**>(&h->fv_acc), accb)) return undo("far partial sums", accb);
         const auto t = make_twiddle_table(kFN);
         if (hipMemcpy(h->fv_tw, t.data(), kFN * sizeof(cf), hipMemcpyHostToDevice) != hipSuccess)
@@ -1225,22 +1216,12 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t
         return t;
     }();
     if (!grid) return NEO_HIP_OK;
-    if (far_group(h) <= 2) {  // pairs (or no far level / one segment): compile-time K = 2
-        if (h->ola) {
-            NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, true, 2>), dim3(grid),
-                                                                                 dim3(lstep_cfg<BB>::WG), 0, s, a))
-        } else {
-            NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, false, 2>), dim3(grid),
-                                                                                 dim3(lstep_cfg<BB>::WG), 0, s, a))
-        }
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, true>), dim3(grid),
+                                                                             dim3(lstep_cfg<BB>::WG), 0, s, a))
     } else {
-        if (h->ola) {
-            NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, true, 0>), dim3(grid),
-                                                                                 dim3(lstep_cfg<BB>::WG), 0, s, a))
-        } else {
-            NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, false, 0>), dim3(grid),
-                                                                                 dim3(lstep_cfg<BB>::WG), 0, s, a))
-        }
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, false>), dim3(grid),
+                                                                             dim3(lstep_cfg<BB>::WG), 0, s, a))
     }
     NEO_HIP_LAUNCH_CHECK();
     return NEO_HIP_OK;
