@@ -3,25 +3,31 @@
 
 Headline (BASELINE.json metric "Msamples/sec UPOLS convolver (block=512,
 IR=10s@48k); achieved HBM GB/s"): configs[4], the 2048-channel UPOLS, B = 512,
-L = 480000 taps (P = 938). The whole configuration fits one MI355X (~45 GB of filter,
-FDL and level buffers of 288 GB), so at N = 1 the workload is all 2048 channels on one
-GPU (`--workload c5full`, the default); at N GPUs, N x 2048 channels, 2048 per GPU
-(weak scaling; the channels are independent, so there is no collective on the data path
-— torch.distributed (gloo) only carries the timing barrier and the max-over-ranks).
-`--workload c5` is the 256-channel per-GPU shard of configs[4] split over 8 GPUs.
+L = 480000 taps (P = 938), channel-sharded across the GPUs of one node. `--workload c5full`
+(the default) is that configuration: 2048 channels IN ALL, rank r of N owning the
+contiguous channel range shard(2048, N, r) — at N = 1 all 2048 on one GPU (the whole
+configuration fits one MI355X: ~60 GB of filter, FDL and level buffers of 288 GB), at
+N = 8 exactly the 256-channel shard per GPU (`scaling` "strong"). The channels are
+independent, so there is no collective on the data path — torch.distributed (gloo) only
+carries the timing barrier and the max over ranks. For N > 1 a secondary `weak` object
+also times 2048 channels per GPU (N x 2048 in all). `--workload c5` is one GPU's
+256-channel shard of the 8-GPU split on its own.
 
-A "step" = one block of B samples through the whole convolver for every channel,
-inputs already resident in HBM, one block per call as a real-time caller runs it
-(block t + 1 is not given to the convolver before block t's output is complete). The
-convolver's default streaming form is the level pipeline (upols_levels.hip): every step
-runs the block step (window r2c, FDL insert, the 15 newest partitions, c2r) plus 1/T of
-the next window of each partition level, so every step does the same work and the line
-is the same at any --steps. `roofline` holds every part of the step (block step,
-Toeplitz level slices, far slice) with its HIP-event time, algorithmic bytes and share of
-the step; its top-level fields are the dominant part's. `latency` is the per-step time
-distribution, `parity` the last timed blocks against the oracle, `per_block_step` the
-plain one-pass-per-block step and `offline` the batched form (blocks up front), both
-timed in the same run; `c2_fft` the 4096 x 65536 batched FFT.
+A "step" = one block of B samples through the whole convolver for every channel, inputs
+already resident in HBM, one call per block. The timed region enqueues the K calls on the
+convolver's stream and synchronizes once at the end (the GPU runs the blocks in stream
+order, each step's kernel after the previous one's); `latency.host_roundtrip_*` is the
+real-time caller's view instead: one call per block and a host wait for that block's output
+before the next call. The convolver's default streaming form is the level pipeline
+(upols_levels.hip): every step runs the block step (window r2c, FDL insert, the 8 newest
+partitions, c2r) plus 1/T of the next window of each partition level, so every step does
+the same work and the line is the same at any --steps. `roofline` holds the step kernel with
+its HIP-event time, algorithmic bytes by role and PMC traffic. `latency` is the per-step GPU
+time distribution plus the host round trip, `parity` the last timed blocks against the
+oracle, `per_block_step` the plain one-pass-per-block step, `offline` the batched form
+(blocks up front), `host_io` the host-buffer boundary (neo_hip_upols_process: the block in
+host memory, PCIe-inclusive, one synchronous call per block), all timed in the same run;
+`c2_fft` the 4096 x 65536 batched FFT.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5full|c5|c4|c3|c2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -46,12 +52,24 @@ PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 vector (packed FMA) peak, 256 CU x 4 SIM
 WARM_SECONDS = 0.25
 
 WORKLOADS = {
-    # name: (channels per GPU, block, taps)
-    "c5full": (2048, 512, 480000),  # headline: the metric's whole 2048-channel configuration per GPU
+    # name: (channels, block, taps); c5full's 2048 are split over the ranks (strong scaling),
+    # the others run per GPU (weak scaling)
+    "c5full": (2048, 512, 480000),  # headline: configs[4], 2048 channels sharded over the GPUs
     "c5": (256, 512, 480000),  # one GPU's shard of 2048 ch / 8 GPUs, B=512, IR 10 s @ 48 kHz
     "c4": (256, 256, 480000),  # 256 ch, B=256, IR 10 s @ 48 kHz
     "c3": (1, 512, 96000),     # 1 ch, B=512, IR 2 s @ 48 kHz
 }
+STRONG = {"c5full"}  # workloads whose channel count is the whole job's, split over the ranks
+
+
+def cpu_threads() -> int:
+    """Host threads this process may use: its CPU affinity mask (the box's CPU share), at
+    most 16 (the pool's per-GPU share; os.cpu_count() reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def parse():
@@ -65,7 +83,9 @@ def parse():
     ap.add_argument("--no-offline", action="store_true", help="skip the batched (blocks up front) line")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed output")
     ap.add_argument("--no-fft", action="store_true", help="skip the c2_fft sub-object of UPOLS runs")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the affinity mask's CPUs, at most 16")
+    ap.add_argument("--no-host-io", action="store_true", help="skip the host_io sub-object")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the secondary weak-scaling object")
     ap.add_argument("--host-io", action="store_true",
                     help="time the host-buffer boundary (neo_hip_upols_process on pinned-staged host memory): "
                          "PCIe-inclusive, reported for DESIGN.md, never the headline value")
@@ -315,12 +335,63 @@ def spin_wait(local: int) -> None:
     hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
 
 
+def rank_channels(workload: str, world: int, rank: int, strong: bool = None):
+    """(channels of this rank, channels of the whole job): a strong workload's channels are
+    split over the ranks (shard), the others are per GPU."""
+    C, _, _ = WORKLOADS[workload]
+    if strong is None:
+        strong = workload in STRONG
+    if strong:
+        lo, hi = shard(C, world, rank)
+        return hi - lo, C
+    return C, C * world
+
+
+def host_io_times(conv, C, B, nblocks, kind, seed=0):
+    """One synchronous neo_hip_upols_process call per block on a host buffer [C][B] (the
+    plugin's processFrame pattern, DenseConvolution.cpp:62-74): kind "pageable" (numpy, the
+    handle's mapped staging) or "pinned" (page-locked torch tensor, read and written in place
+    by the step kernel). The caller's write of the next block into the buffer is not timed.
+    Returns per-call seconds."""
+    import numpy as np
+    import torch
+
+    src = np.random.default_rng(seed).random((C, B), dtype=np.float32) * 2 - 1
+    if kind == "pinned":
+        buf = torch.empty((C, B), dtype=torch.float32).pin_memory()
+        arr = buf.numpy()
+    else:
+        arr = np.empty((C, B), np.float32)
+        buf = arr
+    t_warm = time.perf_counter()
+    while time.perf_counter() - t_warm < WARM_SECONDS:
+        arr[:] = src
+        conv(buf)
+    dt = []
+    for _ in range(nblocks):
+        arr[:] = src
+        t0 = time.perf_counter()
+        conv(buf)
+        dt.append(time.perf_counter() - t0)
+    return dt
+
+
+def host_io_summary(dt, C, B):
+    import numpy as np
+
+    a = np.array(dt)
+    return {"msamples_s": C * B / a.mean() / 1e6, "mean_us": float(a.mean() * 1e6),
+            "p50_us": float(np.percentile(a, 50) * 1e6), "p99_us": float(np.percentile(a, 99) * 1e6),
+            "max_us": float(a.max() * 1e6), "blocks": int(a.size), "pcie_bytes_per_block": 2 * 4 * C * B}
+
+
 def run_upols(args, world, rank, local):
     import numpy as np
     import torch
     import neo
 
-    C, B, L = WORKLOADS[args.workload]
+    _, B, L = WORKLOADS[args.workload]
+    C, C_total = rank_channels(args.workload, world, rank)
     local = device_for(local)
     spin_wait(local)
     dev = torch.device("cuda", local)
@@ -329,6 +400,7 @@ def run_upols(args, world, rank, local):
     conv = neo.UpolsConvolver(C, B, P, device=local)
     conv.set_batch(False)  # streaming: one block per step, as a real-time caller runs it
     levels = conv.ahead_info()[0] and not args.no_ahead
+    conv_far_group = conv.far_group()
     plan = neo.convolution.level_plan(P)
     g = torch.Generator(device=dev).manual_seed(8 + rank)
     ir = torch.rand((C, L), generator=g, device=dev).mul_(2).sub_(1)  # synthetic white-noise IR
@@ -389,7 +461,7 @@ def run_upols(args, world, rank, local):
         det = [(ms / n if n else None) for ms, n in conv.timing_detail()]
         return [max_over_ranks(d, world) if d is not None else None for d in det]
 
-    samples = world * C * B * args.steps
+    samples = C_total * B * args.steps  # all ranks
     # the plain single-block step: one pass over filter + FDL per block (k_upols_step)
     conv.set_ahead(False)
     warm()
@@ -417,6 +489,18 @@ def run_upols(args, world, rank, local):
                   "what": "last 4 blocks of the timed region vs oracle dense_convolve over their input history "
                           "(peak-normalized; bar 1e-5)"}
     det = instrumented()
+    # the real-time caller's round trip: one call per block, the host waits for that block's
+    # output (stream sync, spinning) before the next call
+    rt = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        feed.run(1)
+        sobj.synchronize()
+        rt.append(time.perf_counter() - t0)
+    rt = np.array(rt)
+    rt_p50 = max_over_ranks(float(np.percentile(rt, 50)) * 1e6, world)
+    rt_p99 = max_over_ranks(float(np.percentile(rt, 99)) * 1e6, world)
+    rt_mean = max_over_ranks(float(rt.mean()) * 1e6, world)
     # per-step latency: every step of a separate 256-step run bracketed by events (GPU time of the
     # step, first to last event), the distribution a per-block real-time caller sees
     conv.step_times()
@@ -428,7 +512,11 @@ def run_upols(args, world, rank, local):
     latency = {"steps": int(st.size), "mean_ms": float(st.mean()), "p50_ms": float(np.percentile(st, 50)),
                "p99_ms": float(np.percentile(st, 99)), "max_ms": float(st.max()),
                "max_over_mean": float(st.max() / st.mean()),
-               "note": "GPU time per step (HIP events around every step, which add their own records)"}
+               "host_roundtrip_p50_us": rt_p50, "host_roundtrip_p99_us": rt_p99, "host_roundtrip_mean_us": rt_mean,
+               "host_roundtrip_msamples_s": C_total * B / rt_mean,
+               "note": "p50/p99/max: GPU time per step (HIP events around every step, which add their own records); "
+                       "host_roundtrip: 200 device-resident single-block calls, each followed by a host wait for its "
+                       "output before the next call (max over ranks)"}
 
     if levels:
         roles = algorithmic_bytes(C, B, P, plan)
@@ -459,7 +547,30 @@ def run_upols(args, world, rank, local):
                 "frac": gbs_plain / PEAK_HBM_GBS, "traffic": plain["traffic"], "kernel": plain["kernel"],
                 "kernel_avg_ms": det_plain[0], "steps_per_launch": 1, "algorithmic_bytes_per_launch": bytes_plain,
                 "d2d_copy_gbs": copy_ceiling_gbs(dev)}
-    offline = run_upols_offline(args, conv, C, B, P, x, y, nx * B, stream, world)
+    offline = run_upols_offline(args, conv, C, B, P, x, y, nx * B, stream, world, C_total)
+    host_io = None
+    if not args.no_host_io:
+        conv.set_batch(False)
+        host_io = {"note": "neo_hip_upols_process on a host buffer, one synchronous call per block through the "
+                           "Python binding (PCIe-inclusive; never the headline value)"}
+        for kind in ("pinned", "pageable"):
+            host_io[f"{args.workload}_{kind}"] = host_io_summary(host_io_times(conv, C, B, 200, kind), C, B)
+    del x, y, feed
+    if host_io is not None and args.workload == "c5full" and world == 1:
+        # the 8-GPU split's per-GPU shard (256 channels) as its own handle
+        cs = WORKLOADS["c5"][0]
+        c5 = neo.UpolsConvolver(cs, B, P, device=local)
+        g5 = torch.Generator(device=dev).manual_seed(99)
+        c5.set_impulse(torch.rand((cs, L), generator=g5, device=dev).mul_(2).sub_(1), normalize=True)
+        c5.set_batch(False)
+        for kind in ("pinned", "pageable"):
+            host_io[f"c5_{kind}"] = host_io_summary(host_io_times(c5, cs, B, 200, kind), cs, B)
+        c5.close()
+    weak = None
+    if world > 1 and args.workload in STRONG and not args.no_weak:
+        conv.close()
+        del conv
+        weak = run_weak(args, world, rank, local, B, L)
     res = {
         "metric": "Msamples/sec UPOLS convolver (block=512, IR=10s@48k); achieved HBM GB/s",
         "value": samples / elapsed / 1e6,
@@ -471,13 +582,15 @@ def run_upols(args, world, rank, local):
         "gpu_ms_per_step": gpu_ms.get("levels" if levels else "plain"),  # HIP events around the same steps
         "host_launch_ms": gpu_ms.get(("levels" if levels else "plain") + "_host_launch_ms"),  # t0 -> all steps enqueued
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.workload in STRONG else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (U[-1,1) white-noise input and IR, torch.rand on device)",
-        "config": {"workload": f"UPOLS {args.workload}: {C} ch/GPU x {world} GPU, B={B}, L={L} taps (P={P}), "
-                               f"channel-sharded, one block per step",
-                   "channels_per_gpu": C, "channels_total": C * world, "block": B, "taps": L, "partitions": P,
+        "config": {"workload": f"UPOLS {args.workload}: {C_total} channels in all, {C} on rank 0 of {world} GPU(s) "
+                               f"({'split over the ranks' if args.workload in STRONG else 'per GPU'}), B={B}, "
+                               f"L={L} taps (P={P}), one block per step",
+                   "channels_per_gpu": C, "channels_total": C_total, "block": B, "taps": L, "partitions": P,
+                   "far_group": conv_far_group,
                    "streaming": ("levels: block step p<%d, Toeplitz %s, far %d segments" %
                                  (plan["a0"], list(zip(plan["T"], plan["a"], plan["b"])), plan["nseg"])
                                  if levels else "plain step"),
@@ -487,13 +600,16 @@ def run_upols(args, world, rank, local):
         "parity": parity,
         "per_block_step": plain,
         "offline": offline,
+        "host_io": host_io,
     }
+    if weak is not None:
+        res["weak"] = weak
     if args.workload == "c3":
         res["roofline"]["note"] = "working set L2/MALL-resident: effective GB/s, launch-latency bound"
     return res
 
 
-def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world):
+def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world, C_total):
     """Same convolver and input, blocks available up front (dense_convolve / process_blocks):
     T blocks share one pass over the filter and the FDL. Not the headline (which is the
     real-time one-block-per-pass step); reported beside it. 128 blocks per timed run."""
@@ -526,11 +642,48 @@ def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world):
     bytes_pass = C * 16 * P * B  # filter + FDL streamed once per pass of T blocks
     gbs = bytes_pass / (mac_avg_ms * 1e-3) / 1e9
     traffic = load_pmc_traffic(args.workload + "_offline", "k_batch_mac")
-    return {"value": world * C * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": T,
+    return {"value": C_total * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": T,
             "traffic": traffic, "traffic_over_algorithmic": traffic / bytes_pass if traffic else None,
             "ms_per_block": elapsed * 1e3 / nb, "splits": splits, "kernel": f"k_batch_mac<{B},{T},1>",
             "algorithmic_bytes_per_launch": bytes_pass, "kernel_avg_ms": mac_avg_ms,
             "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS}
+
+
+def run_weak(args, world, rank, local, B, L):
+    """The secondary weak-scaling line: 2048 channels per GPU (N x 2048 in all), the same
+    streaming steps, timed like the headline (barrier + sync around args.steps calls)."""
+    import torch
+    import neo
+
+    C = WORKLOADS[args.workload][0]
+    dev = torch.device("cuda", local)
+    P = neo.num_partitions(L, B)
+    conv = neo.UpolsConvolver(C, B, P, device=local)
+    conv.set_batch(False)
+    g = torch.Generator(device=dev).manual_seed(18 + rank)
+    conv.set_impulse(torch.rand((C, L), generator=g, device=dev).mul_(2).sub_(1), normalize=True)
+    nx = 64
+    x = torch.rand((C, nx * B), generator=g, device=dev).mul_(2).sub_(1)
+    sobj = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    feed = Feed(conv, x, x, nx, B, sobj.cuda_stream)
+    t_warm = time.perf_counter()
+    feed.run(max(args.warmup, 1))
+    torch.cuda.synchronize()
+    while time.perf_counter() - t_warm < WARM_SECONDS:
+        feed.run(64)
+        torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    feed.run(args.steps)
+    torch.cuda.synchronize()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world)
+    conv.close()
+    return {"value": world * C * B * args.steps / el / 1e6, "unit": "Msamples/s", "scaling": "weak",
+            "ms_per_step": el * 1e3 / args.steps, "channels_per_gpu": C, "channels_total": C * world,
+            "note": "secondary: 2048 channels per GPU (not a BASELINE config), the headline's streaming step"}
 
 
 def run_upols_host_io(args, world, rank, local):
@@ -540,27 +693,27 @@ def run_upols_host_io(args, world, rank, local):
     import torch
     import neo
 
-    C, B, L = WORKLOADS[args.workload]
+    _, B, L = WORKLOADS[args.workload]
+    C, C_total = rank_channels(args.workload, world, rank)
     local = device_for(local)
+    spin_wait(local)
     torch.cuda.set_device(local)
     P = neo.num_partitions(L, B)
     conv = neo.UpolsConvolver(C, B, P, device=local)
     g = torch.Generator(device="cuda").manual_seed(8 + rank)
     conv.set_impulse(torch.rand((C, L), generator=g, device="cuda").mul_(2).sub_(1), normalize=True)
-    block = (np.random.default_rng(rank).random((C, B), dtype=np.float32) * 2 - 1)
-    t_warm = time.perf_counter()
-    while time.perf_counter() - t_warm < WARM_SECONDS:
-        conv(block)
-    barrier(world)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        conv(block)
-    barrier(world)
-    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    out = {}
+    for kind in ("pinned", "pageable"):
+        barrier(world)
+        dt = host_io_times(conv, C, B, args.steps, kind, seed=rank)
+        barrier(world)
+        out[kind] = host_io_summary(dt, C, B)
+    el = max_over_ranks(sum(host_io_times(conv, C, B, args.steps, "pinned", seed=rank)), world)
     return {"metric": "Msamples/sec UPOLS convolver, host buffers (PCIe-inclusive, not the headline)",
-            "value": world * C * B * args.steps / elapsed / 1e6, "unit": "Msamples/s", "n_gpus": world,
-            "steps": args.steps, "ms_per_step": elapsed * 1e3 / args.steps,
-            "config": {"workload": f"UPOLS {args.workload} host io", "bytes_per_step_pcie": 2 * 4 * C * B}}
+            "value": C_total * B * args.steps / el / 1e6, "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "ms_per_step": el * 1e3 / args.steps, "host_io": out,
+            "config": {"workload": f"UPOLS {args.workload} host io (pinned buffer; pageable in host_io)",
+                       "bytes_per_step_pcie": 2 * 4 * C * B}}
 
 
 def run_fft(args, world, rank, local):
@@ -618,6 +771,8 @@ def run_fft(args, world, rank, local):
 
 def main():
     args = parse()
+    if args.cpu_threads <= 0:
+        args.cpu_threads = cpu_threads()
     world, rank, local = dist_setup(args)
     if args.workload == "c2":
         res = run_fft(args, world, rank, local)

@@ -56,6 +56,11 @@ typedef struct neo_hip_upols neo_hip_upols;
 NEO_HIP_API const char* neo_hip_last_error(void);
 NEO_HIP_API int neo_hip_version(void);
 NEO_HIP_API int neo_hip_device_count(int* count);
+/* Page-lock a caller-owned host range [p, p + bytes) and map it for every device, so that
+ * host-memory entry points (neo_hip_upols_process) read and write it in place over PCIe
+ * instead of staging it. The caller keeps the range alive until neo_hip_host_unregister(p). */
+NEO_HIP_API int neo_hip_host_register(void* p, int64_t bytes);
+NEO_HIP_API int neo_hip_host_unregister(void* p);
 
 /* -- FFT plans ------------------------------------------------------------
  * Replaces fft_plan<complex<float>> = c2c_dit2_plan (src/neo/fft/fft.hpp:36-52,
@@ -105,6 +110,8 @@ typedef struct neo_hip_upols_opts {
     int levels;           /* single-block steps: -1 auto (streaming levels from 64 partitions), 0 plain step, 1 levels */
     int far_level;        /* streaming levels, partitions >= 256: -1 auto (= 1), 0 a 128-block Toeplitz level (more
                              VALU / LDS work, fewer bytes), 1 the 128-block partition-axis transform level */
+    int far_group;        /* far transform level: 0 auto, else 1..4 windows per phase-1 pass over the stored
+                             segment spectra (auto: 2, or round(sqrt(2 (nseg - 1))) from 32768 16-column units) */
 } neo_hip_upols_opts;
 NEO_HIP_API int neo_hip_upols_create_ex(int channels, int block, int partitions, int device, int method,
                                         const neo_hip_upols_opts* opts, neo_hip_upols** h);
@@ -115,9 +122,11 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
 /* normalize_impulse + uniform_partition of ir [C][L] float straight into the
  * convolver (setup path, DenseConvolution.cpp:78-108); host or device memory. */
 NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int64_t length, int normalize, int is_device);
-/* one block for all channels, in place: io [C][B] float. Host memory: staged
- * through pinned buffers, synchronous (own stream if `stream` is NULL). Device
- * memory: same as process_device on `stream`. */
+/* one block for all channels, in place: io [C][B] float. Host memory, synchronous (own
+ * stream if `stream` is NULL): the step kernel reads and writes the block over PCIe
+ * itself -- in place if io is page-locked (neo_hip_host_register / hipHostMalloc), else
+ * through the handle's mapped pinned staging (one memcpy each way) -- and the call waits by
+ * polling the stream. Device memory: same as process_device on `stream`. */
 NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_device, void* stream);
 /* one block, device pointers, channel c at in + c*ld_in / out + c*ld_out
  * (in == out allowed); asynchronous on `stream` (NULL = HIP null stream). */
@@ -162,14 +171,20 @@ NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* pha
  * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries); the automatic
  * choice of far_level. */
 NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, int* T, int* a, int* b, int* nseg);
+/* windows per far phase-1 pass the handle runs (neo_hip_upols_opts.far_group or the automatic
+ * choice); 0 without a far transform level */
+NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* windows);
 /* -- Multichannel convolver over several devices ------------------------------
  * C channels cut into n contiguous shards, shard i = channels [C i / n, C (i + 1) / n) on
  * devices[i] (a device may repeat), each a neo_hip_upols handle of its own (own stream).
  * The reference steps all channels of a plugin instance in one loop
  * (extra/plugin/src/dsp/DenseConvolution.hpp:35,50-67); channels never interact, so there is
  * no collective: every call below fans out to the shards concurrently (one host thread per
- * shard) and returns when all are done. Shard results are bit for bit those of one handle
- * over all channels. method / opts as neo_hip_upols_create_ex. */
+ * shard) and returns when all are done. Shard results equal those of one handle over all
+ * channels within float summation order: the shape-based code-path choices (far window
+ * group, Toeplitz window parts, fused step, splits) follow each shard's own channel count;
+ * they are bit for bit equal where those choices coincide (the same opts force them).
+ * method / opts as neo_hip_upols_create_ex. */
 typedef struct neo_hip_upols_multi neo_hip_upols_multi;
 NEO_HIP_API int neo_hip_upols_multi_create(int channels, int block, int partitions, const int* devices, int ndevices,
                                            int method, const neo_hip_upols_opts* opts, neo_hip_upols_multi** m);

@@ -113,4 +113,28 @@ inline std::vector<C> make_split_table(int order, int lo_bits)
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// The device address of page-locked host memory (hipHostMalloc, hipHostRegister with the
+// mapped flag, neo_hip_host_register), or nullptr for pageable memory (not an error).
+inline float* host_mapped(void* p)
+{
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: not sticky for later launch checks
+        return nullptr;
+    }
+    return at.type == hipMemoryTypeHost ? static_cast<float*>(at.devicePointer) : nullptr;
+}
+
+// Wait for a stream by polling (a real-time caller's block deadline: no yield to the OS
+// scheduler, whose wake-up adds tens of microseconds per block).
+inline int spin_sync(hipStream_t s)
+{
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return NEO_HIP_OK;
+        if (e != hipErrorNotReady)
+            return fail(NEO_HIP_ERUNTIME, "hipStreamQuery: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
+    }
+}
+
 }  // namespace neo_hip

@@ -27,4 +27,18 @@ NEO_HIP_API int neo_hip_device_count(int* count)
     return NEO_HIP_OK;
 }
 
+NEO_HIP_API int neo_hip_host_register(void* p, int64_t bytes)
+{
+    if (!p || bytes <= 0) return neo_hip::fail(NEO_HIP_EINVAL, "null pointer or empty range");
+    NEO_HIP_CHECK(hipHostRegister(p, size_t(bytes), hipHostRegisterMapped | hipHostRegisterPortable));
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_host_unregister(void* p)
+{
+    if (!p) return neo_hip::fail(NEO_HIP_EINVAL, "null pointer");
+    NEO_HIP_CHECK(hipHostUnregister(p));
+    return NEO_HIP_OK;
+}
+
 }  // extern "C"

@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <utility>
 #include <vector>
@@ -400,8 +401,7 @@ void destroy(upols_t* h)
     (void)hipFree(h->window);
     (void)hipFree(h->tmp);
     (void)hipFree(h->tw);
-    (void)hipFree(h->io);
-    if (h->io_host) (void)hipHostFree(h->io_host);
+    if (h->io_host) (void)hipHostFree(h->io_host);  // h->io is its device mapping
     (void)hipFree(h->samples_dev);
     (void)hipFree(h->part_b);
     (void)hipFree(h->tail);
@@ -485,6 +485,12 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
                                (long long)n, B);
         if (!a16) return fail(NEO_HIP_EINVAL, "device I/O must be 16-byte aligned (ld multiple of 4)");
     }
+    // Streaming levels: a batched pass leaves them to re-prime at the next single-block step
+    // (window 0 of every level computed whole, 2 x 128 far launches), so with the levels on
+    // only whole T-block batches run (the rest stream, one prime per call at most), and a
+    // call of fewer than kStreamKeep batches' blocks on primed levels streams them all.
+    constexpr int kStreamKeep = 4;
+    const bool stream_all = h->ahead && h->lv_n >= 0 && n < int64_t(kStreamKeep) * T * B;
     int64_t done = 0;
     while (done < n) {
         const float* ip = in + done;
@@ -492,7 +498,8 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
         int rc;
         // the largest power-of-two batch (<= T) of whole blocks left, one pass over H + FDL
         int tb = 1;
-        while (tb * 2 <= T && n - done >= int64_t(tb) * 2 * B) tb *= 2;
+        while (!stream_all && tb * 2 <= T && n - done >= int64_t(tb) * 2 * B) tb *= 2;
+        if (h->ahead && tb < T) tb = 1;
         if (h->in_pos == 0 && tb > 1 && a16 && done % 4 == 0) {
             rc = launch_batch(h, ip, ld_in, op, ld_out, tb, s);
             done += int64_t(tb) * B;
@@ -521,11 +528,11 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
                      const neo_hip_upols_opts* opt, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
-    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1};
+    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0};
     if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.far_level < -1 || o.far_level > 1 ||
         o.split_workgroups < 0 ||
         (o.batch_blocks && (o.batch_blocks < 2 || o.batch_blocks > kMaxBatch || (o.batch_blocks & (o.batch_blocks - 1)))) ||
-        o.batch_bins < 0 || o.batch_bins > 2)
+        o.batch_bins < 0 || o.batch_bins > 2 || o.far_group < 0 || o.far_group > 4)
         return fail(NEO_HIP_EINVAL, "invalid convolver options");
     *out = nullptr;
     if (channels < 1) return fail(NEO_HIP_EINVAL, "channels must be >= 1");
@@ -540,6 +547,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->P = partitions;
     h->ring = partitions + kMaxBatch - 1;
     plan_levels(partitions, h->lv, o.far_level);
+    h->far_k = o.far_group;
     if (h->lv.nseg) h->ring = std::max(h->ring, kFarRing);  // far slices read 383 blocks back
     h->ola = ola || v2;
     h->v2 = v2;
@@ -748,17 +756,25 @@ NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_dev
     if (g.rc) return g.rc;
     hipStream_t s = stream ? as_stream(stream) : h->stream;  // host I/O: own stream unless given
     const size_t bytes = size_t(h->C) * h->B * sizeof(float);
-    if (!h->io) {
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->io), bytes));
-        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->io_host), bytes, hipHostMallocDefault));
+    // Host buffers (the plugin's processFrame pattern, DenseConvolution.cpp:62-74): the step
+    // kernel reads the block from host memory and writes the output back itself over PCIe
+    // (zero-copy, no DMA launches). Page-locked memory (neo_hip_host_register, hipHostMalloc)
+    // is used in place; any other buffer goes through the handle's mapped pinned staging.
+    float* dio = host_mapped(io);
+    const bool staged = !dio || (reinterpret_cast<uintptr_t>(dio) & 15);
+    if (staged) {
+        if (!h->io_host) {
+            NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->io_host), bytes,
+                                        hipHostMallocMapped | hipHostMallocCoherent));
+            NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->io), h->io_host, 0));
+        }
+        std::memcpy(h->io_host, io, bytes);
+        dio = h->io;
     }
-    std::copy(io, io + size_t(h->C) * h->B, h->io_host);
-    NEO_HIP_CHECK(hipMemcpyAsync(h->io, h->io_host, bytes, hipMemcpyHostToDevice, s));
-    int rc = h->v2 ? process_samples(h, h->io, h->B, h->io, h->B, h->B, s) : launch_step(h, h->io, h->B, h->io, h->B, s);
+    int rc = h->v2 ? process_samples(h, dio, h->B, dio, h->B, h->B, s) : launch_step(h, dio, h->B, dio, h->B, s);
     if (rc) return rc;
-    NEO_HIP_CHECK(hipMemcpyAsync(h->io_host, h->io, bytes, hipMemcpyDeviceToHost, s));
-    NEO_HIP_CHECK(hipStreamSynchronize(s));
-    std::copy(h->io_host, h->io_host + size_t(h->C) * h->B, io);
+    if ((rc = spin_sync(s))) return rc;  // the block's deadline: poll, do not yield the thread
+    if (staged) std::memcpy(io, h->io_host, bytes);
     return NEO_HIP_OK;
 }
 

@@ -63,8 +63,9 @@ struct neo_hip_upols {
     neo_hip::cf* fv_xf = nullptr;   // far FDL row-pair spectra, ring of nseg slots [C][nseg][256][B]
     neo_hip::cf* fv_ff = nullptr;   // far field [2][C][128][B]
     neo_hip::cf* fv_tw = nullptr;   // 256-point twiddles
-    neo_hip::cf* fv_acc = nullptr;  // far phase-1 sums of two slices [2][units][256][16]
+    neo_hip::cf* fv_acc = nullptr;  // far phase-1 partial sums [K][units][256][16] (K = far_group)
     bool fv_dirty = true;           // far segment spectra to recompute (filter changed)
+    int far_k = 0;                  // far phase-1 windows per pass forced by neo_hip_upols_opts.far_group (0: auto)
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)

@@ -845,7 +845,9 @@ __device__ __forceinline__ void far1_mac(const slice_args& sa, int u, int f0, in
     }
 }
 
-template<int FPL>
+// KMAX: the largest window group the kernel is built for (2: pairs only, the smaller register
+// budget of the shapes below kFarGroupUnits; kFarKMax: any group, far_group's choice)
+template<int FPL, int KMAX>
 __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
 {
     constexpr int FR = 4 * FPL, PPG = kFN / FR;  // f rows per workgroup, workgroups per group
@@ -859,12 +861,17 @@ __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
     if (sa.f1mode == 0 || (cls != sa.f1cls && far_first(cls, K) > sa.f1wn)) {
         far1_mac<FPL, 1>(sa, u, f0, cl & 15);  // one window (priming, or the class has not started)
     } else if (cls == sa.f1cls) {
-        if (K == 2) far1_mac<FPL, 2>(sa, u, f0, cl & 15);
-        else if (K == 3) far1_mac<FPL, 3>(sa, u, f0, cl & 15);
-        else far1_mac<FPL, kFarKMax>(sa, u, f0, cl & 15);
+        if constexpr (KMAX <= 2) {
+            far1_mac<FPL, 2>(sa, u, f0, cl & 15);
+        } else {
+            if (K == 2) far1_mac<FPL, 2>(sa, u, f0, cl & 15);
+            else if (K == 3) far1_mac<FPL, 3>(sa, u, f0, cl & 15);
+            else far1_mac<FPL, kFarKMax>(sa, u, f0, cl & 15);
+        }
     }
 }
 
+template<int KMAX>
 __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
 {
     cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
@@ -927,7 +934,7 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
         // stored by the group's earlier windows' phase 2) were not there when the pass ran
         const int K = sa.fK, cls = (u / kF1UG) % K, first = far_first(cls, K);
         const int jw = sa.f2wn >= first ? (sa.f2wn - cls) % K : 0;
-        for (int s1 = 1; s1 <= jw && s1 < nseg; ++s1) {
+        for (int s1 = 1; s1 <= jw && s1 < nseg && s1 < KMAX; ++s1) {
             cf hv[16], xv[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
@@ -993,13 +1000,13 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
 #ifndef NEO_STEP_WPE
 #define NEO_STEP_WPE 3  // waves per SIMD the step kernel is compiled for (VGPR budget)
 #endif
-template<int B, bool OLA>
+template<int B, bool OLA, int KMAX>
 __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(NEO_STEP_WPE))) void k_lvl_step(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
     int bid = int(blockIdx.x);
     if (bid < a.f2nwg) {
-        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2_role(a, bid, smem);
+        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2_role<KMAX>(a, bid, smem);
         return;
     }
     bid -= a.f2nwg;
@@ -1014,9 +1021,9 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
         toep_level<1>(a, bid, smem) || toep_level<0>(a, bid, smem))
         return;
     if (bid < a.f1nwg && (NEO_ROLES & 8)) {
-        if (a.f1fpl == 4) far1_role<4>(a, bid);
-        else if (a.f1fpl == 2) far1_role<2>(a, bid);
-        else far1_role<1>(a, bid);
+        if (a.f1fpl == 4) far1_role<4, KMAX>(a, bid);
+        else if (a.f1fpl == 2) far1_role<2, KMAX>(a, bid);
+        else far1_role<1, KMAX>(a, bid);
     }
 }
 
@@ -1087,6 +1094,7 @@ static int far_group(const upols_t* h)
 {
     const int ns = h->lv.nseg;
     if (ns < 2) return 1;
+    if (h->far_k) return h->far_k;  // neo_hip_upols_opts.far_group (tests, A/B runs)
     if (int64_t(h->C) * (h->B / 16) < kFarGroupUnits) return 2;
     const int K = int(std::lround(std::sqrt(2.0 * (ns - 1))));
     return std::min(kFarKMax, std::max(2, K));
@@ -1216,13 +1224,18 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t
         return t;
     }();
     if (!grid) return NEO_HIP_OK;
+    // pairs-only build where the window group is <= 2 (fewer VGPRs: every shape below
+    // kFarGroupUnits), else the build for any group
+#define NEO_LVL(OL, KM)                                                                                        \
+    NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, OL, KM>), dim3(grid), \
+                                                                         dim3(lstep_cfg<BB>::WG), 0, s, a))
+    const bool pairs = a.fK <= 2;
     if (h->ola) {
-        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, true>), dim3(grid),
-                                                                             dim3(lstep_cfg<BB>::WG), 0, s, a))
+        if (pairs) NEO_LVL(true, 2) else NEO_LVL(true, kFarKMax)
     } else {
-        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, false>), dim3(grid),
-                                                                             dim3(lstep_cfg<BB>::WG), 0, s, a))
+        if (pairs) NEO_LVL(false, 2) else NEO_LVL(false, kFarKMax)
     }
+#undef NEO_LVL
     NEO_HIP_LAUNCH_CHECK();
     return NEO_HIP_OK;
 }
@@ -1387,5 +1400,14 @@ extern "C" NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int
         if (b) b[l] = lp.b[l];
     }
     if (nseg) *nseg = lp.nseg;
+    return NEO_HIP_OK;
+}
+
+// The far level's phase-1 window group of a handle (far_group: auto or forced by
+// neo_hip_upols_opts.far_group); 0 without a far transform level.
+extern "C" NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* windows)
+{
+    if (!h || !windows) return neo_hip::fail(NEO_HIP_EINVAL, "null handle or output");
+    *windows = h->lv.nseg ? neo_hip::far_group(h) : 0;
     return NEO_HIP_OK;
 }

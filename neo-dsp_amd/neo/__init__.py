@@ -7,7 +7,8 @@ is libneo_hip.so (include/neo_hip.h). Put `<repo>/neo-dsp_amd` on sys.path.
 from . import _native
 from . import convolution
 from . import fft
-from .convolution import (UpolsConvolver, UpolsMultiConvolver, convolve, dense_convolve, direct_convolve, fft_convolve, normalize_impulse,
+from .convolution import (UpolsConvolver, UpolsMultiConvolver, convolve, dense_convolve, direct_convolve, fft_convolve,
+                          host_register, host_unregister, normalize_impulse,
                           num_partitions, split_upola_convolver, split_upols_convolver, uniform_partition,
                           upola_convolver, upola_convolver_v2, upols_convolver)
 
@@ -26,6 +27,8 @@ __all__ = [
     "uniform_partition",
     "normalize_impulse",
     "num_partitions",
+    "host_register",
+    "host_unregister",
     "dense_convolve",
     "convolve",
     "fft_convolve",

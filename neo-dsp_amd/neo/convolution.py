@@ -24,6 +24,8 @@ from . import _native
 
 __all__ = [
     "num_partitions",
+    "host_register",
+    "host_unregister",
     "uniform_partition",
     "normalize_impulse",
     "UpolsConvolver",
@@ -68,6 +70,20 @@ def level_plan(partitions: int) -> dict:
     return {"a0": a0.value, "T": list(T[:n]), "a": list(a[:n]), "b": list(b[:n]), "nseg": ns.value}
 
 
+def host_register(array: np.ndarray) -> np.ndarray:
+    """Page-lock a host array in place (neo_hip_host_register) so that host-buffer calls
+    (UpolsConvolver.__call__) read and write it over PCIe without staging; call
+    host_unregister before the array is freed."""
+    if not (isinstance(array, np.ndarray) and array.flags.c_contiguous):
+        raise TypeError("host_register takes a C-contiguous ndarray")
+    _native.check(_native.load().neo_hip_host_register(_ptr(array), array.nbytes))
+    return array
+
+
+def host_unregister(array: np.ndarray) -> None:
+    _native.check(_native.load().neo_hip_host_unregister(_ptr(array)))
+
+
 def uniform_partition(impulse_response, block_size: int, device: int = 0) -> np.ndarray:
     """[C][L] float32 -> [C][P][B+1] complex64: rfft_2B of each zero-padded B-sample partition."""
     ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
@@ -104,14 +120,15 @@ class UpolsConvolver:
     """
 
     OPTION_DEFAULTS = {"fused": -1, "split_workgroups": 0, "batch_blocks": 0, "batch_bins": 0, "levels": -1,
-                       "far_level": -1}
+                       "far_level": -1, "far_group": 0}
 
     def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols",
                  options: dict | None = None):
         """`options` (neo_hip_upols_create_ex): explicit code-path choices instead of the
         shape-based defaults — fused (-1 auto / 0 / 1), split_workgroups (0 auto),
         batch_blocks (0 auto / 2..32), batch_bins (0 auto / 1 / 2), levels (-1 auto / 0 / 1),
-        far_level (-1 auto / 0 Toeplitz window of 128 blocks / 1 partition-axis transform, for p >= 256).
+        far_level (-1 auto / 0 Toeplitz window of 128 blocks / 1 partition-axis transform, for p >= 256),
+        far_group (0 auto / 1..4 windows per far phase-1 pass over the stored segment spectra).
         Every choice gives the same results up to float summation order."""
         lib = _native.load()
         h = ctypes.c_void_p()
@@ -166,6 +183,12 @@ class UpolsConvolver:
             import torch
 
             assert block.dtype == torch.float32 and block.is_contiguous()
+            if block.numel() != self.channels * self.block_size:
+                raise ValueError("block must hold channels * block_size samples")
+            if not block.is_cuda:  # host tensor (pinned ones are read and written in place)
+                _native.check(_native.load().neo_hip_upols_process(self._h, ctypes.c_void_p(block.data_ptr()), 0,
+                                                                   None))
+                return block
             s = stream or torch.cuda.current_stream(block.device).cuda_stream
             _native.check(_native.load().neo_hip_upols_process(self._h, ctypes.c_void_p(block.data_ptr()), 1,
                                                                ctypes.c_void_p(s)))
@@ -243,6 +266,12 @@ class UpolsConvolver:
         v = [ctypes.c_int() for _ in range(4)]
         _native.check(_native.load().neo_hip_upols_get_ahead(self._h, *[ctypes.byref(x) for x in v]))
         return bool(v[0].value), v[1].value, v[2].value, v[3].value
+
+    def far_group(self) -> int:
+        """Windows per far phase-1 pass this handle runs (0: no far transform level)."""
+        k = ctypes.c_int()
+        _native.check(_native.load().neo_hip_upols_get_far_group(self._h, ctypes.byref(k)))
+        return k.value
 
     # -- instrumentation ------------------------------------------------------
     def set_timing(self, enable, every: int = 1) -> None:

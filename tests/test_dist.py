@@ -89,6 +89,61 @@ def test_shard_ranges():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_bench_strong_scaling_spans():
+    """bench.py --gpus N runs configs[4] itself: 2048 channels IN ALL split over the ranks
+    (N = 8: exactly the 256-channel shard per GPU, DenseConvolution.hpp:50-67 over the
+    node), the other workloads per GPU."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    for world in (1, 2, 4, 8):
+        per = [bench.rank_channels("c5full", world, r) for r in range(world)]
+        assert all(tot == 2048 for _, tot in per)
+        assert sum(c for c, _ in per) == 2048
+        assert [c for c, _ in per] == [2048 // world] * world
+    assert bench.rank_channels("c5full", 8, 7) == (256, 2048)
+    assert bench.rank_channels("c5full", 2, 1) == (1024, 2048)
+    assert bench.rank_channels("c5", 8, 3) == (256, 2048)  # per GPU: weak
+    assert bench.rank_channels("c4", 2, 0) == (256, 512)
+
+
+def _bench_rank_worker(rank, world, port, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path[:0] = [REPO]
+    import bench
+    import torch.distributed as dist
+
+    try:
+        w, r, _ = bench.dist_setup(None)
+        c, tot = bench.rank_channels("c5full", w, r)
+        lo, hi = bench.shard(tot, w, r)
+        m = bench.max_over_ranks(float(c), w)
+        q.put((r, lo, hi, c, tot, m))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((rank, "error", repr(e), None, None, None))
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world8_strong_shards():
+    """Eight gloo ranks (CPU) take bench.py's strong-scaling shards of the 2048 channels:
+    contiguous, disjoint, covering [0, 2048), 256 each."""
+    world, port = 8, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r
+    assert [(r[1], r[2]) for r in res] == [(256 * i, 256 * (i + 1)) for i in range(8)]
+    assert all(r[3] == 256 and r[4] == 2048 and r[5] == 256.0 for r in res)
+
+
 def _hip_worker(rank, world, port, q, C, B, L, nb):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})

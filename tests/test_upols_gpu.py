@@ -137,6 +137,56 @@ def test_set_filter_equals_set_impulse_and_reset(neo_gpu, oracle):
     assert max(np.abs(p - q).max() for p, q in zip(ya, ya2)) == 0.0  # deterministic after reset
 
 
+@pytest.mark.parametrize("levels", [0, 1])
+def test_host_buffers_zero_copy(neo_gpu, oracle, levels):
+    """Host-buffer blocks (neo_hip_upols_process, the plugin's processFrame call,
+    DenseConvolution.cpp:62-74): pageable memory through the mapped staging, page-locked
+    memory (torch pinned tensors = hipHostMalloc; numpy arrays page-locked with
+    neo.host_register) read and written in place by the step kernel. All three equal the
+    device-resident step bit for bit; a misaligned registered view falls back to staging."""
+    torch = pytest.importorskip("torch")
+    B, L, C, nb = 256, 256 * 70, 3, 24
+    ir = np.stack([oracle.noise(980 + c, L) for c in range(C)])
+    P = neo_gpu.num_partitions(L, B)
+    sig = np.stack([oracle.noise(990 + c, B * nb) for c in range(C)])
+    opts = {"levels": levels}
+    dev = neo_gpu.UpolsConvolver(C, B, P, options=opts)
+    dev.set_impulse(ir)
+    dev.set_batch(False)
+    t = torch.from_numpy(sig).cuda()
+    dev.process_blocks(t)
+    torch.cuda.synchronize()
+    ref = t.cpu().numpy()
+    convs = [neo_gpu.UpolsConvolver(C, B, P, options=opts) for _ in range(4)]
+    for c in convs:
+        c.set_impulse(ir)
+    pinned = torch.empty((C, B), dtype=torch.float32).pin_memory()
+    reg = np.empty((C, B + 4), np.float32)  # registered; rows B apart at an offset: a copy lands in it
+    neo_gpu.host_register(reg)
+    try:
+        regv = np.ndarray((C, B), np.float32, buffer=reg, offset=0, strides=(4 * B, 4))
+        odd = np.ndarray((C, B), np.float32, buffer=reg, offset=4, strides=(4 * B, 4))  # 4-byte aligned
+        outs = [np.empty_like(sig) for _ in convs]
+        for i in range(nb):
+            blk = sig[:, i * B:(i + 1) * B]
+            a = np.ascontiguousarray(blk)
+            convs[0](a)
+            outs[0][:, i * B:(i + 1) * B] = a
+            pinned.numpy()[:] = blk
+            convs[1](pinned)
+            outs[1][:, i * B:(i + 1) * B] = pinned.numpy()
+            regv[:] = blk
+            convs[2](regv)
+            outs[2][:, i * B:(i + 1) * B] = regv
+            odd[:] = blk
+            convs[3](odd)
+            outs[3][:, i * B:(i + 1) * B] = odd
+    finally:
+        neo_gpu.host_unregister(reg)
+    for k, o in enumerate(outs):
+        assert np.array_equal(o, ref), k
+
+
 def test_errors(neo_gpu):
     with pytest.raises(RuntimeError):
         neo_gpu.UpolsConvolver(1, 500, 4)  # not a power of two
@@ -214,7 +264,7 @@ def test_full_size_properties(neo_gpu, oracle, C, B, L):
         assert peak_err(ox[c].cpu().numpy(), ref[0]) <= TOL
 
 
-def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans):
+def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans, far_group=None):
     """Default options (streaming levels on, far level on), device input, one block per
     call as a real-time caller steps it, nb blocks: every level's windows repeat many times,
     every far segment meets real FDL rows and the ring wraps. Channels `chans` against the
@@ -226,14 +276,19 @@ def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans):
     P = neo_gpu.num_partitions(L, B)
     conv = neo_gpu.UpolsConvolver(C, B, P)
     assert conv.ahead_info()[0]  # streaming levels are the default here
+    if far_group is not None:
+        assert conv.far_group() == far_group  # the automatic choice at this shape
     conv.set_impulse(ir, normalize=True)
     conv.set_batch(False)  # one block per pass
-    xh = x.cpu().numpy()
+    xh = {c: x[c].cpu().numpy()[None] for c in chans}
+    # one normalization factor over all channels (normalize_impulse.hpp:21-30)
+    irh = oracle.normalize_impulse(ir.cpu().numpy())
+    irc = {c: irh[c:c + 1].copy() for c in chans}
+    del ir, irh
     conv.process_blocks(x)
     torch.cuda.synchronize()
-    irh = oracle.normalize_impulse(ir.cpu().numpy())
     for c in chans:
-        ref = oracle.dense_convolve(xh[c:c + 1], oracle.uniform_partition(irh[c:c + 1], B))
+        ref = oracle.dense_convolve(xh[c], oracle.uniform_partition(irc[c], B))
         assert peak_err(x[c].cpu().numpy(), ref[0]) <= TOL, c
         # the last far window alone (steady state, ring wrapped many times)
         assert peak_err(x[c, -128 * B:].cpu().numpy(), ref[0, -128 * B:]) <= TOL, c
@@ -244,6 +299,51 @@ def test_full_size_c5_shard_steady_state(neo_gpu, oracle):
     L = 480000, P = 938, 6 far segments, ring 969): 1152 blocks (9 far windows), channels 0,
     127, 255."""
     _full_size_streaming(neo_gpu, oracle, 256, 512, 480000, 1152, 77, (0, 127, 255))
+
+
+def test_full_size_c5full_steady_state(neo_gpu, oracle):
+    """The headline workload itself (configs[4]'s 2048 channels on one GPU, B = 512,
+    L = 480000, P = 938: 32768 16-column units, so the far level runs window groups of
+    K = 3, far1_mac<FPL, 3> and phase 2's extra segments): 1152 blocks (9 far windows, the
+    ring of 969 rows wraps), channels 0, 1024 and 2047."""
+    _full_size_streaming(neo_gpu, oracle, 2048, 512, 480000, 1152, 79, (0, 1024, 2047), far_group=3)
+
+
+def test_c3_streaming_exact_shape(neo_gpu, oracle):
+    """configs[2] at its exact shape as the bench steps it (B = 512, L = 96000 -> P = 188,
+    1 channel, streaming levels: block step + Toeplitz 4..32 + no far level): the golden
+    fixture's 200 blocks one block per call, then 640 single-block steps of fresh noise
+    against the oracle's dense_convolve (uniform_partitioned_convolver.hpp:47-65)."""
+    torch = pytest.importorskip("torch")
+    g = np.load(os.path.join(GOLD, "upols_b512_l96000_seed7.npz"))
+    B = 512
+    P = neo_gpu.num_partitions(g["ir"].shape[-1], B)
+    assert P == 188
+    conv = neo_gpu.UpolsConvolver(1, B, P)
+    assert conv.ahead_info()[0]  # the streaming form is the default at this shape
+    conv.set_impulse(np.atleast_2d(g["ir"]), normalize=True)
+    conv.set_batch(False)
+    sig = np.atleast_2d(g["signal"]).astype(np.float32)
+    nb = sig.shape[1] // B
+    t = torch.from_numpy(sig[:, : nb * B].copy()).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    for i in range(nb):  # one call per block, in place
+        p = t.data_ptr() + 4 * i * B
+        conv.process_blocks_ptr(p, p, nb * B, 1, stream)
+    torch.cuda.synchronize()
+    out = np.atleast_2d(g["out"])[:, : nb * B]
+    assert peak_err(t.cpu().numpy(), out) <= TOL
+    assert np.abs(t.cpu().numpy() - out).max() <= 1e-5
+    # fresh noise, 640 blocks (several windows of every level, the ring of 219 rows wraps)
+    nb2 = 640
+    x = np.stack([oracle.noise(4242, B * nb2)])
+    irn = oracle.normalize_impulse(np.atleast_2d(g["ir"]).astype(np.float32))
+    ref = oracle.dense_convolve(x, oracle.uniform_partition(irn, B))
+    conv.reset()
+    tx = torch.from_numpy(x.copy()).cuda()
+    conv.process_blocks(tx)
+    torch.cuda.synchronize()
+    assert peak_err(tx.cpu().numpy(), ref) <= TOL
 
 
 def test_full_size_c4_steady_state(neo_gpu, oracle):
@@ -601,6 +701,39 @@ def test_far_level_steps_vs_oracle(neo_gpu, oracle, method, B, P, C, nb, far):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 520, {"far_level": far}) <= TOL
 
 
+@pytest.mark.parametrize("method", ["upols", "upola"])
+@pytest.mark.parametrize("K", [1, 2, 3, 4])
+@pytest.mark.parametrize("B,P,C", [(32, 700, 1), (32, 1100, 1), (64, 1000, 2)])
+def test_far_window_groups_vs_oracle(neo_gpu, oracle, method, K, B, P, C):
+    """The far level's phase 1 over groups of K windows (neo_hip_upols_opts.far_group forces
+    K; by default only shapes of >= 32768 16-column units, the 2048-channel headline, run
+    K = 3 / 4): far1_mac<FPL, K> for every K, phase 2's segments 1 .. j of window j of a
+    group, the classes' staggered start after priming, and the two kernel builds (pairs
+    only for K <= 2, any group for K > 2). nseg = 4 / 7 / 6 (FPL 4 / 2 / 2), >= 2P + 300
+    single-block steps (many windows, ring wraparound); OLS and OLA. Ring semantics:
+    fdl_index.hpp:23-36."""
+    nb = 2 * P + 320
+    conv_opts = {"far_level": 1, "far_group": K}
+    probe = neo_gpu.UpolsConvolver(C, B, P, options=conv_opts)
+    assert probe.far_group() == K
+    probe.close()
+    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 900 + K, conv_opts) <= TOL
+
+
+def test_far_group_defaults(neo_gpu):
+    """The automatic window group: 2 below 32768 16-column units (every shape but the
+    headline), round(sqrt(2 (nseg - 1))) from there (bench.far_group restates it)."""
+    import bench
+
+    for C, B, P in [(4, 512, 938), (256, 512, 938), (256, 256, 1875), (1, 512, 188), (3, 64, 300)]:
+        c = neo_gpu.UpolsConvolver(C, B, P)
+        nseg = neo_gpu.convolution.level_plan(P)["nseg"]
+        assert c.far_group() == (bench.far_group(nseg, C * B // 16) if nseg else 0), (C, B, P)
+        c.close()
+    with pytest.raises(RuntimeError):
+        neo_gpu.UpolsConvolver(1, 64, 300, options={"far_group": 5})
+
+
 @pytest.mark.parametrize("far", [0, 1])
 def test_far_field_mixed_and_refilter(neo_gpu, oracle, far):
     """Streaming levels across batched passes, toggles at arbitrary blocks and a filter
@@ -629,6 +762,35 @@ def test_far_field_mixed_and_refilter(neo_gpu, oracle, far):
             pos += n
         assert pos == nb
         assert peak_err(out, ref) <= TOL, k
+
+
+def test_batched_calls_keep_levels_primed(neo_gpu, oracle):
+    """process_blocks with batching on and a block count that is not a whole number of
+    batches: only whole T-block batches run (they leave the levels to re-prime once), and
+    once the levels are primed a call of fewer than 4 T blocks streams them all, so repeated
+    33-block calls do not re-prime every call (ahead_info's window position keeps counting)."""
+    torch = pytest.importorskip("torch")
+    B, P, C = 64, 300, 2
+    L = B * P
+    ir = np.stack([oracle.noise(960 + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    nb = 33 * 6
+    sig = np.stack([oracle.noise(970 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts)
+    conv = neo_gpu.UpolsConvolver(C, B, P)
+    conv.filter(parts)
+    assert conv.ahead_info()[0] and conv.batch_info()[0] == 32
+    t = torch.from_numpy(sig).cuda()
+    phases = []
+    for k in range(6):
+        seg = t[:, k * 33 * B:(k + 1) * 33 * B].contiguous()
+        conv.process_blocks(seg)
+        t[:, k * 33 * B:(k + 1) * 33 * B] = seg
+        phases.append(conv.ahead_info()[1])
+    torch.cuda.synchronize()
+    # call 0: one batch of 32, one streamed block (primes); then 33 streamed blocks per call
+    assert phases == [(1 + 33 * k) % 128 for k in range(6)], phases
+    assert peak_err(t.cpu().numpy(), ref) <= TOL
 
 
 @pytest.mark.parametrize("far", [0, 1])
