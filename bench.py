@@ -285,18 +285,19 @@ def algorithmic_bytes(C, B, P, plan):
                FDL row, 16B per bin each), one slab row per level and the far-field row (8B each)
     Toeplitz level (window T, band [a, b)), C*B/T columns per step: per column b - a filter
                rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
-    far level, C*B/128 columns per step: per column 256 FDL rows, the new row-pair spectrum
-               (256 f) stored, its segment spectrum and 128 far-field entries; phase 1 takes K
-               windows per pass over the nseg - 1 older row-pair and segment spectra (1/K per
-               window), and phase 2 segments 1 .. j of window j of a group (K - 1 spectrum pairs
-               per window on average): 256 (3 + 2 (nseg - 1) / K + K - 1) + 128 values per
-               window, K = far_group(nseg, units) (upols_levels.hip)."""
+    far level, C*B/128 columns per step (on average: 127 slices per 128-block window): per
+               column 256 FDL rows and the new row-pair spectrum (256 f) stored by phase 2a,
+               read back with its segment spectrum by phase 2b one step later, 128 far-field
+               entries; phase 1 takes K windows per pass over the nseg - 1 older row-pair and
+               segment spectra (1/K per window), and 2b segments 1 .. j of window j of a group
+               (K - 1 spectrum pairs per window on average): 256 (4 + 2 (nseg - 1) / K + K - 1)
+               + 128 values per window, K = far_group(nseg, units) (upols_levels.hip)."""
     nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
     block = C * B * (16 + 16 + 16 * (plan["a0"] - 1) + 8 * nlev)
     toep = sum(C * B / T * 8 * (2 * (b - a) + 2 * T - 1) for T, a, b in zip(plan["T"], plan["a"], plan["b"]))
     ns = plan["nseg"]
     K = far_group(ns, C * B // 16)
-    far = C * B / 128 * 8 * (256 * (3 + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
+    far = C * B / 128 * 8 * (256 * (4 + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
     return {"block": block, "toeplitz": toep, "far": far}
 
 

@@ -152,12 +152,15 @@ struct slice_args {
     int fK;                              // windows per phase-1 pass (1: one window per pass)
     int f1g0, f1gs, f1mode, f1cls;       // first group, group step; 0 single, 1 the class's groups, 2 every group; class
     cf* f1acc;  // partial sums [fK (window mod fK)][fU][256 f][16]
-    // far phase 2 (the slice phase 1 did one step earlier): the fresh row pairs' transforms
-    // (stored to their ring slots) and products, the sum, the inverse transform
+    // far phase 2a (the slice phase 1 takes in the same launch): the fresh row pairs'
+    // transforms, stored to their ring slots
     int f2nwg, f2u0, f2tw, f2wn;
-    int f2grp;    // phase-1 window groups on: a unit in window j of its group takes segments 1..j here
+    // far phase 2b (the slice of the previous launch): the stored fresh spectra's products,
+    // phase 1's partial sums, the window group's extra segments, the inverse transform
+    int f3nwg, f3u0, f3wn;
+    int f2grp;    // phase-1 window groups on: a unit in window j of its group takes segments 1..j in 2b
     cf* f2acc;    // as f1acc
-    cf* f2ff;     // the target far window [C][128][B]
+    cf* f3ff;     // 2b's target far window [C][128][B]
 };
 
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
@@ -871,8 +874,10 @@ __device__ __forceinline__ void far1_role(const slice_args& sa, int bid)
     }
 }
 
-template<int KMAX>
-__device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* smem)
+// far phase 2a: the fresh row pairs (segments s < fnfresh: s = 0 in steady state, all of them
+// when the level primes) -> 256-point transforms along the partition axis, packed bin 0 ->
+// their XF ring slots, which 2b reads one launch later
+__device__ __forceinline__ void far2a_role(const slice_args& sa, int bid, char* smem)
 {
     cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
     cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
@@ -886,21 +891,12 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
     const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));
     const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;
     tws[t] = sa.twf[t];
-    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
     const __amdgpu_buffer_rsrc_t fres =
         buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
     const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
     const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
-    // v[i] at f = a + 16 i (col_fft's output and input layout): the stored segments' sum from
-    // phase 1 + the fresh segments' products, kept in acc between segments (priming: every
-    // segment is fresh) so that it is not live across a transform
-    cf v[16];
-    const __amdgpu_buffer_rsrc_t ares =
-        buf_rsrc(sa.f2acc + int64_t((sa.f2wn % sa.fK) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
-    const int ao = (a * 16 + cp) * int(sizeof(cf)), as = 16 * 16 * int(sizeof(cf));  // f = a + 16 i
     for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
-        // fresh row pair: rows tw - (s + 3) 128 + a + 16 n (the ring holds >= kFarRing > 256
-        // rows: one wrap at most)
+        // rows tw - (s + 3) 128 + a + 16 n (the ring holds >= kFarRing > 256 rows: one wrap at most)
         cf x[16];
         int r0 = (sa.f2tw - (s + 3) * kFarT + a) % sa.ring;
         r0 = r0 < 0 ? r0 + sa.ring : r0;
@@ -912,48 +908,81 @@ __device__ __forceinline__ void far2_role(const slice_args& sa, int bid, char* s
         __syncthreads();  // twiddles; the previous segment's LDS use is done
         col_fft<-1, 16>(x, lds, tws, a, cp, true);
         if (unit0) bin0_exchange<true>(x, z, a, cp);  // uniform per workgroup
-        cf hv[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) hv[i] = buf_ld(hres, vo, s * spec + int(16 * i * fs * int(sizeof(cf))));
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = buf_ld(ares, ao, i * as);
+        for (int i = 0; i < 16; ++i) buf_st(x[i], xres, vo, slot(s) * spec + int(16 * i * fs * int(sizeof(cf))));
+    }
+}
+
+// far phase 2b, one launch after 2a for the same units: v[i] at f = a + 16 i (col_fft's layout)
+// = phase 1's partial sums (stored segments) + the fresh segments' products XF_s . HF_s from
+// the slots 2a wrote + (window groups) segments 1 .. j of window j of the unit's phase-1 group;
+// unpack bin 0, inverse transform, the window's 128 far-field rows
+template<int KMAX>
+__device__ __forceinline__ void far2b_role(const slice_args& sa, int bid, char* smem)
+{
+    cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
+    cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
+    cf* tws = z + kFN;                       // twiddles
+    const int t = threadIdx.x, a = t >> 4, cp = t & 15;
+    const int gpc = sa.B / 16, u = sa.f3u0 + bid, c = u / gpc, g = u - c * gpc, k = g * 16 + cp;
+    const bool unit0 = g == 0;  // uniform per workgroup: the unit holding packed bin 0
+    const int M = sa.M, nseg = sa.nseg;
+    auto slot = [&](int s) { return ((sa.f3wn - s - 1) % M + M) % M; };
+    const int64_t fs = sa.B;
+    const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));
+    const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;
+    tws[t] = sa.twf[t];
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+    const __amdgpu_buffer_rsrc_t ares =
+        buf_rsrc(sa.f2acc + int64_t((sa.f3wn % sa.fK) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
+    const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
+    const int ao = (a * 16 + cp) * int(sizeof(cf)), as = 16 * 16 * int(sizeof(cf));  // f = a + 16 i
+    auto z0 = [&](int i) { return unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0; };
+    cf v[16];
+    {  // the partial sums and segment 0's spectra in one round of loads
+        cf hv[16], xv[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            buf_st(x[i], xres, vo, slot(s) * spec + int(16 * i * fs * int(sizeof(cf))));
+            v[i] = buf_ld(ares, ao, i * as);
+            hv[i] = buf_ld(hres, vo, int(16 * i * fs * int(sizeof(cf))));
+            xv[i] = buf_ld(xres, vo, slot(0) * spec + int(16 * i * fs * int(sizeof(cf))));
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
             f2v w = {v[i].x, v[i].y};
-            pk_coef(hv[i], unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0).mac(w, x[i]);
+            pk_coef(hv[i], z0(i)).mac(w, xv[i]);
             v[i] = cf{w.x, w.y};
         }
-        if (s + 1 < s0) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) buf_st(v[i], ares, ao, i * as);
-        }
     }
+    // the other fresh segments (priming: every segment), then the window group's segments
+    // 1 .. j (slots f3wn - 2 .. f3wn - j - 1, stored by the group's earlier windows; not
+    // there when the group's phase-1 pass ran)
+    int jw = 0;
     if (sa.f2grp) {  // uniform per workgroup
-        // window j of this unit's phase-1 group: segments 1 .. j (slots f2wn - 2 .. f2wn - j - 1,
-        // stored by the group's earlier windows' phase 2) were not there when the pass ran
         const int K = sa.fK, cls = (u / kF1UG) % K, first = far_first(cls, K);
-        const int jw = sa.f2wn >= first ? (sa.f2wn - cls) % K : 0;
-        for (int s1 = 1; s1 <= jw && s1 < nseg && s1 < KMAX; ++s1) {
-            cf hv[16], xv[16];
+        jw = sa.f3wn >= first ? (sa.f3wn - cls) % K : 0;
+    }
+    const int s1 = s0 > 1 ? s0 : (jw + 1 < nseg ? jw + 1 : nseg);  // segments [1, s1) from slots
+    for (int s = 1; s < s1 && (s0 > 1 || s < KMAX); ++s) {  // uniform per workgroup
+        cf hv[16], xv[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                hv[i] = buf_ld(hres, vo, s1 * spec + int(16 * i * fs * int(sizeof(cf))));
-                xv[i] = buf_ld(xres, vo, slot(s1) * spec + int(16 * i * fs * int(sizeof(cf))));
-            }
+        for (int i = 0; i < 16; ++i) {
+            hv[i] = buf_ld(hres, vo, s * spec + int(16 * i * fs * int(sizeof(cf))));
+            xv[i] = buf_ld(xres, vo, slot(s) * spec + int(16 * i * fs * int(sizeof(cf))));
+        }
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                f2v w = {v[i].x, v[i].y};
-                pk_coef(hv[i], unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0).mac(w, xv[i]);
-                v[i] = cf{w.x, w.y};
-            }
+        for (int i = 0; i < 16; ++i) {
+            f2v w = {v[i].x, v[i].y};
+            pk_coef(hv[i], z0(i)).mac(w, xv[i]);
+            v[i] = cf{w.x, w.y};
         }
     }
-    __syncthreads();  // twiddles; the bin-0 exchange of the last segment is done
+    __syncthreads();  // twiddles
     if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
     col_fft<1, 16>(v, lds, tws, a, cp, true);
     constexpr float sc = 1.0f / kFN;
-    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f2ff + int64_t(c) * kFarT * fs, spec / 2);
+    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * kFarT * fs, spec / 2);
 #pragma unroll
     for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128
         buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
@@ -1005,8 +1034,13 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
     int bid = int(blockIdx.x);
+    if (bid < a.f3nwg) {
+        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2b_role<KMAX>(a, bid, smem);
+        return;
+    }
+    bid -= a.f3nwg;
     if (bid < a.f2nwg) {
-        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2_role<KMAX>(a, bid, smem);
+        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2a_role(a, bid, smem);
         return;
     }
     bid -= a.f2nwg;
@@ -1218,7 +1252,7 @@ static slice_args base_args(const upols_t* h)
 
 static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t s)
 {
-    const unsigned grid = unsigned(a.f2nwg + a.nblk + a.f1nwg) + [&] {
+    const unsigned grid = unsigned(a.f3nwg + a.f2nwg + a.nblk + a.f1nwg) + [&] {
         unsigned t = 0;
         for (int l = 0; l < a.ntp; ++l) t += unsigned(a.tp[l].nwg);
         return t;
@@ -1240,21 +1274,29 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t
     return NEO_HIP_OK;
 }
 
-// far phase 1 of step n: slice (n + 1) mod 128 of window W = (n + 1) / 128 + 1 (one step ahead
-// of its phase 2), the unit groups of class W mod K for the windows W .. W + K - 1 (far1_mac); in
-// the first windows after priming (W < K) the classes that have not started, for window W alone
-static void far1_args(const upols_t* h, int64_t n, slice_args& a)
+// The far level's units are cut into kFarS = kFarT - 1 slices per window: slice q of window W
+// runs phase 1 and 2a at step q of window W - 1 (2a reads FDL rows up to the last block before
+// that window) and 2b at step q + 1 (<= the window's last step: the far field is complete when
+// window W's first block runs).
+constexpr int kFarS = kFarT - 1;
+
+static int far_u(int64_t U, int q) { return int(q * U / kFarS); }
+
+// far phase 1 for slice q of window W: the unit groups of class W mod K for the windows
+// W .. W + K - 1 (far1_mac); in the first windows after priming (W < K) the classes that have
+// not started, for window W alone
+static void far1_args(const upols_t* h, int64_t W, int q, slice_args& a)
 {
-    const int64_t U = far_units(h), n1 = n + 1, st = n1 % kFarT, W = n1 / kFarT + 1;
+    const int64_t U = far_units(h);
     const int K = far_group(h);
     a.f1wn = int(W);
-    far1_range(h, a, int(st * U / kFarT), int((st + 1) * U / kFarT), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
+    far1_range(h, a, far_u(U, q), far_u(U, q + 1), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
 }
 
 // The launch of step n >= 0 (block t0 + n at ring row w): the block and slice n mod T of
 // window n / T + 1 of every Toeplitz level (its rows end at the window in progress, so every
-// window's slabs are complete when its first block runs); far phase 2 of slice n mod 128 of
-// window n / 128 + 1 and phase 1 of the next slice.
+// window's slabs are complete when its first block runs); with q = n mod 128 and W = n / 128 + 1,
+// far phase 1 and 2a of slice q (q < kFarS) and far phase 2b of slice q - 1 (q >= 1) of window W.
 static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, float* out, int64_t ld_out,
                        hipStream_t s)
 {
@@ -1295,23 +1337,29 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
     if (lp.nseg) {
         a.ff = h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B;
         a.fcs = int64_t(kFarT) * B;
-        const int64_t U = int64_t(C) * (B / 16), st = n % kFarT, W = n / kFarT + 1;
-        const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
-        a.f2u0 = u0;
-        a.f2nwg = u1 - u0;
-        a.f2tw = ring_add(w, W * kFarT - n, R);
-        a.f2wn = int(W);
-        a.f2grp = far_group(h) > 1;
-        a.f2ff = h->fv_ff + (W & 1) * C * kFarT * B;
-        far1_args(h, n, a);
+        const int64_t U = far_units(h), W = n / kFarT + 1;
+        const int q = int(n % kFarT);
+        if (q < kFarS) {
+            a.f2u0 = far_u(U, q);
+            a.f2nwg = far_u(U, q + 1) - a.f2u0;
+            a.f2tw = ring_add(w, W * kFarT - n, R);
+            a.f2wn = int(W);
+            far1_args(h, W, q, a);
+        }
+        if (q >= 1) {
+            a.f3u0 = far_u(U, q - 1);
+            a.f3nwg = far_u(U, q) - a.f3u0;
+            a.f3wn = int(W);
+            a.f2grp = far_group(h) > 1;
+            a.f3ff = h->fv_ff + (W & 1) * C * kFarT * B;
+        }
     }
     return launch_step_kernel(h, a, s);
 }
 
 // First streaming step after a reset / filter change / batched pass (block t0 at ring row w):
 // window 0 of every level, starting at t0, computed whole (all units; the far level
-// transforms every segment), then phase 1 of the far level's first slice of window 1 (the
-// launch of "step -1").
+// transforms every segment: slice by slice, 2a of slice q beside 2b of slice q - 1).
 static int lvl_prime(upols_t* h, hipStream_t s)
 {
     const level_plan& lp = h->lv;
@@ -1340,28 +1388,28 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     }
     if (int rc = launch_step_kernel(h, a, s)) return rc;
     if (!lp.nseg) return NEO_HIP_OK;
-    // far window 0, every segment transformed, in slices (the partial sums hold one)
-    slice_args f = base_args(h);
-    f.fnfresh = lp.nseg;
-    f.f1wn = 0;
-    f.f2tw = w;
-    f.f2wn = 0;
-    f.f2ff = h->fv_ff;
-    const int64_t U = int64_t(C) * (B / 16);
-    for (int st = 0; st < kFarT; ++st) {
-        const int u0 = int(st * U / kFarT), u1 = int((st + 1) * U / kFarT);
-        if (u1 <= u0) continue;
-        far1_range(h, f, u0, u1, 0, 0);  // zero partial sums (no stored segments)
-        f.f2nwg = 0;
-        if (int rc = launch_step_kernel(h, f, s)) return rc;
-        f.f1nwg = 0;
-        f.f2u0 = u0;
-        f.f2nwg = u1 - u0;
+    // far window 0, every segment transformed (fnfresh = nseg), in slices
+    const int64_t U = far_units(h);
+    for (int q = 0; q <= kFarS; ++q) {
+        slice_args f = base_args(h);
+        f.fnfresh = lp.nseg;
+        if (q < kFarS) {
+            f.f1wn = 0;
+            far1_range(h, f, far_u(U, q), far_u(U, q + 1), 0, 0);  // zero partial sums (no stored segments)
+            f.f2u0 = far_u(U, q);
+            f.f2nwg = far_u(U, q + 1) - f.f2u0;
+            f.f2tw = w;
+            f.f2wn = 0;
+        }
+        if (q >= 1) {
+            f.f3u0 = far_u(U, q - 1);
+            f.f3nwg = far_u(U, q) - f.f3u0;
+            f.f3wn = 0;
+            f.f3ff = h->fv_ff;
+        }
         if (int rc = launch_step_kernel(h, f, s)) return rc;
     }
-    slice_args p = base_args(h);
-    far1_args(h, -1, p);
-    return launch_step_kernel(h, p, s);
+    return NEO_HIP_OK;
 }
 
 int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)

@@ -409,6 +409,62 @@ int oracle_upols_run(oracle_upols* u, float* signal, size_t num_blocks)
     return 0;
 }
 
+/* The standalone overlap stages with any filter size F (overlap_test.cpp:21-64 drives them
+ * with F in {8 .. 1024}): transform size n = 2^next_order(B + F - 1) (overlap_save.hpp:53;
+ * overlap_add.hpp:43-46, output_size<full>(B, F) = B + F - 1). The callback here multiplies
+ * the n/2 + 1 bins by G (NULL: the no-op callback of the reference's test).
+ *   kind 0, overlap_save::operator() (:84-112): slide the n-sample window left by B
+ *     (slide_window_left, :37-49: n / B - 1 block copies), block -> window[n - B, n), rfft,
+ *     callback, irfft into a separate real buffer, 1/n, real[n - B, n) -> block.
+ *   kind 1, overlap_add::operator() (:76-106): block -> window[0, B), window[B, 2B) = 0 (only
+ *     that "padding"; window[2B, n) keeps the previous irfft output), rfft, callback, irfft
+ *     back INTO the window, 1/n, block = window[0, B) + overlap, overlap = window[B, 2B). */
+int oracle_overlap_stage(int kind, size_t block, size_t filter, const float* G, float* signal, size_t num_blocks)
+{
+    int order = 0;
+    while (((size_t)1 << order) < block + filter - 1) ++order;  /* next_order = log2(bit_ceil) */
+    const size_t n = (size_t)1 << order, bins = n / 2 + 1;
+    if (n < block) return -1;
+    float* window = (float*)calloc(n, sizeof(float));
+    float* cbuf = (float*)calloc(2 * n, sizeof(float));
+    float* rbuf = (float*)calloc(n, sizeof(float));
+    float* overlap = (float*)calloc(block, sizeof(float));
+    int rc = 0;
+    const float scale = 1.0f / (float)n;
+    for (size_t b = 0; b < num_blocks && rc == 0; ++b) {
+        float* blk = signal + b * block;
+        if (kind == 0) {
+            const size_t steps = n / block;
+            for (size_t i = 0; i + 1 < steps; ++i) memcpy(window + i * block, window + (i + 1) * block, sizeof(float) * block);
+            memcpy(window + (n - block), blk, sizeof(float) * block);
+        } else {
+            memcpy(window, blk, sizeof(float) * block);
+            memset(window + block, 0, sizeof(float) * (2 * block <= n ? block : n - block));
+        }
+        rc = oracle_rfft(order, window, cbuf);
+        if (rc) break;
+        if (G) {
+            for (size_t k = 0; k < bins; ++k) {
+                const float a = cbuf[2 * k], c = cbuf[2 * k + 1], x = G[2 * k], y = G[2 * k + 1];
+                cbuf[2 * k] = a * x - c * y;
+                cbuf[2 * k + 1] = a * y + c * x;
+            }
+        }
+        if (kind == 0) {
+            rc = oracle_irfft(order, cbuf, rbuf);
+            for (size_t i = 0; i < n; ++i) rbuf[i] *= scale;
+            memcpy(blk, rbuf + (n - block), sizeof(float) * block);
+        } else {
+            rc = oracle_irfft(order, cbuf, window);
+            for (size_t i = 0; i < n; ++i) window[i] *= scale;
+            for (size_t i = 0; i < block; ++i) blk[i] = window[i] + overlap[i];
+            if (2 * block <= n) memcpy(overlap, window + block, sizeof(float) * block);
+        }
+    }
+    free(window); free(cbuf); free(rbuf); free(overlap);
+    return rc;
+}
+
 /* no-op-callback overlap_save (overlap_test.cpp:21-53): the identity stage */
 int oracle_overlap_save_identity(size_t block, float* signal, size_t num_blocks)
 {

@@ -9,6 +9,7 @@ extern "C" {
 int oracle_fft_c2c(int order, int dir, float* x);
 int oracle_rfft(int order, const float* in, float* out);
 int oracle_irfft(int order, const float* in, float* out);
+int oracle_overlap_stage(int kind, size_t block, size_t filter, const float* G, float* signal, size_t num_blocks);
 void oracle_normalize_impulse(float* ir, size_t channels, size_t length);
 size_t oracle_num_partitions(size_t length, size_t block);
 int oracle_uniform_partition(const float* ir, size_t channels, size_t length, size_t block, float* out);

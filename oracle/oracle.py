@@ -76,6 +76,7 @@ def lib():
         L.oracle_upola_create.restype = ctypes.c_void_p
         L.oracle_dense_convolve_method.argtypes = [_f32p, _f32p, _f32p, _sz, _sz, _sz, _sz, ctypes.c_int, ctypes.c_int]
         L.oracle_overlap_add_identity.argtypes = [_sz, _f32p, _sz]
+        L.oracle_overlap_stage.argtypes = [ctypes.c_int, _sz, _sz, ctypes.c_void_p, _f32p, _sz]
         L.oracle_fft_convolve.argtypes = [_f32p, _sz, _f32p, _sz, _f32p]
         L.oracle_direct_convolve.argtypes = [_f32p, _sz, _f32p, _sz, _f32p]
         _lib = L
@@ -271,6 +272,30 @@ def dense_convolve(signal: np.ndarray, partitions: np.ndarray, threads: int = 1,
     if rc:
         raise RuntimeError("oracle dense_convolve failed")
     return out
+
+
+def overlap_transform_size(block: int, filter_size: int) -> int:
+    """2^next_order(B + F - 1) (overlap_save.hpp:53, overlap_add.hpp:43-46)."""
+    n = 1
+    while n < block + filter_size - 1:
+        n *= 2
+    return n
+
+
+def overlap_stage(kind: str, signal: np.ndarray, block: int, filter_size: int, G=None) -> np.ndarray:
+    """The standalone overlap_save / overlap_add stage (kind "save" / "add") over consecutive
+    blocks of a 1-D signal, transform size overlap_transform_size(B, F), callback = multiply the
+    n/2 + 1 bins by G (None: no-op)."""
+    s = np.array(signal, dtype=np.float32, copy=True)
+    g = None
+    if G is not None:
+        g = np.ascontiguousarray(G, dtype=np.complex64)
+        assert g.shape == (overlap_transform_size(block, filter_size) // 2 + 1,)
+    rc = lib().oracle_overlap_stage(0 if kind == "save" else 1, block, filter_size,
+                                    None if g is None else g.ctypes.data_as(ctypes.c_void_p), s, s.shape[0] // block)
+    if rc:
+        raise RuntimeError("oracle overlap stage failed")
+    return s
 
 
 def overlap_add_identity(signal: np.ndarray, block: int) -> np.ndarray:

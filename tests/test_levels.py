@@ -6,7 +6,7 @@ Per bin the convolver output is Y[t] = sum_p H[p] X[t - p]
 t - p). The HIP path splits the partitions into the bands of neo_hip_upols_level_plan: the
 block itself takes partitions 0..a0-1, each Toeplitz level computes its next window during
 the current one (a slice of the bins per step, from FDL rows before the current window), and
-the far level does the same in two phases one step apart. All of it runs in ONE launch per
+the far level does the same in three phases (phase 1 and 2a in one step, 2b in the next). All of it runs in ONE launch per
 step (k_lvl_step), so no role may read what another role of the same step writes. This test
 replays exactly that schedule — the ring positions the host passes (tw), the slice ranges,
 the double-buffered slabs, the far level's XF ring of row-pair spectra, its partial sums (phase 1 in window pairs) and
@@ -27,6 +27,7 @@ import pytest
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "neo-dsp_amd"))
 
 FT, FA, FN = 128, 256, 256  # far window, first far partition, transform length
+FS = FT - 1  # far slices per window (kFarS)
 
 
 def plan(P):
@@ -44,9 +45,16 @@ class Sim:
     def __init__(self, H, lp, G=4, Kw=None):
         self.H, self.lp, self.G = H, lp, G
         ns = lp["nseg"]
-        # windows per phase-1 pass (upols_levels.hip far_group), or a forced value
-        self.Kw = Kw or (1 if ns < 2 else min(4, max(2, int(np.floor(np.sqrt(2.0 * (ns - 1)) + 0.5)))))
         self.P, self.K = H.shape
+        # windows per phase-1 pass: the kernel's automatic choice for this many 16-column units
+        # (bench.far_group restates upols_levels.hip far_group), or a forced value
+        # (neo_hip_upols_opts.far_group)
+        if Kw is None:
+            sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+            import bench
+
+            Kw = bench.far_group(ns, max(1, self.K // 16))
+        self.Kw = Kw
         self.R = self.P + 31
         if lp["nseg"]:
             self.R = max(self.R, 2 * FA)
@@ -112,15 +120,22 @@ class Sim:
                     acc += self.XF[(wn - (s - j) - 1) % self.M, :, k] * self.HF[s, :, k]
                 self.acc[(wn + j) % K, :, k] = acc
 
-    def far2(self, tw, wn, k0, k1, nfresh, grp=False):
-        """phase 2: the fresh row pairs' transforms (stored to their slots) and products,
-        segments 1 .. j for window j of a phase-1 group, the inverse transform into the far field"""
-        ns, K = self.lp["nseg"], self.Kw
-        acc = self.acc[wn % K, :, k0:k1].copy()
+    def far2a(self, tw, wn, k0, k1, nfresh):
+        """phase 2a: the fresh row pairs' transforms, stored to their slots"""
+        ns = self.lp["nseg"]
         for s in range(min(nfresh, ns)):
             slot = (wn - s - 1) % self.M
             rows = [(tw - (s + 3) * FT + i) % self.R for i in range(FN)]
             self.XF[slot, :, k0:k1] = np.fft.fft(self.ring[rows, k0:k1], axis=0)
+
+    def far2b(self, wn, k0, k1, nfresh, grp=False):
+        """phase 2b (one step after 2a): the partial sums, the fresh segments' products from
+        their slots, segments 1 .. j for window j of a phase-1 group, the inverse transform
+        into the far field"""
+        ns, K = self.lp["nseg"], self.Kw
+        acc = self.acc[wn % K, :, k0:k1].copy()
+        for s in range(min(nfresh, ns)):
+            slot = (wn - s - 1) % self.M
             acc += self.XF[slot, :, k0:k1] * self.HF[s, :, k0:k1]
         if grp:
             for k in range(k0, k1):
@@ -130,11 +145,13 @@ class Sim:
                     acc[:, k - k0] += self.XF[(wn - s - 1) % self.M, :, k] * self.HF[s, :, k]
         self.ff[wn & 1, :, k0:k1] = np.fft.ifft(acc, axis=0)[FT:]
 
-    def far1_slice(self, n, w):
-        """phase 1 of step n: slice (n + 1) mod 128 of window (n + 1) / 128 + 1, in groups"""
-        n1 = n + 1
-        st, W = n1 % FT, n1 // FT + 1
-        k0, k1 = st * self.K // FT, (st + 1) * self.K // FT
+    def span(self, q):
+        """columns of far slice q (kFarS = 127 slices per window)"""
+        return q * self.K // FS, (q + 1) * self.K // FS
+
+    def far1_slice(self, W, q):
+        """phase 1 for slice q of window W, in groups"""
+        k0, k1 = self.span(q)
         if k1 > k0:
             K = self.Kw
             self.far1(W, k0, k1, 1, 0 if K == 1 else (2 if W < K else 1), W % K)
@@ -151,11 +168,14 @@ class Sim:
                 k0, k1 = u0 * K // U, u1 * K // U
                 out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w + W * T - n) % R, k0, k1, W & 1))
         if lp["nseg"]:
-            st, W = n % FT, n // FT + 1
-            k0, k1 = st * K // FT, (st + 1) * K // FT
-            if k1 > k0:
-                out.append(lambda: self.far2((w + W * FT - n) % R, W, k0, k1, 1, self.Kw > 1))
-            out.append(lambda: self.far1_slice(n, w))
+            q, W = n % FT, n // FT + 1
+            if q < FS:  # phase 1 and 2a of slice q
+                k0, k1 = self.span(q)
+                out.append(lambda: self.far1_slice(W, q))
+                out.append(lambda k0=k0, k1=k1: self.far2a((w + W * FT - n) % R, W, k0, k1, 1))
+            if q >= 1:  # 2b of slice q - 1
+                k0, k1 = self.span(q - 1)
+                out.append(lambda k0=k0, k1=k1: self.far2b(W, k0, k1, 1, self.Kw > 1))
         return out
 
     def prime(self):
@@ -163,9 +183,14 @@ class Sim:
             self.toep(l, self.w, 0, self.K, 0)
         if self.lp["nseg"]:
             ns = self.lp["nseg"]
-            self.far1(0, 0, self.K, ns)
-            self.far2(self.w, 0, 0, self.K, ns)
-            self.far1_slice(-1, (self.w - 1) % self.R)
+            for q in range(FS + 1):  # launch q: phase 1 + 2a of slice q, 2b of slice q - 1
+                if q < FS:
+                    k0, k1 = self.span(q)
+                    self.far1(0, k0, k1, ns)
+                    self.far2a(self.w, 0, k0, k1, ns)
+                if q >= 1:
+                    k0, k1 = self.span(q - 1)
+                    self.far2b(0, k0, k1, ns)
         self.n = 0
 
     def step(self, x):

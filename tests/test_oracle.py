@@ -90,16 +90,35 @@ def test_multiply_add_kat(oracle, n):
     assert np.all(r == 0) and np.all(i == 16)
 
 
+@pytest.mark.parametrize("kind", ["save", "add"])
 @pytest.mark.parametrize("B", [128, 512])
 @pytest.mark.parametrize("F", [8, 9, 10, 17, 127, 128, 129, 130, 512, 999, 1024])
-def test_overlap_save_identity(oracle, B, F):
-    """overlap_test.cpp:21-64: a no-op callback gives output == input (abs and RMSE 1e-5).
-    (The transform size follows the filter size only through next_order(B+F-1); the
-    restatement's stage uses F = B as the convolver does, which is the F >= B case.)"""
+def test_overlap_stage_identity(oracle, kind, B, F):
+    """overlap_test.cpp:21-64: overlap_save / overlap_add(B, F), a no-op callback gives
+    output == input (abs and RMSE 1e-5); transform_size >= B + F - 1 and the callback sees
+    transform_size / 2 + 1 bins (the restatement's transform size follows F)."""
+    n = oracle.overlap_transform_size(B, F)
+    assert n >= B + F - 1 and n // 2 < B + F - 1
     sig = oracle.noise(F, B * 8)
-    out = oracle.overlap_save_identity(sig, B)
+    out = oracle.overlap_stage(kind, sig, B, F)
     assert np.abs(out - sig).max() <= 1e-5
     assert np.sqrt(np.mean((out - sig) ** 2)) <= 1e-5
+    if F == B:  # the convolver's own stage (F = B) is the same as the dedicated restatement
+        ref = oracle.overlap_save_identity(sig, B) if kind == "save" else oracle.overlap_add_identity(sig, B)
+        assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("B,F", [(128, 8), (128, 129), (512, 999), (64, 64)])
+def test_overlap_save_filter_is_linear_convolution(oracle, B, F):
+    """overlap_save with the callback multiplying by the spectrum of an F-tap filter is the
+    linear convolution (n >= B + F - 1: no wrap reaches the kept samples), checked in float64."""
+    n = oracle.overlap_transform_size(B, F)
+    h = oracle.noise(700 + F, F)
+    G = np.fft.rfft(np.concatenate([h, np.zeros(n - F, np.float32)]).astype(np.float64)).astype(np.complex64)
+    x = oracle.noise(800 + B, B * 12)
+    out = oracle.overlap_stage("save", x, B, F, G)
+    ref = np.convolve(x.astype(np.float64), h.astype(np.float64))[: x.size]
+    assert np.abs(out - ref).max() / np.abs(ref).max() <= 1e-5
 
 
 @pytest.mark.parametrize("B", [128, 256, 512, 1024])
