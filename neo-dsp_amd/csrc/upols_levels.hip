@@ -161,13 +161,17 @@ struct slice_args {
     int f2grp;    // phase-1 window groups on: a unit in window j of its group takes segments 1..j in 2b
     cf* f2acc;    // as f1acc
     cf* f3ff;     // 2b's target far window [C][128][B]
+    void* tl;     // timeline builds (NEO_TIMELINE): per-workgroup records of the launch
 };
 
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
 // they meet, 16 columns each, column-major with padded strides
 constexpr int kT32Band = 192;                                       // [64, 256)
+constexpr int kT32Chunk = 96;                                       // partitions per LDS tile load
 constexpr int kFarLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange, twiddles
-constexpr int kT32Lds = 16 * ((kT32Band + 2) + (kT32Band + 34)) * int(sizeof(cf));  // toep_tile<32, 192>: 53760 B, 3 workgroups per CU
+// toep_tile<32, 192, ., 96>: 29184 B. With every role <= 36864 B (the far roles), 4 workgroups
+// fit a CU's 160 KB (the whole band in one tile, 53760 B, allowed 3)
+constexpr int kT32Lds = 16 * ((kT32Chunk + 2) + (kT32Chunk + 34)) * int(sizeof(cf));
 constexpr int kSliceLds = kFarLds > kT32Lds ? kFarLds : kT32Lds;
 
 // Block role (lanes 0 .. B/2 - 1 of the workgroup, the others idle): lane i gathers, for the
@@ -529,84 +533,96 @@ __device__ __forceinline__ void t32_walk(const cf* hc, const cf* xc, int ib, int
 
 // Toeplitz level with window T through LDS, for every level (band [a, b), b - a <= NB):
 // 32 / T units of 16 columns per workgroup, each with the whole window. A unit's filter rows
-// and the FDL rows they meet (b - a and b - a + T - 1 rows of 16 columns: its distinct data,
-// loaded once, coalesced) go to an LDS tile, column-major; lane (col, q4, half) then owns
-// outputs 4 q4 .. 4 q4 + 3 of its column over half of the band (t32_walk), and the halves
-// meet through LDS.
-template<int T, int NB, int JH>
+// and the FDL rows they meet go to an LDS tile, column-major, in chunks of NC partitions
+// (NC partitions of filter and NC + T - 1 FDL rows of 16 columns: the unit's distinct data,
+// loaded once, coalesced; the next chunk's loads in flight during the walk of this one); lane
+// (col, quad, half) then owns outputs 4 quad .. 4 quad + 3 of its column over half of each
+// chunk (t32_walk), and the halves meet through LDS at the end.
+template<int T, int NB, int JH, int NC = NB>
 struct toep_tile {
     static constexpr int UPW = 32 / T, LPU = 256 / UPW, NQ = LPU / 16;  // units per workgroup, lanes per unit
     static constexpr int TP = T / JH, QUADS = TP / 4, NG = NQ / QUADS;  // outputs per unit, lanes per column, band groups
-    static constexpr int HS = NB + 2, XS = NB + TP + 2;                 // even column strides (16-B aligned pair reads)
-    static constexpr int NH = (NB + NQ - 1) / NQ, NXL = (NB + TP - 1 + NQ - 1) / NQ;
+    static constexpr int HS = NC + 2, XS = NC + TP + 2;                 // even column strides (16-B aligned pair reads)
+    static constexpr int NH = (NC + NQ - 1) / NQ, NXL = (NC + TP - 1 + NQ - 1) / NQ;
     static constexpr int LDS = UPW * 16 * (HS + XS) * int(sizeof(cf));
-    static_assert(NG >= 2 && NQ % QUADS == 0 && TP % 4 == 0, "toeplitz tile geometry");
+    static_assert(NG >= 2 && NQ % QUADS == 0 && TP % 4 == 0 && NB % NC == 0, "toeplitz tile geometry");
 };
 
 // unit u = (column group u / JH, window part u mod JH of T / JH outputs); JH = 2 where a step
 // has few units (one channel: the part halves the longest chain of the step)
-template<int T, int NB, int JH>
+template<int T, int NB, int JH, int NC = NB>
 __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
 {
-    using G = toep_tile<T, NB, JH>;
+    using G = toep_tile<T, NB, JH, NC>;
     static_assert(G::LDS <= kSliceLds, "toeplitz tile");
     const int t = threadIdx.x, us = t / G::LPU, lt = t % G::LPU, col = lt & 15, q = lt >> 4;
-    cf* hs = reinterpret_cast<cf*>(smem) + us * 16 * (G::HS + G::XS);  // hs[col][m] = H[p = a + m]
-    cf* xs = hs + 16 * G::HS;                                          // xs[col][i] = X[the oldest row + i]
+    cf* hs = reinterpret_cast<cf*>(smem) + us * 16 * (G::HS + G::XS);  // hs[col][m] = H[p = a + mc + m]
+    cf* xs = hs + 16 * G::HS;                                          // xs[col][i] = X[the chunk's oldest row + i]
     const int u = ta.u0 + bid * G::UPW + us, gpc = sa.B / 16;
     const bool live = u < ta.u1;
     const int uc = live ? u : ta.u1 - 1, jp = uc % JH, cg = uc / JH, c = cg / gpc, g = cg - c * gpc;
-    const int k = g * 16 + col, nb = ta.b - ta.a, nx = nb + G::TP - 1, R = sa.ring, jpart = jp * G::TP;
-    int rb = ta.tw + jpart - (ta.b - 1);  // the oldest row (b - 1 < 256 < R: one wrap at most)
-    rb = rb < 0 ? rb + R : rb;
-    cf hv[G::NH], xv[G::NXL];  // every load of the lane in flight, then the LDS writes
-    if constexpr (G::UPW == 1) {  // channel uniform: buffer loads, row offsets in SGPRs
-        const int cu = __builtin_amdgcn_readfirstlane(c), ps8 = int(sa.pstride * int(sizeof(cf)));
-        const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(cu) * sa.cstride, int64_t(ta.b) * ps8);
-        const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(cu) * sa.cstride, int64_t(R) * ps8);
-#pragma unroll
-        for (int i = 0; i < G::NH; ++i) {
-            const int m = q + G::NQ * i;
-            if (m < nb) hv[i] = buf_ld(hres, (ta.a + m) * ps8 + k * int(sizeof(cf)), 0);
-        }
-#pragma unroll
-        for (int i = 0; i < G::NXL; ++i) {
-            const int r = q + G::NQ * i;
-            if (r < nx) xv[i] = buf_ld(xres, (rb + r >= R ? rb + r - R : rb + r) * ps8 + k * int(sizeof(cf)), 0);
-        }
-    } else {
-        const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
-        const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
-#pragma unroll
-        for (int i = 0; i < G::NH; ++i) {
-            const int m = q + G::NQ * i;
-            if (live && m < nb) hv[i] = ld_nt(Hc + int64_t(ta.a + m) * sa.pstride);
-        }
-#pragma unroll
-        for (int i = 0; i < G::NXL; ++i) {
-            const int r = q + G::NQ * i;
-            if (live && r < nx) xv[i] = ld_nt(Xc + int64_t(rb + r >= R ? rb + r - R : rb + r) * sa.pstride);
-        }
-    }
-    const int odd = nb & 1;  // FDL column shift: keeps the pair reads 16-B aligned (t32_walk)
-    if (live) {
-#pragma unroll
-        for (int i = 0; i < G::NH; ++i)
-            if (q + G::NQ * i < nb) hs[col * G::HS + q + G::NQ * i] = hv[i];
-#pragma unroll
-        for (int i = 0; i < G::NXL; ++i)
-            if (q + G::NQ * i < nx) xs[col * G::XS + odd + q + G::NQ * i] = xv[i];
-    }
-    __syncthreads();
+    const int k = g * 16 + col, nb = ta.b - ta.a, R = sa.ring, jpart = jp * G::TP;
     // lane (col, quad, group): outputs 4 quad .. 4 quad + 3 of the part, partitions of band group
-    const int grp = q / G::QUADS, j0 = 4 * (q - grp * G::QUADS), nq = ((nb + G::NG - 1) / G::NG + 1) & ~1;
-    const int m0 = grp * nq < nb ? grp * nq : nb, m1 = m0 + nq < nb ? m0 + nq : nb;
+    const int grp = q / G::QUADS, j0 = 4 * (q - grp * G::QUADS);
     f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
     const cf* hc = hs + col * G::HS;
-    const cf* xc = xs + col * G::XS + odd;
-    if (live && m0 < m1) {
-        if (g == 0) t32_walk<true>(hc, xc, j0 + nb - 1, m0, m1, col == 0, acc);  // uniform per unit
-        else t32_walk<false>(hc, xc, j0 + nb - 1, m0, m1, false, acc);
+    cf hv[G::NH], xv[G::NXL];  // one chunk's loads of the lane, all in flight
+    auto load = [&](int mc) {
+        const int nc = nb - mc < NC ? nb - mc : NC, nx = nc + G::TP - 1;
+        // the chunk's oldest row: tw + jpart - (a + mc + nc - 1) (b - 1 < 256 < R: one wrap at most)
+        int rb = ta.tw + jpart - (ta.a + mc + nc - 1);
+        rb = rb < 0 ? rb + R : rb;
+        if constexpr (G::UPW == 1) {  // channel uniform: buffer loads, row offsets in SGPRs
+            const int cu = __builtin_amdgcn_readfirstlane(c), ps8 = int(sa.pstride * int(sizeof(cf)));
+            const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(cu) * sa.cstride, int64_t(ta.b) * ps8);
+            const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(cu) * sa.cstride, int64_t(R) * ps8);
+#pragma unroll
+            for (int i = 0; i < G::NH; ++i) {
+                const int m = q + G::NQ * i;
+                if (m < nc) hv[i] = buf_ld(hres, (ta.a + mc + m) * ps8 + k * int(sizeof(cf)), 0);
+            }
+#pragma unroll
+            for (int i = 0; i < G::NXL; ++i) {
+                const int r = q + G::NQ * i;
+                if (r < nx) xv[i] = buf_ld(xres, (rb + r >= R ? rb + r - R : rb + r) * ps8 + k * int(sizeof(cf)), 0);
+            }
+        } else {
+            const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
+            const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
+#pragma unroll
+            for (int i = 0; i < G::NH; ++i) {
+                const int m = q + G::NQ * i;
+                if (live && m < nc) hv[i] = ld_nt(Hc + int64_t(ta.a + mc + m) * sa.pstride);
+            }
+#pragma unroll
+            for (int i = 0; i < G::NXL; ++i) {
+                const int r = q + G::NQ * i;
+                if (live && r < nx) xv[i] = ld_nt(Xc + int64_t(rb + r >= R ? rb + r - R : rb + r) * sa.pstride);
+            }
+        }
+    };
+    load(0);
+    for (int mc = 0; mc < nb; mc += NC) {  // uniform per workgroup
+        const int nc = nb - mc < NC ? nb - mc : NC, nx = nc + G::TP - 1;
+        const int odd = nc & 1;  // FDL column shift: keeps the pair reads 16-B aligned (t32_walk)
+        if (mc) __syncthreads();  // the previous chunk's walk is done with the tile
+        if (live) {
+#pragma unroll
+            for (int i = 0; i < G::NH; ++i)
+                if (q + G::NQ * i < nc) hs[col * G::HS + q + G::NQ * i] = hv[i];
+#pragma unroll
+            for (int i = 0; i < G::NXL; ++i)
+                if (q + G::NQ * i < nx) xs[col * G::XS + odd + q + G::NQ * i] = xv[i];
+        }
+        __syncthreads();
+        if (mc + NC < nb) load(mc + NC);  // the next chunk's loads in flight during this walk
+        const int nq = ((nc + G::NG - 1) / G::NG + 1) & ~1;
+        const int m0 = grp * nq < nc ? grp * nq : nc, m1 = m0 + nq < nc ? m0 + nq : nc;
+        const cf* xc = xs + col * G::XS + odd;
+        if (live && m0 < m1) {
+            if (g == 0) t32_walk<true>(hc, xc, j0 + nc - 1, m0, m1, col == 0, acc);  // uniform per unit
+            else t32_walk<false>(hc, xc, j0 + nc - 1, m0, m1, false, acc);
+        }
     }
     __syncthreads();  // the tiles are free: the band groups meet there
     constexpr int LG = 16 * G::QUADS;          // lanes per band group
@@ -635,7 +651,7 @@ __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_a
 // FDL rows through its L2). The band goes through an LDS tile in chunks of kBigNC
 // partitions; lane (col, quad, quarter) owns 4 outputs of the part over a quarter of each
 // chunk (t32_walk), and the quarters meet through LDS at the end.
-constexpr int kBigJH = 8, kBigJP = kBigT / kBigJH, kBigNC = 192;
+constexpr int kBigJH = 8, kBigJP = kBigT / kBigJH, kBigNC = 128;
 constexpr int kBigHS = kBigNC + 2, kBigXS = kBigNC + kBigJP + 2;  // even column strides
 static_assert(16 * (kBigHS + kBigXS) * int(sizeof(cf)) <= kSliceLds, "big level tile");
 
@@ -989,7 +1005,7 @@ __device__ __forceinline__ void far2b_role(const slice_args& sa, int bid, char* 
 }
 
 #ifndef NEO_ROLES
-#define NEO_ROLES 31  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2
+#define NEO_ROLES 63  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2a, 32 far 2b
 #endif
 
 // Toeplitz level L of the step kernel (window T = kLvT0 << L, geometry as toep_geom): runs the
@@ -1012,8 +1028,8 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
         if (NEO_ROLES & 2) toep_lds_role<16, 32, 1>(a, ta, bid, smem);
     } else if constexpr (L == 3) {
         if (NEO_ROLES & 4) {
-            if (ta.jh == 2) toep_lds_role<32, kT32Band, 2>(a, ta, bid, smem);  // uniform per launch
-            else toep_lds_role<32, kT32Band, 1>(a, ta, bid, smem);
+            if (ta.jh == 2) toep_lds_role<32, kT32Band, 2, kT32Chunk>(a, ta, bid, smem);  // uniform per launch
+            else toep_lds_role<32, kT32Band, 1, kT32Chunk>(a, ta, bid, smem);
         }
     } else {
         if (NEO_ROLES & 4) toep_big_role(a, ta, bid, smem);
@@ -1027,38 +1043,65 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
 // row w and reads its slabs / far field (finished in earlier launches); the slices read FDL
 // rows before the current window and write the next window's slabs / far field.
 #ifndef NEO_STEP_WPE
-#define NEO_STEP_WPE 3  // waves per SIMD the step kernel is compiled for (VGPR budget)
+#define NEO_STEP_WPE 4  // waves per SIMD the step kernel is compiled for (VGPR budget: 128)
 #endif
+// B = 1024 runs 512-lane workgroups (the block role's bin pairs): two waves per SIMD each
+template<int B>
+constexpr int step_wpe() { return B > 512 ? 2 : NEO_STEP_WPE; }
+// the roles of one workgroup; returns the role (timeline builds: 1 far 2b, 2 far 2a, 3 block,
+// 4 + L Toeplitz level L, 9 far phase 1)
 template<int B, bool OLA, int KMAX>
-__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(NEO_STEP_WPE))) void k_lvl_step(slice_args a)
+__device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
 {
-    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
     int bid = int(blockIdx.x);
     if (bid < a.f3nwg) {
-        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2b_role<KMAX>(a, bid, smem);
-        return;
+        if ((NEO_ROLES & 32) && threadIdx.x < 256) far2b_role<KMAX>(a, bid, smem);
+        return 1;
     }
     bid -= a.f3nwg;
     if (bid < a.f2nwg) {
         if ((NEO_ROLES & 16) && threadIdx.x < 256) far2a_role(a, bid, smem);
-        return;
+        return 2;
     }
     bid -= a.f2nwg;
     if (bid < a.nblk) {
         if (NEO_ROLES & 1) block_role<B, OLA>(a, bid, smem);
-        return;
+        return 3;
     }
     bid -= a.nblk;
-    if (threadIdx.x >= 256) return;
+    if (threadIdx.x >= 256) return 0;
     // level l has window T = kLvT0 << l (plan_levels), one code copy per level; largest first
-    if (toep_level<4>(a, bid, smem) || toep_level<3>(a, bid, smem) || toep_level<2>(a, bid, smem) ||
-        toep_level<1>(a, bid, smem) || toep_level<0>(a, bid, smem))
-        return;
+    if (toep_level<4>(a, bid, smem)) return 8;
+    if (toep_level<3>(a, bid, smem)) return 7;
+    if (toep_level<2>(a, bid, smem)) return 6;
+    if (toep_level<1>(a, bid, smem)) return 5;
+    if (toep_level<0>(a, bid, smem)) return 4;
     if (bid < a.f1nwg && (NEO_ROLES & 8)) {
         if (a.f1fpl == 4) far1_role<4, KMAX>(a, bid);
         else if (a.f1fpl == 2) far1_role<2, KMAX>(a, bid);
         else far1_role<1, KMAX>(a, bid);
     }
+    return 9;
+}
+
+template<int B, bool OLA, int KMAX>
+__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(step_wpe<B>()))) void k_lvl_step(slice_args a)
+{
+    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
+#ifdef NEO_TIMELINE  // diagnostic builds: per-workgroup start / end (100 MHz clock) and role
+    const unsigned long long t0 = wall_clock64();
+    const int role = lvl_roles<B, OLA, KMAX>(a, smem);
+    __syncthreads();
+    if (threadIdx.x == 0 && a.tl) {
+        unsigned long long* r = static_cast<unsigned long long*>(a.tl) + 3 * int64_t(blockIdx.x);
+        r[0] = t0;
+        r[1] = wall_clock64();
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15;  // HW_REG_XCC_ID
+        r[2] = (unsigned long long)(role) | ((unsigned long long)(__smid()) << 32) | ((unsigned long long)(xcc) << 56);
+    }
+#else
+    (void)lvl_roles<B, OLA, KMAX>(a, smem);
+#endif
 }
 
 // Segment spectra (grid C x NSEG x B/16): hf[c][s][f][k] = DFT256 over r < 128 of
@@ -1250,14 +1293,30 @@ static slice_args base_args(const upols_t* h)
     return a;
 }
 
-static int launch_step_kernel(const upols_t* h, const slice_args& a, hipStream_t s)
+#ifdef NEO_TIMELINE
+// diagnostic builds: the records of the last step-kernel launch of a handle
+static void* g_tl = nullptr;
+static int64_t g_tl_n = 0, g_tl_cap = 0;
+#endif
+
+static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStream_t s)
 {
+    slice_args a = a_in;
     const unsigned grid = unsigned(a.f3nwg + a.f2nwg + a.nblk + a.f1nwg) + [&] {
         unsigned t = 0;
         for (int l = 0; l < a.ntp; ++l) t += unsigned(a.tp[l].nwg);
         return t;
     }();
     if (!grid) return NEO_HIP_OK;
+#ifdef NEO_TIMELINE
+    if (int64_t(grid) > g_tl_cap) {
+        (void)hipFree(g_tl);
+        g_tl_cap = int64_t(grid) * 2;
+        NEO_HIP_CHECK(hipMalloc(&g_tl, size_t(g_tl_cap) * 24));
+    }
+    a.tl = g_tl;
+    g_tl_n = grid;
+#endif
     // pairs-only build where the window group is <= 2 (fewer VGPRs: every shape below
     // kFarGroupUnits), else the build for any group
 #define NEO_LVL(OL, KM)                                                                                        \
@@ -1459,3 +1518,16 @@ extern "C" NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* wi
     *windows = h->lv.nseg ? neo_hip::far_group(h) : 0;
     return NEO_HIP_OK;
 }
+
+#ifdef NEO_TIMELINE
+// diagnostic builds only (not in include/neo_hip.h): copy the last step launch's per-workgroup
+// records {start, end, role | cu << 32} (wall_clock64 ticks) into out, up to cap workgroups
+extern "C" NEO_HIP_API int neo_hip_diag_timeline(unsigned long long* out, int64_t cap, int64_t* count)
+{
+    NEO_HIP_CHECK(hipDeviceSynchronize());
+    const int64_t n = std::min(cap, neo_hip::g_tl_n);
+    if (n > 0) NEO_HIP_CHECK(hipMemcpy(out, neo_hip::g_tl, size_t(n) * 24, hipMemcpyDeviceToHost));
+    if (count) *count = neo_hip::g_tl_n;
+    return NEO_HIP_OK;
+}
+#endif
