@@ -31,6 +31,20 @@
 
 namespace neo_hip {
 
+// timeline builds: thread 0 stamps the workgroup's mid-point (a role's loads landed)
+#ifdef NEO_TIMELINE
+#define NEO_TL_MARK(a)                                                                                 \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && (a).tl)                                                                \
+            static_cast<unsigned long long*>((a).tl)[4 * int64_t(blockIdx.x) + 3] = wall_clock64();    \
+    } while (0)
+#else
+#define NEO_TL_MARK(a) \
+    do {               \
+    } while (0)
+#endif
+
+
 // ---------------------------------------------------------------------------------------
 // level plan (host; also exported for the CPU schedule test, neo_hip_upols_level_plan)
 void plan_levels(int P, level_plan& lp, int far)
@@ -167,11 +181,10 @@ struct slice_args {
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
 // they meet, 16 columns each, column-major with padded strides
 constexpr int kT32Band = 192;                                       // [64, 256)
-constexpr int kT32Chunk = 96;                                       // partitions per LDS tile load
 constexpr int kFarLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange, twiddles
-// toep_tile<32, 192, ., 96>: 29184 B. With every role <= 36864 B (the far roles), 4 workgroups
-// fit a CU's 160 KB (the whole band in one tile, 53760 B, allowed 3)
-constexpr int kT32Lds = 16 * ((kT32Chunk + 2) + (kT32Chunk + 34)) * int(sizeof(cf));
+// toep_tile<32, 192>: 53760 B, 3 workgroups per CU (VGPRs allow 3 too; the band in two chunks
+// of 96, 29184 B, with a 128-VGPR budget for 4 per CU measured slower: spills, serialized chunks)
+constexpr int kT32Lds = 16 * ((kT32Band + 2) + (kT32Band + 34)) * int(sizeof(cf));
 constexpr int kSliceLds = kFarLds > kT32Lds ? kFarLds : kT32Lds;
 
 // Block role (lanes 0 .. B/2 - 1 of the workgroup, the others idle): lane i gathers, for the
@@ -304,6 +317,7 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
         }
     }
     __syncthreads();
+    NEO_TL_MARK(a);
     if (pair) {
         // bin pair (k0, k1): r2c split, FDL row w, Y = rest + H0 X, c2r join; w(B - k) = -conj(w(k))
         const cf wa = k0 == 0 ? cf{1.f, 0.f} : twiddle<2 * B, -1>(tw + K::TW1, k0);
@@ -533,96 +547,85 @@ __device__ __forceinline__ void t32_walk(const cf* hc, const cf* xc, int ib, int
 
 // Toeplitz level with window T through LDS, for every level (band [a, b), b - a <= NB):
 // 32 / T units of 16 columns per workgroup, each with the whole window. A unit's filter rows
-// and the FDL rows they meet go to an LDS tile, column-major, in chunks of NC partitions
-// (NC partitions of filter and NC + T - 1 FDL rows of 16 columns: the unit's distinct data,
-// loaded once, coalesced; the next chunk's loads in flight during the walk of this one); lane
-// (col, quad, half) then owns outputs 4 quad .. 4 quad + 3 of its column over half of each
-// chunk (t32_walk), and the halves meet through LDS at the end.
-template<int T, int NB, int JH, int NC = NB>
+// and the FDL rows they meet (b - a and b - a + T - 1 rows of 16 columns: its distinct data,
+// loaded once, coalesced) go to an LDS tile, column-major; lane (col, q4, half) then owns
+// outputs 4 q4 .. 4 q4 + 3 of its column over half of the band (t32_walk), and the halves
+// meet through LDS.
+template<int T, int NB, int JH>
 struct toep_tile {
     static constexpr int UPW = 32 / T, LPU = 256 / UPW, NQ = LPU / 16;  // units per workgroup, lanes per unit
     static constexpr int TP = T / JH, QUADS = TP / 4, NG = NQ / QUADS;  // outputs per unit, lanes per column, band groups
-    static constexpr int HS = NC + 2, XS = NC + TP + 2;                 // even column strides (16-B aligned pair reads)
-    static constexpr int NH = (NC + NQ - 1) / NQ, NXL = (NC + TP - 1 + NQ - 1) / NQ;
+    static constexpr int HS = NB + 2, XS = NB + TP + 2;                 // even column strides (16-B aligned pair reads)
+    static constexpr int NH = (NB + NQ - 1) / NQ, NXL = (NB + TP - 1 + NQ - 1) / NQ;
     static constexpr int LDS = UPW * 16 * (HS + XS) * int(sizeof(cf));
-    static_assert(NG >= 2 && NQ % QUADS == 0 && TP % 4 == 0 && NB % NC == 0, "toeplitz tile geometry");
+    static_assert(NG >= 2 && NQ % QUADS == 0 && TP % 4 == 0, "toeplitz tile geometry");
 };
 
 // unit u = (column group u / JH, window part u mod JH of T / JH outputs); JH = 2 where a step
 // has few units (one channel: the part halves the longest chain of the step)
-template<int T, int NB, int JH, int NC = NB>
+template<int T, int NB, int JH>
 __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_arg& ta, int bid, char* smem)
 {
-    using G = toep_tile<T, NB, JH, NC>;
+    using G = toep_tile<T, NB, JH>;
     static_assert(G::LDS <= kSliceLds, "toeplitz tile");
     const int t = threadIdx.x, us = t / G::LPU, lt = t % G::LPU, col = lt & 15, q = lt >> 4;
-    cf* hs = reinterpret_cast<cf*>(smem) + us * 16 * (G::HS + G::XS);  // hs[col][m] = H[p = a + mc + m]
-    cf* xs = hs + 16 * G::HS;                                          // xs[col][i] = X[the chunk's oldest row + i]
+    cf* hs = reinterpret_cast<cf*>(smem) + us * 16 * (G::HS + G::XS);  // hs[col][m] = H[p = a + m]
+    cf* xs = hs + 16 * G::HS;                                          // xs[col][i] = X[the oldest row + i]
     const int u = ta.u0 + bid * G::UPW + us, gpc = sa.B / 16;
     const bool live = u < ta.u1;
     const int uc = live ? u : ta.u1 - 1, jp = uc % JH, cg = uc / JH, c = cg / gpc, g = cg - c * gpc;
-    const int k = g * 16 + col, nb = ta.b - ta.a, R = sa.ring, jpart = jp * G::TP;
+    const int k = g * 16 + col, nb = ta.b - ta.a, nx = nb + G::TP - 1, R = sa.ring, jpart = jp * G::TP;
+    int rb = ta.tw + jpart - (ta.b - 1);  // the oldest row (b - 1 < 256 < R: one wrap at most)
+    rb = rb < 0 ? rb + R : rb;
+    cf hv[G::NH], xv[G::NXL];  // every load of the lane in flight, then the LDS writes
+    if constexpr (G::UPW == 1) {  // channel uniform: buffer loads, row offsets in SGPRs
+        const int cu = __builtin_amdgcn_readfirstlane(c), ps8 = int(sa.pstride * int(sizeof(cf)));
+        const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(cu) * sa.cstride, int64_t(ta.b) * ps8);
+        const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(cu) * sa.cstride, int64_t(R) * ps8);
+#pragma unroll
+        for (int i = 0; i < G::NH; ++i) {
+            const int m = q + G::NQ * i;
+            if (m < nb) hv[i] = buf_ld(hres, (ta.a + m) * ps8 + k * int(sizeof(cf)), 0);
+        }
+#pragma unroll
+        for (int i = 0; i < G::NXL; ++i) {
+            const int r = q + G::NQ * i;
+            if (r < nx) xv[i] = buf_ld(xres, (rb + r >= R ? rb + r - R : rb + r) * ps8 + k * int(sizeof(cf)), 0);
+        }
+    } else {
+        const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
+        const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
+#pragma unroll
+        for (int i = 0; i < G::NH; ++i) {
+            const int m = q + G::NQ * i;
+            if (live && m < nb) hv[i] = ld_nt(Hc + int64_t(ta.a + m) * sa.pstride);
+        }
+#pragma unroll
+        for (int i = 0; i < G::NXL; ++i) {
+            const int r = q + G::NQ * i;
+            if (live && r < nx) xv[i] = ld_nt(Xc + int64_t(rb + r >= R ? rb + r - R : rb + r) * sa.pstride);
+        }
+    }
+    const int odd = nb & 1;  // FDL column shift: keeps the pair reads 16-B aligned (t32_walk)
+    if (live) {
+#pragma unroll
+        for (int i = 0; i < G::NH; ++i)
+            if (q + G::NQ * i < nb) hs[col * G::HS + q + G::NQ * i] = hv[i];
+#pragma unroll
+        for (int i = 0; i < G::NXL; ++i)
+            if (q + G::NQ * i < nx) xs[col * G::XS + odd + q + G::NQ * i] = xv[i];
+    }
+    __syncthreads();
+    NEO_TL_MARK(sa);
     // lane (col, quad, group): outputs 4 quad .. 4 quad + 3 of the part, partitions of band group
-    const int grp = q / G::QUADS, j0 = 4 * (q - grp * G::QUADS);
+    const int grp = q / G::QUADS, j0 = 4 * (q - grp * G::QUADS), nq = ((nb + G::NG - 1) / G::NG + 1) & ~1;
+    const int m0 = grp * nq < nb ? grp * nq : nb, m1 = m0 + nq < nb ? m0 + nq : nb;
     f2v acc[4] = {f2v(0.f), f2v(0.f), f2v(0.f), f2v(0.f)};
     const cf* hc = hs + col * G::HS;
-    cf hv[G::NH], xv[G::NXL];  // one chunk's loads of the lane, all in flight
-    auto load = [&](int mc) {
-        const int nc = nb - mc < NC ? nb - mc : NC, nx = nc + G::TP - 1;
-        // the chunk's oldest row: tw + jpart - (a + mc + nc - 1) (b - 1 < 256 < R: one wrap at most)
-        int rb = ta.tw + jpart - (ta.a + mc + nc - 1);
-        rb = rb < 0 ? rb + R : rb;
-        if constexpr (G::UPW == 1) {  // channel uniform: buffer loads, row offsets in SGPRs
-            const int cu = __builtin_amdgcn_readfirstlane(c), ps8 = int(sa.pstride * int(sizeof(cf)));
-            const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(cu) * sa.cstride, int64_t(ta.b) * ps8);
-            const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.fdl + int64_t(cu) * sa.cstride, int64_t(R) * ps8);
-#pragma unroll
-            for (int i = 0; i < G::NH; ++i) {
-                const int m = q + G::NQ * i;
-                if (m < nc) hv[i] = buf_ld(hres, (ta.a + mc + m) * ps8 + k * int(sizeof(cf)), 0);
-            }
-#pragma unroll
-            for (int i = 0; i < G::NXL; ++i) {
-                const int r = q + G::NQ * i;
-                if (r < nx) xv[i] = buf_ld(xres, (rb + r >= R ? rb + r - R : rb + r) * ps8 + k * int(sizeof(cf)), 0);
-            }
-        } else {
-            const cf* Hc = sa.H + int64_t(c) * sa.cstride + k;
-            const cf* Xc = sa.fdl + int64_t(c) * sa.cstride + k;
-#pragma unroll
-            for (int i = 0; i < G::NH; ++i) {
-                const int m = q + G::NQ * i;
-                if (live && m < nc) hv[i] = ld_nt(Hc + int64_t(ta.a + mc + m) * sa.pstride);
-            }
-#pragma unroll
-            for (int i = 0; i < G::NXL; ++i) {
-                const int r = q + G::NQ * i;
-                if (live && r < nx) xv[i] = ld_nt(Xc + int64_t(rb + r >= R ? rb + r - R : rb + r) * sa.pstride);
-            }
-        }
-    };
-    load(0);
-    for (int mc = 0; mc < nb; mc += NC) {  // uniform per workgroup
-        const int nc = nb - mc < NC ? nb - mc : NC, nx = nc + G::TP - 1;
-        const int odd = nc & 1;  // FDL column shift: keeps the pair reads 16-B aligned (t32_walk)
-        if (mc) __syncthreads();  // the previous chunk's walk is done with the tile
-        if (live) {
-#pragma unroll
-            for (int i = 0; i < G::NH; ++i)
-                if (q + G::NQ * i < nc) hs[col * G::HS + q + G::NQ * i] = hv[i];
-#pragma unroll
-            for (int i = 0; i < G::NXL; ++i)
-                if (q + G::NQ * i < nx) xs[col * G::XS + odd + q + G::NQ * i] = xv[i];
-        }
-        __syncthreads();
-        if (mc + NC < nb) load(mc + NC);  // the next chunk's loads in flight during this walk
-        const int nq = ((nc + G::NG - 1) / G::NG + 1) & ~1;
-        const int m0 = grp * nq < nc ? grp * nq : nc, m1 = m0 + nq < nc ? m0 + nq : nc;
-        const cf* xc = xs + col * G::XS + odd;
-        if (live && m0 < m1) {
-            if (g == 0) t32_walk<true>(hc, xc, j0 + nc - 1, m0, m1, col == 0, acc);  // uniform per unit
-            else t32_walk<false>(hc, xc, j0 + nc - 1, m0, m1, false, acc);
-        }
+    const cf* xc = xs + col * G::XS + odd;
+    if (live && m0 < m1) {
+        if (g == 0) t32_walk<true>(hc, xc, j0 + nb - 1, m0, m1, col == 0, acc);  // uniform per unit
+        else t32_walk<false>(hc, xc, j0 + nb - 1, m0, m1, false, acc);
     }
     __syncthreads();  // the tiles are free: the band groups meet there
     constexpr int LG = 16 * G::QUADS;          // lanes per band group
@@ -651,7 +654,7 @@ __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_a
 // FDL rows through its L2). The band goes through an LDS tile in chunks of kBigNC
 // partitions; lane (col, quad, quarter) owns 4 outputs of the part over a quarter of each
 // chunk (t32_walk), and the quarters meet through LDS at the end.
-constexpr int kBigJH = 8, kBigJP = kBigT / kBigJH, kBigNC = 128;
+constexpr int kBigJH = 8, kBigJP = kBigT / kBigJH, kBigNC = 192;
 constexpr int kBigHS = kBigNC + 2, kBigXS = kBigNC + kBigJP + 2;  // even column strides
 static_assert(16 * (kBigHS + kBigXS) * int(sizeof(cf)) <= kSliceLds, "big level tile");
 
@@ -923,6 +926,7 @@ __device__ __forceinline__ void far2a_role(const slice_args& sa, int bid, char* 
         }
         __syncthreads();  // twiddles; the previous segment's LDS use is done
         col_fft<-1, 16>(x, lds, tws, a, cp, true);
+        if (s == 0) NEO_TL_MARK(sa);
         if (unit0) bin0_exchange<true>(x, z, a, cp);  // uniform per workgroup
 #pragma unroll
         for (int i = 0; i < 16; ++i) buf_st(x[i], xres, vo, slot(s) * spec + int(16 * i * fs * int(sizeof(cf))));
@@ -995,6 +999,7 @@ __device__ __forceinline__ void far2b_role(const slice_args& sa, int bid, char* 
         }
     }
     __syncthreads();  // twiddles
+    NEO_TL_MARK(sa);
     if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
     col_fft<1, 16>(v, lds, tws, a, cp, true);
     constexpr float sc = 1.0f / kFN;
@@ -1028,8 +1033,8 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
         if (NEO_ROLES & 2) toep_lds_role<16, 32, 1>(a, ta, bid, smem);
     } else if constexpr (L == 3) {
         if (NEO_ROLES & 4) {
-            if (ta.jh == 2) toep_lds_role<32, kT32Band, 2, kT32Chunk>(a, ta, bid, smem);  // uniform per launch
-            else toep_lds_role<32, kT32Band, 1, kT32Chunk>(a, ta, bid, smem);
+            if (ta.jh == 2) toep_lds_role<32, kT32Band, 2>(a, ta, bid, smem);  // uniform per launch
+            else toep_lds_role<32, kT32Band, 1>(a, ta, bid, smem);
         }
     } else {
         if (NEO_ROLES & 4) toep_big_role(a, ta, bid, smem);
@@ -1043,7 +1048,7 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
 // row w and reads its slabs / far field (finished in earlier launches); the slices read FDL
 // rows before the current window and write the next window's slabs / far field.
 #ifndef NEO_STEP_WPE
-#define NEO_STEP_WPE 4  // waves per SIMD the step kernel is compiled for (VGPR budget: 128)
+#define NEO_STEP_WPE 3  // waves per SIMD the step kernel is compiled for (VGPR budget: 168)
 #endif
 // B = 1024 runs 512-lane workgroups (the block role's bin pairs): two waves per SIMD each
 template<int B>
@@ -1093,7 +1098,7 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
     const int role = lvl_roles<B, OLA, KMAX>(a, smem);
     __syncthreads();
     if (threadIdx.x == 0 && a.tl) {
-        unsigned long long* r = static_cast<unsigned long long*>(a.tl) + 3 * int64_t(blockIdx.x);
+        unsigned long long* r = static_cast<unsigned long long*>(a.tl) + 4 * int64_t(blockIdx.x);
         r[0] = t0;
         r[1] = wall_clock64();
         const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15;  // HW_REG_XCC_ID
@@ -1312,7 +1317,8 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
     if (int64_t(grid) > g_tl_cap) {
         (void)hipFree(g_tl);
         g_tl_cap = int64_t(grid) * 2;
-        NEO_HIP_CHECK(hipMalloc(&g_tl, size_t(g_tl_cap) * 24));
+        NEO_HIP_CHECK(hipMalloc(&g_tl, size_t(g_tl_cap) * 32));
+        NEO_HIP_CHECK(hipMemset(g_tl, 0, size_t(g_tl_cap) * 32));
     }
     a.tl = g_tl;
     g_tl_n = grid;
@@ -1521,12 +1527,13 @@ extern "C" NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* wi
 
 #ifdef NEO_TIMELINE
 // diagnostic builds only (not in include/neo_hip.h): copy the last step launch's per-workgroup
-// records {start, end, role | cu << 32} (wall_clock64 ticks) into out, up to cap workgroups
+// records {start, end, role | cu << 32 | xcc << 56, mid} (wall_clock64 ticks; mid 0 where the
+// role stamps none) into out, up to cap workgroups
 extern "C" NEO_HIP_API int neo_hip_diag_timeline(unsigned long long* out, int64_t cap, int64_t* count)
 {
     NEO_HIP_CHECK(hipDeviceSynchronize());
     const int64_t n = std::min(cap, neo_hip::g_tl_n);
-    if (n > 0) NEO_HIP_CHECK(hipMemcpy(out, neo_hip::g_tl, size_t(n) * 24, hipMemcpyDeviceToHost));
+    if (n > 0) NEO_HIP_CHECK(hipMemcpy(out, neo_hip::g_tl, size_t(n) * 32, hipMemcpyDeviceToHost));
     if (count) *count = neo_hip::g_tl_n;
     return NEO_HIP_OK;
 }

@@ -49,7 +49,7 @@ def main():
     feed.run(args.warmup)
     torch.cuda.synchronize()
     cap = 1 << 16
-    buf = np.zeros((cap, 3), np.uint64)
+    buf = np.zeros((cap, 4), np.uint64)
     cnt = ctypes.c_int64()
     per = {}
     per_xcc = {}
@@ -80,18 +80,22 @@ def main():
             d["smed"].append(np.median(st[m]))
             d["s1"].append(st[m].max())
             dur = en[m] - st[m]
+            mid = r[:, 3][m]
+            if (mid > 0).all():  # the role's mid-point stamp: loads landed (us after the workgroup's start)
+                d.setdefault("mid", []).append(np.median((mid - r[:, 0][m]) / 100.0))
             d["dmed"].append(np.median(dur))
             d["dmax"].append(dur.max())
             d["e1"].append(en[m].max())
     out = {"workload": args.workload, "steps": args.steps, "span_us_median": float(np.median(spans)),
            "span_us_p90": float(np.percentile(spans, 90)), "roles": {}}
     print(f"{args.workload}: step span median {np.median(spans):.2f} us, p90 {np.percentile(spans, 90):.2f}")
-    print(f"{'role':8s} {'wgs':>5s} {'start0':>7s} {'startmed':>8s} {'start1':>7s} {'durmed':>7s} {'durmax':>7s} {'end1':>7s}")
+    print(f"{'role':8s} {'wgs':>5s} {'start0':>7s} {'startmed':>8s} {'start1':>7s} {'durmed':>7s} {'durmax':>7s} {'end1':>7s} "
+          f"{'midmed':>7s}")
     for k in sorted(per):
         d = {key: float(np.median(v)) for key, v in per[k].items()}
         out["roles"][ROLES.get(k, str(k))] = d
         print(f"{ROLES.get(k, str(k)):8s} {d['n']:5.0f} {d['s0']:7.2f} {d['smed']:8.2f} {d['s1']:7.2f} {d['dmed']:7.2f} "
-              f"{d['dmax']:7.2f} {d['e1']:7.2f}")
+              f"{d['dmax']:7.2f} {d['e1']:7.2f} {d.get('mid', float('nan')):7.2f}")
     out["xcc"] = {}
     for xc in sorted(per_xcc):
         d = {key: float(np.median(v)) for key, v in per_xcc[xc].items()}
