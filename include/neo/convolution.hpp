@@ -347,6 +347,71 @@ private:
     std::vector<float> _buf;
 };
 
+namespace detail {
+struct overlap_deleter {
+    void operator()(neo_hip_overlap* h) const noexcept { neo_hip_overlap_destroy(h); }
+};
+
+/// overlap_save / overlap_add (overlap_save.hpp:19-112, overlap_add.hpp:23-107) on the GPU:
+/// ctor(block_size, filter_size), transform size 2^next_order(B + F - 1); operator()(block,
+/// callback) runs the window update and rfft on the device, hands the callback the
+/// transform_size() / 2 + 1 bins (a host view it may modify in place), then the irfft, 1/n and
+/// the output block, in place.
+template<typename Complex, int Kind>
+struct hip_overlap {
+    static_assert(std::same_as<Complex, std::complex<float>>);
+    using value_type = Complex;
+    using complex_type = Complex;
+    using real_type = typename Complex::value_type;
+    using size_type = std::size_t;
+
+    hip_overlap(size_type block_size, size_type filter_size)
+    {
+        neo_hip_overlap* h = nullptr;
+        neo::hip::check(neo_hip_overlap_create(Kind, 1, std::int64_t(block_size), std::int64_t(filter_size),
+                                               neo::hip::detail::default_device(), &h));
+        _h.reset(h);
+        std::int64_t b = 0, f = 0, n = 0;
+        neo::hip::check(neo_hip_overlap_info(h, &b, &f, &n));
+        _block = size_type(b);
+        _filter = size_type(f);
+        _n = size_type(n);
+        _bins.resize(_n / 2 + 1);
+        _buf.resize(_block);
+    }
+
+    [[nodiscard]] auto block_size() const noexcept -> size_type { return _block; }
+    [[nodiscard]] auto filter_size() const noexcept -> size_type { return _filter; }
+    [[nodiscard]] auto transform_size() const noexcept -> size_type { return _n; }
+
+    template<typename Vec, typename Callback>
+        requires neo::hip::detail::vector_like<Vec>
+    auto operator()(Vec block, Callback callback) -> void
+    {
+        float* io = _buf.data();
+        bool const direct = neo::hip::detail::contiguous(block) && std::size_t(block.extent(0)) == _block;
+        if (direct) io = block.data_handle();
+        else neo::hip::detail::gather(block, _buf.data());
+        neo::hip::check_or_abort(neo_hip_overlap_forward(_h.get(), io, std::int64_t(_block), _bins.data(), 0, nullptr));
+        callback(neo::hip::make_view(_bins.data(), _bins.size()));
+        neo::hip::check_or_abort(neo_hip_overlap_inverse(_h.get(), _bins.data(), io, std::int64_t(_block), 0, nullptr));
+        if (!direct) neo::hip::detail::scatter(_buf.data(), block);
+    }
+
+private:
+    std::unique_ptr<neo_hip_overlap, overlap_deleter> _h;
+    size_type _block{}, _filter{}, _n{};
+    std::vector<Complex> _bins;
+    std::vector<float> _buf;
+};
+}  // namespace detail
+
+template<typename Complex>
+using overlap_save = detail::hip_overlap<Complex, 0>;
+
+template<typename Complex>
+using overlap_add = detail::hip_overlap<Complex, 1>;
+
 template<typename Complex>
 using upols_convolver = hip_upols_convolver<Complex>;
 

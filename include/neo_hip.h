@@ -218,6 +218,26 @@ NEO_HIP_API int neo_hip_upols_timing_detail(neo_hip_upols* h, double* ms, int64_
 NEO_HIP_API int neo_hip_upols_step_times(neo_hip_upols* h, double* ms, int64_t cap, int64_t* count);
 NEO_HIP_API int neo_hip_upols_info(neo_hip_upols* h, int* channels, int* block, int* partitions, int* splits);
 
+/* -- standalone overlap stages (overlap_save.hpp:19-112, overlap_add.hpp:23-107) -----------
+ * C independent stages of block B (a power of two) for filters of F taps, transform size
+ * n = 2^next_order(B + F - 1) (<= 2^27). The reference's operator()(block, callback) split
+ * at the callback: forward = window update + rfft -> spectrum [C][n/2 + 1] complex (what the
+ * callback sees), inverse = irfft of the (processed) spectrum, 1/n, output block. kind 0 =
+ * overlap_save (window slid left by B, block at its end; output = the last B samples), 1 =
+ * overlap_add (block at the window's start, [B, 2B) zeroed; output = first B + overlap, the
+ * irfft written back into the window as the reference does). Blocks: channel c at in + c*ld.
+ * Host memory: synchronous (own stream if NULL); device memory: asynchronous on `stream`. */
+typedef struct neo_hip_overlap neo_hip_overlap;
+NEO_HIP_API int neo_hip_overlap_create(int kind, int channels, int64_t block, int64_t filter, int device,
+                                       neo_hip_overlap** h);
+NEO_HIP_API int neo_hip_overlap_destroy(neo_hip_overlap* h);
+NEO_HIP_API int neo_hip_overlap_info(neo_hip_overlap* h, int64_t* block, int64_t* filter, int64_t* transform_size);
+NEO_HIP_API int neo_hip_overlap_reset(neo_hip_overlap* h);
+NEO_HIP_API int neo_hip_overlap_forward(neo_hip_overlap* h, const float* in, int64_t ld_in, void* spectrum,
+                                        int is_device, void* stream);
+NEO_HIP_API int neo_hip_overlap_inverse(neo_hip_overlap* h, const void* spectrum, float* out, int64_t ld_out,
+                                        int is_device, void* stream);
+
 /* -- setup path (uniform_partition.hpp:12-26, normalize_impulse.hpp:11-33) -- */
 NEO_HIP_API int neo_hip_num_partitions(int64_t length, int block, int64_t* partitions);
 /* ir [C][L] float -> out [C][P][B+1] complex; host or device pointers. */

@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 namespace neo_hip {
@@ -1042,6 +1043,18 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
     return true;
 }
 
+// the lanes past 256 of a larger workgroup: move bid past level L's workgroups (or stop there)
+template<int L>
+__device__ __forceinline__ bool toep_skip(const slice_args& a, int& bid)
+{
+    if (L >= a.ntp) return false;
+    if (bid >= a.tp[L].nwg) {
+        bid -= a.tp[L].nwg;
+        return false;
+    }
+    return true;
+}
+
 // The step kernel (k_lvl_step): one launch per block, workgroups by role, the longest chains
 // first -- far phase 2, the block itself, the Toeplitz slices (largest window first), far
 // phase 1. No role reads what another role of the same launch writes: the block writes FDL
@@ -1053,40 +1066,81 @@ __device__ __forceinline__ bool toep_level(const slice_args& a, int& bid, char* 
 // B = 1024 runs 512-lane workgroups (the block role's bin pairs): two waves per SIMD each
 template<int B>
 constexpr int step_wpe() { return B > 512 ? 2 : NEO_STEP_WPE; }
-// the roles of one workgroup; returns the role (timeline builds: 1 far 2b, 2 far 2a, 3 block,
-// 4 + L Toeplitz level L, 9 far phase 1)
+// the roles of one workgroup, in dispatch order (the longest chains first); returns the role
+// (timeline builds: 1 far 2b, 2 far 2a, 3 block, 4 + L Toeplitz level L, 9 far phase 1)
+#ifndef NEO_ORDER
+#define NEO_ORDER 0  // diagnostic builds: 1 far phase 1 before the Toeplitz levels T <= 16, 2 Toeplitz T >= 32 first
+#endif
 template<int B, bool OLA, int KMAX>
 __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
 {
     int bid = int(blockIdx.x);
-    if (bid < a.f3nwg) {
+    auto far2b = [&]() {
+        if (bid >= a.f3nwg) {
+            bid -= a.f3nwg;
+            return false;
+        }
         if ((NEO_ROLES & 32) && threadIdx.x < 256) far2b_role<KMAX>(a, bid, smem);
-        return 1;
-    }
-    bid -= a.f3nwg;
-    if (bid < a.f2nwg) {
+        return true;
+    };
+    auto far2a = [&]() {
+        if (bid >= a.f2nwg) {
+            bid -= a.f2nwg;
+            return false;
+        }
         if ((NEO_ROLES & 16) && threadIdx.x < 256) far2a_role(a, bid, smem);
-        return 2;
-    }
-    bid -= a.f2nwg;
-    if (bid < a.nblk) {
+        return true;
+    };
+    auto block = [&]() {
+        if (bid >= a.nblk) {
+            bid -= a.nblk;
+            return false;
+        }
         if (NEO_ROLES & 1) block_role<B, OLA>(a, bid, smem);
-        return 3;
-    }
-    bid -= a.nblk;
-    if (threadIdx.x >= 256) return 0;
-    // level l has window T = kLvT0 << l (plan_levels), one code copy per level; largest first
-    if (toep_level<4>(a, bid, smem)) return 8;
-    if (toep_level<3>(a, bid, smem)) return 7;
-    if (toep_level<2>(a, bid, smem)) return 6;
-    if (toep_level<1>(a, bid, smem)) return 5;
-    if (toep_level<0>(a, bid, smem)) return 4;
-    if (bid < a.f1nwg && (NEO_ROLES & 8)) {
-        if (a.f1fpl == 4) far1_role<4, KMAX>(a, bid);
-        else if (a.f1fpl == 2) far1_role<2, KMAX>(a, bid);
-        else far1_role<1, KMAX>(a, bid);
-    }
-    return 9;
+        return true;
+    };
+    auto far1 = [&]() {
+        if (bid >= a.f1nwg) {
+            bid -= a.f1nwg;
+            return false;
+        }
+        if ((NEO_ROLES & 8) && threadIdx.x < 256) {
+            if (a.f1fpl == 4) far1_role<4, KMAX>(a, bid);
+            else if (a.f1fpl == 2) far1_role<2, KMAX>(a, bid);
+            else far1_role<1, KMAX>(a, bid);
+        }
+        return true;
+    };
+    // Toeplitz level L (window T = kLvT0 << L, plan_levels), one code copy per level; workgroups
+    // of more than 256 lanes (B = 1024) take part with their first 256
+    auto toep = [&](auto L) { return threadIdx.x < 256 ? toep_level<decltype(L)::value>(a, bid, smem)
+                                                       : toep_skip<decltype(L)::value>(a, bid); };
+    using L0 = std::integral_constant<int, 0>;
+    using L1 = std::integral_constant<int, 1>;
+    using L2 = std::integral_constant<int, 2>;
+    using L3 = std::integral_constant<int, 3>;
+    using L4 = std::integral_constant<int, 4>;
+#if NEO_ORDER == 2
+    if (toep(L4{})) return 8;
+    if (toep(L3{})) return 7;
+#endif
+    if (far2b()) return 1;
+    if (far2a()) return 2;
+    if (block()) return 3;
+#if NEO_ORDER != 2
+    if (toep(L4{})) return 8;
+    if (toep(L3{})) return 7;
+#endif
+#if NEO_ORDER == 1
+    if (far1()) return 9;
+#endif
+    if (toep(L2{})) return 6;
+    if (toep(L1{})) return 5;
+    if (toep(L0{})) return 4;
+#if NEO_ORDER != 1
+    if (far1()) return 9;
+#endif
+    return 0;
 }
 
 template<int B, bool OLA, int KMAX>
@@ -1096,6 +1150,7 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
 #ifdef NEO_TIMELINE  // diagnostic builds: per-workgroup start / end (100 MHz clock) and role
     const unsigned long long t0 = wall_clock64();
     const int role = lvl_roles<B, OLA, KMAX>(a, smem);
+    if constexpr (lstep_cfg<B>::WG > 256) return;  // lanes past 256 leave the roles early: no final barrier
     __syncthreads();
     if (threadIdx.x == 0 && a.tl) {
         unsigned long long* r = static_cast<unsigned long long*>(a.tl) + 4 * int64_t(blockIdx.x);

@@ -73,6 +73,12 @@ SIGNATURES = {
     "neo_hip_upols_multi_set_impulse": (_i, [_vp, _vp, _i64, _i]),
     "neo_hip_upols_multi_process_samples": (_i, [_vp, _vp, _i64, _vp, _i64, _i64]),
     "neo_hip_upols_multi_reset": (_i, [_vp]),
+    "neo_hip_overlap_create": (_i, [_i, _i, _i64, _i64, _i, ctypes.POINTER(_vp)]),
+    "neo_hip_overlap_destroy": (_i, [_vp]),
+    "neo_hip_overlap_info": (_i, [_vp] + [ctypes.POINTER(_i64)] * 3),
+    "neo_hip_overlap_reset": (_i, [_vp]),
+    "neo_hip_overlap_forward": (_i, [_vp, _vp, _i64, _vp, _i, _vp]),
+    "neo_hip_overlap_inverse": (_i, [_vp, _vp, _vp, _i64, _i, _vp]),
     "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
     "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),
     "neo_hip_normalize_impulse": (_i, [_vp, _i, _i64, _i, _i]),

@@ -31,6 +31,9 @@ __all__ = [
     "UpolsConvolver",
     "upols_convolver",
     "split_upols_convolver",
+    "OverlapStage",
+    "overlap_save",
+    "overlap_add",
     "upola_convolver",
     "split_upola_convolver",
     "upola_convolver_v2",
@@ -397,6 +400,126 @@ class UpolsMultiConvolver:
             self.close()
         except Exception:
             pass
+
+
+class OverlapStage:
+    """C independent overlap stages on the GPU (neo_hip_overlap_*): overlap_save
+    (overlap_save.hpp:19-112) or overlap_add (overlap_add.hpp:23-107) of block B for F-tap
+    filters, transform size 2^next_order(B + F - 1). forward(block) updates the window and
+    returns the n/2 + 1 bins the reference's callback sees; inverse(spectrum, out) runs the
+    irfft, 1/n and writes the output block. Host arrays (synchronous) or CUDA tensors."""
+
+    KINDS = {"save": 0, "add": 1}
+
+    def __init__(self, kind: str, channels: int, block_size: int, filter_size: int, device: int = 0):
+        if kind not in self.KINDS:
+            raise ValueError(f"kind must be 'save' or 'add', got {kind!r}")
+        h = ctypes.c_void_p()
+        _native.check(_native.load().neo_hip_overlap_create(self.KINDS[kind], int(channels), int(block_size),
+                                                            int(filter_size), int(device), ctypes.byref(h)))
+        self._h = h
+        self.kind, self.channels, self.device = kind, channels, device
+        b, f, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _native.check(_native.load().neo_hip_overlap_info(h, ctypes.byref(b), ctypes.byref(f), ctypes.byref(n)))
+        self._block, self._filter, self._n = b.value, f.value, n.value
+
+    def block_size(self) -> int:
+        return self._block
+
+    def filter_size(self) -> int:
+        return self._filter
+
+    def transform_size(self) -> int:
+        return self._n
+
+    def forward(self, block, spectrum=None, stream: int = 0):
+        """block [C][B] float32 -> spectrum [C][n/2 + 1] complex64 (new array / tensor if None)."""
+        lib = _native.load()
+        bins = self._n // 2 + 1
+        if _is_torch(block) and block.is_cuda:
+            import torch
+
+            spec = spectrum if spectrum is not None else torch.empty((self.channels, bins), dtype=torch.complex64,
+                                                                     device=block.device)
+            s = stream or torch.cuda.current_stream(block.device).cuda_stream
+            ld = block.stride(0) if block.dim() == 2 else block.shape[-1]  # channel c at c * ld
+            _native.check(lib.neo_hip_overlap_forward(self._h, ctypes.c_void_p(block.data_ptr()), ld,
+                                                      ctypes.c_void_p(spec.data_ptr()), 1, ctypes.c_void_p(s)))
+            return spec
+        x = np.ascontiguousarray(np.asarray(block, dtype=np.float32).reshape(self.channels, -1))
+        if x.shape[1] != self._block:
+            raise ValueError(f"block must be [{self.channels}][{self._block}]")
+        spec = np.empty((self.channels, bins), np.complex64) if spectrum is None else spectrum
+        _native.check(lib.neo_hip_overlap_forward(self._h, _ptr(x), x.shape[1], _ptr(spec), 0, None))
+        return spec
+
+    def inverse(self, spectrum, out, stream: int = 0):
+        """spectrum [C][n/2 + 1] complex64 -> out [C][B] float32 (in place)."""
+        lib = _native.load()
+        if _is_torch(out) and out.is_cuda:
+            import torch
+
+            s = stream or torch.cuda.current_stream(out.device).cuda_stream
+            ld = out.stride(0) if out.dim() == 2 else out.shape[-1]
+            _native.check(lib.neo_hip_overlap_inverse(self._h, ctypes.c_void_p(spectrum.data_ptr()),
+                                                      ctypes.c_void_p(out.data_ptr()), ld, 1, ctypes.c_void_p(s)))
+            return out
+        spec = np.ascontiguousarray(spectrum, dtype=np.complex64)
+        if not (isinstance(out, np.ndarray) and out.dtype == np.float32 and out.flags.c_contiguous):
+            raise TypeError("out must be a C-contiguous float32 array")
+        _native.check(lib.neo_hip_overlap_inverse(self._h, _ptr(spec), _ptr(out), out.shape[-1], 0, None))
+        return out
+
+    def reset(self) -> None:
+        _native.check(_native.load().neo_hip_overlap_reset(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _native.load().neo_hip_overlap_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class overlap_save:
+    """Drop-in for neo::convolution::overlap_save<complex<float>> (overlap_save.hpp:19-112):
+    overlap_save(block_size, filter_size); __call__(block, callback) processes one block of a
+    1-D float32 array in place, callback(bins) sees (and may modify in place) the
+    transform_size() / 2 + 1 bins."""
+
+    _kind = "save"
+
+    def __init__(self, block_size: int, filter_size: int, device: int = 0):
+        self._stage = OverlapStage(self._kind, 1, block_size, filter_size, device)
+
+    def block_size(self) -> int:
+        return self._stage.block_size()
+
+    def filter_size(self) -> int:
+        return self._stage.filter_size()
+
+    def transform_size(self) -> int:
+        return self._stage.transform_size()
+
+    def __call__(self, block, callback):
+        if not (isinstance(block, np.ndarray) and block.dtype == np.float32 and block.flags.c_contiguous):
+            raise TypeError("block must be a C-contiguous float32 array")
+        if block.size != self.block_size():
+            raise ValueError(f"block must hold {self.block_size()} samples")
+        spec = self._stage.forward(block.reshape(1, -1))
+        callback(spec[0])
+        self._stage.inverse(spec, block.reshape(1, -1))
+        return block
+
+
+class overlap_add(overlap_save):
+    """Drop-in for neo::convolution::overlap_add<complex<float>> (overlap_add.hpp:23-107)."""
+
+    _kind = "add"
 
 
 class upols_convolver:

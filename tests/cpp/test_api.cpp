@@ -354,6 +354,41 @@ static void test_rfftfreq()
     REQUIRE(std::abs(neo::rfftfreq<double>(2, 1, 1.0 / 44100.0) - 22050.0) < 1e-9);
 }
 
+// overlap_test.cpp:21-64 (no-op callback, B x F sizes) and a filter callback against the
+// restatement (oracle_overlap_stage), overlap_save and overlap_add
+template<typename Stage, int Kind>
+static void test_overlap_stage()
+{
+    for (std::size_t B : {128U, 512U}) {
+        for (std::size_t F : {8U, 9U, 10U, 17U, 127U, 128U, 129U, 130U, 512U, 999U, 1024U}) {
+            Stage stage{B, F};
+            REQUIRE(stage.block_size() == B && stage.filter_size() == F);
+            REQUIRE(stage.transform_size() >= B + F - 1);
+            auto const sig = rnoise(F, B * 8);
+            auto out = sig;
+            for (std::size_t i = 0; i < out.size(); i += B) {
+                stage(neo::hip::make_view(out.data() + i, B),
+                      [&](auto io) { REQUIRE(std::size_t(io.extent(0)) == stage.transform_size() / 2 + 1); });
+            }
+            REQUIRE(max_abs_diff(out, sig) <= 1e-5);
+        }
+    }
+    std::size_t const B = 128, F = 129;
+    Stage stage{B, F};
+    auto G = cnoise(91, stage.transform_size() / 2 + 1);
+    auto x = rnoise(92, B * 10);
+    auto ref = x;
+    REQUIRE(oracle_overlap_stage(Kind, B, F, reinterpret_cast<float const*>(G.data()), ref.data(), 10) == 0);
+    for (std::size_t i = 0; i < x.size(); i += B) {
+        stage(neo::hip::make_view(x.data() + i, B), [&](auto io) {
+            for (std::size_t k = 0; k < std::size_t(io.extent(0)); ++k) io(k) *= G[k];
+        });
+    }
+    double peak = 0;
+    for (float v : ref) peak = std::max(peak, double(std::abs(v)));
+    REQUIRE(max_abs_diff(x, ref) <= 1e-5 * peak);
+}
+
 int main()
 {
     test_fdl_index();
@@ -373,6 +408,8 @@ int main()
     test_multidevice_equals_multichannel();
     test_double_precision();
     test_stft();
+    test_overlap_stage<neo::convolution::overlap_save<cf>, 0>();
+    test_overlap_stage<neo::convolution::overlap_add<cf>, 1>();
     std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);
     return failures ? 1 : 0;
 }
