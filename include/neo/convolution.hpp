@@ -22,6 +22,10 @@
 #include <cstddef>
 #include <memory>
 #include <stdexcept>
+#include <map>
+#include <mutex>
+#include <array>
+#include <utility>
 #include <vector>
 
 namespace neo::convolution {
@@ -348,6 +352,109 @@ private:
 };
 
 namespace detail {
+struct group_deleter {
+    void operator()(neo_hip_upols_group* g) const noexcept { neo_hip_upols_group_destroy(g); }
+};
+
+/// the process-wide group of single-channel convolvers of one shape (neo_hip_upols_group_*)
+inline auto acquire_group(std::size_t block, std::size_t partitions, method m, int device)
+    -> std::shared_ptr<neo_hip_upols_group>
+{
+    static std::mutex mu;
+    static std::map<std::array<std::size_t, 4>, std::weak_ptr<neo_hip_upols_group>> groups;
+    std::lock_guard<std::mutex> lk{mu};
+    auto const key = std::array<std::size_t, 4>{block, partitions, std::size_t(m == method::upola), std::size_t(device)};
+    if (auto g = groups[key].lock()) return g;
+    neo_hip_upols_group* raw = nullptr;
+    neo::hip::check(neo_hip_upols_group_create(int(block), int(partitions), m == method::upola ? 1 : 0, device, &raw));
+    auto g = std::shared_ptr<neo_hip_upols_group>(raw, group_deleter{});
+    groups[key] = g;
+    return g;
+}
+}  // namespace detail
+
+/// Single-channel drop-in for upols_convolver<complex<float>> (uniform_partitioned_convolver.hpp:13-65)
+/// whose instances of one shape form a group (neo_hip_upols_group_*, include/neo_hip.h): in the
+/// plugin's frame pattern (DenseConvolution.cpp:62-74: every instance called once per frame on a
+/// buffer of its own) a frame of all instances is ONE launch instead of one launch and one wait
+/// per instance; each instance's outputs are its own sequential convolver's in any pattern. A
+/// coalesced frame's first call reads the other instances' buffers of the previous frame: they
+/// must stay valid while the instances live. upols_convolver is this type when
+/// NEO_HIP_CONVOLVER_GROUPS is defined.
+template<typename Complex, method M = method::upols>
+struct grouped_upols_convolver {
+    static_assert(std::same_as<Complex, std::complex<float>>);
+    using value_type = Complex;
+    using accumulator_type = neo::hip::array<Complex, 1>;
+
+    grouped_upols_convolver() = default;
+    grouped_upols_convolver(grouped_upols_convolver&& o) noexcept
+        : _g{std::move(o._g)}, _id{std::exchange(o._id, -1)}, _B{o._B}, _P{o._P}, _block{std::move(o._block)}
+    {}
+    auto operator=(grouped_upols_convolver&& o) noexcept -> grouped_upols_convolver&
+    {
+        if (this != &o) {
+            leave();
+            _g = std::move(o._g);
+            _id = std::exchange(o._id, -1);
+            _B = o._B;
+            _P = o._P;
+            _block = std::move(o._block);
+        }
+        return *this;
+    }
+    ~grouped_upols_convolver() { leave(); }
+
+    template<typename InMat>
+        requires neo::hip::detail::matrix_like<InMat>
+    auto filter(InMat filter) -> void
+    {
+        auto const P = std::size_t(filter.extent(0)), bins = std::size_t(filter.extent(1));
+        std::vector<Complex> h(P * bins);
+        for (std::size_t p = 0; p < P; ++p)
+            for (std::size_t k = 0; k < bins; ++k) h[p * bins + k] = Complex(neo::hip::detail::at(filter, p, k));
+        if (!_g || _P != P || _B != bins - 1) {
+            leave();
+            _g = detail::acquire_group(bins - 1, P, M, neo::hip::detail::default_device());
+            neo::hip::check(neo_hip_upols_group_join(_g.get(), &_id));
+            _B = bins - 1;
+            _P = P;
+            _block.resize(_B);
+        }
+        neo::hip::check(neo_hip_upols_group_set_filter(_g.get(), _id, h.data(), 0));
+    }
+
+    template<typename Vec>
+        requires neo::hip::detail::vector_like<Vec>
+    auto operator()(Vec block) -> void
+    {
+        if (neo::hip::detail::contiguous(block)) {
+            neo::hip::check_or_abort(neo_hip_upols_group_process(_g.get(), _id, block.data_handle()));
+            return;
+        }
+        neo::hip::detail::gather(block, _block.data());
+        neo::hip::check_or_abort(neo_hip_upols_group_process(_g.get(), _id, _block.data()));
+        neo::hip::detail::scatter(_block.data(), block);
+    }
+
+    /// the group this instance belongs to (diagnostics: neo_hip_upols_group_stats)
+    [[nodiscard]] auto group() const noexcept -> neo_hip_upols_group* { return _g.get(); }
+
+private:
+    void leave() noexcept
+    {
+        if (_g && _id >= 0) (void)neo_hip_upols_group_leave(_g.get(), _id);
+        _g.reset();
+        _id = -1;
+    }
+
+    std::shared_ptr<neo_hip_upols_group> _g;
+    int _id = -1;
+    std::size_t _B = 0, _P = 0;
+    std::vector<float> _block;
+};
+
+namespace detail {
 struct overlap_deleter {
     void operator()(neo_hip_overlap* h) const noexcept { neo_hip_overlap_destroy(h); }
 };
@@ -412,6 +519,20 @@ using overlap_save = detail::hip_overlap<Complex, 0>;
 template<typename Complex>
 using overlap_add = detail::hip_overlap<Complex, 1>;
 
+#ifdef NEO_HIP_CONVOLVER_GROUPS
+template<typename Complex>
+using upols_convolver = grouped_upols_convolver<Complex>;
+
+template<typename Complex>
+using split_upols_convolver = grouped_upols_convolver<Complex>;
+
+/// dense_convolver.hpp:23-24, 32-35 (overlap-add stage, same FDL MAC)
+template<typename Complex>
+using upola_convolver = grouped_upols_convolver<Complex, method::upola>;
+
+template<typename Complex>
+using split_upola_convolver = grouped_upols_convolver<Complex, method::upola>;
+#else
 template<typename Complex>
 using upols_convolver = hip_upols_convolver<Complex>;
 
@@ -424,6 +545,7 @@ using upola_convolver = hip_upols_convolver<Complex, method::upola>;
 
 template<typename Complex>
 using split_upola_convolver = hip_upols_convolver<Complex, method::upola>;
+#endif
 
 /// dense_convolver.hpp:28
 template<typename Complex>

@@ -112,6 +112,8 @@ typedef struct neo_hip_upols_opts {
                              VALU / LDS work, fewer bytes), 1 the 128-block partition-axis transform level */
     int far_group;        /* far transform level: 0 auto, else 1..4 windows per phase-1 pass over the stored
                              segment spectra (auto: 2, or round(sqrt(2 (nseg - 1))) from 32768 16-column units) */
+    int toep_split;       /* 32-block Toeplitz level: 0 auto (2 below 256 16-column units), 1 whole windows per
+                             workgroup, 2 two window halves */
 } neo_hip_upols_opts;
 NEO_HIP_API int neo_hip_upols_create_ex(int channels, int block, int partitions, int device, int method,
                                         const neo_hip_upols_opts* opts, neo_hip_upols** h);
@@ -204,6 +206,30 @@ NEO_HIP_API int neo_hip_upols_multi_set_impulse(neo_hip_upols_multi* m, const fl
 NEO_HIP_API int neo_hip_upols_multi_process_samples(neo_hip_upols_multi* m, const float* in, int64_t ld_in, float* out,
                                                     int64_t ld_out, int64_t num_samples);
 NEO_HIP_API int neo_hip_upols_multi_reset(neo_hip_upols_multi* m);
+/* -- Groups of single-channel convolvers (upols_group.hip) ---------------------------------
+ * Members are C independent one-channel upols / upola convolvers of one shape, each with its
+ * own filter and state, as the plugin's std::vector<upols_convolver> (DenseConvolution.hpp:35)
+ * holds them; process(member, io) is that member's operator()(block): one block of B samples,
+ * host memory, in place, complete on return. While the callers follow the plugin's frame
+ * pattern (every member called once per frame on a buffer of its own that it reuses), the
+ * group steps every member in ONE launch at a frame's first call, from the blocks in the other
+ * members' buffers, and later calls only verify their block (a different block re-runs that
+ * member's block step alone); any other pattern runs each member on a handle of its own. Either
+ * way each member's outputs are those of its own sequential convolver. NOTE: a coalesced frame's
+ * first call READS the buffers the other members passed in the previous frame: they must stay
+ * valid while the group lives (the plugin's channel buffers do). method 0 upols, 1 upola. */
+typedef struct neo_hip_upols_group neo_hip_upols_group;
+NEO_HIP_API int neo_hip_upols_group_create(int block, int partitions, int method, int device, neo_hip_upols_group** g);
+NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g);
+NEO_HIP_API int neo_hip_upols_group_join(neo_hip_upols_group* g, int* member);
+NEO_HIP_API int neo_hip_upols_group_leave(neo_hip_upols_group* g, int member);
+/* filter [P][B+1] complex (uniform_partition layout of one channel); resets the member's state */
+NEO_HIP_API int neo_hip_upols_group_set_filter(neo_hip_upols_group* g, int member, const void* filter, int is_device);
+NEO_HIP_API int neo_hip_upols_group_process(neo_hip_upols_group* g, int member, float* io);
+NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int member);
+/* coalesced now; one-launch frame steps, member calls, block re-runs, mode switches so far */
+NEO_HIP_API int neo_hip_upols_group_stats(neo_hip_upols_group* g, int* coalesced, int64_t* frame_steps, int64_t* calls,
+                                          int64_t* redos, int64_t* switches);
 /* Kernel timing with HIP events recorded on the launch stream (for the roofline in
  * bench.py): enable = n > 0 brackets every n-th launch group with events (0 = off).
  * timing() returns the summed ms of the bracketed part and the count of timed groups:

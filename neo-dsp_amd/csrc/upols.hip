@@ -528,11 +528,11 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
                      const neo_hip_upols_opts* opt, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
-    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0};
+    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0, 0};
     if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.far_level < -1 || o.far_level > 1 ||
         o.split_workgroups < 0 ||
         (o.batch_blocks && (o.batch_blocks < 2 || o.batch_blocks > kMaxBatch || (o.batch_blocks & (o.batch_blocks - 1)))) ||
-        o.batch_bins < 0 || o.batch_bins > 2 || o.far_group < 0 || o.far_group > 4)
+        o.batch_bins < 0 || o.batch_bins > 2 || o.far_group < 0 || o.far_group > 4 || o.toep_split < 0 || o.toep_split > 2)
         return fail(NEO_HIP_EINVAL, "invalid convolver options");
     *out = nullptr;
     if (channels < 1) return fail(NEO_HIP_EINVAL, "channels must be >= 1");
@@ -548,6 +548,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->ring = partitions + kMaxBatch - 1;
     plan_levels(partitions, h->lv, o.far_level);
     h->far_k = o.far_group;
+    h->toep_jh = o.toep_split;
     if (h->lv.nseg) h->ring = std::max(h->ring, kFarRing);  // far slices read 383 blocks back
     h->ola = ola || v2;
     h->v2 = v2;

@@ -1,0 +1,420 @@
+// upols_group.hip — many single-channel upols_convolver instances stepped as ONE multichannel
+// launch per frame, with each instance's own semantics kept exactly.
+//
+// The reference's plugin holds std::vector<upols_convolver> and calls them one after the other
+// on the channels of a frame, each call in place and complete on return
+// (extra/plugin/src/dsp/DenseConvolution.hpp:35, DenseConvolution.cpp:62-74). Each of those
+// calls as a GPU round trip of its own costs a launch and a wait per channel. A group holds the
+// instances of one shape (block, partitions, method, device):
+//   independent mode  every member has its own one-channel handle; calls run immediately. The
+//                     group watches the calls: once two consecutive frames (every live member
+//                     called exactly once, all with the same block count, distinct buffers) went
+//                     by, the members' states move into ONE shared handle (coalesced mode).
+//   coalesced mode    the first call of a frame (the leader) steps ALL members in one launch: its
+//                     own block, and for every other member the contents of the buffer it passed
+//                     in the previous frame (speculation: the plugin's AudioBlock channels are
+//                     filled before the loop over the convolvers). A later member's call compares
+//                     its block with the block speculated for it: equal -> its output is already
+//                     computed; different -> its channel's block step runs again with the real
+//                     block (previous block restored: the step's other roles never read the
+//                     current block's FDL row, so the redo reproduces the one-channel step bit
+//                     for bit). A member called twice before the others (or joining, leaving,
+//                     changing its filter) ends coalescing: the states move back into one-channel
+//                     handles (a speculatively stepped member one block back) before the call.
+// So every output equals the instance's own sequential step; the launch count per frame drops
+// from one per channel to one while the caller keeps the plugin's call pattern. Handles of a
+// group force the shared handle's code-path choices (far window group, Toeplitz window parts),
+// so both modes compute the same sums in the same order.
+#include "upols_handle.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace {
+using neo_hip::cf;
+using neo_hip::fail;
+
+struct member {
+    bool live = false;
+    neo_hip_upols* own = nullptr;  // independent mode: the member's one-channel handle
+    bool filtered = false;
+    int64_t steps = 0;             // blocks processed since the filter was set
+    const float* io_last = nullptr;
+    const float* io_prev = nullptr;  // the buffer of the frame before (coalescing needs stable buffers)
+    bool pending = false;          // coalesced: stepped by the frame's leader, call not yet seen
+    bool seen = false;             // independent: called in the frame being observed
+    int slot = -1;                 // coalesced: channel in the shared handle
+};
+}  // namespace
+
+struct neo_hip_upols_group {
+    int device = 0, B = 0, P = 0, method = 0;
+    std::mutex mu;
+    std::vector<member> m;
+    bool coalesced = false;
+    neo_hip_upols* shared = nullptr;
+    std::vector<int> slot_member;     // shared handle channel -> member
+    float* in_pin = nullptr;          // mapped pinned [C][B]: the frame's input blocks
+    float* out_pin = nullptr;         // mapped pinned [C][B]: the frame's output blocks
+    float* in_dev = nullptr;          // their device addresses
+    float* out_dev = nullptr;
+    float* prev_bak = nullptr;        // device [C][B]: the previous blocks before the frame's step
+    int64_t step_n = 0;               // the frame step's level index and FDL ring row (for redos)
+    int step_w = 0;
+    int npending = 0;
+    int nseen = 0, good_frames = 0;
+    int64_t stat_steps = 0, stat_calls = 0, stat_redos = 0, stat_switches = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+using group_t = neo_hip_upols_group;
+
+int live_count(const group_t* g)
+{
+    int n = 0;
+    for (const auto& x : g->m) n += x.live;
+    return n;
+}
+
+// the code-path choices every handle of the group uses: those of the shared handle over the
+// live members (the far window group and the Toeplitz window parts depend on the channel count)
+neo_hip_upols_opts group_opts(const group_t* g, int C)
+{
+    neo_hip_upols_opts o{-1, 0, 0, 0, -1, -1, 0, 0};
+    o.far_group = neo_hip::far_group_for(C, g->B, g->P);
+    o.toep_split = neo_hip::toep_split_for(C, g->B);
+    return o;
+}
+
+// one channel's state (filter rows, FDL ring, previous block) from (src, cs) to (dst, cd); both
+// handles have the same block, partitions and ring
+int copy_channel(neo_hip_upols* dst, int cd, const neo_hip_upols* src, int cs, const float* prev_src, hipStream_t s)
+{
+    const size_t rows = size_t(src->ring) * size_t(src->B) * sizeof(cf);
+    NEO_HIP_CHECK(hipMemcpyAsync(dst->H + int64_t(cd) * dst->cstride, src->H + int64_t(cs) * src->cstride,
+                                 size_t(src->P) * size_t(src->B) * sizeof(cf), hipMemcpyDeviceToDevice, s));
+    NEO_HIP_CHECK(hipMemcpyAsync(dst->fdl + int64_t(cd) * dst->cstride, src->fdl + int64_t(cs) * src->cstride, rows,
+                                 hipMemcpyDeviceToDevice, s));
+    NEO_HIP_CHECK(hipMemcpyAsync(dst->prev + int64_t(cd) * dst->B, prev_src + int64_t(cs) * src->B,
+                                 size_t(src->B) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return NEO_HIP_OK;
+}
+
+void free_shared(group_t* g)
+{
+    if (g->shared) neo_hip_upols_destroy(g->shared);
+    g->shared = nullptr;
+    if (g->in_pin) (void)hipHostFree(g->in_pin);
+    if (g->out_pin) (void)hipHostFree(g->out_pin);
+    (void)hipFree(g->prev_bak);
+    g->in_pin = g->out_pin = g->in_dev = g->out_dev = g->prev_bak = nullptr;
+    g->slot_member.clear();
+}
+
+int make_own(group_t* g, member& x, int C)
+{
+    if (x.own) return NEO_HIP_OK;
+    const neo_hip_upols_opts o = group_opts(g, C);
+    return neo_hip_upols_create_ex(1, g->B, g->P, g->device, g->method, &o, &x.own);
+}
+
+// independent -> coalesced: every live member's state into one shared handle
+int coalesce(group_t* g)
+{
+    const int C = live_count(g);
+    const neo_hip_upols_opts o = group_opts(g, C);
+    int rc = neo_hip_upols_create_ex(C, g->B, g->P, g->device, g->method, &o, &g->shared);
+    if (rc) return rc;
+    const size_t io = size_t(C) * size_t(g->B) * sizeof(float);
+    NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->in_pin), io, hipHostMallocMapped | hipHostMallocCoherent));
+    NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->out_pin), io, hipHostMallocMapped | hipHostMallocCoherent));
+    NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g->in_dev), g->in_pin, 0));
+    NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g->out_dev), g->out_pin, 0));
+    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&g->prev_bak), io));
+    neo_hip_upols* sh = g->shared;
+    int c = 0, wpos = -1;
+    for (int i = 0; i < int(g->m.size()); ++i) {
+        member& x = g->m[size_t(i)];
+        if (!x.live) continue;
+        if ((rc = copy_channel(sh, c, x.own, 0, x.own->prev, g->stream))) return rc;
+        if (wpos >= 0 && wpos != x.own->wpos) return fail(NEO_HIP_ERUNTIME, "group members out of step");
+        wpos = x.own->wpos;
+        x.slot = c++;
+        x.pending = false;
+        g->slot_member.push_back(i);
+    }
+    NEO_HIP_CHECK(hipStreamSynchronize(g->stream));
+    sh->wpos = wpos;
+    neo_hip::lvl_filter_changed(sh);  // far segment spectra of the copied filters; the levels re-prime
+    sh->batch = false;
+    for (auto& x : g->m)
+        if (x.live) {
+            neo_hip_upols_destroy(x.own);
+            x.own = nullptr;
+        }
+    g->coalesced = true;
+    g->npending = 0;
+    ++g->stat_switches;
+    return NEO_HIP_OK;
+}
+
+// coalesced -> independent: every live member's state into a one-channel handle of its own; a
+// member the frame's leader stepped ahead of its call goes back to before that step (previous
+// block from the backup, ring row of the step: its own call writes that row again)
+int split(group_t* g)
+{
+    neo_hip_upols* sh = g->shared;
+    const int C = live_count(g);
+    for (auto& x : g->m) {
+        if (!x.live) continue;
+        int rc = make_own(g, x, C);
+        if (rc) return rc;
+        const bool back = x.pending;
+        if (x.slot >= 0) {
+            if ((rc = copy_channel(x.own, 0, sh, x.slot, back ? g->prev_bak : sh->prev, g->stream))) return rc;
+            x.own->wpos = back ? g->step_w : sh->wpos;
+            if (back) --x.steps;
+        }
+        neo_hip::lvl_filter_changed(x.own);
+        x.own->batch = false;
+        x.pending = false;
+        x.slot = -1;
+        x.seen = false;
+    }
+    NEO_HIP_CHECK(hipStreamSynchronize(g->stream));
+    free_shared(g);
+    g->coalesced = false;
+    g->npending = 0;
+    g->nseen = 0;
+    g->good_frames = 0;
+    ++g->stat_switches;
+    return NEO_HIP_OK;
+}
+
+// independent mode: one call, then the frame bookkeeping that decides on coalescing
+int call_independent(group_t* g, int i, float* io)
+{
+    member& x = g->m[size_t(i)];
+    if (x.seen) {  // called again before the frame completed: not the lock-step pattern
+        for (auto& y : g->m) y.seen = false;
+        g->nseen = 0;
+        g->good_frames = 0;
+    }
+    int rc = neo_hip_upols_process(x.own, io, 0, nullptr);
+    if (rc) return rc;
+    ++x.steps;
+    x.io_prev = x.io_last;
+    x.io_last = io;
+    x.seen = true;
+    if (++g->nseen < live_count(g)) return NEO_HIP_OK;
+    // a complete frame: equal block counts, distinct buffers, each the member's buffer of the
+    // frame before (the leader of a coalesced frame reads them)
+    bool ok = live_count(g) >= 2 && x.own->ahead;
+    std::vector<const float*> ptrs;
+    for (auto& y : g->m) {
+        if (!y.live) continue;
+        ok = ok && y.filtered && y.steps == x.steps && y.io_last && y.io_last == y.io_prev;
+        ptrs.push_back(y.io_last);
+        y.seen = false;
+    }
+    std::sort(ptrs.begin(), ptrs.end());
+    for (size_t k = 1; k < ptrs.size() && ok; ++k) ok = ptrs[k] != ptrs[k - 1];
+    g->nseen = 0;
+    g->good_frames = ok ? g->good_frames + 1 : 0;
+    if (g->good_frames >= 2 && coalesce(g) != NEO_HIP_OK) {  // not fatal: the members keep their own handles
+        free_shared(g);
+        for (auto& y : g->m) y.slot = -1;
+        g->good_frames = 0;
+    }
+    return NEO_HIP_OK;
+}
+
+// coalesced mode: the leader's step over every member, or a later member's commit / redo
+int call_coalesced(group_t* g, int i, float* io)
+{
+    member& x = g->m[size_t(i)];
+    neo_hip_upols* sh = g->shared;
+    const size_t bb = size_t(g->B) * sizeof(float);
+    if (x.pending) {
+        float* spec_in = g->in_pin + int64_t(x.slot) * g->B;
+        float* out = g->out_pin + int64_t(x.slot) * g->B;
+        if (std::memcmp(io, spec_in, bb) != 0) {  // the caller's block differs: this channel's step again
+            std::memcpy(spec_in, io, bb);
+            NEO_HIP_CHECK(hipMemcpyAsync(sh->prev + int64_t(x.slot) * g->B, g->prev_bak + int64_t(x.slot) * g->B, bb,
+                                         hipMemcpyDeviceToDevice, g->stream));
+            int rc = neo_hip::launch_block_only(sh, g->step_n, g->step_w, x.slot, g->in_dev + int64_t(x.slot) * g->B,
+                                                g->out_dev + int64_t(x.slot) * g->B, g->stream);
+            if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
+            ++g->stat_redos;
+        }
+        std::memcpy(io, out, bb);
+        x.pending = false;
+        x.io_last = io;
+        --g->npending;
+        return NEO_HIP_OK;
+    }
+    if (g->npending > 0) {  // called again before the others took their blocks: back to one handle each
+        int rc = split(g);
+        if (rc) return rc;
+        return call_independent(g, i, io);
+    }
+    // the frame's leader: every member's block (its own, the others' buffers of the last frame)
+    for (const auto& y : g->m)
+        if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
+    NEO_HIP_CHECK(hipMemcpyAsync(g->prev_bak, sh->prev, size_t(sh->C) * bb, hipMemcpyDeviceToDevice, g->stream));
+    g->step_w = sh->wpos;
+    int rc = neo_hip::launch_levels(sh, g->in_dev, g->B, g->out_dev, g->B, g->stream);
+    if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
+    g->step_n = sh->lv_n - 1;
+    ++g->stat_steps;
+    std::memcpy(io, g->out_pin + int64_t(x.slot) * g->B, bb);
+    x.io_last = io;
+    for (auto& y : g->m) {
+        if (!y.live) continue;
+        ++y.steps;
+        if (&y != &x) {
+            y.pending = true;
+            ++g->npending;
+        }
+    }
+    return NEO_HIP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+NEO_HIP_API int neo_hip_upols_group_create(int block, int partitions, int method, int device, neo_hip_upols_group** out)
+{
+    if (!out) return fail(NEO_HIP_EINVAL, "group pointer is null");
+    *out = nullptr;
+    if (method != 0 && method != 1) return fail(NEO_HIP_EINVAL, "groups take method 0 (upols) or 1 (upola)");
+    if (!neo_hip::valid_block(block)) return fail(NEO_HIP_EINVAL, "block must be a power of two in [16, 4096]");
+    if (partitions < 1) return fail(NEO_HIP_EINVAL, "partitions must be >= 1");
+    neo_hip::device_guard dg(device);
+    if (dg.rc) return dg.rc;
+    auto* g = new group_t{};
+    (void)hipGetDevice(&g->device);
+    g->B = block;
+    g->P = partitions;
+    g->method = method;
+    if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete g;
+        return fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed");
+    }
+    *out = g;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
+{
+    if (!g) return NEO_HIP_OK;
+    neo_hip::device_guard dg(g->device);
+    (void)hipStreamSynchronize(g->stream);
+    free_shared(g);
+    for (auto& x : g->m)
+        if (x.own) neo_hip_upols_destroy(x.own);
+    (void)hipStreamDestroy(g->stream);
+    delete g;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_join(neo_hip_upols_group* g, int* id)
+{
+    if (!g || !id) return fail(NEO_HIP_EINVAL, "null group or id");
+    std::lock_guard<std::mutex> lk(g->mu);
+    neo_hip::device_guard dg(g->device);
+    if (dg.rc) return dg.rc;
+    if (g->coalesced)
+        if (int rc = split(g)) return rc;
+    size_t i = 0;
+    while (i < g->m.size() && g->m[i].live) ++i;
+    if (i == g->m.size()) g->m.emplace_back();
+    g->m[i] = member{};
+    g->m[i].live = true;
+    const int rc = make_own(g, g->m[i], live_count(g));
+    if (rc) {
+        g->m[i].live = false;
+        return rc;
+    }
+    *id = int(i);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_leave(neo_hip_upols_group* g, int id)
+{
+    if (!g || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live) return fail(NEO_HIP_EINVAL, "no such member");
+    std::lock_guard<std::mutex> lk(g->mu);
+    neo_hip::device_guard dg(g->device);
+    if (g->coalesced)
+        if (int rc = split(g)) return rc;
+    member& x = g->m[size_t(id)];
+    if (x.own) neo_hip_upols_destroy(x.own);
+    x = member{};
+    for (auto& y : g->m) y.seen = false;
+    g->nseen = 0;
+    g->good_frames = 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_set_filter(neo_hip_upols_group* g, int id, const void* filter, int is_device)
+{
+    if (!g || !filter || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live)
+        return fail(NEO_HIP_EINVAL, "no such member or null filter");
+    std::lock_guard<std::mutex> lk(g->mu);
+    neo_hip::device_guard dg(g->device);
+    if (dg.rc) return dg.rc;
+    if (g->coalesced)
+        if (int rc = split(g)) return rc;
+    member& x = g->m[size_t(id)];
+    if (int rc = neo_hip_upols_set_filter(x.own, filter, is_device)) return rc;  // resets its state
+    x.own->batch = false;
+    x.filtered = true;
+    x.steps = 0;
+    x.seen = false;
+    for (auto& y : g->m) y.seen = false;
+    g->nseen = 0;
+    g->good_frames = 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_process(neo_hip_upols_group* g, int id, float* io)
+{
+    if (!g || !io || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live)
+        return fail(NEO_HIP_EINVAL, "no such member or null block");
+    std::lock_guard<std::mutex> lk(g->mu);
+    neo_hip::device_guard dg(g->device);
+    if (dg.rc) return dg.rc;
+    ++g->stat_calls;
+    return g->coalesced ? call_coalesced(g, id, io) : call_independent(g, id, io);
+}
+
+NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int id)
+{
+    if (!g || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live) return fail(NEO_HIP_EINVAL, "no such member");
+    std::lock_guard<std::mutex> lk(g->mu);
+    neo_hip::device_guard dg(g->device);
+    if (g->coalesced)
+        if (int rc = split(g)) return rc;
+    member& x = g->m[size_t(id)];
+    if (int rc = neo_hip_upols_reset(x.own)) return rc;
+    x.steps = 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_stats(neo_hip_upols_group* g, int* coalesced, int64_t* frame_steps, int64_t* calls,
+                                          int64_t* redos, int64_t* switches)
+{
+    if (!g) return fail(NEO_HIP_EINVAL, "null group");
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (coalesced) *coalesced = g->coalesced;
+    if (frame_steps) *frame_steps = g->stat_steps;
+    if (calls) *calls = g->stat_calls;
+    if (redos) *redos = g->stat_redos;
+    if (switches) *switches = g->stat_switches;
+    return NEO_HIP_OK;
+}
+
+}  // extern "C"

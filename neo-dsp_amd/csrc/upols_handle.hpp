@@ -66,6 +66,7 @@ struct neo_hip_upols {
     neo_hip::cf* fv_acc = nullptr;  // far phase-1 partial sums [K][units][256][16] (K = far_group)
     bool fv_dirty = true;           // far segment spectra to recompute (filter changed)
     int far_k = 0;                  // far phase-1 windows per pass forced by neo_hip_upols_opts.far_group (0: auto)
+    int toep_jh = 0;                // T = 32 window parts forced by neo_hip_upols_opts.toep_split (0: auto)
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
@@ -166,6 +167,13 @@ inline int timing_mark(upols_t::ev_group* g, int i, hipStream_t s)
 int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
 // far: -1 auto (= 1), 0 the big Toeplitz level, 1 the far level
 void plan_levels(int P, level_plan& lp, int far = -1);
+// the block role of streaming step n (FDL ring row w) again for channel c alone, with another
+// input block (upols_group.hip: a speculatively stepped channel whose caller's block differed);
+// the step's slabs and far field must not have been overwritten since
+int launch_block_only(upols_t* h, int64_t n, int w, int c, const float* in, float* out, hipStream_t s);
+// the automatic far phase-1 window group / T = 32 window parts a handle of C channels would use
+int far_group_for(int C, int B, int P);
+int toep_split_for(int C, int B);
 void lvl_free(upols_t* h);
 void lvl_filter_changed(upols_t* h);
 // upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device

@@ -139,7 +139,8 @@ struct slice_args {
     int ring, C, B;
     int64_t cstride, pstride;
     // block role: this step's block, one workgroup per channel (nblk = 0 in priming launches)
-    int nblk;
+    // from channel blk_c0 on
+    int nblk, blk_c0;
     const float* in;
     int64_t ld_in;
     float* out;
@@ -1096,7 +1097,7 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
             bid -= a.nblk;
             return false;
         }
-        if (NEO_ROLES & 1) block_role<B, OLA>(a, bid, smem);
+        if (NEO_ROLES & 1) block_role<B, OLA>(a, a.blk_c0 + bid, smem);
         return true;
     };
     auto far1 = [&]() {
@@ -1227,14 +1228,27 @@ static int64_t far_units(const upols_t* h) { return int64_t(h->C) * (h->B / 16);
 // 512, the 2048-channel headline: 3 % faster), so K = 2 below kFarGroupUnits units
 constexpr int64_t kFarGroupUnits = 32768;  // 256 units per step
 
+static int far_group_auto(int C, int B, int ns)
+{
+    if (ns < 2) return 1;
+    if (int64_t(C) * (B / 16) < kFarGroupUnits) return 2;
+    const int K = int(std::lround(std::sqrt(2.0 * (ns - 1))));
+    return std::min(kFarKMax, std::max(2, K));
+}
+
+int far_group_for(int C, int B, int P)
+{
+    level_plan lp;
+    plan_levels(P, lp);
+    return lp.nseg ? far_group_auto(C, B, lp.nseg) : 0;
+}
+
 static int far_group(const upols_t* h)
 {
     const int ns = h->lv.nseg;
     if (ns < 2) return 1;
     if (h->far_k) return h->far_k;  // neo_hip_upols_opts.far_group (tests, A/B runs)
-    if (int64_t(h->C) * (h->B / 16) < kFarGroupUnits) return 2;
-    const int K = int(std::lround(std::sqrt(2.0 * (ns - 1))));
-    return std::min(kFarKMax, std::max(2, K));
+    return far_group_auto(h->C, h->B, ns);
 }
 
 // far phase 1 over the slice units [u0, u1): mode 0 one window per group, 1 only the groups of
@@ -1322,9 +1336,11 @@ static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) 
 // Toeplitz role geometry per window T (k_lvl_step's level roles): window parts per column
 // group and units per workgroup. T = 32 splits its window in two where a step has fewer than
 // 8 of its units (few channels: the part halves the step's longest chain).
+int toep_split_for(int C, int B) { return C * (B / 16) < 8 * 32 ? 2 : 1; }
+
 static void toep_geom(const upols_t* h, int T, int& JH, int& UPW)
 {
-    JH = T == kBigT ? kBigJH : (T == 32 && h->C * (h->B / 16) < 8 * 32 ? 2 : 1);
+    JH = T == kBigT ? kBigJH : (T == 32 ? (h->toep_jh ? h->toep_jh : toep_split_for(h->C, h->B)) : 1);
     UPW = T <= 8 ? 16 : (T <= 32 ? 32 / T : 1);  // toep_role<T, 2T, 1, 1>: 16 units; toep_tile: 32 / T
 }
 
@@ -1473,6 +1489,36 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
             a.f2grp = far_group(h) > 1;
             a.f3ff = h->fv_ff + (W & 1) * C * kFarT * B;
         }
+    }
+    return launch_step_kernel(h, a, s);
+}
+
+// The block role of step n (FDL ring row w) for channel c alone: the same slabs and far-field
+// row as that step, input / output blocks of channel c (ld 0: one channel)
+int launch_block_only(upols_t* h, int64_t n, int w, int c, const float* in, float* out, hipStream_t s)
+{
+    const level_plan& lp = h->lv;
+    const int B = h->B, C = h->C;
+    if (c < 0 || c >= C || n < 0) return fail(NEO_HIP_EINVAL, "block redo: channel %d / step %lld", c, (long long)n);
+    slice_args a = base_args(h);
+    a.nblk = 1;
+    a.blk_c0 = c;
+    a.in = in;
+    a.ld_in = 0;
+    a.out = out;
+    a.ld_out = 0;
+    a.prev = h->prev;
+    a.twg = h->tw;
+    a.w = w;
+    a.a0 = lp.a0;
+    for (int l = 0; l < lp.n; ++l) {
+        const int T = lp.T[l];
+        a.sl[a.nsl] = h->lv_slab[l] + ((n / T & 1) * C * T + n % T) * B;
+        a.scs[a.nsl++] = int64_t(T) * B;
+    }
+    if (lp.nseg) {
+        a.ff = h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B;
+        a.fcs = int64_t(kFarT) * B;
     }
     return launch_step_kernel(h, a, s);
 }

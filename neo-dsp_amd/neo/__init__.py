@@ -8,7 +8,7 @@ from . import _native
 from . import convolution
 from . import fft
 from .convolution import (UpolsConvolver, UpolsMultiConvolver, convolve, dense_convolve, direct_convolve, fft_convolve,
-                          host_register, host_unregister, normalize_impulse, overlap_add, overlap_save, OverlapStage,
+                          host_register, host_unregister, normalize_impulse, overlap_add, overlap_save, OverlapStage, UpolsGroup,
                           num_partitions, split_upola_convolver, split_upols_convolver, uniform_partition,
                           upola_convolver, upola_convolver_v2, upols_convolver)
 
@@ -30,6 +30,7 @@ __all__ = [
     "overlap_save",
     "overlap_add",
     "OverlapStage",
+    "UpolsGroup",
     "host_register",
     "host_unregister",
     "dense_convolve",

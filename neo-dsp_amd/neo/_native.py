@@ -26,7 +26,7 @@ class UpolsOpts(ctypes.Structure):
     """neo_hip_upols_opts (include/neo_hip.h)."""
     _fields_ = [("fused", ctypes.c_int), ("split_workgroups", ctypes.c_int), ("batch_blocks", ctypes.c_int),
                 ("batch_bins", ctypes.c_int), ("levels", ctypes.c_int), ("far_level", ctypes.c_int),
-                ("far_group", ctypes.c_int)]
+                ("far_group", ctypes.c_int), ("toep_split", ctypes.c_int)]
 
 
 # every symbol declared in include/neo_hip.h: (name, restype, argtypes)
@@ -79,6 +79,14 @@ SIGNATURES = {
     "neo_hip_overlap_reset": (_i, [_vp]),
     "neo_hip_overlap_forward": (_i, [_vp, _vp, _i64, _vp, _i, _vp]),
     "neo_hip_overlap_inverse": (_i, [_vp, _vp, _vp, _i64, _i, _vp]),
+    "neo_hip_upols_group_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "neo_hip_upols_group_destroy": (_i, [_vp]),
+    "neo_hip_upols_group_join": (_i, [_vp, ctypes.POINTER(_i)]),
+    "neo_hip_upols_group_leave": (_i, [_vp, _i]),
+    "neo_hip_upols_group_set_filter": (_i, [_vp, _i, _vp, _i]),
+    "neo_hip_upols_group_process": (_i, [_vp, _i, _vp]),
+    "neo_hip_upols_group_reset": (_i, [_vp, _i]),
+    "neo_hip_upols_group_stats": (_i, [_vp, ctypes.POINTER(_i)] + [ctypes.POINTER(_i64)] * 4),
     "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
     "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),
     "neo_hip_normalize_impulse": (_i, [_vp, _i, _i64, _i, _i]),

@@ -32,6 +32,7 @@ __all__ = [
     "upols_convolver",
     "split_upols_convolver",
     "OverlapStage",
+    "UpolsGroup",
     "overlap_save",
     "overlap_add",
     "upola_convolver",
@@ -123,7 +124,7 @@ class UpolsConvolver:
     """
 
     OPTION_DEFAULTS = {"fused": -1, "split_workgroups": 0, "batch_blocks": 0, "batch_bins": 0, "levels": -1,
-                       "far_level": -1, "far_group": 0}
+                       "far_level": -1, "far_group": 0, "toep_split": 0}
 
     def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols",
                  options: dict | None = None):
@@ -131,7 +132,8 @@ class UpolsConvolver:
         shape-based defaults — fused (-1 auto / 0 / 1), split_workgroups (0 auto),
         batch_blocks (0 auto / 2..32), batch_bins (0 auto / 1 / 2), levels (-1 auto / 0 / 1),
         far_level (-1 auto / 0 Toeplitz window of 128 blocks / 1 partition-axis transform, for p >= 256),
-        far_group (0 auto / 1..4 windows per far phase-1 pass over the stored segment spectra).
+        far_group (0 auto / 1..4 windows per far phase-1 pass over the stored segment spectra),
+        toep_split (0 auto / 1 / 2 window parts per unit of the 32-block Toeplitz level).
         Every choice gives the same results up to float summation order."""
         lib = _native.load()
         h = ctypes.c_void_p()
@@ -520,6 +522,66 @@ class overlap_add(overlap_save):
     """Drop-in for neo::convolution::overlap_add<complex<float>> (overlap_add.hpp:23-107)."""
 
     _kind = "add"
+
+
+class UpolsGroup:
+    """Single-channel convolvers of one shape stepped together (neo_hip_upols_group_*): members
+    join(), take a filter [P][B+1] each and process one host block [B] per call, in place; while
+    the calls follow the plugin's frame pattern (DenseConvolution.cpp:62-74: every member once
+    per frame, each on a buffer of its own) a frame is ONE launch, else each member runs on a
+    handle of its own; outputs are each member's own sequential convolver's either way."""
+
+    def __init__(self, block_size: int, partitions: int, method: str = "upols", device: int = 0):
+        methods = {"upols": 0, "upola": 1}
+        if method not in methods:
+            raise ValueError("groups take method 'upols' or 'upola'")
+        h = ctypes.c_void_p()
+        _native.check(_native.load().neo_hip_upols_group_create(int(block_size), int(partitions), methods[method],
+                                                                int(device), ctypes.byref(h)))
+        self._h = h
+        self.block_size, self.partitions = block_size, partitions
+
+    def join(self) -> int:
+        i = ctypes.c_int()
+        _native.check(_native.load().neo_hip_upols_group_join(self._h, ctypes.byref(i)))
+        return i.value
+
+    def leave(self, member: int) -> None:
+        _native.check(_native.load().neo_hip_upols_group_leave(self._h, int(member)))
+
+    def filter(self, member: int, partitions) -> None:
+        H = np.ascontiguousarray(partitions, dtype=np.complex64)
+        if H.shape != (self.partitions, self.block_size + 1):
+            raise ValueError(f"filter shape {H.shape} != {(self.partitions, self.block_size + 1)}")
+        _native.check(_native.load().neo_hip_upols_group_set_filter(self._h, int(member), _ptr(H), 0))
+
+    def __call__(self, member: int, block: np.ndarray) -> np.ndarray:
+        if not (isinstance(block, np.ndarray) and block.dtype == np.float32 and block.flags.c_contiguous
+                and block.size == self.block_size):
+            raise TypeError("block must be a C-contiguous float32 array of block_size samples")
+        _native.check(_native.load().neo_hip_upols_group_process(self._h, int(member), _ptr(block)))
+        return block
+
+    def reset(self, member: int) -> None:
+        _native.check(_native.load().neo_hip_upols_group_reset(self._h, int(member)))
+
+    def stats(self) -> dict:
+        c = ctypes.c_int()
+        v = [ctypes.c_int64() for _ in range(4)]
+        _native.check(_native.load().neo_hip_upols_group_stats(self._h, ctypes.byref(c), *[ctypes.byref(x) for x in v]))
+        return {"coalesced": bool(c.value), "frame_steps": v[0].value, "calls": v[1].value, "redos": v[2].value,
+                "switches": v[3].value}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _native.load().neo_hip_upols_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class upols_convolver:

@@ -13,7 +13,7 @@ BIN = os.path.join(CPP, "bin", "test_api")
 
 def build():
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "liboracle.so"])
-    subprocess.check_call(["make", "-s", "-C", CPP])
+    subprocess.check_call(["make", "-s", "-C", CPP, "bin/test_api", "bin/test_group"])
     return BIN
 
 
@@ -29,3 +29,14 @@ def test_cpp_api_on_gpu():
     r = subprocess.run([b], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all C++ API tests passed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_convolver_groups_on_gpu():
+    """The plugin's std::vector<upols_convolver> pattern with the group-backed alias
+    (NEO_HIP_CONVOLVER_GROUPS, tests/cpp/test_group.cpp): 256 instances equal one
+    upols_multichannel bit for bit, one launch per frame after two watched frames."""
+    build()
+    r = subprocess.run([os.path.join(CPP, "bin", "test_group")], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "group test passed" in r.stdout
