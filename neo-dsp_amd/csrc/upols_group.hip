@@ -8,8 +8,9 @@
 // instances of one shape (block, partitions, method, device):
 //   independent mode  every member has its own one-channel handle; calls run immediately. The
 //                     group watches the calls: once two consecutive frames (every live member
-//                     called exactly once, all with the same block count, distinct buffers) went
-//                     by, the members' states move into ONE shared handle (coalesced mode).
+//                     called exactly once, all with the same block count, each on the buffer it
+//                     used in the frame before, the buffers distinct) went by, the members'
+//                     states move into ONE shared handle (coalesced mode).
 //   coalesced mode    the first call of a frame (the leader) steps ALL members in one launch: its
 //                     own block, and for every other member the contents of the buffer it passed
 //                     in the previous frame (speculation: the plugin's AudioBlock channels are

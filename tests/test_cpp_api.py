@@ -35,7 +35,7 @@ def test_cpp_api_on_gpu():
 def test_cpp_convolver_groups_on_gpu():
     """The plugin's std::vector<upols_convolver> pattern with the group-backed alias
     (NEO_HIP_CONVOLVER_GROUPS, tests/cpp/test_group.cpp): 256 instances equal one
-    upols_multichannel bit for bit, one launch per frame after two watched frames."""
+    upols_multichannel bit for bit, one launch per frame after three watched frames."""
     build()
     r = subprocess.run([os.path.join(CPP, "bin", "test_group")], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr

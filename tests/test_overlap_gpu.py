@@ -76,11 +76,13 @@ def test_overlap_stage_device_multichannel(neo_gpu, oracle, kind):
         host.inverse(spec, blk)
         ref[:, t * B:(t + 1) * B] = blk
     xt = torch.from_numpy(x).cuda()
-    Gt = torch.from_numpy(G).cuda()
     for t in range(nb):
         view = xt[:, t * B:]  # channel c at c * ld, ld = B * nb
         spec = dev.forward(view)
-        spec *= Gt
+        torch.cuda.synchronize()
+        sh = spec.cpu().numpy()
+        sh *= G  # the same callback arithmetic as the host path (numpy complex64)
+        spec.copy_(torch.from_numpy(sh))
         dev.inverse(spec, view)
     torch.cuda.synchronize()
     assert np.array_equal(xt.cpu().numpy(), ref)
