@@ -86,6 +86,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the affinity mask's CPUs, at most 16")
     ap.add_argument("--no-host-io", action="store_true", help="skip the host_io sub-object")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the secondary weak-scaling object")
+    ap.add_argument("--far-group", type=int, default=0,
+                    help="neo_hip_upols_opts.far_group: 0 auto, 1..4 windows per far phase-1 pass")
+    ap.add_argument("--step-group", type=int, default=0,
+                    help="neo_hip_upols_opts.step_group: 0 auto, 1 one launch per step, 2 / 4 step groups")
     ap.add_argument("--host-io", action="store_true",
                     help="time the host-buffer boundary (neo_hip_upols_process on pinned-staged host memory): "
                          "PCIe-inclusive, reported for DESIGN.md, never the headline value")
@@ -278,7 +282,7 @@ def far_group(nseg: int, units: int) -> int:
     return min(4, max(2, int(math.floor(math.sqrt(2.0 * (nseg - 1)) + 0.5))))
 
 
-def algorithmic_bytes(C, B, P, plan):
+def algorithmic_bytes(C, B, P, plan, G=1, far_k=0):
     """Algorithmic bytes per streaming step of the step kernel k_lvl_step, by role:
     block:     window (previous block + this block), previous-block write, output (4 x 4B per
                sample), FDL row write and H0 (2 x 8B per bin), partitions 1 .. a0 - 1 (filter +
@@ -291,14 +295,21 @@ def algorithmic_bytes(C, B, P, plan):
                entries; phase 1 takes K windows per pass over the nseg - 1 older row-pair and
                segment spectra (1/K per window), and 2b segments 1 .. j of window j of a group
                (K - 1 spectrum pairs per window on average): 256 (4 + 2 (nseg - 1) / K + K - 1)
-               + 128 values per window, K = far_group(nseg, units) (upols_levels.hip)."""
+               + 128 values per window, K = far_group(nseg, units) (upols_levels.hip).
+    Step groups (G > 1): the levels with T < 2 G run in the block's launch ("toeplitz_block"), the
+    others in the background launches of G steps ("toeplitz")."""
     nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
     block = C * B * (16 + 16 + 16 * (plan["a0"] - 1) + 8 * nlev)
-    toep = sum(C * B / T * 8 * (2 * (b - a) + 2 * T - 1) for T, a, b in zip(plan["T"], plan["a"], plan["b"]))
+    lv = [(T, C * B / T * 8 * (2 * (b - a) + 2 * T - 1)) for T, a, b in zip(plan["T"], plan["a"], plan["b"])]
+    toep = sum(v for T, v in lv if G == 1 or T >= 2 * G)
+    toep_block = sum(v for T, v in lv if G > 1 and T < 2 * G)
     ns = plan["nseg"]
-    K = far_group(ns, C * B // 16)
+    K = far_group(ns, C * B // 16) if not far_k else far_k
     far = C * B / 128 * 8 * (256 * (4 + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
-    return {"block": block, "toeplitz": toep, "far": far}
+    out = {"block": block, "toeplitz": toep, "far": far}
+    if G > 1:
+        out["toeplitz_block"] = toep_block
+    return out
 
 
 def oracle_parity(x, y, feed, irh, B, chans, K=4, threads=16):
@@ -398,10 +409,12 @@ def run_upols(args, world, rank, local):
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     P = neo.num_partitions(L, B)
-    conv = neo.UpolsConvolver(C, B, P, device=local)
+    conv = neo.UpolsConvolver(C, B, P, device=local, options={"step_group": args.step_group,
+                                                              "far_group": args.far_group})
     conv.set_batch(False)  # streaming: one block per step, as a real-time caller runs it
     levels = conv.ahead_info()[0] and not args.no_ahead
     conv_far_group = conv.far_group()
+    G = conv.step_group()
     plan = neo.convolution.level_plan(P)
     g = torch.Generator(device=dev).manual_seed(8 + rank)
     ir = torch.rand((C, L), generator=g, device=dev).mul_(2).sub_(1)  # synthetic white-noise IR
@@ -519,8 +532,8 @@ def run_upols(args, world, rank, local):
                        "host_roundtrip: 200 device-resident single-block calls, each followed by a host wait for its "
                        "output before the next call (max over ranks)"}
 
-    if levels:
-        roles = algorithmic_bytes(C, B, P, plan)
+    if levels and G == 1:
+        roles = algorithmic_bytes(C, B, P, plan, 1, conv_far_group)
         # one launch per step: HIP events around a second run of the timed steps, or the wall
         # time of the timed steps where that is smaller (with timing events on it the stream's
         # launches slow down; at one channel the event run is host-bound)
@@ -543,6 +556,38 @@ def run_upols(args, world, rank, local):
                           "%.4f ms" % det[0],
                 "algorithmic_bytes_per_launch": by,
                 "kernels": kernels, "d2d_copy_gbs": copy_ceiling_gbs(dev)}
+    elif levels:
+        # step groups: the block launch of every step on the caller's stream and one background
+        # launch of the level slices per G steps, overlapping; per-kernel HIP events (the C-ABI's
+        # timing parts 0 / 1, on the stream each kernel runs on) give each kernel's launch time,
+        # the wall time of the timed steps the whole step's
+        roles = algorithmic_bytes(C, B, P, plan, G, conv_far_group)
+        step_ms = elapsed * 1e3 / args.steps
+        by_blk = roles["block"] + roles["toeplitz_block"]
+        by_sl = G * (roles["toeplitz"] + roles["far"])
+        by = by_blk + by_sl / G
+        kb, ks = f"k_lvl_block<{B}>", "k_lvl_slices"
+        kernels = []
+        for kname, b, ms, per in ((ks, by_sl, det[1], G), (kb, by_blk, det[0], 1)):
+            g = b / (ms * 1e-3) / 1e9
+            kernels.append({"kernel": kname, "ms_per_launch": ms, "launches_per_step": 1.0 / per,
+                            "algorithmic_bytes_per_launch": b, "achieved_gbs": g, "frac": g / PEAK_HBM_GBS,
+                            "traffic": load_pmc_traffic(args.workload, kname)})
+        kernels[0]["bytes_by_role"] = {"toeplitz": G * roles["toeplitz"], "far": G * roles["far"]}
+        kernels[1]["bytes_by_role"] = {"block": roles["block"], "toeplitz": roles["toeplitz_block"]}
+        dom = kernels[0]
+        gbs = by / (step_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": dom["frac"], "traffic": dom["traffic"],
+                "traffic_over_algorithmic": dom["traffic"] / by_sl if dom["traffic"] else None, "kernel": ks,
+                "kernel_avg_ms": det[1], "steps_per_launch": G,
+                "timing": "HIP events around every launch of each kernel on its own stream (slices: the handle's "
+                          "background stream; block: the caller's), averaged; the two kernels overlap",
+                "algorithmic_bytes_per_launch": by_sl, "kernels": kernels,
+                "step": {"ms_per_step": step_ms, "algorithmic_bytes_per_step": by, "achieved_gbs": gbs,
+                         "frac": gbs / PEAK_HBM_GBS, "bytes_by_role": roles,
+                         "note": "all algorithmic bytes of a step over the wall time per step of the timed region"},
+                "d2d_copy_gbs": copy_ceiling_gbs(dev)}
     else:
         roof = {"bound": "hbm", "achieved": gbs_plain, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": gbs_plain / PEAK_HBM_GBS, "traffic": plain["traffic"], "kernel": plain["kernel"],
@@ -591,7 +636,7 @@ def run_upols(args, world, rank, local):
                                f"({'split over the ranks' if args.workload in STRONG else 'per GPU'}), B={B}, "
                                f"L={L} taps (P={P}), one block per step",
                    "channels_per_gpu": C, "channels_total": C_total, "block": B, "taps": L, "partitions": P,
-                   "far_group": conv_far_group,
+                   "far_group": conv_far_group, "step_group": G,
                    "streaming": ("levels: block step p<%d, Toeplitz %s, far %d segments" %
                                  (plan["a0"], list(zip(plan["T"], plan["a"], plan["b"])), plan["nseg"])
                                  if levels else "plain step"),

@@ -114,6 +114,11 @@ typedef struct neo_hip_upols_opts {
                              segment spectra (auto: 2, or round(sqrt(2 (nseg - 1))) from 32768 16-column units) */
     int toep_split;       /* 32-block Toeplitz level: 0 auto (2 below 256 16-column units), 1 whole windows per
                              workgroup, 2 two window halves */
+    int step_group;       /* streaming levels: 0 auto, 1 one launch per block (the block and 1/T of every level's
+                             next window), 2 or 4 step groups: the block of every call as a launch of its own on the
+                             caller's stream, the level slices of G calls as ONE launch on the handle's background
+                             stream, issued at the group's first call (ordered by events; the output of a call is
+                             complete when the caller's stream reaches it, as with G = 1) */
 } neo_hip_upols_opts;
 NEO_HIP_API int neo_hip_upols_create_ex(int channels, int block, int partitions, int device, int method,
                                         const neo_hip_upols_opts* opts, neo_hip_upols** h);
@@ -176,6 +181,9 @@ NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, 
 /* windows per far phase-1 pass the handle runs (neo_hip_upols_opts.far_group or the automatic
  * choice); 0 without a far transform level */
 NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* windows);
+/* steps per background launch of the streaming levels' slices (neo_hip_upols_opts.step_group or
+ * the automatic choice): 1 = one launch per step */
+NEO_HIP_API int neo_hip_upols_get_step_group(neo_hip_upols* h, int* steps);
 /* -- Multichannel convolver over several devices ------------------------------
  * C channels cut into n contiguous shards, shard i = channels [C i / n, C (i + 1) / n) on
  * devices[i] (a device may repeat), each a neo_hip_upols handle of its own (own stream).
@@ -235,7 +243,9 @@ NEO_HIP_API int neo_hip_upols_group_stats(neo_hip_upols_group* g, int* coalesced
  * timing() returns the summed ms of the bracketed part and the count of timed groups:
  * the MAC kernel of a plain or batched step, the whole step of a streaming-level step.
  * timing_detail() returns per part (ms[4], launches[4]): streaming-level steps 0 = the
- * step kernel; plain / batched steps 0 = MAC kernel. Both drain the events. */
+ * step kernel (step groups: the block launch and the wait for the previous group's slices,
+ * 1 = the slice launches on the background stream, one per G steps); plain / batched steps
+ * 0 = MAC kernel. Both drain the events. */
 NEO_HIP_API int neo_hip_upols_set_timing(neo_hip_upols* h, int enable);
 NEO_HIP_API int neo_hip_upols_timing(neo_hip_upols* h, double* mac_ms, int64_t* launches);
 NEO_HIP_API int neo_hip_upols_timing_detail(neo_hip_upols* h, double* ms, int64_t* launches);

@@ -376,6 +376,7 @@ namespace {
 
 int reset_state(upols_t* h, hipStream_t s)
 {
+    if (int rc = lvl_join(h, s)) return rc;
     NEO_HIP_CHECK(hipMemsetAsync(h->fdl, 0, size_t(h->C) * h->ring * h->B * sizeof(cf), s));
     NEO_HIP_CHECK(hipMemsetAsync(h->prev, 0, size_t(h->C) * h->B * sizeof(float), s));
     NEO_HIP_CHECK(hipMemsetAsync(h->arrivals, 0, size_t(h->C) * sizeof(int), s));
@@ -414,6 +415,7 @@ void destroy(upols_t* h)
 int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
     if (h->ahead) return launch_levels(h, in, ld_in, out, ld_out, s);
+    if (int rc = lvl_join(h, s)) return rc;
     upols_t::ev_group* ev = nullptr;
     if (int rc = timing_begin(h, 2, &ev)) return rc;
     if (int rc = timing_mark(ev, 0, s)) return rc;
@@ -450,6 +452,7 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
 int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int n, hipStream_t s)
 {
     const int sum_first = h->in_pos == 0;
+    if (int rc = lvl_join(h, s)) return rc;
     h->lv_n = -1;
     if (sum_first) {  // tail MAC over partitions p >= 1 into the split slabs
         const unsigned grid = unsigned(h->C) * unsigned(h->S);
@@ -528,11 +531,12 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
                      const neo_hip_upols_opts* opt, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
-    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0, 0};
+    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0, 0, 0};
     if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.far_level < -1 || o.far_level > 1 ||
         o.split_workgroups < 0 ||
         (o.batch_blocks && (o.batch_blocks < 2 || o.batch_blocks > kMaxBatch || (o.batch_blocks & (o.batch_blocks - 1)))) ||
-        o.batch_bins < 0 || o.batch_bins > 2 || o.far_group < 0 || o.far_group > 4 || o.toep_split < 0 || o.toep_split > 2)
+        o.batch_bins < 0 || o.batch_bins > 2 || o.far_group < 0 || o.far_group > 4 || o.toep_split < 0 || o.toep_split > 2 ||
+        (o.step_group != 0 && o.step_group != 1 && o.step_group != 2 && o.step_group != 4))
         return fail(NEO_HIP_EINVAL, "invalid convolver options");
     *out = nullptr;
     if (channels < 1) return fail(NEO_HIP_EINVAL, "channels must be >= 1");
@@ -549,6 +553,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     plan_levels(partitions, h->lv, o.far_level);
     h->far_k = o.far_group;
     h->toep_jh = o.toep_split;
+    h->sg = o.step_group ? o.step_group : step_group_for(channels, block, partitions);
     if (h->lv.nseg) h->ring = std::max(h->ring, kFarRing);  // far slices read 383 blocks back
     h->ola = ola || v2;
     h->v2 = v2;
@@ -868,12 +873,12 @@ static int drain_events(upols_t* h)
         NEO_HIP_CHECK(hipEventSynchronize(e.e[e.n - 1]));
         float tot = 0.f;
         NEO_HIP_CHECK(hipEventElapsedTime(&tot, e.e[0], e.e[e.n - 1]));
-        h->group_ms.push_back(tot);
+        if (e.part == 0) h->group_ms.push_back(tot);  // step times: the caller's stream only
         for (int k = 0; k + 1 < e.n; ++k) {
             float t = 0.f;
             NEO_HIP_CHECK(hipEventElapsedTime(&t, e.e[k], e.e[k + 1]));
-            h->part_ms[k] += t;
-            ++h->part_n[k];
+            h->part_ms[k + e.part] += t;
+            ++h->part_n[k + e.part];
         }
         if (e.n >= 3) {
             h->part_ms[3] += tot;

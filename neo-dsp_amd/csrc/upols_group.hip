@@ -84,9 +84,10 @@ int live_count(const group_t* g)
 // live members (the far window group and the Toeplitz window parts depend on the channel count)
 neo_hip_upols_opts group_opts(const group_t* g, int C)
 {
-    neo_hip_upols_opts o{-1, 0, 0, 0, -1, -1, 0, 0};
+    neo_hip_upols_opts o{-1, 0, 0, 0, -1, -1, 0, 0, 0};
     o.far_group = neo_hip::far_group_for(C, g->B, g->P);
     o.toep_split = neo_hip::toep_split_for(C, g->B);
+    o.step_group = neo_hip::step_group_for(C, g->B, g->P);
     return o;
 }
 

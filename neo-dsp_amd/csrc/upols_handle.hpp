@@ -6,6 +6,7 @@
 #include "common.hpp"
 
 #include <cstdint>
+#include <deque>
 #include <utility>
 #include <vector>
 
@@ -67,6 +68,15 @@ struct neo_hip_upols {
     bool fv_dirty = true;           // far segment spectra to recompute (filter changed)
     int far_k = 0;                  // far phase-1 windows per pass forced by neo_hip_upols_opts.far_group (0: auto)
     int toep_jh = 0;                // T = 32 window parts forced by neo_hip_upols_opts.toep_split (0: auto)
+    // step groups (neo_hip_upols_opts.step_group, G = sg): G = 1 runs a step as ONE launch (the
+    // block and 1/T of every level's next window); G > 1 runs the block of every call alone on the
+    // caller's stream and the level slices of G steps as one launch on the handle's background
+    // stream bg, one step group ahead (events ev_blk / ev_sl order the two; upols_levels.hip)
+    int sg = 1;
+    hipStream_t bg = nullptr;
+    hipEvent_t ev_blk = nullptr, ev_sl[2] = {}, ev_join = nullptr;
+    bool bg_busy = false;  // slices enqueued on bg since the last join
+    int64_t bg_launches = 0;
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
@@ -89,8 +99,9 @@ struct neo_hip_upols {
     struct ev_group {
         hipEvent_t e[4] = {};
         int n = 0;
+        int part = 0;  // first part index its intervals add to (1: a step group's slice launch on bg)
     };
-    std::vector<ev_group> events;  // pool, reused across timing windows
+    std::deque<ev_group> events;   // pool, reused across timing windows (stable addresses while growing)
     size_t events_used = 0;
     double part_ms[4] = {};        // drained event time per part (see neo_hip_upols_timing_detail)
     int64_t part_n[4] = {};
@@ -154,6 +165,7 @@ inline int timing_begin(upols_t* h, int nev, upols_t::ev_group** out)
     }
     *out = &h->events[h->events_used++];
     (*out)->n = nev;
+    (*out)->part = 0;
     return NEO_HIP_OK;
 }
 inline int timing_mark(upols_t::ev_group* g, int i, hipStream_t s)
@@ -174,6 +186,10 @@ int launch_block_only(upols_t* h, int64_t n, int w, int c, const float* in, floa
 // the automatic far phase-1 window group / T = 32 window parts a handle of C channels would use
 int far_group_for(int C, int B, int P);
 int toep_split_for(int C, int B);
+int step_group_for(int C, int B, int P);
+// order everything enqueued on the background stream (step-group slices) before later work on s;
+// every path that writes the FDL ring or the level buffers other than a streaming step calls it
+int lvl_join(upols_t* h, hipStream_t s);
 void lvl_free(upols_t* h);
 void lvl_filter_changed(upols_t* h);
 // upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device

@@ -1072,7 +1072,9 @@ constexpr int step_wpe() { return B > 512 ? 2 : NEO_STEP_WPE; }
 #ifndef NEO_ORDER
 #define NEO_ORDER 0  // diagnostic builds: 1 far phase 1 before the Toeplitz levels T <= 16, 2 Toeplitz T >= 32 first
 #endif
-template<int B, bool OLA, int KMAX>
+// PART: 0 every role (one launch per step), 1 the block role alone, 2 every role but the block
+// (step groups: the block of each call and the level slices of G calls in launches of their own)
+template<int B, bool OLA, int KMAX, int PART = 0>
 __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
 {
     int bid = int(blockIdx.x);
@@ -1093,6 +1095,7 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
         return true;
     };
     auto block = [&]() {
+        if constexpr (PART == 2) return false;
         if (bid >= a.nblk) {
             bid -= a.nblk;
             return false;
@@ -1100,6 +1103,10 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
         if (NEO_ROLES & 1) block_role<B, OLA>(a, a.blk_c0 + bid, smem);
         return true;
     };
+    if constexpr (PART == 1) {  // the block and the levels too short for the background (T < 2 G)
+        if (block()) return 3;
+        return threadIdx.x < 256 && toep_level<0>(a, bid, smem) ? 4 : 0;
+    }
     auto far1 = [&]() {
         if (bid >= a.f1nwg) {
             bid -= a.f1nwg;
@@ -1142,6 +1149,29 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
     if (far1()) return 9;
 #endif
     return 0;
+}
+
+// LDS of the block role alone: the block's spectrum, the transform buffer, the twiddles
+template<int B>
+constexpr int block_lds() { return (B + upols_cfg<B>::LL + upols_cfg<B>::TW1 + upols_cfg<B>::TW2) * int(sizeof(cf)); }
+
+// step groups: the block role of one step (the caller's stream) and the slice of the 4-block
+// Toeplitz level where G = 4 (toep_role<4>: no LDS); the block's LDS only -- more workgroups
+// resident per CU than the step kernel's 53.8 KB tile allows
+template<int B, bool OLA>
+__global__ __launch_bounds__(lstep_cfg<B>::WG) void k_lvl_block(slice_args a)
+{
+    __shared__ __attribute__((aligned(16))) char smem[block_lds<B>()];
+    (void)lvl_roles<B, OLA, 2, 1>(a, smem);
+}
+
+// step groups: every role but the block for the slices of G steps (the background stream);
+// 256 lanes (the roles' geometry), the step kernel's register budget
+template<int KMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NEO_STEP_WPE))) void k_lvl_slices(slice_args a)
+{
+    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
+    (void)lvl_roles<512, false, KMAX, 2>(a, smem);
 }
 
 template<int B, bool OLA, int KMAX>
@@ -1313,6 +1343,16 @@ static int lvl_buffers(upols_t* h)
 
 void lvl_free(upols_t* h)
 {
+    if (h->bg) {  // slices still in flight read and write the buffers freed below
+        (void)hipStreamSynchronize(h->bg);
+        (void)hipStreamDestroy(h->bg);
+        h->bg = nullptr;
+        for (hipEvent_t* e : {&h->ev_blk, &h->ev_sl[0], &h->ev_sl[1], &h->ev_join}) {
+            (void)hipEventDestroy(*e);
+            *e = nullptr;
+        }
+        h->bg_busy = false;
+    }
     for (auto& p : h->lv_slab) {
         (void)hipFree(p);
         p = nullptr;
@@ -1337,6 +1377,18 @@ static int ring_add(int64_t r, int64_t d, int R) { return int(((r + d) % R + R) 
 // group and units per workgroup. T = 32 splits its window in two where a step has fewer than
 // 8 of its units (few channels: the part halves the step's longest chain).
 int toep_split_for(int C, int B) { return C * (B / 16) < 8 * 32 ? 2 : 1; }
+
+// steps per background launch of the level slices (launch_levels): 4 from kStepGroupUnits
+// 16-column units (same-box A/B, ms per step at G = 1 / 4: C5 0.0183 / 0.0165, C4 0.0155 / 0.0134,
+// c5full 0.1213 / 0.1215 with the host round trip per block 133 -> 63 us; at one channel, C3, the
+// block launch and the cross-stream waits cost more than the overlap gives: 0.0063 / 0.0083)
+constexpr int64_t kStepGroupUnits = 2048;
+
+int step_group_for(int C, int B, int P)
+{
+    (void)P;
+    return int64_t(C) * (B / 16) >= kStepGroupUnits && B <= 1024 ? 4 : 1;
+}
 
 static void toep_geom(const upols_t* h, int T, int& JH, int& UPW)
 {
@@ -1375,7 +1427,8 @@ static void* g_tl = nullptr;
 static int64_t g_tl_n = 0, g_tl_cap = 0;
 #endif
 
-static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStream_t s)
+// kernel of a launch: part 0 the step kernel (every role), 1 the block alone, 2 the slices alone
+static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStream_t s, int part = 0)
 {
     slice_args a = a_in;
     const unsigned grid = unsigned(a.f3nwg + a.f2nwg + a.nblk + a.f1nwg) + [&] {
@@ -1396,27 +1449,42 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
 #endif
     // pairs-only build where the window group is <= 2 (fewer VGPRs: every shape below
     // kFarGroupUnits), else the build for any group
+    const bool pairs = a.fK <= 2;
+    if (part == 1) {
+        if (h->ola) {
+            NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_block<BB, true>), dim3(grid),
+                                                                                  dim3(lstep_cfg<BB>::WG), 0, s, a))
+        } else {
+            NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_block<BB, false>), dim3(grid),
+                                                                                  dim3(lstep_cfg<BB>::WG), 0, s, a))
+        }
+    } else if (part == 2) {
+        if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(grid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_lvl_slices<kFarKMax>), dim3(grid), dim3(256), 0, s, a);
+    } else {
 #define NEO_LVL(OL, KM)                                                                                        \
     NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, OL, KM>), dim3(grid), \
                                                                          dim3(lstep_cfg<BB>::WG), 0, s, a))
-    const bool pairs = a.fK <= 2;
-    if (h->ola) {
-        if (pairs) NEO_LVL(true, 2) else NEO_LVL(true, kFarKMax)
-    } else {
-        if (pairs) NEO_LVL(false, 2) else NEO_LVL(false, kFarKMax)
-    }
+        if (h->ola) {
+            if (pairs) NEO_LVL(true, 2) else NEO_LVL(true, kFarKMax)
+        } else {
+            if (pairs) NEO_LVL(false, 2) else NEO_LVL(false, kFarKMax)
+        }
 #undef NEO_LVL
+    }
     NEO_HIP_LAUNCH_CHECK();
     return NEO_HIP_OK;
 }
 
-// The far level's units are cut into kFarS = kFarT - 1 slices per window: slice q of window W
-// runs phase 1 and 2a at step q of window W - 1 (2a reads FDL rows up to the last block before
-// that window) and 2b at step q + 1 (<= the window's last step: the far field is complete when
-// window W's first block runs).
-constexpr int kFarS = kFarT - 1;
+// The far level's units are cut into slices per window. G = 1: kFarT - 1 slices, slice q of
+// window W runs phase 1 and 2a at step q of window W - 1 (2a reads FDL rows up to the last block
+// before that window) and 2b at step q + 1 (<= the window's last: the far field is complete when
+// window W's first block runs). G > 1 (step groups, slice_part): kFarT / G - 2 slices, phase 1
+// and 2a of slice q at step group q + 1 of window W - 1 (its launch waits only for the blocks
+// before the previous group), 2b at group q + 2.
+static int far_nslices(const upols_t* h) { return h->sg == 1 ? kFarT - 1 : kFarT / h->sg - 2; }
 
-static int far_u(int64_t U, int q) { return int(q * U / kFarS); }
+static int far_u(int64_t U, int q, int ns) { return int(q * U / ns); }
 
 // far phase 1 for slice q of window W: the unit groups of class W mod K for the windows
 // W .. W + K - 1 (far1_mac); in the first windows after priming (W < K) the classes that have
@@ -1424,22 +1492,20 @@ static int far_u(int64_t U, int q) { return int(q * U / kFarS); }
 static void far1_args(const upols_t* h, int64_t W, int q, slice_args& a)
 {
     const int64_t U = far_units(h);
-    const int K = far_group(h);
+    const int K = far_group(h), ns = far_nslices(h);
     a.f1wn = int(W);
-    far1_range(h, a, far_u(U, q), far_u(U, q + 1), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
+    far1_range(h, a, far_u(U, q, ns), far_u(U, q + 1, ns), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
 }
 
-// The launch of step n >= 0 (block t0 + n at ring row w): the block and slice n mod T of
-// window n / T + 1 of every Toeplitz level (its rows end at the window in progress, so every
-// window's slabs are complete when its first block runs); with q = n mod 128 and W = n / 128 + 1,
-// far phase 1 and 2a of slice q (q < kFarS) and far phase 2b of slice q - 1 (q >= 1) of window W.
-static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, float* out, int64_t ld_out,
-                       hipStream_t s)
+// The block role of step n (block t0 + n at FDL ring row w) for the channels [c0, c0 + nc): its
+// slab row of every Toeplitz level and its far-field row (windows finished in earlier launches)
+static void block_part(const upols_t* h, int64_t n, int w, int c0, int nc, const float* in, int64_t ld_in, float* out,
+                       int64_t ld_out, slice_args& a)
 {
     const level_plan& lp = h->lv;
-    const int B = h->B, C = h->C, R = h->ring, w = h->wpos;
-    slice_args a = base_args(h);
-    a.nblk = C;
+    const int B = h->B, C = h->C;
+    a.nblk = nc;
+    a.blk_c0 = c0;
     a.in = in;
     a.ld_in = ld_in;
     a.out = out;
@@ -1453,74 +1519,124 @@ static int launch_step(upols_t* h, int64_t n, const float* in, int64_t ld_in, fl
         a.sl[a.nsl] = h->lv_slab[l] + ((n / T & 1) * C * T + n % T) * B;
         a.scs[a.nsl++] = int64_t(T) * B;
     }
-    for (int l = 0; l < lp.n; ++l) {
-        const int T = lp.T[l];
-        int JH, UPW;
-        toep_geom(h, T, JH, UPW);
-        const int64_t U = int64_t(C) * (B / 16) * JH, st = n % T, W = n / T + 1;
-        toep_arg& ta = a.tp[l];  // slot l = level l (the kernel dispatches on it), empty slices allowed
-        ta.u0 = int(st * U / T);
-        ta.u1 = int((st + 1) * U / T);
-        ta.slab = h->lv_slab[l] + (W & 1) * C * T * B;
-        ta.T = T;
-        ta.a = lp.a[l];
-        ta.b = lp.b[l];
-        ta.tw = ring_add(w, W * T - n, R);  // block t0 + n at row w; the window starts at t0 + W T
-        ta.nwg = ta.u1 > ta.u0 ? (ta.u1 - ta.u0 + UPW - 1) / UPW : 0;
-        ta.jh = JH;
-        a.ntp = l + 1;
-    }
     if (lp.nseg) {
         a.ff = h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B;
         a.fcs = int64_t(kFarT) * B;
-        const int64_t U = far_units(h), W = n / kFarT + 1;
-        const int q = int(n % kFarT);
-        if (q < kFarS) {
-            a.f2u0 = far_u(U, q);
-            a.f2nwg = far_u(U, q + 1) - a.f2u0;
-            a.f2tw = ring_add(w, W * kFarT - n, R);
+    }
+}
+
+// A Toeplitz level's slice: units [u0, u1) of window W (first block t0 + W T) into its slab buffer
+static void toep_slice(const upols_t* h, int l, int64_t W, int64_t u0, int64_t u1, int64_t n, int w, slice_args& a)
+{
+    const int T = h->lv.T[l];
+    int JH, UPW;
+    toep_geom(h, T, JH, UPW);
+    toep_arg& ta = a.tp[l];  // slot l = level l (the kernel dispatches on it), empty slices allowed
+    ta.u0 = int(u0);
+    ta.u1 = int(u1);
+    ta.slab = h->lv_slab[l] + (W & 1) * h->C * T * h->B;
+    ta.T = T;
+    ta.a = h->lv.a[l];
+    ta.b = h->lv.b[l];
+    ta.tw = ring_add(w, W * T - n, h->ring);  // block t0 + n at row w
+    ta.nwg = ta.u1 > ta.u0 ? (ta.u1 - ta.u0 + UPW - 1) / UPW : 0;
+    ta.jh = JH;
+    a.ntp = std::max(a.ntp, l + 1);
+}
+
+static int64_t toep_units(const upols_t* h, int T)
+{
+    int JH, UPW;
+    toep_geom(h, T, JH, UPW);
+    return int64_t(h->C) * (h->B / 16) * JH;
+}
+
+// The slices the launch of step n (block t0 + n at ring row w) carries. G = 1: slice n mod T of
+// window n / T + 1 of every Toeplitz level (its rows end before the window in progress, so every
+// window's slabs are complete when its first block runs) and, with q = n mod 128 and W = n / 128 + 1,
+// far phase 1 and 2a of slice q (q < 127) and far phase 2b of slice q - 1 (q >= 1) of window W.
+// G > 1, block launches: the levels with T < 2 G, as for G = 1.
+static void block_levels(const upols_t* h, int64_t n, int w, slice_args& a)
+{
+    for (int l = 0; l < h->lv.n; ++l) {
+        const int T = h->lv.T[l];
+        if (h->sg > 1 && T >= 2 * h->sg) break;
+        const int64_t U = toep_units(h, T), st = n % T;
+        toep_slice(h, l, n / T + 1, st * U / T, (st + 1) * U / T, n, w, a);
+    }
+    if (h->sg > 1 || !h->lv.nseg) return;
+    const int64_t U = far_units(h), W = n / kFarT + 1;
+    const int q = int(n % kFarT), ns = far_nslices(h);
+    if (q < ns) {
+        a.f2u0 = far_u(U, q, ns);
+        a.f2nwg = far_u(U, q + 1, ns) - a.f2u0;
+        a.f2tw = ring_add(w, W * kFarT - n, h->ring);
+        a.f2wn = int(W);
+        far1_args(h, W, q, a);
+    }
+    if (q >= 1) {
+        a.f3u0 = far_u(U, q - 1, ns);
+        a.f3nwg = far_u(U, q, ns) - a.f3u0;
+        a.f3wn = int(W);
+        a.f2grp = far_group(h) > 1;
+        a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+    }
+}
+
+// G > 1: the background launch issued at step n0 (a multiple of G; block t0 + n0 at ring row w0).
+// It may read only the blocks before n0 - G (it waits for those, not for the group before it), and
+// the block launch of step n0 + G waits for it. So a level of window T >= 2 G computes window W + 1
+// in T / G - 1 parts at the steps t_W + G j, j = 1 .. T / G - 1 (part j - 1; its rows end at t_W - 1),
+// the last due one group before t_{W+1}; the far level's slice q (kFarT / G - 2 of them) runs
+// phase 1 and 2a at group q + 1 and 2b at group q + 2 of the window before.
+static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
+{
+    const level_plan& lp = h->lv;
+    const int G = h->sg;
+    for (int l = 0; l < lp.n; ++l) {
+        const int T = lp.T[l];
+        if (T < 2 * G) continue;  // in the block launches
+        const int64_t j = (n0 % T) / G, np = T / G - 1, U = toep_units(h, T);
+        if (j >= 1) toep_slice(h, l, n0 / T + 1, (j - 1) * U / np, j * U / np, n0, w0, a);
+    }
+    if (lp.nseg) {
+        const int64_t U = far_units(h), W = n0 / kFarT + 1;
+        const int q = int(n0 % kFarT) / G, ns = far_nslices(h);
+        if (q >= 1 && q <= ns) {
+            a.f2u0 = far_u(U, q - 1, ns);
+            a.f2nwg = far_u(U, q, ns) - a.f2u0;
+            a.f2tw = ring_add(w0, W * kFarT - n0, h->ring);
             a.f2wn = int(W);
-            far1_args(h, W, q, a);
+            far1_args(h, W, q - 1, a);
         }
-        if (q >= 1) {
-            a.f3u0 = far_u(U, q - 1);
-            a.f3nwg = far_u(U, q) - a.f3u0;
+        if (q >= 2) {
+            a.f3u0 = far_u(U, q - 2, ns);
+            a.f3nwg = far_u(U, q - 1, ns) - a.f3u0;
             a.f3wn = int(W);
             a.f2grp = far_group(h) > 1;
-            a.f3ff = h->fv_ff + (W & 1) * C * kFarT * B;
+            a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
         }
     }
-    return launch_step_kernel(h, a, s);
 }
 
 // The block role of step n (FDL ring row w) for channel c alone: the same slabs and far-field
-// row as that step, input / output blocks of channel c (ld 0: one channel)
+// row as that step, input / output blocks of channel c (ld 0: one channel); the kernel that
+// ran the step's block (step groups: the block kernel)
 int launch_block_only(upols_t* h, int64_t n, int w, int c, const float* in, float* out, hipStream_t s)
 {
-    const level_plan& lp = h->lv;
-    const int B = h->B, C = h->C;
-    if (c < 0 || c >= C || n < 0) return fail(NEO_HIP_EINVAL, "block redo: channel %d / step %lld", c, (long long)n);
+    if (c < 0 || c >= h->C || n < 0) return fail(NEO_HIP_EINVAL, "block redo: channel %d / step %lld", c, (long long)n);
     slice_args a = base_args(h);
-    a.nblk = 1;
-    a.blk_c0 = c;
-    a.in = in;
-    a.ld_in = 0;
-    a.out = out;
-    a.ld_out = 0;
-    a.prev = h->prev;
-    a.twg = h->tw;
-    a.w = w;
-    a.a0 = lp.a0;
-    for (int l = 0; l < lp.n; ++l) {
-        const int T = lp.T[l];
-        a.sl[a.nsl] = h->lv_slab[l] + ((n / T & 1) * C * T + n % T) * B;
-        a.scs[a.nsl++] = int64_t(T) * B;
-    }
-    if (lp.nseg) {
-        a.ff = h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B;
-        a.fcs = int64_t(kFarT) * B;
-    }
-    return launch_step_kernel(h, a, s);
+    block_part(h, n, w, c, 1, in, 0, out, 0, a);
+    return launch_step_kernel(h, a, s, h->sg > 1 ? 1 : 0);
+}
+
+int lvl_join(upols_t* h, hipStream_t s)
+{
+    if (!h->bg_busy) return NEO_HIP_OK;
+    NEO_HIP_CHECK(hipEventRecord(h->ev_join, h->bg));
+    NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_join, 0));
+    h->bg_busy = false;
+    return NEO_HIP_OK;
 }
 
 // First streaming step after a reset / filter change / batched pass (block t0 at ring row w):
@@ -1530,6 +1646,7 @@ static int lvl_prime(upols_t* h, hipStream_t s)
 {
     const level_plan& lp = h->lv;
     const int B = h->B, C = h->C, w = h->wpos;
+    if (int rc = lvl_join(h, s)) return rc;  // slices of an earlier run still in flight on bg
     if (lp.nseg && h->fv_dirty) {
         const unsigned grid = unsigned(C) * unsigned(lp.nseg) * unsigned(B / 16);
         hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->fv_hf, h->fv_tw, B, h->P, lp.nseg,
@@ -1556,20 +1673,21 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     if (!lp.nseg) return NEO_HIP_OK;
     // far window 0, every segment transformed (fnfresh = nseg), in slices
     const int64_t U = far_units(h);
-    for (int q = 0; q <= kFarS; ++q) {
+    const int ns = far_nslices(h);
+    for (int q = 0; q <= ns; ++q) {
         slice_args f = base_args(h);
         f.fnfresh = lp.nseg;
-        if (q < kFarS) {
+        if (q < ns) {
             f.f1wn = 0;
-            far1_range(h, f, far_u(U, q), far_u(U, q + 1), 0, 0);  // zero partial sums (no stored segments)
-            f.f2u0 = far_u(U, q);
-            f.f2nwg = far_u(U, q + 1) - f.f2u0;
+            far1_range(h, f, far_u(U, q, ns), far_u(U, q + 1, ns), 0, 0);  // zero partial sums (no stored segments)
+            f.f2u0 = far_u(U, q, ns);
+            f.f2nwg = far_u(U, q + 1, ns) - f.f2u0;
             f.f2tw = w;
             f.f2wn = 0;
         }
         if (q >= 1) {
-            f.f3u0 = far_u(U, q - 1);
-            f.f3nwg = far_u(U, q) - f.f3u0;
+            f.f3u0 = far_u(U, q - 1, ns);
+            f.f3nwg = far_u(U, q, ns) - f.f3u0;
             f.f3wn = 0;
             f.f3ff = h->fv_ff;
         }
@@ -1578,18 +1696,59 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     return NEO_HIP_OK;
 }
 
+// background stream and events of the step groups (created on the first grouped step)
+static int group_streams(upols_t* h)
+{
+    if (h->bg) return NEO_HIP_OK;
+    int lo = 0, hi = 0;
+    NEO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    NEO_HIP_CHECK(hipStreamCreateWithPriority(&h->bg, hipStreamNonBlocking, lo));  // lo: the least urgent
+    for (hipEvent_t* e : {&h->ev_blk, &h->ev_sl[0], &h->ev_sl[1], &h->ev_join})
+        NEO_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return NEO_HIP_OK;
+}
+
+// One streaming step (block t0 + n, n = lv_n). G = 1: one launch, the block and 1/T of every
+// level's next window. G > 1: the block (with the levels of T < 2 G) is a launch of its own on the
+// caller's stream; at every G-th step the background stream gets one launch of slices (slice_part),
+// after the blocks before the previous group (ev_blk, recorded there), and the block waits for
+// the previous group's background launch (ev_sl). With one group of slack on each side neither
+// stream waits for the other in steady state. The background launch is issued when its group's
+// first call comes, so a block redone before that call (upols_group.hip) is the one it reads.
 int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
     int rc = lvl_buffers(h);
     if (rc) return rc;
-    if (h->lv_n < 0) {
+    if (h->sg > 1 && (rc = group_streams(h))) return rc;
+    const bool primed = h->lv_n < 0;
+    if (primed) {
         if ((rc = lvl_prime(h, s))) return rc;
         h->lv_n = 0;
     }
     const int64_t n = h->lv_n;
-    upols_t::ev_group* ev = nullptr;
+    const int G = h->sg;
+    slice_args a = base_args(h);
+    block_part(h, n, h->wpos, 0, h->C, in, ld_in, out, ld_out, a);
+    block_levels(h, n, h->wpos, a);
+    if (G > 1 && n % G == 0) {
+        if (primed) NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the priming launches
+        NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
+        slice_args b = base_args(h);
+        slice_part(h, n, h->wpos, b);
+        upols_t::ev_group* eb = nullptr;
+        if ((rc = timing_begin(h, 2, &eb)) || (rc = timing_mark(eb, 0, h->bg))) return rc;
+        if (eb) eb->part = 1;
+        if ((rc = launch_step_kernel(h, b, h->bg, 2))) return rc;
+        if ((rc = timing_mark(eb, 1, h->bg))) return rc;
+        NEO_HIP_CHECK(hipEventRecord(h->ev_sl[(n / G) & 1], h->bg));
+        NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the blocks before this group: the next group's launch
+        h->bg_busy = true;
+        ++h->bg_launches;
+        if (!primed) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_sl[(n / G - 1) & 1], 0));
+    }
+    upols_t::ev_group* ev = nullptr;  // the step's (block's) launch alone
     if ((rc = timing_begin(h, 2, &ev)) || (rc = timing_mark(ev, 0, s))) return rc;
-    if ((rc = launch_step(h, n, in, ld_in, out, ld_out, s))) return rc;
+    if ((rc = launch_step_kernel(h, a, s, G > 1 ? 1 : 0))) return rc;
     if ((rc = timing_mark(ev, 1, s))) return rc;
     h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
     h->lv_n = n + 1;
@@ -1623,6 +1782,13 @@ extern "C" NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* wi
 {
     if (!h || !windows) return neo_hip::fail(NEO_HIP_EINVAL, "null handle or output");
     *windows = h->lv.nseg ? neo_hip::far_group(h) : 0;
+    return NEO_HIP_OK;
+}
+
+extern "C" NEO_HIP_API int neo_hip_upols_get_step_group(neo_hip_upols* h, int* steps)
+{
+    if (!h || !steps) return neo_hip::fail(NEO_HIP_EINVAL, "null handle or output");
+    *steps = h->sg;
     return NEO_HIP_OK;
 }
 

@@ -124,7 +124,7 @@ class UpolsConvolver:
     """
 
     OPTION_DEFAULTS = {"fused": -1, "split_workgroups": 0, "batch_blocks": 0, "batch_bins": 0, "levels": -1,
-                       "far_level": -1, "far_group": 0, "toep_split": 0}
+                       "far_level": -1, "far_group": 0, "toep_split": 0, "step_group": 0}
 
     def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols",
                  options: dict | None = None):
@@ -133,7 +133,9 @@ class UpolsConvolver:
         batch_blocks (0 auto / 2..32), batch_bins (0 auto / 1 / 2), levels (-1 auto / 0 / 1),
         far_level (-1 auto / 0 Toeplitz window of 128 blocks / 1 partition-axis transform, for p >= 256),
         far_group (0 auto / 1..4 windows per far phase-1 pass over the stored segment spectra),
-        toep_split (0 auto / 1 / 2 window parts per unit of the 32-block Toeplitz level).
+        toep_split (0 auto / 1 / 2 window parts per unit of the 32-block Toeplitz level),
+        step_group (0 auto / 1 one launch per block / 2 or 4: the block of every call alone on the
+        caller's stream, the level slices of G calls as one launch on a background stream).
         Every choice gives the same results up to float summation order."""
         lib = _native.load()
         h = ctypes.c_void_p()
@@ -276,6 +278,12 @@ class UpolsConvolver:
         """Windows per far phase-1 pass this handle runs (0: no far transform level)."""
         k = ctypes.c_int()
         _native.check(_native.load().neo_hip_upols_get_far_group(self._h, ctypes.byref(k)))
+        return k.value
+
+    def step_group(self) -> int:
+        """Steps per background launch of the streaming levels' slices (1: one launch per step)."""
+        k = ctypes.c_int()
+        _native.check(_native.load().neo_hip_upols_get_step_group(self._h, ctypes.byref(k)))
         return k.value
 
     # -- instrumentation ------------------------------------------------------

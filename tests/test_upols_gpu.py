@@ -720,6 +720,111 @@ def test_far_window_groups_vs_oracle(neo_gpu, oracle, method, K, B, P, C):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 900 + K, conv_opts) <= TOL
 
 
+@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("method,B,P,C,nb,opts", [
+    ("upols", 512, 40, 3, 75, {}), ("upola", 128, 40, 2, 100, {}), ("upols", 16, 7, 2, 40, {}),
+    ("upols", 32, 700, 1, 1720, {"far_group": 3}), ("upola", 64, 1000, 2, 2320, {"far_group": 4}),
+    ("upols", 32, 1100, 1, 2520, {"far_group": 2}), ("upols", 256, 300, 2, 420, {"far_level": 0}),
+    ("upola", 1024, 270, 1, 300, {}), ("upols", 32, 257, 2, 654, {"far_level": 1})])
+def test_step_groups_vs_oracle(neo_gpu, oracle, G, method, B, P, C, nb, opts):
+    """Step groups (neo_hip_upols_opts.step_group = G): the block of every call alone on the
+    caller's stream, the level slices of G calls as one launch on the background stream, the far
+    level in kFarT / G - 1 slices per window; every band, the far window groups K = 2..4, the
+    128-block Toeplitz level, several windows and ring wraparound; OLS and OLA
+    (uniform_partitioned_convolver.hpp:47-65, fdl_index.hpp:23-36)."""
+    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 1300 + P, dict(opts, step_group=G)) <= TOL
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_step_groups_equal_one_launch(neo_gpu, oracle, G):
+    """The same sums in the same order as the one-launch step: bit-identical outputs."""
+    torch = pytest.importorskip("torch")
+    B, P, C, nb = 64, 1000, 2, 700
+    ir = np.stack([oracle.noise(1400 + c, B * P) for c in range(C)])
+    sig = torch.from_numpy(np.stack([oracle.noise(1410 + c, B * nb) for c in range(C)])).cuda()
+    outs = []
+    for g in (1, G):
+        conv = neo_gpu.UpolsConvolver(C, B, P, options={"step_group": g})
+        conv.set_impulse(ir)
+        conv.set_batch(False)
+        t = sig.clone()
+        conv.process_blocks(t)
+        torch.cuda.synchronize()
+        outs.append(t.cpu().numpy())
+        conv.close()
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_step_groups_mixed_paths(neo_gpu, oracle):
+    """Step groups across batched passes, plain steps, host blocks, level toggles, a reset and
+    a filter change (each joins the background stream before it touches the FDL ring or the
+    level buffers), one block per call and many per call, against the oracle."""
+    torch = pytest.importorskip("torch")
+    B, P, C = 64, 420, 2
+    L = B * P
+    irs = [np.stack([oracle.noise(1500 + 7 * k + c, L) for c in range(C)]) for k in range(2)]
+    parts = [oracle.uniform_partition(oracle.normalize_impulse(ir), B) for ir in irs]
+    conv = neo_gpu.UpolsConvolver(C, B, P, options={"step_group": 4})
+    for k in range(2):
+        nb = 1100
+        sig = np.stack([oracle.noise(1520 + 3 * k + c, B * nb) for c in range(C)])
+        ref = oracle.dense_convolve(sig, parts[k])
+        conv.filter(parts[k])
+        t = torch.from_numpy(sig).cuda()
+        pos = 0
+        for kind, n in [("stream", 301), ("batch", 64), ("one", 7), ("off", 5), ("stream", 3), ("host", 2),
+                        ("stream", 290), ("batch", 33), ("one", 6), ("stream", 389)]:
+            seg = t[:, pos * B:(pos + n) * B].contiguous()
+            if kind == "host":
+                torch.cuda.synchronize()
+                h = seg.cpu().numpy().copy()
+                for i in range(n):
+                    blk = np.ascontiguousarray(h[:, i * B:(i + 1) * B])
+                    conv(blk)  # the host-buffer call (zero-copy block)
+                    h[:, i * B:(i + 1) * B] = blk
+                seg = torch.from_numpy(h).cuda()
+            elif kind == "one":
+                for i in range(n):
+                    blk = seg[:, i * B:(i + 1) * B].contiguous()
+                    conv(blk)
+                    seg[:, i * B:(i + 1) * B] = blk
+            else:
+                conv.set_ahead(kind != "off")
+                conv.set_batch(kind == "batch")
+                conv.process_blocks(seg)
+                conv.set_ahead(True)
+            t[:, pos * B:(pos + n) * B] = seg
+            pos += n
+        assert pos == nb
+        torch.cuda.synchronize()
+        assert peak_err(t.cpu().numpy(), ref) <= TOL, k
+    conv.reset()
+    x = torch.zeros((C, B * 40), device="cuda")
+    conv.set_batch(False)
+    conv.process_blocks(x)
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(x).item() == 0  # silence after a reset
+
+
+def test_step_group_timing_detail(neo_gpu):
+    """timing_detail() with step groups: part 0 the block launches (every timed step), part 1
+    the slice launches on the background stream (one per G steps)."""
+    torch = pytest.importorskip("torch")
+    conv = neo_gpu.UpolsConvolver(4, 256, 300, options={"step_group": 4})
+    conv.set_batch(False)
+    x = torch.zeros((4, 256 * 16), device="cuda")
+    conv.set_timing(True)
+    conv.process_blocks(x)
+    torch.cuda.synchronize()
+    conv.set_timing(False)
+    parts = conv.timing_detail()
+    assert [n for _, n in parts] == [16, 4, 0, 0]
+    assert parts[0][0] > 0 and parts[1][0] > 0  # the first background launch (step 0) is empty
+    assert conv.step_group() == 4
+    with pytest.raises(RuntimeError):
+        neo_gpu.UpolsConvolver(1, 64, 300, options={"step_group": 3})
+
+
 def test_far_group_defaults(neo_gpu):
     """The automatic window group: 2 below 32768 16-column units (every shape but the
     headline), round(sqrt(2 (nseg - 1))) from there (bench.far_group restates it)."""

@@ -20,9 +20,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 
 
-def mean_counter(path, kernel):
+def mean_counter(path, kernel, every_grid=False):
     """mean counter value over the kernel's dispatches with its most common grid (the
-    steady-state launches: priming launches of the step kernel have other grids)"""
+    steady-state launches: priming launches of the step kernel have other grids), or over
+    every dispatch (every_grid: the step groups' slice launches, whose grids cycle with the
+    level windows -- their mean over many windows is the steady-state mean)"""
     rows = []
     with open(path) as f:
         for row in csv.DictReader(f):
@@ -34,14 +36,16 @@ def mean_counter(path, kernel):
     for g, _ in rows:
         grids[g] = grids.get(g, 0) + 1
     g = max(grids, key=grids.get)
-    vals = [v for gg, v in rows if gg == g]
+    vals = [v for gg, v in rows if every_grid or gg == g]
     return sum(vals) / len(vals), len(vals)
 
 
-def summarize(tag, workload, kernel, alg, label=None):
+def summarize(tag, workload, kernel, alg, label=None, every_grid=False):
     label = label or workload
-    fetch, nf = mean_counter(os.path.join(OUT, f"pmc_{workload}_FETCH_SIZE_{tag}", "run_counter_collection.csv"), kernel)
-    write, nw = mean_counter(os.path.join(OUT, f"pmc_{workload}_WRITE_SIZE_{tag}", "run_counter_collection.csv"), kernel)
+    fetch, nf = mean_counter(os.path.join(OUT, f"pmc_{workload}_FETCH_SIZE_{tag}", "run_counter_collection.csv"), kernel,
+                             every_grid)
+    write, nw = mean_counter(os.path.join(OUT, f"pmc_{workload}_WRITE_SIZE_{tag}", "run_counter_collection.csv"), kernel,
+                             every_grid)
     if fetch is None or write is None:
         print(f"{label}: no dispatches of {kernel!r}", file=sys.stderr)
         return None
@@ -75,7 +79,12 @@ def main():
             continue
         b = bench_line(tag, w)
         r = b["roofline"]
-        summarize(tag, w, "k_lvl_step", r["algorithmic_bytes_per_launch"], w)
+        if r.get("steps_per_launch", 1) > 1:  # step groups: the slice and block kernels
+            for k in r["kernels"]:
+                name = k["kernel"].split("<")[0]
+                summarize(tag, w, name, k["algorithmic_bytes_per_launch"], f"{w}_{name}", every_grid=True)
+        else:
+            summarize(tag, w, "k_lvl_step", r["algorithmic_bytes_per_launch"], w)
         summarize(tag, w, "k_upols_step", b["per_block_step"]["algorithmic_bytes_per_launch"], w + "_plain")
         if b.get("offline"):
             summarize(tag, w, "k_batch_mac", b["offline"]["algorithmic_bytes_per_launch"], w + "_offline")
