@@ -115,7 +115,7 @@ typedef struct neo_hip_upols_opts {
     int toep_split;       /* 32-block Toeplitz level: 0 auto (2 below 256 16-column units), 1 whole windows per
                              workgroup, 2 two window halves */
     int step_group;       /* streaming levels: 0 auto, 1 one launch per block (the block and 1/T of every level's
-                             next window), 2 or 4 step groups: the block of every call as a launch of its own on the
+                             next window), 2, 4 or 8 step groups: the block of every call as a launch of its own on the
                              caller's stream, the level slices of G calls as ONE launch on the handle's background
                              stream, issued at the group's first call (ordered by events; the output of a call is
                              complete when the caller's stream reaches it, as with G = 1) */

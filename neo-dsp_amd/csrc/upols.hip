@@ -536,7 +536,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
         o.split_workgroups < 0 ||
         (o.batch_blocks && (o.batch_blocks < 2 || o.batch_blocks > kMaxBatch || (o.batch_blocks & (o.batch_blocks - 1)))) ||
         o.batch_bins < 0 || o.batch_bins > 2 || o.far_group < 0 || o.far_group > 4 || o.toep_split < 0 || o.toep_split > 2 ||
-        (o.step_group != 0 && o.step_group != 1 && o.step_group != 2 && o.step_group != 4))
+        (o.step_group != 0 && o.step_group != 1 && o.step_group != 2 && o.step_group != 4 && o.step_group != 8))
         return fail(NEO_HIP_EINVAL, "invalid convolver options");
     *out = nullptr;
     if (channels < 1) return fail(NEO_HIP_EINVAL, "channels must be >= 1");

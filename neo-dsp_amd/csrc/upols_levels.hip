@@ -1105,7 +1105,9 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
     };
     if constexpr (PART == 1) {  // the block and the levels too short for the background (T < 2 G)
         if (block()) return 3;
-        return threadIdx.x < 256 && toep_level<0>(a, bid, smem) ? 4 : 0;
+        if (threadIdx.x >= 256) return 0;
+        if (toep_level<0>(a, bid, smem)) return 4;
+        return toep_level<1>(a, bid, smem) ? 5 : 0;
     }
     auto far1 = [&]() {
         if (bid >= a.f1nwg) {
@@ -1731,8 +1733,15 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     block_part(h, n, h->wpos, 0, h->C, in, ld_in, out, ld_out, a);
     block_levels(h, n, h->wpos, a);
     if (G > 1 && n % G == 0) {
+        // Every background level has T >= 2 G, so its windows (and the far level's) start at
+        // multiples of 2 G: a background launch at an odd group (n = G mod 2 G) needs the blocks
+        // before n - G, one at an even group only those before n - 2 G (its predecessor on bg
+        // waited for them), and only the block of an even group starts windows whose slabs the
+        // previous background launch finished. So one cross-stream wait per 2 G steps each way
+        // (each costs the waiting queue ~10 us of idle time on MI355X, kernel traces).
+        const bool odd = (n / G) & 1;
         if (primed) NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the priming launches
-        NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
+        if (odd || primed) NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
         slice_args b = base_args(h);
         slice_part(h, n, h->wpos, b);
         upols_t::ev_group* eb = nullptr;
@@ -1740,11 +1749,14 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
         if (eb) eb->part = 1;
         if ((rc = launch_step_kernel(h, b, h->bg, 2))) return rc;
         if ((rc = timing_mark(eb, 1, h->bg))) return rc;
-        NEO_HIP_CHECK(hipEventRecord(h->ev_sl[(n / G) & 1], h->bg));
-        NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the blocks before this group: the next group's launch
         h->bg_busy = true;
         ++h->bg_launches;
-        if (!primed) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_sl[(n / G - 1) & 1], 0));
+        if (odd) {
+            NEO_HIP_CHECK(hipEventRecord(h->ev_sl[0], h->bg));  // due at the next even group's block
+        } else {
+            NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the blocks before n: the next odd group's launch
+            if (!primed) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_sl[0], 0));
+        }
     }
     upols_t::ev_group* ev = nullptr;  // the step's (block's) launch alone
     if ((rc = timing_begin(h, 2, &ev)) || (rc = timing_mark(ev, 0, s))) return rc;

@@ -720,7 +720,7 @@ def test_far_window_groups_vs_oracle(neo_gpu, oracle, method, K, B, P, C):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 900 + K, conv_opts) <= TOL
 
 
-@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("G", [2, 4, 8])
 @pytest.mark.parametrize("method,B,P,C,nb,opts", [
     ("upols", 512, 40, 3, 75, {}), ("upola", 128, 40, 2, 100, {}), ("upols", 16, 7, 2, 40, {}),
     ("upols", 32, 700, 1, 1720, {"far_group": 3}), ("upola", 64, 1000, 2, 2320, {"far_group": 4}),
@@ -735,7 +735,7 @@ def test_step_groups_vs_oracle(neo_gpu, oracle, G, method, B, P, C, nb, opts):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 1300 + P, dict(opts, step_group=G)) <= TOL
 
 
-@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("G", [2, 4, 8])
 def test_step_groups_equal_one_launch(neo_gpu, oracle, G):
     """The same sums in the same order as the one-launch step: bit-identical outputs."""
     torch = pytest.importorskip("torch")
