@@ -13,8 +13,11 @@ the double-buffered slabs, the far level's XF ring of row-pair spectra, its part
 256-point partition-axis transforms — on random spectra, with history before the levels
 start, ring wraparound and re-priming, running the roles of every step in a random order
 (with the block's FDL row written at a random point among them), and checks every output
-block. It pins the index arithmetic the kernels share with the host code; the kernels'
-arithmetic itself is pinned by the GPU parity tests against the oracle.
+block. With step groups (neo_hip_upols_opts.step_group) the levels of T >= 2 G run in background
+launches every G steps on a second stream; the replay runs their roles at random points between
+the blocks they wait for and the block that waits for them (test_level_schedule_step_groups).
+It pins the index arithmetic the kernels share with the host code; the kernels' arithmetic
+itself is pinned by the GPU parity tests against the oracle.
 """
 from __future__ import annotations
 
@@ -42,8 +45,10 @@ def plan(P):
 class Sim:
     """float64 replay of the level pipeline for one channel of K bins."""
 
-    def __init__(self, H, lp, G=4, Kw=None):
-        self.H, self.lp, self.G = H, lp, G
+    def __init__(self, H, lp, G=4, Kw=None, sg=1):
+        self.H, self.lp, self.G, self.sg = H, lp, G, sg
+        self.ns = FS if sg == 1 else FT // sg - 2  # far slices per window (far_nslices)
+        self.pending = []  # step groups: background launches [roles left, due block] in stream order
         ns = lp["nseg"]
         self.P, self.K = H.shape
         # windows per phase-1 pass: the kernel's automatic choice for this many 16-column units
@@ -77,8 +82,16 @@ class Sim:
             self.ff = np.zeros((2, FT, self.K), complex)
             self.acc = np.zeros((self.Kw, FN, self.K), complex)
 
+    def join(self):
+        """lvl_join: every background launch enqueued so far completes"""
+        while self.pending:
+            roles, _ = self.pending.pop(0)
+            for r in roles:
+                r()
+
     def plain(self, x):
         """One plain step (all partitions from the ring); the levels re-prime after it."""
+        self.join()
         self.ring[self.w] = x
         y = (self.H * self.ring[(self.w - np.arange(self.P)) % self.R]).sum(0)
         self.w = (self.w + 1) % self.R
@@ -146,8 +159,8 @@ class Sim:
         self.ff[wn & 1, :, k0:k1] = np.fft.ifft(acc, axis=0)[FT:]
 
     def span(self, q):
-        """columns of far slice q (kFarS = 127 slices per window)"""
-        return q * self.K // FS, (q + 1) * self.K // FS
+        """columns of far slice q (far_nslices: 127 slices per window, kFarT / G - 2 with step groups)"""
+        return q * self.K // self.ns, (q + 1) * self.K // self.ns
 
     def far1_slice(self, W, q):
         """phase 1 for slice q of window W, in groups"""
@@ -157,17 +170,20 @@ class Sim:
             self.far1(W, k0, k1, 1, 0 if K == 1 else (2 if W < K else 1), W % K)
 
     def roles(self, n, w):
-        """the slice roles of step n (block at ring row w), as closures"""
+        """the slice roles of step n's launch (block at ring row w), as closures; step groups: the
+        levels of T < 2 sg (block_levels)"""
         lp, K, R = self.lp, self.K, self.R
         out = []
         for l, T in enumerate(lp["T"]):
+            if self.sg > 1 and T >= 2 * self.sg:
+                break
             U = K // 16 if K >= 16 else K  # 16-column units (toep_geom: one window part each)
             st, W = n % T, n // T + 1
             u0, u1 = st * U // T, (st + 1) * U // T
             if u1 > u0:
                 k0, k1 = u0 * K // U, u1 * K // U
                 out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w + W * T - n) % R, k0, k1, W & 1))
-        if lp["nseg"]:
+        if lp["nseg"] and self.sg == 1:
             q, W = n % FT, n // FT + 1
             if q < FS:  # phase 1 and 2a of slice q
                 k0, k1 = self.span(q)
@@ -178,13 +194,39 @@ class Sim:
                 out.append(lambda k0=k0, k1=k1: self.far2b(W, k0, k1, 1, self.Kw > 1))
         return out
 
+    def bg_roles(self, n0, w0):
+        """step groups: the background launch issued at step n0 (slice_part), as closures"""
+        lp, K, R, G = self.lp, self.K, self.R, self.sg
+        out = []
+        for l, T in enumerate(lp["T"]):
+            if T < 2 * G:
+                continue
+            U = K // 16 if K >= 16 else K
+            j, np_, W = (n0 % T) // G, T // G - 1, n0 // T + 1
+            if j >= 1:
+                k0, k1 = (j - 1) * U // np_ * K // U, j * U // np_ * K // U
+                if k1 > k0:
+                    out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w0 + W * T - n0) % R, k0, k1, W & 1))
+        if lp["nseg"]:
+            q, W = (n0 % FT) // G, n0 // FT + 1
+            if 1 <= q <= self.ns:  # phase 1 and 2a of slice q - 1
+                k0, k1 = self.span(q - 1)
+                out.append(lambda: self.far1_slice(W, q - 1))
+                out.append(lambda k0=k0, k1=k1: self.far2a((w0 + W * FT - n0) % R, W, k0, k1, 1))
+            if q >= 2:  # 2b of slice q - 2
+                k0, k1 = self.span(q - 2)
+                out.append(lambda k0=k0, k1=k1: self.far2b(W, k0, k1, 1, self.Kw > 1))
+        return [out[i] for i in self.rng.permutation(len(out))]  # any order inside a launch
+
     def prime(self):
+        self.join()
         for l in range(len(self.lp["T"])):
             self.toep(l, self.w, 0, self.K, 0)
         if self.lp["nseg"]:
             ns = self.lp["nseg"]
-            for q in range(FS + 1):  # launch q: phase 1 + 2a of slice q, 2b of slice q - 1
-                if q < FS:
+            FS_ = self.ns
+            for q in range(FS_ + 1):  # launch q: phase 1 + 2a of slice q, 2b of slice q - 1
+                if q < FS_:
                     k0, k1 = self.span(q)
                     self.far1(0, k0, k1, ns)
                     self.far2a(self.w, 0, k0, k1, ns)
@@ -211,8 +253,36 @@ class Sim:
             self.ring[w] = x
 
         jobs = self.roles(n, w) + [block_read, block_write]
-        for i in self.rng.permutation(len(jobs)):
-            jobs[i]()
+        jobs = [jobs[i] for i in self.rng.permutation(len(jobs))]
+        G = self.sg
+        if G > 1:
+            if n % G == 0:
+                # issued now; it waits for the blocks before n - G (odd group) / n - 2 G (even:
+                # its predecessor waited for those), so it may run beside the blocks from there on
+                # (those already done here); due before the next even group's block
+                odd = (n // G) & 1
+                self.pending.append([self.bg_roles(n, w), n + G if odd else n + 2 * G])
+            # the block of an even group waits for every background launch due by now
+            while self.pending and self.pending[0][1] <= n:
+                roles, _ = self.pending.pop(0)
+                for r in roles:
+                    r()
+            # background roles (in stream order) interleaved at random with this launch's
+            bgq = [r for p in self.pending for r in p[0]]
+            k = int(self.rng.integers(0, len(bgq) + 1))
+            slots = set(self.rng.choice(len(jobs) + k, size=k, replace=False).tolist()) if k else set()
+            it, jt = iter(bgq[:k]), iter(jobs)
+            jobs = [next(it) if i in slots else next(jt) for i in range(len(jobs) + k)]
+            left = k  # drop the executed roles from the pending launches
+            while left:
+                p = self.pending[0]
+                d = min(left, len(p[0]))
+                del p[0][:d]
+                left -= d
+                if not p[0]:
+                    self.pending.pop(0)
+        for j in jobs:
+            j()
         self.w = (w + 1) % R
         self.n = n + 1
         return y[0]
@@ -286,6 +356,31 @@ def test_level_schedule_window_groups(P, Kw):
     H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
     sim = Sim(H, lp, Kw=Kw)
     nb = 2 * P + 700
+    X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
+    worst = 0.0
+    for t in range(nb):
+        y = sim.plain(X[t]) if (t < 37 or nb // 2 <= t < nb // 2 + 3) else sim.step(X[t])
+        m = min(P, t + 1)
+        ref = (H[:m] * X[t - np.arange(m)]).sum(0)
+        worst = max(worst, float(np.abs(y - ref).max() / (np.abs(ref).max() + 1e-300)))
+    assert worst < 1e-12, worst
+
+
+@pytest.mark.parametrize("P,sg,Kw", [(40, 2, None), (100, 4, None), (300, 4, None), (300, 8, None), (700, 2, 3),
+                                     (700, 4, 2), (1100, 8, 4), (450, 4, 3)])
+def test_level_schedule_step_groups(P, sg, Kw):
+    """Step groups (neo_hip_upols_opts.step_group = sg): the block launch of every step (the
+    block and the levels of T < 2 sg) and a background launch every sg steps (slice_part: level
+    T's window W + 1 in T / sg - 1 parts at t_W + sg j, the far level's slices phase 1 / 2a one
+    group and 2b two groups after the window start), the background launches running at random
+    points between the blocks they wait for (before n - sg, odd groups) and the even-group block
+    that waits for them; across plain steps (join) and re-priming."""
+    lp = plan(P)
+    rng = np.random.default_rng(P + 10 * sg)
+    K = 32
+    H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
+    sim = Sim(H, lp, Kw=Kw, sg=sg)
+    nb = max(3 * P, 2 * P + 300) if lp["nseg"] else 3 * P + 60
     X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
     worst = 0.0
     for t in range(nb):
