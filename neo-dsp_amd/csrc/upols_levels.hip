@@ -1429,15 +1429,18 @@ static void* g_tl = nullptr;
 static int64_t g_tl_n = 0, g_tl_cap = 0;
 #endif
 
+static unsigned launch_grid(const slice_args& a)
+{
+    unsigned t = unsigned(a.f3nwg + a.f2nwg + a.nblk + a.f1nwg);
+    for (int l = 0; l < a.ntp; ++l) t += unsigned(a.tp[l].nwg);
+    return t;
+}
+
 // kernel of a launch: part 0 the step kernel (every role), 1 the block alone, 2 the slices alone
 static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStream_t s, int part = 0)
 {
     slice_args a = a_in;
-    const unsigned grid = unsigned(a.f3nwg + a.f2nwg + a.nblk + a.f1nwg) + [&] {
-        unsigned t = 0;
-        for (int l = 0; l < a.ntp; ++l) t += unsigned(a.tp[l].nwg);
-        return t;
-    }();
+    const unsigned grid = launch_grid(a);
     if (!grid) return NEO_HIP_OK;
 #ifdef NEO_TIMELINE
     if (int64_t(grid) > g_tl_cap) {
@@ -1704,6 +1707,9 @@ static int group_streams(upols_t* h)
     if (h->bg) return NEO_HIP_OK;
     int lo = 0, hi = 0;
     NEO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+#ifdef NEO_BG_PRIO_NORMAL  // diagnostic builds (A/B): the background stream at the default priority
+    lo = 0;
+#endif
     NEO_HIP_CHECK(hipStreamCreateWithPriority(&h->bg, hipStreamNonBlocking, lo));  // lo: the least urgent
     for (hipEvent_t* e : {&h->ev_blk, &h->ev_sl[0], &h->ev_sl[1], &h->ev_join})
         NEO_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -1744,8 +1750,8 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
         if (odd || primed) NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
         slice_args b = base_args(h);
         slice_part(h, n, h->wpos, b);
-        upols_t::ev_group* eb = nullptr;
-        if ((rc = timing_begin(h, 2, &eb)) || (rc = timing_mark(eb, 0, h->bg))) return rc;
+        upols_t::ev_group* eb = nullptr;  // timed when it launches (the first group after a window start may be empty)
+        if (launch_grid(b) && ((rc = timing_begin(h, 2, &eb)) || (rc = timing_mark(eb, 0, h->bg)))) return rc;
         if (eb) eb->part = 1;
         if ((rc = launch_step_kernel(h, b, h->bg, 2))) return rc;
         if ((rc = timing_mark(eb, 1, h->bg))) return rc;

@@ -818,8 +818,10 @@ def test_step_group_timing_detail(neo_gpu):
     torch.cuda.synchronize()
     conv.set_timing(False)
     parts = conv.timing_detail()
-    assert [n for _, n in parts] == [16, 4, 0, 0]
-    assert parts[0][0] > 0 and parts[1][0] > 0  # the first background launch (step 0) is empty
+    # 16 block launches; background launches at steps 0, 4, 8, 12, the first one empty (nothing of
+    # a window starting at step 0 is due yet: the levels primed it) and not timed
+    assert [n for _, n in parts] == [16, 3, 0, 0]
+    assert parts[0][0] > 0 and parts[1][0] > 0
     assert conv.step_group() == 4
     with pytest.raises(RuntimeError):
         neo_gpu.UpolsConvolver(1, 64, 300, options={"step_group": 3})

@@ -8,8 +8,9 @@ cd "$R"
 O=$R/gpurun_out
 mkdir -p $O
 TAG=${1:-r2}
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1; echo "pytest exit=$?" >> $O/pytest_gpu_$TAG.log
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1; rc=$?; echo "pytest exit=$rc" >> $O/pytest_gpu_$TAG.log
 tail -2 $O/pytest_gpu_$TAG.log
+[ $rc -lt 124 ] || exit $rc  # a crash or a time limit: nothing more on the GPU in this call
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 && \
 timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_c5full_$TAG.json 2> $O/bench_c5full_$TAG.err && \
 timeout -k 10 600 python bench.py --workload c5 --gpus 1 --steps 20 --warmup 5 --no-fft > $O/bench_c5_$TAG.json 2> $O/bench_c5_$TAG.err && \
@@ -18,6 +19,8 @@ timeout -k 10 600 python bench.py --workload c2 --steps 20 --warmup 3 > $O/bench
 timeout -k 10 300 python bench.py --workload c4 --steps 128 --no-cpu-baseline --no-fft > $O/bench_c4_$TAG.json 2> $O/bench_c4_$TAG.err && \
 timeout -k 10 300 python bench.py --workload c3 --steps 256 --no-cpu-baseline --no-fft > $O/bench_c3_$TAG.json 2> $O/bench_c3_$TAG.err && \
 timeout -k 10 300 python bench.py --workload c5 --host-io --steps 200 > $O/bench_c5_hostio_$TAG.json 2> $O/bench_c5_hostio_$TAG.err && \
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+  bench.py --gpus 2 --steps 20 --warmup 5 --no-fft --no-host-io > $O/bench_c5full_n2_$TAG.json 2> $O/bench_c5full_n2_$TAG.err && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5full_$TAG -o run -- python3 $R/bench.py --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5full_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$TAG -o run -- python3 $R/bench.py --workload c5 --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5_$TAG.log 2>&1 && \
