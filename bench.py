@@ -578,7 +578,7 @@ def run_upols(args, world, rank, local):
             g = b / (ms * 1e-3) / 1e9
             kernels.append({"kernel": kname, "ms_per_launch": ms, "launches_per_step": 1.0 / per,
                             "algorithmic_bytes_per_launch": b, "achieved_gbs": g, "frac": g / PEAK_HBM_GBS,
-                            "traffic": load_pmc_traffic(args.workload, kname)})
+                            "traffic": load_pmc_traffic(f"{args.workload}_{kname.split('<')[0]}", kname.split("<")[0])})
         kernels[0]["bytes_by_role"] = {"toeplitz": G * roles["toeplitz"], "far": G * roles["far"]}
         kernels[1]["bytes_by_role"] = {"block": roles["block"], "toeplitz": roles["toeplitz_block"]}
         dom = kernels[0]
