@@ -291,7 +291,8 @@ def algorithmic_bytes(C, B, P, plan, G=1, far_k=0):
                rows + b - a + T - 1 FDL rows + T slab entries (8 B each)
     far level, C*B/128 columns per step (on average: 127 slices per 128-block window): per
                column 256 FDL rows and the new row-pair spectrum (256 f) stored by phase 2a,
-               read back with its segment spectrum by phase 2b one step later, 128 far-field
+               read back with its segment spectrum by phase 2b one step later (step groups: kept
+               in registers, one workgroup doing both, far2c_role), 128 far-field
                entries; phase 1 takes K windows per pass over the nseg - 1 older row-pair and
                segment spectra (1/K per window), and 2b segments 1 .. j of window j of a group
                (K - 1 spectrum pairs per window on average): 256 (4 + 2 (nseg - 1) / K + K - 1)
@@ -305,7 +306,9 @@ def algorithmic_bytes(C, B, P, plan, G=1, far_k=0):
     toep_block = sum(v for T, v in lv if G > 1 and T < 2 * G)
     ns = plan["nseg"]
     K = far_group(ns, C * B // 16) if not far_k else far_k
-    far = C * B / 128 * 8 * (256 * (4 + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
+    # step groups: phase 2 keeps the fresh spectrum in registers (far2c_role), 3 instead of 4
+    fresh = 4 if G == 1 else 3
+    far = C * B / 128 * 8 * (256 * (fresh + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
     out = {"block": block, "toeplitz": toep, "far": far}
     if G > 1:
         out["toeplitz_block"] = toep_block

@@ -175,6 +175,7 @@ struct slice_args {
     // phase 1's partial sums, the window group's extra segments, the inverse transform
     int f3nwg, f3u0, f3wn;
     int f2grp;    // phase-1 window groups on: a unit in window j of its group takes segments 1..j in 2b
+    int f2comb;   // step groups: 2b also runs 2a's fresh transform for its units (f2tw: its rows), no slot read-back
     cf* f2acc;    // as f1acc
     cf* f3ff;     // 2b's target far window [C][128][B]
     void* tl;     // timeline builds (NEO_TIMELINE): per-workgroup records of the launch
@@ -1011,6 +1012,96 @@ __device__ __forceinline__ void far2b_role(const slice_args& sa, int bid, char* 
         buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
 }
 
+// far phase 2 in one workgroup (step groups' background launches, where phase 2's chain is not
+// the step's longest): the fresh row pair's transform (stored to its slot for later windows, as
+// 2a) kept in registers for the products of 2b -- no write-then-read of the slot within a window.
+// Steady state only (one fresh segment); priming runs 2a and 2b.
+template<int KMAX>
+__device__ __forceinline__ void far2c_role(const slice_args& sa, int bid, char* smem)
+{
+    cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
+    cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
+    cf* tws = z + kFN;                       // twiddles
+    const int t = threadIdx.x, a = t >> 4, cp = t & 15;
+    const int gpc = sa.B / 16, u = sa.f3u0 + bid, c = u / gpc, g = u - c * gpc, k = g * 16 + cp;
+    const bool unit0 = g == 0;  // uniform per workgroup: the unit holding packed bin 0
+    const int M = sa.M, nseg = sa.nseg;
+    auto slot = [&](int s) { return ((sa.f3wn - s - 1) % M + M) % M; };
+    const int64_t fs = sa.B;
+    const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));
+    tws[t] = sa.twf[t];
+    const __amdgpu_buffer_rsrc_t fres =
+        buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+    const __amdgpu_buffer_rsrc_t ares =
+        buf_rsrc(sa.f2acc + int64_t((sa.f3wn % sa.fK) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
+    const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
+    const int ao = (a * 16 + cp) * int(sizeof(cf)), as = 16 * 16 * int(sizeof(cf));  // f = a + 16 i
+    auto z0 = [&](int i) { return unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0; };
+    // the fresh row pair: rows tw - 3 128 + a + 16 n (one wrap of the ring at most)
+    cf x[16];
+    {
+        int r0 = (sa.f2tw - 3 * kFarT + a) % sa.ring;
+        r0 = r0 < 0 ? r0 + sa.ring : r0;
+#pragma unroll
+        for (int n = 0; n < 16; ++n) {
+            const int r = r0 + 16 * n >= sa.ring ? r0 + 16 * n - sa.ring : r0 + 16 * n;
+            x[n] = buf_ld(fres, int((int64_t(r) * sa.pstride + k) * int(sizeof(cf))), 0);
+        }
+    }
+    __syncthreads();  // twiddles
+    col_fft<-1, 16>(x, lds, tws, a, cp, true);
+    if (unit0) bin0_exchange<true>(x, z, a, cp);  // uniform per workgroup
+    cf v[16];
+    {
+        cf hv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            v[i] = buf_ld(ares, ao, i * as);
+            hv[i] = buf_ld(hres, vo, int(16 * i * fs * int(sizeof(cf))));
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) buf_st(x[i], xres, vo, slot(0) * spec + int(16 * i * fs * int(sizeof(cf))));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            f2v w = {v[i].x, v[i].y};
+            pk_coef(hv[i], z0(i)).mac(w, x[i]);
+            v[i] = cf{w.x, w.y};
+        }
+    }
+    // the window group's segments 1 .. j (slots f3wn - 2 .. f3wn - j - 1), as far2b_role
+    int jw = 0;
+    if (sa.f2grp) {  // uniform per workgroup
+        const int K = sa.fK, cls = (u / kF1UG) % K, first = far_first(cls, K);
+        jw = sa.f3wn >= first ? (sa.f3wn - cls) % K : 0;
+    }
+    const int s1 = jw + 1 < nseg ? jw + 1 : nseg;
+    for (int s = 1; s < s1 && s < KMAX; ++s) {  // uniform per workgroup
+        cf hv[16], xv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            hv[i] = buf_ld(hres, vo, s * spec + int(16 * i * fs * int(sizeof(cf))));
+            xv[i] = buf_ld(xres, vo, slot(s) * spec + int(16 * i * fs * int(sizeof(cf))));
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            f2v w = {v[i].x, v[i].y};
+            pk_coef(hv[i], z0(i)).mac(w, xv[i]);
+            v[i] = cf{w.x, w.y};
+        }
+    }
+    __syncthreads();  // the pack exchange's reads of z are done
+    NEO_TL_MARK(sa);
+    if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
+    col_fft<1, 16>(v, lds, tws, a, cp, true);
+    constexpr float sc = 1.0f / kFN;
+    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * kFarT * fs, spec / 2);
+#pragma unroll
+    for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128
+        buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
+}
+
 #ifndef NEO_ROLES
 #define NEO_ROLES 63  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2a, 32 far 2b
 #endif
@@ -1083,7 +1174,10 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
             bid -= a.f3nwg;
             return false;
         }
-        if ((NEO_ROLES & 32) && threadIdx.x < 256) far2b_role<KMAX>(a, bid, smem);
+        if ((NEO_ROLES & 32) && threadIdx.x < 256) {
+            if (a.f2comb) far2c_role<KMAX>(a, bid, smem);  // uniform per launch
+            else far2b_role<KMAX>(a, bid, smem);
+        }
         return true;
     };
     auto far2a = [&]() {
@@ -1485,8 +1579,8 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
 // window W runs phase 1 and 2a at step q of window W - 1 (2a reads FDL rows up to the last block
 // before that window) and 2b at step q + 1 (<= the window's last: the far field is complete when
 // window W's first block runs). G > 1 (step groups, slice_part): kFarT / G - 2 slices, phase 1
-// and 2a of slice q at step group q + 1 of window W - 1 (its launch waits only for the blocks
-// before the previous group), 2b at group q + 2.
+// of slice q at step group q + 1 of window W - 1 (its launch waits only for the blocks before the
+// previous group), phase 2 (far2c_role: 2a and 2b in one workgroup) at group q + 2.
 static int far_nslices(const upols_t* h) { return h->sg == 1 ? kFarT - 1 : kFarT / h->sg - 2; }
 
 static int far_u(int64_t U, int q, int ns) { return int(q * U / ns); }
@@ -1593,7 +1687,7 @@ static void block_levels(const upols_t* h, int64_t n, int w, slice_args& a)
 // the block launch of step n0 + G waits for it. So a level of window T >= 2 G computes window W + 1
 // in T / G - 1 parts at the steps t_W + G j, j = 1 .. T / G - 1 (part j - 1; its rows end at t_W - 1),
 // the last due one group before t_{W+1}; the far level's slice q (kFarT / G - 2 of them) runs
-// phase 1 and 2a at group q + 1 and 2b at group q + 2 of the window before.
+// phase 1 at group q + 1 and phase 2 (2a and 2b in one workgroup) at group q + 2 of the window before.
 static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
 {
     const level_plan& lp = h->lv;
@@ -1607,19 +1701,15 @@ static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
     if (lp.nseg) {
         const int64_t U = far_units(h), W = n0 / kFarT + 1;
         const int q = int(n0 % kFarT) / G, ns = far_nslices(h);
-        if (q >= 1 && q <= ns) {
-            a.f2u0 = far_u(U, q - 1, ns);
-            a.f2nwg = far_u(U, q, ns) - a.f2u0;
-            a.f2tw = ring_add(w0, W * kFarT - n0, h->ring);
-            a.f2wn = int(W);
-            far1_args(h, W, q - 1, a);
-        }
-        if (q >= 2) {
+        if (q >= 1 && q <= ns) far1_args(h, W, q - 1, a);  // phase 1 of slice q - 1
+        if (q >= 2) {  // phase 2 of slice q - 2, 2a and 2b in one workgroup per unit (far2c_role)
             a.f3u0 = far_u(U, q - 2, ns);
             a.f3nwg = far_u(U, q - 1, ns) - a.f3u0;
             a.f3wn = int(W);
             a.f2grp = far_group(h) > 1;
             a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+            a.f2tw = ring_add(w0, W * kFarT - n0, h->ring);
+            a.f2comb = 1;
         }
     }
 }

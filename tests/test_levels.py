@@ -209,13 +209,16 @@ class Sim:
                     out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w0 + W * T - n0) % R, k0, k1, W & 1))
         if lp["nseg"]:
             q, W = (n0 % FT) // G, n0 // FT + 1
-            if 1 <= q <= self.ns:  # phase 1 and 2a of slice q - 1
-                k0, k1 = self.span(q - 1)
+            if 1 <= q <= self.ns:  # phase 1 of slice q - 1
                 out.append(lambda: self.far1_slice(W, q - 1))
-                out.append(lambda k0=k0, k1=k1: self.far2a((w0 + W * FT - n0) % R, W, k0, k1, 1))
-            if q >= 2:  # 2b of slice q - 2
+            if q >= 2:  # phase 2 of slice q - 2: 2a and 2b in one workgroup (far2c_role)
                 k0, k1 = self.span(q - 2)
-                out.append(lambda k0=k0, k1=k1: self.far2b(W, k0, k1, 1, self.Kw > 1))
+                tw = (w0 + W * FT - n0) % R
+
+                def far2c(k0=k0, k1=k1, tw=tw):
+                    self.far2a(tw, W, k0, k1, 1)
+                    self.far2b(W, k0, k1, 1, self.Kw > 1)
+                out.append(far2c)
         return [out[i] for i in self.rng.permutation(len(out))]  # any order inside a launch
 
     def prime(self):

@@ -737,7 +737,10 @@ def test_step_groups_vs_oracle(neo_gpu, oracle, G, method, B, P, C, nb, opts):
 
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_step_groups_equal_one_launch(neo_gpu, oracle, G):
-    """The same sums in the same order as the one-launch step: bit-identical outputs."""
+    """The same sums in the same order as the one-launch step. Not bit-identical: the step
+    groups' far phase 2 (far2c_role) runs the fresh transform in the workgroup that uses it, and
+    the compiler may contract its butterflies' multiply-adds differently there than in far2a_role;
+    equal to a few float32 roundings (measured 0 with 2a / 2b split in both)."""
     torch = pytest.importorskip("torch")
     B, P, C, nb = 64, 1000, 2, 700
     ir = np.stack([oracle.noise(1400 + c, B * P) for c in range(C)])
@@ -752,7 +755,7 @@ def test_step_groups_equal_one_launch(neo_gpu, oracle, G):
         torch.cuda.synchronize()
         outs.append(t.cpu().numpy())
         conv.close()
-    assert np.array_equal(outs[0], outs[1])
+    assert peak_err(outs[1], outs[0]) <= 1e-6
 
 
 def test_step_groups_mixed_paths(neo_gpu, oracle):
