@@ -90,6 +90,11 @@ def parse():
                     help="neo_hip_upols_opts.far_group: 0 auto, 1..4 windows per far phase-1 pass")
     ap.add_argument("--step-group", type=int, default=0,
                     help="neo_hip_upols_opts.step_group: 0 auto, 1 one launch per step, 2 / 4 step groups")
+    ap.add_argument("--far-level", type=int, default=-1,
+                    help="neo_hip_upols_opts.far_level: -1 auto, 0 128-block Toeplitz, 1 transform with stored "
+                         "spectra, 2 transform recomputed every window")
+    ap.add_argument("--far-phase2", type=int, default=0,
+                    help="neo_hip_upols_opts.far_phase2 (G = 1): 0 auto, 1 one workgroup per unit, 2 two steps")
     ap.add_argument("--host-io", action="store_true",
                     help="time the host-buffer boundary (neo_hip_upols_process on pinned-staged host memory): "
                          "PCIe-inclusive, reported for DESIGN.md, never the headline value")
@@ -282,7 +287,7 @@ def far_group(nseg: int, units: int) -> int:
     return min(4, max(2, int(math.floor(math.sqrt(2.0 * (nseg - 1)) + 0.5))))
 
 
-def algorithmic_bytes(C, B, P, plan, G=1, far_k=0):
+def algorithmic_bytes(C, B, P, plan, G=1, far_k=0, far_form=1):
     """Algorithmic bytes per streaming step of the step kernel k_lvl_step, by role:
     block:     window (previous block + this block), previous-block write, output (4 x 4B per
                sample), FDL row write and H0 (2 x 8B per bin), partitions 1 .. a0 - 1 (filter +
@@ -297,6 +302,9 @@ def algorithmic_bytes(C, B, P, plan, G=1, far_k=0):
                segment spectra (1/K per window), and 2b segments 1 .. j of window j of a group
                (K - 1 spectrum pairs per window on average): 256 (4 + 2 (nseg - 1) / K + K - 1)
                + 128 values per window, K = far_group(nseg, units) (upols_levels.hip).
+               far_form 2 (recomputed every window, far2r_role): per column and window the
+               (nseg + 1) 128 FDL rows of the segments' row pairs, the P - 256 filter rows of the
+               band and the 128 field rows.
     Step groups (G > 1): the levels with T < 2 G run in the block's launch ("toeplitz_block"), the
     others in the background launches of G steps ("toeplitz")."""
     nlev = len(plan["T"]) + (1 if plan["nseg"] else 0)
@@ -309,6 +317,8 @@ def algorithmic_bytes(C, B, P, plan, G=1, far_k=0):
     # step groups: phase 2 keeps the fresh spectrum in registers (far2c_role), 3 instead of 4
     fresh = 4 if G == 1 else 3
     far = C * B / 128 * 8 * (256 * (fresh + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
+    if ns and far_form == 2:
+        far = C * B / 128 * 8 * ((ns + 1) * 128 + (P - 256) + 128)
     out = {"block": block, "toeplitz": toep, "far": far}
     if G > 1:
         out["toeplitz_block"] = toep_block
@@ -413,10 +423,13 @@ def run_upols(args, world, rank, local):
     torch.cuda.set_device(dev)
     P = neo.num_partitions(L, B)
     conv = neo.UpolsConvolver(C, B, P, device=local, options={"step_group": args.step_group,
-                                                              "far_group": args.far_group})
+                                                              "far_group": args.far_group,
+                                                              "far_phase2": args.far_phase2,
+                                                              "far_level": args.far_level})
     conv.set_batch(False)  # streaming: one block per step, as a real-time caller runs it
     levels = conv.ahead_info()[0] and not args.no_ahead
     conv_far_group = conv.far_group()
+    conv_far_form = conv.far_form()
     G = conv.step_group()
     plan = neo.convolution.level_plan(P)
     g = torch.Generator(device=dev).manual_seed(8 + rank)
@@ -466,6 +479,7 @@ def run_upols(args, world, rank, local):
         t2 = time.perf_counter()
         e0.record(sobj)
         feed.run(args.steps)
+        conv.join_background(stream)  # step groups: the background slice launches issued by these steps
         e1.record(sobj)
         t3 = time.perf_counter()
         torch.cuda.synchronize()
@@ -542,7 +556,7 @@ def run_upols(args, world, rank, local):
                        "output before the next call (max over ranks)"}
 
     if levels and G == 1:
-        roles = algorithmic_bytes(C, B, P, plan, 1, conv_far_group)
+        roles = algorithmic_bytes(C, B, P, plan, 1, conv_far_group, conv_far_form)
         # one launch per step: HIP events around a second run of the timed steps, or the wall
         # time of the timed steps where that is smaller (with timing events on it the stream's
         # launches slow down; at one channel the event run is host-bound)
@@ -570,32 +584,40 @@ def run_upols(args, world, rank, local):
         # launch of the level slices per G steps, overlapping; per-kernel HIP events (the C-ABI's
         # timing parts 0 / 1, on the stream each kernel runs on) give each kernel's launch time,
         # the wall time of the timed steps the whole step's
-        roles = algorithmic_bytes(C, B, P, plan, G, conv_far_group)
-        step_ms = elapsed * 1e3 / args.steps
+        roles = algorithmic_bytes(C, B, P, plan, G, conv_far_group, conv_far_form)
         by_blk = roles["block"] + roles["toeplitz_block"]
         by_sl = G * (roles["toeplitz"] + roles["far"])
         by = by_blk + by_sl / G
-        kb, ks = f"k_lvl_block<{B}>", "k_lvl_slices"
+        kb, ks = f"k_lvl_block<{B}>", f"k_lvl_slices<{2 if conv_far_group <= 2 else 4}>"
         kernels = []
         for kname, b, ms, per in ((ks, by_sl, det[1], G), (kb, by_blk, det[0], 1)):
             g = b / (ms * 1e-3) / 1e9
             kernels.append({"kernel": kname, "ms_per_launch": ms, "launches_per_step": 1.0 / per,
-                            "algorithmic_bytes_per_launch": b, "achieved_gbs": g, "frac": g / PEAK_HBM_GBS,
-                            "traffic": load_pmc_traffic(f"{args.workload}_{kname.split('<')[0]}", kname.split("<")[0])})
+                            "algorithmic_bytes_per_launch": b, "achieved_gbs_alone": g,
+                            "traffic": load_pmc_traffic(f"{args.workload}_{kname.split('<')[0]}", kname.split("<")[0]),
+                            "note": "launch time measured while the other kernel runs beside it (shared HBM), so "
+                                    "bytes / launch time understates the kernel; the step pair is the roofline unit"})
         kernels[0]["bytes_by_role"] = {"toeplitz": G * roles["toeplitz"], "far": G * roles["far"]}
         kernels[1]["bytes_by_role"] = {"block": roles["block"], "toeplitz": roles["toeplitz_block"]}
-        dom = kernels[0]
+        # the roofline unit is the step: G block launches and one slice launch per G steps run side
+        # by side on two streams, so the dominant "kernel" is that pair; its GPU time per step is the
+        # HIP-event time on the launch stream around a second run of the timed steps with the
+        # background launches joined onto it (neo_hip_upols_join_background), or the wall time of
+        # the timed steps where that is smaller
+        step_ms = min(gpu_ms["levels"], elapsed * 1e3 / args.steps)
         gbs = by / (step_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": dom["frac"], "traffic": dom["traffic"],
-                "traffic_over_algorithmic": dom["traffic"] / by_sl if dom["traffic"] else None, "kernel": ks,
-                "kernel_avg_ms": det[1], "steps_per_launch": G,
-                "timing": "HIP events around every launch of each kernel on its own stream (slices: the handle's "
-                          "background stream; block: the caller's), averaged; the two kernels overlap",
-                "algorithmic_bytes_per_launch": by_sl, "kernels": kernels,
-                "step": {"ms_per_step": step_ms, "algorithmic_bytes_per_step": by, "achieved_gbs": gbs,
-                         "frac": gbs / PEAK_HBM_GBS, "bytes_by_role": roles,
-                         "note": "all algorithmic bytes of a step over the wall time per step of the timed region"},
+        tr = [k["traffic"] for k in kernels]
+        traffic = tr[0] / G + tr[1] if all(tr) else None
+        roof = {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
+                "traffic_over_algorithmic": traffic / by if traffic else None,
+                "kernel": f"{kb} x{G} + {ks} x1 (one step group, two streams, overlapped)",
+                "kernel_avg_ms": step_ms, "steps_per_launch": 1, "step_group": G,
+                "timing": "GPU time per step: min(HIP events on the launch stream around a second run of the timed "
+                          "steps, background slice launches joined onto that stream before the closing event; "
+                          "wall time of the timed steps); per-kernel launch times in kernels[] (events around "
+                          "every launch, each on its own stream)",
+                "algorithmic_bytes_per_launch": by, "bytes_by_role": roles, "kernels": kernels,
                 "d2d_copy_gbs": copy_ceiling_gbs(dev)}
     else:
         roof = {"bound": "hbm", "achieved": gbs_plain, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -646,6 +668,8 @@ def run_upols(args, world, rank, local):
                                f"L={L} taps (P={P}), one block per step",
                    "channels_per_gpu": C, "channels_total": C_total, "block": B, "taps": L, "partitions": P,
                    "far_group": conv_far_group, "step_group": G,
+                   "far_form": {0: "none", 1: "transform, stored spectra", 2: "transform recomputed every window",
+                                3: "128-block Toeplitz"}[conv_far_form],
                    "streaming": ("levels: block step p<%d, Toeplitz %s, far %d segments" %
                                  (plan["a0"], list(zip(plan["T"], plan["a"], plan["b"])), plan["nseg"])
                                  if levels else "plain step"),

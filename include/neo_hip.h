@@ -109,7 +109,10 @@ typedef struct neo_hip_upols_opts {
     int batch_bins;       /* batched passes: 0 auto (1), else bins per lane vector (1 or 2) */
     int levels;           /* single-block steps: -1 auto (streaming levels from 64 partitions), 0 plain step, 1 levels */
     int far_level;        /* streaming levels, partitions >= 256: -1 auto (= 1), 0 a 128-block Toeplitz level (more
-                             VALU / LDS work, fewer bytes), 1 the 128-block partition-axis transform level */
+                             VALU / LDS work), 1 the 128-block partition-axis transform level with stored segment
+                             and row-pair spectra, 2 the same transform recomputed every window from the filter and
+                             FDL rows (fewest bytes; 2 nseg + 1 transforms per unit and window: more VALU, a longer
+                             chain) */
     int far_group;        /* far transform level: 0 auto, else 1..4 windows per phase-1 pass over the stored
                              segment spectra (auto: 2, or round(sqrt(2 (nseg - 1))) from 32768 16-column units) */
     int toep_split;       /* 32-block Toeplitz level: 0 auto (2 below 256 16-column units), 1 whole windows per
@@ -119,6 +122,10 @@ typedef struct neo_hip_upols_opts {
                              caller's stream, the level slices of G calls as ONE launch on the handle's background
                              stream, issued at the group's first call (ordered by events; the output of a call is
                              complete when the caller's stream reaches it, as with G = 1) */
+    int far_phase2;       /* far transform level, G = 1: 0 auto, 1 one workgroup per unit (the fresh row pair's
+                             transform kept in registers for the window's products), 2 two steps (the fresh
+                             transform stored to its slot, read back with the products one step later: half the
+                             chain per step); step groups always run 1 */
 } neo_hip_upols_opts;
 NEO_HIP_API int neo_hip_upols_create_ex(int channels, int block, int partitions, int device, int method,
                                         const neo_hip_upols_opts* opts, neo_hip_upols** h);
@@ -181,9 +188,20 @@ NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, 
 /* windows per far phase-1 pass the handle runs (neo_hip_upols_opts.far_group or the automatic
  * choice); 0 without a far transform level */
 NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* windows);
+/* the form of the handle's p >= 256 band: 0 none, 1 partition-axis transform with stored segment
+ * and row-pair spectra (far phase 1 + 2), 2 the same transform recomputed every window from the
+ * filter and FDL rows (neo_hip_upols_opts.far_level 2), 3 the
+ * 128-block Toeplitz level (far_level 0) */
+NEO_HIP_API int neo_hip_upols_get_far_form(neo_hip_upols* h, int* form);
 /* steps per background launch of the streaming levels' slices (neo_hip_upols_opts.step_group or
  * the automatic choice): 1 = one launch per step */
 NEO_HIP_API int neo_hip_upols_get_step_group(neo_hip_upols* h, int* steps);
+/* make `stream` wait (device-side, no host wait) for every background slice launch of the
+ * handle's step groups issued so far; a no-op with one launch per step. Outputs never need
+ * it (a block's launch already waits for the slices it reads); a caller bracketing steps with
+ * events on `stream`, or reusing the device's bandwidth right after, does. No reference
+ * counterpart: the reference's operator() is synchronous (uniform_partitioned_convolver.hpp:47-65). */
+NEO_HIP_API int neo_hip_upols_join_background(neo_hip_upols* h, void* stream);
 /* -- Multichannel convolver over several devices ------------------------------
  * C channels cut into n contiguous shards, shard i = channels [C i / n, C (i + 1) / n) on
  * devices[i] (a device may repeat), each a neo_hip_upols handle of its own (own stream).

@@ -531,12 +531,13 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
                      const neo_hip_upols_opts* opt, neo_hip_upols** out)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
-    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0, 0, 0};
-    if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.far_level < -1 || o.far_level > 1 ||
+    const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0, 0, 0, 0};
+    if (o.fused < -1 || o.fused > 1 || o.levels < -1 || o.levels > 1 || o.far_level < -1 || o.far_level > 2 ||
         o.split_workgroups < 0 ||
         (o.batch_blocks && (o.batch_blocks < 2 || o.batch_blocks > kMaxBatch || (o.batch_blocks & (o.batch_blocks - 1)))) ||
         o.batch_bins < 0 || o.batch_bins > 2 || o.far_group < 0 || o.far_group > 4 || o.toep_split < 0 || o.toep_split > 2 ||
-        (o.step_group != 0 && o.step_group != 1 && o.step_group != 2 && o.step_group != 4 && o.step_group != 8))
+        (o.step_group != 0 && o.step_group != 1 && o.step_group != 2 && o.step_group != 4 && o.step_group != 8) ||
+        o.far_phase2 < 0 || o.far_phase2 > 2)
         return fail(NEO_HIP_EINVAL, "invalid convolver options");
     *out = nullptr;
     if (channels < 1) return fail(NEO_HIP_EINVAL, "channels must be >= 1");
@@ -553,8 +554,18 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     plan_levels(partitions, h->lv, o.far_level);
     h->far_k = o.far_group;
     h->toep_jh = o.toep_split;
+    h->f2mode = o.far_phase2;
     h->sg = o.step_group ? o.step_group : step_group_for(channels, block, partitions);
+    // the far level's form: the stored spectra (phase 1 + 2) by default; recomputed every window
+    // (far2r_role) on request -- fewer bytes (C5: 15 instead of 23 rows per column and step) but
+    // 2 nseg + 1 transforms per unit and window: same-box A/B with step groups, stored vs
+    // recomputed, us per step: c5full 107-109 vs 115-124 (VALU), C5 15.9 vs 15.8-16.4, C4 12.4 vs
+    // 18-20 (the 27-transform chain of 13 segments bounds the background launch)
+    h->far_raw = h->lv.nseg && o.far_level == 2;
     if (h->lv.nseg) h->ring = std::max(h->ring, kFarRing);  // far slices read 383 blocks back
+    // recomputed: a window's slices read the band's rows back to t_W - 128 (nseg + 2) > t_W - P - 128
+    // while blocks up to t_W + 3 may be written beside them (step groups)
+    if (h->far_raw) h->ring = std::max(h->ring, partitions + 2 * kFarT);
     h->ola = ola || v2;
     h->v2 = v2;
     h->fused = 2.0 * 8.0 * double(channels) * double(partitions) * double(block) < double(kFusedMaxBytes);

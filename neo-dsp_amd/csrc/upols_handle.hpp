@@ -68,6 +68,9 @@ struct neo_hip_upols {
     bool fv_dirty = true;           // far segment spectra to recompute (filter changed)
     int far_k = 0;                  // far phase-1 windows per pass forced by neo_hip_upols_opts.far_group (0: auto)
     int toep_jh = 0;                // T = 32 window parts forced by neo_hip_upols_opts.toep_split (0: auto)
+    int f2mode = 0;                 // far phase 2 at G = 1 forced by neo_hip_upols_opts.far_phase2 (0: auto)
+    bool far_raw = false;           // far level recomputed every window from the filter and FDL rows
+                                    // (neo_hip_upols_opts.far_level 2; far2r_role): no fv_hf / fv_xf / fv_acc
     // step groups (neo_hip_upols_opts.step_group, G = sg): G = 1 runs a step as ONE launch (the
     // block and 1/T of every level's next window); G > 1 runs the block of every call alone on the
     // caller's stream and the level slices of G steps as one launch on the handle's background

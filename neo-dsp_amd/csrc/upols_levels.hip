@@ -157,7 +157,7 @@ struct slice_args {
     int ntp;
     toep_arg tp[kLvToep];
     // far level (16-column units), common
-    int M, nseg, fnfresh;
+    int M, nseg, fnfresh, P;
     const cf* hf;
     cf* xf;
     const cf* twf;
@@ -175,7 +175,8 @@ struct slice_args {
     // phase 1's partial sums, the window group's extra segments, the inverse transform
     int f3nwg, f3u0, f3wn;
     int f2grp;    // phase-1 window groups on: a unit in window j of its group takes segments 1..j in 2b
-    int f2comb;   // step groups: 2b also runs 2a's fresh transform for its units (f2tw: its rows), no slot read-back
+    int f2comb;   // 1: 2b also runs 2a's fresh transform for its units (f2tw: its rows), no slot read-back (far2c_role);
+                  // 2: the recomputed far level (far2r_role, every segment from the filter and FDL rows)
     cf* f2acc;    // as f1acc
     cf* f3ff;     // 2b's target far window [C][128][B]
     void* tl;     // timeline builds (NEO_TIMELINE): per-workgroup records of the launch
@@ -184,7 +185,8 @@ struct slice_args {
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
 // they meet, 16 columns each, column-major with padded strides
 constexpr int kT32Band = 192;                                       // [64, 256)
-constexpr int kFarLds = (16 * 16 * 16 + 2 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange, twiddles
+constexpr int kFarLds = (16 * 16 * 16 + 2 * 256 + 8 * 256) * int(sizeof(cf));  // far roles: transposes, bin-0 exchange,
+                                                                               // twiddles, far2r_role's half pair
 // toep_tile<32, 192>: 53760 B, 3 workgroups per CU (VGPRs allow 3 too; the band in two chunks
 // of 96, 29184 B, with a 128-VGPR budget for 4 per CU measured slower: spills, serialized chunks)
 constexpr int kT32Lds = 16 * ((kT32Band + 2) + (kT32Band + 34)) * int(sizeof(cf));
@@ -1102,6 +1104,85 @@ __device__ __forceinline__ void far2c_role(const slice_args& sa, int bid, char* 
         buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
 }
 
+// Far level, recomputed form (neo_hip_upols_opts.far_level = 2; the default with step groups):
+// one workgroup per 16-column unit and window computes the window's whole far field from the
+// filter's and the FDL's own rows, nothing stored between windows but the field. Segment s
+// (partitions [128 (s + 2), 128 (s + 3))) meets the row pair tw - (s + 3) 128 + r, r < 256; the
+// pair of s + 1 is the pair of s moved back 128 rows, so its second half (n >= 8 in col_fft's
+// layout) is the first half of the pair before, kept in registers: each FDL row of the band is
+// read once per window. The segment's 128 filter rows (zero-padded to 256, zero past P) are
+// transformed beside it (the same packed bin 0 as k_lvf_filter), the products accumulate in
+// registers, one inverse transform gives samples 128..255: the field. Per column and window
+// (nseg + 1) 128 FDL rows, P - 256 filter rows and 128 field rows -- against 2 (nseg - 1) / K + K
+// + 2 stored spectra, the fresh pair, its slot and phase 1's partial sums of the stored form --
+// at 2 nseg + 1 transforms per unit and window.
+__device__ __forceinline__ void far2r_role(const slice_args& sa, int bid, char* smem)
+{
+    cf* lds = reinterpret_cast<cf*>(smem);  // [16][16][16] transposes
+    cf* z = lds + 16 * 16 * 16;              // bin-0 exchange
+    cf* tws = z + kFN;                       // twiddles
+    const int t = threadIdx.x, a = t >> 4, cp = t & 15;
+    cf* xh = tws + kFN + t;  // [8][256]: raw rows of the pair before, first half (this pair's second half)
+    const int gpc = sa.B / 16, u = sa.f3u0 + bid, c = u / gpc, g = u - c * gpc, k = g * 16 + cp;
+    const bool unit0 = g == 0;  // uniform per workgroup: the unit holding packed bin 0
+    const int64_t fs = sa.B;
+    tws[t] = sa.twf[t];
+    const int rb = int(int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
+    const __amdgpu_buffer_rsrc_t fres = buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, rb);
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.H + int64_t(c) * sa.cstride, rb);
+    const int ko = k * int(sizeof(cf));
+    auto z0 = [&](int i) { return unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0; };
+    f2v acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = f2v(0.f);
+    int r0 = (sa.f2tw - 3 * kFarT + a) % sa.ring;  // pair 0's row a (the ring holds > P + 256 rows)
+    r0 = r0 < 0 ? r0 + sa.ring : r0;
+    for (int s = 0; s < sa.nseg; ++s) {  // uniform per workgroup
+        cf x[16], hv[16];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int r = r0 + 16 * n >= sa.ring ? r0 + 16 * n - sa.ring : r0 + 16 * n;
+            x[n] = buf_ld(fres, int(int64_t(r) * sa.pstride * int(sizeof(cf))) + ko, 0);
+            const int p = (s + 2) * kFarT + a + 16 * n;
+            hv[n] = p < sa.P ? buf_ld(hres, int(int64_t(p) * sa.pstride * int(sizeof(cf))) + ko, 0) : cf{0.f, 0.f};
+            hv[n + 8] = cf{0.f, 0.f};
+        }
+        if (s == 0) {
+#pragma unroll
+            for (int n = 8; n < 16; ++n) {
+                const int r = r0 + 16 * n >= sa.ring ? r0 + 16 * n - sa.ring : r0 + 16 * n;
+                x[n] = buf_ld(fres, int(int64_t(r) * sa.pstride * int(sizeof(cf))) + ko, 0);
+            }
+        } else {
+#pragma unroll
+            for (int n = 8; n < 16; ++n) x[n] = xh[(n - 8) * 256];  // this lane's own stores
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) xh[n * 256] = x[n];
+        r0 = r0 - kFarT < 0 ? r0 - kFarT + sa.ring : r0 - kFarT;
+        if (s == 0) __syncthreads();  // twiddles (later segments: col_fft's closing barrier)
+        col_fft<-1, 16>(x, lds, tws, a, cp, true);
+        if (unit0) bin0_exchange<true>(x, z, a, cp);  // uniform per workgroup
+        col_fft<-1, 16>(hv, lds, tws, a, cp, true);   // its barriers also order bin0_exchange's z reads
+        if (unit0) bin0_exchange<true>(hv, z, a, cp);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) pk_coef(hv[i], z0(i)).mac(acc[i], x[i]);
+    }
+    cf v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = cf{acc[i].x, acc[i].y};
+    __syncthreads();  // the last pack exchange's reads of z are done
+    NEO_TL_MARK(sa);
+    if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
+    col_fft<1, 16>(v, lds, tws, a, cp, true);
+    constexpr float sc = 1.0f / kFN;
+    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * kFarT * fs, int(kFN * fs * int(sizeof(cf))) / 2);
+    const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
+#pragma unroll
+    for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128
+        buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
+}
+
 #ifndef NEO_ROLES
 #define NEO_ROLES 63  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2a, 32 far 2b
 #endif
@@ -1156,8 +1237,15 @@ __device__ __forceinline__ bool toep_skip(const slice_args& a, int& bid)
 #define NEO_STEP_WPE 3  // waves per SIMD the step kernel is compiled for (VGPR budget: 168)
 #endif
 // B = 1024 runs 512-lane workgroups (the block role's bin pairs): two waves per SIMD each
-template<int B>
-constexpr int step_wpe() { return B > 512 ? 2 : NEO_STEP_WPE; }
+// KMAX = 1 (the recomputed far level, far2r_role: 184 VGPRs) runs two waves per SIMD, which also
+// leaves a block-kernel wave (136 VGPRs) room beside two slice waves on a SIMD
+#ifndef NEO_RAW_WPE
+#define NEO_RAW_WPE 2  // diagnostic builds: 3 (the recomputed far level then spills)
+#endif
+template<int KMAX>
+constexpr int slices_wpe() { return KMAX == 1 ? NEO_RAW_WPE : NEO_STEP_WPE; }
+template<int B, int KMAX = 2>
+constexpr int step_wpe() { return B > 512 ? 2 : (KMAX == 1 ? NEO_RAW_WPE : NEO_STEP_WPE); }
 // the roles of one workgroup, in dispatch order (the longest chains first); returns the role
 // (timeline builds: 1 far 2b, 2 far 2a, 3 block, 4 + L Toeplitz level L, 9 far phase 1)
 #ifndef NEO_ORDER
@@ -1175,7 +1263,8 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
             return false;
         }
         if ((NEO_ROLES & 32) && threadIdx.x < 256) {
-            if (a.f2comb) far2c_role<KMAX>(a, bid, smem);  // uniform per launch
+            if constexpr (KMAX == 1) far2r_role(a, bid, smem);  // the recomputed far level's build
+            else if (a.f2comb) far2c_role<KMAX>(a, bid, smem);  // uniform per launch
             else far2b_role<KMAX>(a, bid, smem);
         }
         return true;
@@ -1185,7 +1274,8 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
             bid -= a.f2nwg;
             return false;
         }
-        if ((NEO_ROLES & 16) && threadIdx.x < 256) far2a_role(a, bid, smem);
+        if constexpr (KMAX > 1)
+            if ((NEO_ROLES & 16) && threadIdx.x < 256) far2a_role(a, bid, smem);
         return true;
     };
     auto block = [&]() {
@@ -1208,10 +1298,12 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
             bid -= a.f1nwg;
             return false;
         }
-        if ((NEO_ROLES & 8) && threadIdx.x < 256) {
-            if (a.f1fpl == 4) far1_role<4, KMAX>(a, bid);
-            else if (a.f1fpl == 2) far1_role<2, KMAX>(a, bid);
-            else far1_role<1, KMAX>(a, bid);
+        if constexpr (KMAX > 1) {  // no phase 1 in the recomputed form
+            if ((NEO_ROLES & 8) && threadIdx.x < 256) {
+                if (a.f1fpl == 4) far1_role<4, KMAX>(a, bid);
+                else if (a.f1fpl == 2) far1_role<2, KMAX>(a, bid);
+                else far1_role<1, KMAX>(a, bid);
+            }
         }
         return true;
     };
@@ -1264,14 +1356,14 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) void k_lvl_block(slice_args a)
 // step groups: every role but the block for the slices of G steps (the background stream);
 // 256 lanes (the roles' geometry), the step kernel's register budget
 template<int KMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NEO_STEP_WPE))) void k_lvl_slices(slice_args a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(slices_wpe<KMAX>()))) void k_lvl_slices(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
     (void)lvl_roles<512, false, KMAX, 2>(a, smem);
 }
 
 template<int B, bool OLA, int KMAX>
-__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(step_wpe<B>()))) void k_lvl_step(slice_args a)
+__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(step_wpe<B, KMAX>()))) void k_lvl_step(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
 #ifdef NEO_TIMELINE  // diagnostic builds: per-workgroup start / end (100 MHz clock) and role
@@ -1372,7 +1464,7 @@ int far_group_for(int C, int B, int P)
 static int far_group(const upols_t* h)
 {
     const int ns = h->lv.nseg;
-    if (ns < 2) return 1;
+    if (ns < 2 || h->far_raw) return 1;  // recomputed: every window on its own
     if (h->far_k) return h->far_k;  // neo_hip_upols_opts.far_group (tests, A/B runs)
     return far_group_auto(h->C, h->B, ns);
 }
@@ -1422,12 +1514,14 @@ static int lvl_buffers(upols_t* h)
     if (lp.nseg) {
         const size_t spec = C * size_t(lp.nseg) * kFN * B * sizeof(cf);
         const size_t ffb = 2 * C * kFarT * B * sizeof(cf);
-        if (!alloc(reinterpret_cast<void**>(&h->fv_hf), spec)) return undo("far segment spectra", spec);
-        if (!alloc(reinterpret_cast<void**>(&h->fv_xf), spec)) return undo("far FDL spectra", spec);
+        if (!h->far_raw) {  // the stored form: segment and row-pair spectra, phase 1 -> 2 partial sums
+            if (!alloc(reinterpret_cast<void**>(&h->fv_hf), spec)) return undo("far segment spectra", spec);
+            if (!alloc(reinterpret_cast<void**>(&h->fv_xf), spec)) return undo("far FDL spectra", spec);
+            const size_t accb = size_t(far_group(h)) * size_t(far_units(h)) * kFN * 16 * sizeof(cf);
+            if (!alloc(reinterpret_cast<void**>(&h->fv_acc), accb)) return undo("far partial sums", accb);
+        }
         if (!alloc(reinterpret_cast<void**>(&h->fv_ff), ffb)) return undo("far field", ffb);
         if (!alloc(reinterpret_cast<void**>(&h->fv_tw), kFN * sizeof(cf))) return undo("far twiddles", kFN * sizeof(cf));
-        const size_t accb = size_t(far_group(h)) * size_t(far_units(h)) * kFN * 16 * sizeof(cf);  // phase 1 -> 2
-        if (!alloc(reinterpret_cast<void**>(&h->fv_acc), accb)) return undo("far partial sums", accb);
         const auto t = make_twiddle_table(kFN);
         if (hipMemcpy(h->fv_tw, t.data(), kFN * sizeof(cf), hipMemcpyHostToDevice) != hipSuccess)
             return undo("far twiddle upload", kFN * sizeof(cf));
@@ -1513,6 +1607,7 @@ static slice_args base_args(const upols_t* h)
         a.hf = h->fv_hf;
         a.xf = h->fv_xf;
         a.twf = h->fv_tw;
+        a.P = h->P;
     }
     return a;
 }
@@ -1548,7 +1643,7 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
 #endif
     // pairs-only build where the window group is <= 2 (fewer VGPRs: every shape below
     // kFarGroupUnits), else the build for any group
-    const bool pairs = a.fK <= 2;
+    const bool pairs = a.fK <= 2, raw = h->far_raw;
     if (part == 1) {
         if (h->ola) {
             NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_block<BB, true>), dim3(grid),
@@ -1558,16 +1653,17 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
                                                                                   dim3(lstep_cfg<BB>::WG), 0, s, a))
         }
     } else if (part == 2) {
-        if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(grid), dim3(256), 0, s, a);
+        if (raw) hipLaunchKernelGGL((k_lvl_slices<1>), dim3(grid), dim3(256), 0, s, a);
+        else if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(grid), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_lvl_slices<kFarKMax>), dim3(grid), dim3(256), 0, s, a);
     } else {
 #define NEO_LVL(OL, KM)                                                                                        \
     NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, OL, KM>), dim3(grid), \
                                                                          dim3(lstep_cfg<BB>::WG), 0, s, a))
         if (h->ola) {
-            if (pairs) NEO_LVL(true, 2) else NEO_LVL(true, kFarKMax)
+            if (raw) NEO_LVL(true, 1) else if (pairs) NEO_LVL(true, 2) else NEO_LVL(true, kFarKMax)
         } else {
-            if (pairs) NEO_LVL(false, 2) else NEO_LVL(false, kFarKMax)
+            if (raw) NEO_LVL(false, 1) else if (pairs) NEO_LVL(false, 2) else NEO_LVL(false, kFarKMax)
         }
 #undef NEO_LVL
     }
@@ -1594,6 +1690,20 @@ static void far1_args(const upols_t* h, int64_t W, int q, slice_args& a)
     const int K = far_group(h), ns = far_nslices(h);
     a.f1wn = int(W);
     far1_range(h, a, far_u(U, q, ns), far_u(U, q + 1, ns), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
+}
+
+// the recomputed far level's slice q of window W (far2r_role), issued at step n (block t0 + n at
+// ring row w): every unit of the slice computes the window's field from rows before t_W - 128
+static void far_raw_args(const upols_t* h, int64_t W, int q, int w, int64_t n, slice_args& a)
+{
+    const int64_t U = far_units(h);
+    const int ns = far_nslices(h);
+    a.f3u0 = far_u(U, q, ns);
+    a.f3nwg = far_u(U, q + 1, ns) - a.f3u0;
+    a.f3wn = int(W);
+    a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+    a.f2tw = ring_add(w, W * kFarT - n, h->ring);
+    a.f2comb = 2;
 }
 
 // The block role of step n (block t0 + n at FDL ring row w) for the channels [c0, c0 + nc): its
@@ -1643,6 +1753,20 @@ static void toep_slice(const upols_t* h, int l, int64_t W, int64_t u0, int64_t u
     a.ntp = std::max(a.ntp, l + 1);
 }
 
+// Far phase 2 at G = 1 in one workgroup per unit (far2c_role, one step after phase 1) or in
+// two (2a: the fresh transform -> its slot, beside phase 1; 2b: the products and the inverse one
+// step later). One workgroup reads the fresh spectrum back from registers instead of its slot,
+// fewer bytes; two halve the chain, which bounds the step where a step has few far units.
+// Step groups always run one (their background launches have a group of slack).
+constexpr int64_t kFarWholeUnits = 32768;  // 256 units per step, as kFarGroupUnits
+
+static bool far2_whole(const upols_t* h)
+{
+    if (h->sg > 1) return true;
+    if (h->f2mode) return h->f2mode == 1;  // neo_hip_upols_opts.far_phase2
+    return far_units(h) >= kFarWholeUnits;
+}
+
 static int64_t toep_units(const upols_t* h, int T)
 {
     int JH, UPW;
@@ -1666,6 +1790,23 @@ static void block_levels(const upols_t* h, int64_t n, int w, slice_args& a)
     if (h->sg > 1 || !h->lv.nseg) return;
     const int64_t U = far_units(h), W = n / kFarT + 1;
     const int q = int(n % kFarT), ns = far_nslices(h);
+    if (h->far_raw) {  // recomputed: slice q - 1 of window W whole (far2r_role)
+        if (q >= 1 && q <= ns) far_raw_args(h, W, q - 1, w, n, a);
+        return;
+    }
+    if (far2_whole(h)) {  // phase 1 of slice q, phase 2 (far2c_role) of slice q - 1
+        if (q < ns) far1_args(h, W, q, a);
+        if (q >= 1 && q <= ns) {
+            a.f3u0 = far_u(U, q - 1, ns);
+            a.f3nwg = far_u(U, q, ns) - a.f3u0;
+            a.f3wn = int(W);
+            a.f2grp = far_group(h) > 1;
+            a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+            a.f2tw = ring_add(w, W * kFarT - n, h->ring);
+            a.f2comb = 1;
+        }
+        return;
+    }
     if (q < ns) {
         a.f2u0 = far_u(U, q, ns);
         a.f2nwg = far_u(U, q + 1, ns) - a.f2u0;
@@ -1698,7 +1839,10 @@ static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
         const int64_t j = (n0 % T) / G, np = T / G - 1, U = toep_units(h, T);
         if (j >= 1) toep_slice(h, l, n0 / T + 1, (j - 1) * U / np, j * U / np, n0, w0, a);
     }
-    if (lp.nseg) {
+    if (lp.nseg && h->far_raw) {  // recomputed: slice q - 2 of window W whole, at phase 2's time
+        const int q = int(n0 % kFarT) / G;
+        if (q >= 2 && q - 2 < far_nslices(h)) far_raw_args(h, n0 / kFarT + 1, q - 2, w0, n0, a);
+    } else if (lp.nseg) {
         const int64_t U = far_units(h), W = n0 / kFarT + 1;
         const int q = int(n0 % kFarT) / G, ns = far_nslices(h);
         if (q >= 1 && q <= ns) far1_args(h, W, q - 1, a);  // phase 1 of slice q - 1
@@ -1742,7 +1886,7 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     const level_plan& lp = h->lv;
     const int B = h->B, C = h->C, w = h->wpos;
     if (int rc = lvl_join(h, s)) return rc;  // slices of an earlier run still in flight on bg
-    if (lp.nseg && h->fv_dirty) {
+    if (lp.nseg && h->fv_dirty && !h->far_raw) {
         const unsigned grid = unsigned(C) * unsigned(lp.nseg) * unsigned(B / 16);
         hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->fv_hf, h->fv_tw, B, h->P, lp.nseg,
                            h->cstride, h->pstride);
@@ -1764,8 +1908,16 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         ta.u1 = C * (B / 16) * JH;
         ta.nwg = (ta.u1 + UPW - 1) / UPW;
     }
+    if (lp.nseg && h->far_raw) {  // recomputed: window 0's field whole, every unit in the same launch
+        a.f3u0 = 0;
+        a.f3nwg = int(far_units(h));
+        a.f3wn = 0;
+        a.f3ff = h->fv_ff;
+        a.f2tw = w;
+        a.f2comb = 2;
+    }
     if (int rc = launch_step_kernel(h, a, s)) return rc;
-    if (!lp.nseg) return NEO_HIP_OK;
+    if (!lp.nseg || h->far_raw) return NEO_HIP_OK;
     // far window 0, every segment transformed (fnfresh = nseg), in slices
     const int64_t U = far_units(h);
     const int ns = far_nslices(h);
@@ -1893,11 +2045,26 @@ extern "C" NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* wi
     return NEO_HIP_OK;
 }
 
+extern "C" NEO_HIP_API int neo_hip_upols_get_far_form(neo_hip_upols* h, int* form)
+{
+    if (!h || !form) return neo_hip::fail(NEO_HIP_EINVAL, "null handle or output");
+    *form = h->lv.nseg ? (h->far_raw ? 2 : 1) : (h->lv.n && h->lv.T[h->lv.n - 1] == neo_hip::kBigT ? 3 : 0);
+    return NEO_HIP_OK;
+}
+
 extern "C" NEO_HIP_API int neo_hip_upols_get_step_group(neo_hip_upols* h, int* steps)
 {
     if (!h || !steps) return neo_hip::fail(NEO_HIP_EINVAL, "null handle or output");
     *steps = h->sg;
     return NEO_HIP_OK;
+}
+
+extern "C" NEO_HIP_API int neo_hip_upols_join_background(neo_hip_upols* h, void* stream)
+{
+    if (!h) return neo_hip::fail(NEO_HIP_EINVAL, "null handle");
+    neo_hip::device_guard g(h->device);
+    if (g.rc) return g.rc;
+    return neo_hip::lvl_join(h, static_cast<hipStream_t>(stream));
 }
 
 #ifdef NEO_TIMELINE

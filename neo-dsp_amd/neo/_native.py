@@ -26,7 +26,8 @@ class UpolsOpts(ctypes.Structure):
     """neo_hip_upols_opts (include/neo_hip.h)."""
     _fields_ = [("fused", ctypes.c_int), ("split_workgroups", ctypes.c_int), ("batch_blocks", ctypes.c_int),
                 ("batch_bins", ctypes.c_int), ("levels", ctypes.c_int), ("far_level", ctypes.c_int),
-                ("far_group", ctypes.c_int), ("toep_split", ctypes.c_int), ("step_group", ctypes.c_int)]
+                ("far_group", ctypes.c_int), ("toep_split", ctypes.c_int), ("step_group", ctypes.c_int),
+                ("far_phase2", ctypes.c_int)]
 
 
 # every symbol declared in include/neo_hip.h: (name, restype, argtypes)
@@ -65,6 +66,8 @@ SIGNATURES = {
     "neo_hip_upols_level_plan": (_i, [_i] + [ctypes.POINTER(_i)] * 6),
     "neo_hip_upols_get_far_group": (_i, [_vp, ctypes.POINTER(_i)]),
     "neo_hip_upols_get_step_group": (_i, [_vp, ctypes.POINTER(_i)]),
+    "neo_hip_upols_join_background": (_i, [_vp, _vp]),
+    "neo_hip_upols_get_far_form": (_i, [_vp, ctypes.POINTER(_i)]),
     "neo_hip_upols_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "neo_hip_upols_multi_create": (_i, [_i, _i, _i, _vp, _i, _i, _vp, ctypes.POINTER(_vp)]),
     "neo_hip_upols_multi_destroy": (_i, [_vp]),

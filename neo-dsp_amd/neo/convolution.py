@@ -124,19 +124,22 @@ class UpolsConvolver:
     """
 
     OPTION_DEFAULTS = {"fused": -1, "split_workgroups": 0, "batch_blocks": 0, "batch_bins": 0, "levels": -1,
-                       "far_level": -1, "far_group": 0, "toep_split": 0, "step_group": 0}
+                       "far_level": -1, "far_group": 0, "toep_split": 0, "step_group": 0,
+                       "far_phase2": 0}
 
     def __init__(self, channels: int, block_size: int, partitions: int, device: int = 0, method: str = "upols",
                  options: dict | None = None):
         """`options` (neo_hip_upols_create_ex): explicit code-path choices instead of the
         shape-based defaults — fused (-1 auto / 0 / 1), split_workgroups (0 auto),
         batch_blocks (0 auto / 2..32), batch_bins (0 auto / 1 / 2), levels (-1 auto / 0 / 1),
-        far_level (-1 auto / 0 Toeplitz window of 128 blocks / 1 partition-axis transform, for p >= 256),
+        far_level (-1 auto / 0 Toeplitz window of 128 blocks / 1 partition-axis transform with stored spectra /
+        2 the transform recomputed every window, for p >= 256),
         far_group (0 auto / 1..4 windows per far phase-1 pass over the stored segment spectra),
         toep_split (0 auto / 1 / 2 window parts per unit of the 32-block Toeplitz level),
         step_group (0 auto / 1 one launch per block / 2 or 4: the block of every call alone on the
-        caller's stream, the level slices of G calls as one launch on a background stream).
-        Every choice gives the same results up to float summation order."""
+        caller's stream, the level slices of G calls as one launch on a background stream),
+        far_phase2 (G = 1: 0 auto / 1 one workgroup per unit / 2 the fresh transform one step
+        before the products). Every choice gives the same results up to float summation order."""
         lib = _native.load()
         h = ctypes.c_void_p()
         methods = {"upols": 0, "upola": 1, "upola_v2": 2}
@@ -285,6 +288,18 @@ class UpolsConvolver:
         k = ctypes.c_int()
         _native.check(_native.load().neo_hip_upols_get_step_group(self._h, ctypes.byref(k)))
         return k.value
+
+    def far_form(self) -> int:
+        """The p >= 256 band's form: 0 none, 1 transform with stored spectra, 2 transform recomputed
+        every window, 3 the 128-block Toeplitz level (neo_hip_upols_get_far_form)."""
+        k = ctypes.c_int()
+        _native.check(_native.load().neo_hip_upols_get_far_form(self._h, ctypes.byref(k)))
+        return k.value
+
+    def join_background(self, stream=None) -> None:
+        """Make `stream` (a raw hipStream_t, None = the null stream) wait for the background
+        slice launches of the step groups issued so far (device-side; no host wait)."""
+        _native.check(_native.load().neo_hip_upols_join_background(self._h, ctypes.c_void_p(stream)))
 
     # -- instrumentation ------------------------------------------------------
     def set_timing(self, enable, every: int = 1) -> None:

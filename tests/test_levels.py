@@ -45,8 +45,10 @@ def plan(P):
 class Sim:
     """float64 replay of the level pipeline for one channel of K bins."""
 
-    def __init__(self, H, lp, G=4, Kw=None, sg=1):
+    def __init__(self, H, lp, G=4, Kw=None, sg=1, whole=False, raw=False):
         self.H, self.lp, self.G, self.sg = H, lp, G, sg
+        self.whole = whole  # G = 1: far phase 2 in one workgroup per unit (far2_whole)
+        self.raw = raw  # the recomputed far level (far2r_role: every segment from ring rows each window)
         self.ns = FS if sg == 1 else FT // sg - 2  # far slices per window (far_nslices)
         self.pending = []  # step groups: background launches [roles left, due block] in stream order
         ns = lp["nseg"]
@@ -63,6 +65,8 @@ class Sim:
         self.R = self.P + 31
         if lp["nseg"]:
             self.R = max(self.R, 2 * FA)
+        if lp["nseg"] and raw:
+            self.R = max(self.R, self.P + 2 * FT)  # upols.hip: the recomputed level reads back P + 128 rows
         self.ring = np.zeros((self.R, self.K), complex)
         self.w = 0
         self.n = -1
@@ -158,6 +162,15 @@ class Sim:
                     acc[:, k - k0] += self.XF[(wn - s - 1) % self.M, :, k] * self.HF[s, :, k]
         self.ff[wn & 1, :, k0:k1] = np.fft.ifft(acc, axis=0)[FT:]
 
+    def far2r(self, tw, wn, k0, k1):
+        """the recomputed far level (far2r_role): window wn's field from the row pairs of every
+        segment (rows tw - (s + 3) 128 + r, r < 256) and the segment spectra, nothing stored"""
+        acc = np.zeros((FN, k1 - k0), complex)
+        for s in range(self.lp["nseg"]):
+            rows = [(tw - (s + 3) * FT + i) % self.R for i in range(FN)]
+            acc += np.fft.fft(self.ring[rows, k0:k1], axis=0) * self.HF[s, :, k0:k1]
+        self.ff[wn & 1, :, k0:k1] = np.fft.ifft(acc, axis=0)[FT:]
+
     def span(self, q):
         """columns of far slice q (far_nslices: 127 slices per window, kFarT / G - 2 with step groups)"""
         return q * self.K // self.ns, (q + 1) * self.K // self.ns
@@ -183,7 +196,24 @@ class Sim:
             if u1 > u0:
                 k0, k1 = u0 * K // U, u1 * K // U
                 out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w + W * T - n) % R, k0, k1, W & 1))
-        if lp["nseg"] and self.sg == 1:
+        if lp["nseg"] and self.sg == 1 and self.raw:
+            q, W = n % FT, n // FT + 1
+            if 1 <= q <= FS:  # slice q - 1 of window W whole
+                k0, k1 = self.span(q - 1)
+                out.append(lambda k0=k0, k1=k1, tw=(w + W * FT - n) % R: self.far2r(tw, W, k0, k1))
+        elif lp["nseg"] and self.sg == 1 and self.whole:
+            q, W = n % FT, n // FT + 1
+            if q < FS:  # phase 1 of slice q
+                out.append(lambda: self.far1_slice(W, q))
+            if q >= 1:  # phase 2 of slice q - 1: 2a and 2b in one workgroup (far2c_role)
+                k0, k1 = self.span(q - 1)
+                tw = (w + W * FT - n) % R
+
+                def far2c(k0=k0, k1=k1, tw=tw):
+                    self.far2a(tw, W, k0, k1, 1)
+                    self.far2b(W, k0, k1, 1, self.Kw > 1)
+                out.append(far2c)
+        elif lp["nseg"] and self.sg == 1:
             q, W = n % FT, n // FT + 1
             if q < FS:  # phase 1 and 2a of slice q
                 k0, k1 = self.span(q)
@@ -207,7 +237,12 @@ class Sim:
                 k0, k1 = (j - 1) * U // np_ * K // U, j * U // np_ * K // U
                 if k1 > k0:
                     out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w0 + W * T - n0) % R, k0, k1, W & 1))
-        if lp["nseg"]:
+        if lp["nseg"] and self.raw:
+            q, W = (n0 % FT) // G, n0 // FT + 1
+            if 2 <= q and q - 2 < self.ns:  # slice q - 2 of window W whole, at phase 2's time
+                k0, k1 = self.span(q - 2)
+                out.append(lambda k0=k0, k1=k1, tw=(w0 + W * FT - n0) % R: self.far2r(tw, W, k0, k1))
+        elif lp["nseg"]:
             q, W = (n0 % FT) // G, n0 // FT + 1
             if 1 <= q <= self.ns:  # phase 1 of slice q - 1
                 out.append(lambda: self.far1_slice(W, q - 1))
@@ -225,7 +260,9 @@ class Sim:
         self.join()
         for l in range(len(self.lp["T"])):
             self.toep(l, self.w, 0, self.K, 0)
-        if self.lp["nseg"]:
+        if self.lp["nseg"] and self.raw:
+            self.far2r(self.w, 0, 0, self.K)
+        elif self.lp["nseg"]:
             ns = self.lp["nseg"]
             FS_ = self.ns
             for q in range(FS_ + 1):  # launch q: phase 1 + 2a of slice q, 2b of slice q - 1
@@ -384,6 +421,52 @@ def test_level_schedule_step_groups(P, sg, Kw):
     H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
     sim = Sim(H, lp, Kw=Kw, sg=sg)
     nb = max(3 * P, 2 * P + 300) if lp["nseg"] else 3 * P + 60
+    X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
+    worst = 0.0
+    for t in range(nb):
+        y = sim.plain(X[t]) if (t < 37 or nb // 2 <= t < nb // 2 + 3) else sim.step(X[t])
+        m = min(P, t + 1)
+        ref = (H[:m] * X[t - np.arange(m)]).sum(0)
+        worst = max(worst, float(np.abs(y - ref).max() / (np.abs(ref).max() + 1e-300)))
+    assert worst < 1e-12, worst
+
+
+@pytest.mark.parametrize("P,Kw", [(300, 2), (700, 2), (700, 3), (1100, 4), (450, 1)])
+def test_level_schedule_far_phase2_whole(P, Kw):
+    """G = 1 with far phase 2 in one workgroup per unit (neo_hip_upols_opts.far_phase2 = 1,
+    far2_whole): phase 1 of slice q at step q, the fresh transform, the products and the inverse
+    of slice q - 1 at step q, in one role (the fresh spectrum written to its slot in the same
+    role), across re-priming."""
+    lp = plan(P)
+    rng = np.random.default_rng(P + 100 * Kw)
+    K = 32
+    H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
+    sim = Sim(H, lp, Kw=Kw, whole=True)
+    nb = 2 * P + 700
+    X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
+    worst = 0.0
+    for t in range(nb):
+        y = sim.plain(X[t]) if (t < 37 or nb // 2 <= t < nb // 2 + 3) else sim.step(X[t])
+        m = min(P, t + 1)
+        ref = (H[:m] * X[t - np.arange(m)]).sum(0)
+        worst = max(worst, float(np.abs(y - ref).max() / (np.abs(ref).max() + 1e-300)))
+    assert worst < 1e-12, worst
+
+
+@pytest.mark.parametrize("P,sg", [(257, 1), (300, 1), (700, 1), (450, 4), (700, 4), (1100, 8), (1100, 2), (385, 4)])
+def test_level_schedule_far_recomputed(P, sg):
+    """The recomputed far level (neo_hip_upols_opts.far_level = 2, far2r_role): slice q of window W takes every segment from the ring's rows and the segment
+    spectra at once (G = 1: at step q + 1 of window W - 1; step groups: with phase 2's background
+    launch, group q + 2), nothing stored between windows but the field; the ring of P + 256 rows
+    the handle allocates, background launches at random points inside their windows, across
+    plain steps and re-priming."""
+    lp = plan(P)
+    assert lp["nseg"]
+    rng = np.random.default_rng(P + 1000 * sg)
+    K = 32
+    H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
+    sim = Sim(H, lp, sg=sg, raw=True)
+    nb = 2 * P + 700
     X = rng.standard_normal((nb, K)) + 1j * rng.standard_normal((nb, K))
     worst = 0.0
     for t in range(nb):

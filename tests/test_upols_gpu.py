@@ -264,7 +264,7 @@ def test_full_size_properties(neo_gpu, oracle, C, B, L):
         assert peak_err(ox[c].cpu().numpy(), ref[0]) <= TOL
 
 
-def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans, far_group=None):
+def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans, far_group=None, far_level=-1, far_form=None):
     """Default options (streaming levels on, far level on), device input, one block per
     call as a real-time caller steps it, nb blocks: every level's windows repeat many times,
     every far segment meets real FDL rows and the ring wraps. Channels `chans` against the
@@ -274,10 +274,12 @@ def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans, far_group=No
     ir = (torch.rand((C, L), generator=g, device="cuda") * 2 - 1).contiguous()
     x = (torch.rand((C, B * nb), generator=g, device="cuda") * 2 - 1).contiguous()
     P = neo_gpu.num_partitions(L, B)
-    conv = neo_gpu.UpolsConvolver(C, B, P)
+    conv = neo_gpu.UpolsConvolver(C, B, P, options={"far_level": far_level})
     assert conv.ahead_info()[0]  # streaming levels are the default here
     if far_group is not None:
         assert conv.far_group() == far_group  # the automatic choice at this shape
+    if far_form is not None:
+        assert conv.far_form() == far_form
     conv.set_impulse(ir, normalize=True)
     conv.set_batch(False)  # one block per pass
     xh = {c: x[c].cpu().numpy()[None] for c in chans}
@@ -294,19 +296,24 @@ def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans, far_group=No
         assert peak_err(x[c, -128 * B:].cpu().numpy(), ref[0, -128 * B:]) <= TOL, c
 
 
-def test_full_size_c5_shard_steady_state(neo_gpu, oracle):
+@pytest.mark.parametrize("far_level,form", [(-1, 1), (2, 2)])
+def test_full_size_c5_shard_steady_state(neo_gpu, oracle, far_level, form):
     """The headline path at its own shape (configs[4] per-GPU shard: 256 ch, B = 512,
-    L = 480000, P = 938, 6 far segments, ring 969): 1152 blocks (9 far windows), channels 0,
-    127, 255."""
-    _full_size_streaming(neo_gpu, oracle, 256, 512, 480000, 1152, 77, (0, 127, 255))
+    L = 480000, P = 938, 6 far segments, ring 1194 / 969): 1152 blocks (9 far windows), channels
+    0, 127, 255; the default far level (stored spectra) and the one recomputed every window."""
+    _full_size_streaming(neo_gpu, oracle, 256, 512, 480000, 1152, 77, (0, 127, 255), far_level=far_level,
+                         far_form=form)
 
 
-def test_full_size_c5full_steady_state(neo_gpu, oracle):
+@pytest.mark.parametrize("far_level,form,K", [(-1, 1, 3), (2, 2, 1)])
+def test_full_size_c5full_steady_state(neo_gpu, oracle, far_level, form, K):
     """The headline workload itself (configs[4]'s 2048 channels on one GPU, B = 512,
-    L = 480000, P = 938: 32768 16-column units, so the far level runs window groups of
-    K = 3, far1_mac<FPL, 3> and phase 2's extra segments): 1152 blocks (9 far windows, the
-    ring of 969 rows wraps), channels 0, 1024 and 2047."""
-    _full_size_streaming(neo_gpu, oracle, 2048, 512, 480000, 1152, 79, (0, 1024, 2047), far_group=3)
+    L = 480000, P = 938): the default far level (stored spectra), which at 32768 16-column units
+    runs window groups of K = 3 (far1_mac<FPL, 3> and phase 2's extra segments), and the one
+    recomputed every window: 1152 blocks (9 far windows, the ring wraps), channels 0, 1024 and
+    2047."""
+    _full_size_streaming(neo_gpu, oracle, 2048, 512, 480000, 1152, 79, (0, 1024, 2047), far_group=K,
+                         far_level=far_level, far_form=form)
 
 
 def test_c3_streaming_exact_shape(neo_gpu, oracle):
@@ -720,11 +727,25 @@ def test_far_window_groups_vs_oracle(neo_gpu, oracle, method, K, B, P, C):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 900 + K, conv_opts) <= TOL
 
 
+@pytest.mark.parametrize("f2", [1, 2])
+@pytest.mark.parametrize("method,B,P,C,K", [("upols", 32, 700, 1, 3), ("upola", 64, 1000, 2, 4), ("upols", 32, 1100, 1, 2),
+                                            ("upols", 256, 300, 2, 0), ("upola", 1024, 270, 1, 0), ("upols", 16, 1000, 1, 1)])
+def test_far_phase2_forms_vs_oracle(neo_gpu, oracle, f2, method, B, P, C, K):
+    """One launch per step (step_group 1) with far phase 2 in one workgroup per unit (far_phase2
+    = 1, far2c_role one step after phase 1; the default from 32768 16-column units) or in two
+    steps (2: 2a beside phase 1, 2b one step later): window groups K = 1..4, several windows,
+    ring wraparound, OLS and OLA, against the oracle (fdl_index.hpp:23-36)."""
+    nb = 2 * P + 320
+    opts = {"far_level": 1, "far_group": K, "step_group": 1, "far_phase2": f2}
+    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 1700 + P, opts) <= TOL
+
+
 @pytest.mark.parametrize("G", [2, 4, 8])
 @pytest.mark.parametrize("method,B,P,C,nb,opts", [
     ("upols", 512, 40, 3, 75, {}), ("upola", 128, 40, 2, 100, {}), ("upols", 16, 7, 2, 40, {}),
-    ("upols", 32, 700, 1, 1720, {"far_group": 3}), ("upola", 64, 1000, 2, 2320, {"far_group": 4}),
-    ("upols", 32, 1100, 1, 2520, {"far_group": 2}), ("upols", 256, 300, 2, 420, {"far_level": 0}),
+    ("upols", 32, 700, 1, 1720, {"far_group": 3, "far_level": 1}),
+    ("upola", 64, 1000, 2, 2320, {"far_group": 4, "far_level": 1}),
+    ("upols", 32, 1100, 1, 2520, {"far_group": 2, "far_level": 1}), ("upols", 256, 300, 2, 420, {"far_level": 0}),
     ("upola", 1024, 270, 1, 300, {}), ("upols", 32, 257, 2, 654, {"far_level": 1})])
 def test_step_groups_vs_oracle(neo_gpu, oracle, G, method, B, P, C, nb, opts):
     """Step groups (neo_hip_upols_opts.step_group = G): the block of every call alone on the
@@ -733,6 +754,23 @@ def test_step_groups_vs_oracle(neo_gpu, oracle, G, method, B, P, C, nb, opts):
     128-block Toeplitz level, several windows and ring wraparound; OLS and OLA
     (uniform_partitioned_convolver.hpp:47-65, fdl_index.hpp:23-36)."""
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 1300 + P, dict(opts, step_group=G)) <= TOL
+
+
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+@pytest.mark.parametrize("method,B,P,C", [("upols", 32, 700, 1), ("upola", 64, 1000, 2), ("upols", 16, 1000, 1),
+                                          ("upols", 1024, 270, 1), ("upols", 256, 300, 2), ("upola", 32, 257, 2),
+                                          ("upols", 128, 600, 3)])
+def test_far_recomputed_vs_oracle(neo_gpu, oracle, G, method, B, P, C):
+    """The recomputed far level (neo_hip_upols_opts.far_level = 2, far2r_role): every segment
+    from the filter's and the FDL's rows each window, one launch per step (G = 1) and step
+    groups; one and several segments, a last segment of one partition, the packed bin 0,
+    B = 16..1024, several windows and ring wraparound, OLS and OLA, against the oracle (uniform_partitioned_convolver.hpp:47-65, fdl_index.hpp:23-36)."""
+    nb = 2 * P + 320
+    opts = {"far_level": 2, "step_group": G}
+    probe = neo_gpu.UpolsConvolver(C, B, P, options=opts)
+    assert probe.far_form() == 2 and probe.step_group() == G
+    probe.close()
+    assert _stream(neo_gpu, oracle, method, B, P, C, nb, 1900 + P + G, opts) <= TOL
 
 
 @pytest.mark.parametrize("G", [2, 4, 8])
@@ -836,10 +874,19 @@ def test_far_group_defaults(neo_gpu):
     import bench
 
     for C, B, P in [(4, 512, 938), (256, 512, 938), (256, 256, 1875), (1, 512, 188), (3, 64, 300)]:
-        c = neo_gpu.UpolsConvolver(C, B, P)
+        c = neo_gpu.UpolsConvolver(C, B, P, options={"far_level": 1})  # the stored form
         nseg = neo_gpu.convolution.level_plan(P)["nseg"]
         assert c.far_group() == (bench.far_group(nseg, C * B // 16) if nseg else 0), (C, B, P)
         c.close()
+        # the automatic form: stored spectra; recomputed (one window per pass) on request
+        c = neo_gpu.UpolsConvolver(C, B, P)
+        assert c.far_form() == (1 if nseg else 0), (C, B, P)
+        assert c.far_group() == (bench.far_group(nseg, C * B // 16) if nseg else 0), (C, B, P)
+        c.close()
+        if nseg:
+            c = neo_gpu.UpolsConvolver(C, B, P, options={"far_level": 2})
+            assert c.far_form() == 2 and c.far_group() == 1, (C, B, P)
+            c.close()
     with pytest.raises(RuntimeError):
         neo_gpu.UpolsConvolver(1, 64, 300, options={"far_group": 5})
 

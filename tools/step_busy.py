@@ -1,0 +1,45 @@
+"""GPU busy time per streaming step from a rocprofv3 kernel trace (run_kernel_trace.csv) of a
+bench.py run with step groups: the block launches of the main handle (the k_lvl_block grid with
+the most GPU time) and every k_lvl_slices launch between the first and the last of them; the
+union of their [start, end) intervals divided by the number of block launches. The two kernels
+run side by side on two streams, so per-kernel average durations add up to more than a step;
+this is the figure bench.py's roofline.kernel_avg_ms (the step pair) is compared against.
+
+    python tools/step_busy.py <run_kernel_trace.csv> [algorithmic_bytes_per_step]
+"""
+import collections
+import csv
+import json
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+blk = [r for r in rows if "k_lvl_block" in r["Kernel_Name"]]
+tot = collections.Counter()
+for r in blk:
+    tot[r["Grid_Size_X"]] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+grid = tot.most_common(1)[0][0]  # the main handle's launches: the most GPU time
+blk = [r for r in blk if r["Grid_Size_X"] == grid]
+iv = lambda r: (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+b = sorted(iv(r) for r in blk)
+lo, hi = b[0][0], b[-1][1]
+sl = sorted(iv(r) for r in rows if "k_lvl_slices" in r["Kernel_Name"] and lo <= int(r["Start_Timestamp"]) <= hi)
+busy, cur = 0, None
+for s, e in sorted(b + sl):
+    if cur is None or s > cur[1]:
+        if cur:
+            busy += cur[1] - cur[0]
+        cur = [s, e]
+    else:
+        cur[1] = max(cur[1], e)
+busy += cur[1] - cur[0]
+out = {"trace": sys.argv[1], "block_grid": int(grid), "block_launches": len(b), "slice_launches": len(sl),
+       "busy_ns": busy, "busy_us_per_step": busy / len(b) / 1e3,
+       "block_avg_us": sum(e - s for s, e in b) / len(b) / 1e3,
+       "slices_avg_us": sum(e - s for s, e in sl) / max(len(sl), 1) / 1e3,
+       "note": "union of block and slice launch intervals / block launches (idle gaps between host-synchronized "
+               "runs not counted)"}
+if len(sys.argv) > 2:
+    by = float(sys.argv[2])
+    out["algorithmic_bytes_per_step"] = by
+    out["achieved_gbs"] = by / (out["busy_us_per_step"] * 1e-6) / 1e9
+print(json.dumps(out))
