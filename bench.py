@@ -588,7 +588,7 @@ def run_upols(args, world, rank, local):
         by_blk = roles["block"] + roles["toeplitz_block"]
         by_sl = G * (roles["toeplitz"] + roles["far"])
         by = by_blk + by_sl / G
-        kb, ks = f"k_lvl_block<{B}>", f"k_lvl_slices<{2 if conv_far_group <= 2 else 4}>"
+        kb, ks = f"k_lvl_block<{B}>", f"k_lvl_slices<{1 if conv_far_form == 2 else (2 if conv_far_group <= 2 else 4)}>"
         kernels = []
         for kname, b, ms, per in ((ks, by_sl, det[1], G), (kb, by_blk, det[0], 1)):
             g = b / (ms * 1e-3) / 1e9

@@ -1774,6 +1774,14 @@ static int64_t toep_units(const upols_t* h, int T)
     return int64_t(h->C) * (h->B / 16) * JH;
 }
 
+// Step groups: the Toeplitz levels stepped in the block launches, 1/T of the next window per step
+// (the others in the background launches, T / G - 1 parts per window). T < 2 G must (a background
+// launch may not read the blocks of its own group); larger windows may (diagnostic builds).
+#ifndef NEO_BLOCK_TMAX
+#define NEO_BLOCK_TMAX 0
+#endif
+static bool block_level(const upols_t* h, int T) { return T < 2 * h->sg || T <= NEO_BLOCK_TMAX; }
+
 // The slices the launch of step n (block t0 + n at ring row w) carries. G = 1: slice n mod T of
 // window n / T + 1 of every Toeplitz level (its rows end before the window in progress, so every
 // window's slabs are complete when its first block runs) and, with q = n mod 128 and W = n / 128 + 1,
@@ -1783,7 +1791,7 @@ static void block_levels(const upols_t* h, int64_t n, int w, slice_args& a)
 {
     for (int l = 0; l < h->lv.n; ++l) {
         const int T = h->lv.T[l];
-        if (h->sg > 1 && T >= 2 * h->sg) break;
+        if (h->sg > 1 && !block_level(h, T)) break;
         const int64_t U = toep_units(h, T), st = n % T;
         toep_slice(h, l, n / T + 1, st * U / T, (st + 1) * U / T, n, w, a);
     }
@@ -1835,7 +1843,7 @@ static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
     const int G = h->sg;
     for (int l = 0; l < lp.n; ++l) {
         const int T = lp.T[l];
-        if (T < 2 * G) continue;  // in the block launches
+        if (block_level(h, T)) continue;  // in the block launches
         const int64_t j = (n0 % T) / G, np = T / G - 1, U = toep_units(h, T);
         if (j >= 1) toep_slice(h, l, n0 / T + 1, (j - 1) * U / np, j * U / np, n0, w0, a);
     }

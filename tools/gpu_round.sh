@@ -22,10 +22,10 @@ timeout -k 10 300 python bench.py --workload c5 --host-io --steps 200 > $O/bench
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
   bench.py --gpus 2 --steps 20 --warmup 5 --no-fft --no-host-io > $O/bench_c5full_n2_$TAG.json 2> $O/bench_c5full_n2_$TAG.err && \
 cd /tmp && export TMPDIR=/tmp && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5full_$TAG -o run -- python3 $R/bench.py --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5full_$TAG.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$TAG -o run -- python3 $R/bench.py --workload c5 --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5_$TAG.log 2>&1 && \
+NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5full_$TAG -o run -- python3 $R/bench.py --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5full_$TAG.log 2>&1 && \
+NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$TAG -o run -- python3 $R/bench.py --workload c5 --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2_$TAG -o run -- python3 $R/bench.py --workload c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_c2_$TAG.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- python3 $R/bench.py --workload c4 --steps 128 --no-cpu-baseline --no-parity --no-fft > $O/prof_c4_$TAG.log 2>&1 && \
+NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- python3 $R/bench.py --workload c4 --steps 128 --no-cpu-baseline --no-parity --no-fft > $O/prof_c4_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$TAG -o run -- python3 $R/bench.py --workload c3 --steps 256 --no-cpu-baseline --no-parity --no-fft > $O/prof_c3_$TAG.log 2>&1 && \
 cd $R && bash tools/gpu_pmc.sh $TAG
 echo "round exit=$?"

@@ -6,6 +6,11 @@ run side by side on two streams, so per-kernel average durations add up to more 
 this is the figure bench.py's roofline.kernel_avg_ms (the step pair) is compared against.
 
     python tools/step_busy.py <run_kernel_trace.csv> [algorithmic_bytes_per_step]
+
+With a trace of a NEO_BENCH_MARK=1 run the figure is taken over the streaming timed region alone
+(between the last marker add and the marker mul after it, as tools/trace_region.py), i.e. the
+same steps bench.py's wall clock times; otherwise over every block launch of the main handle
+(which includes the instrumented, latency and host round-trip runs).
 """
 import collections
 import csv
@@ -13,6 +18,15 @@ import json
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+region = None
+small = [i for i, r in enumerate(rows) if int(r["Grid_Size_X"]) <= 512]
+adds = [i for i in small if "OnSelf_add" in rows[i]["Kernel_Name"]]
+if adds:
+    muls = [i for i in small if "MulFunctor" in rows[i]["Kernel_Name"] and i > adds[-1]]
+    if muls:
+        region = (int(rows[adds[-1]]["End_Timestamp"]), int(rows[muls[0]]["Start_Timestamp"]))
+        rows = [r for r in rows if region[0] <= int(r["Start_Timestamp"]) < region[1]]
 blk = [r for r in rows if "k_lvl_block" in r["Kernel_Name"]]
 tot = collections.Counter()
 for r in blk:
@@ -32,7 +46,8 @@ for s, e in sorted(b + sl):
     else:
         cur[1] = max(cur[1], e)
 busy += cur[1] - cur[0]
-out = {"trace": sys.argv[1], "block_grid": int(grid), "block_launches": len(b), "slice_launches": len(sl),
+out = {"trace": sys.argv[1], "timed_region_only": region is not None,
+       "region_us": (region[1] - region[0]) / 1e3 if region else None, "block_grid": int(grid), "block_launches": len(b), "slice_launches": len(sl),
        "busy_ns": busy, "busy_us_per_step": busy / len(b) / 1e3,
        "block_avg_us": sum(e - s for s, e in b) / len(b) / 1e3,
        "slices_avg_us": sum(e - s for s, e in sl) / max(len(sl), 1) / 1e3,
