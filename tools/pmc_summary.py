@@ -79,7 +79,7 @@ def main():
             continue
         b = bench_line(tag, w)
         r = b["roofline"]
-        if r.get("steps_per_launch", 1) > 1:  # step groups: the slice and block kernels
+        if r.get("step_group", r.get("steps_per_launch", 1)) > 1:  # step groups: the slice and block kernels
             for k in r["kernels"]:
                 name = k["kernel"].split("<")[0]
                 summarize(tag, w, name, k["algorithmic_bytes_per_launch"], f"{w}_{name}", every_grid=True)
