@@ -47,6 +47,8 @@ def test_host_validation_without_gpu():
     assert lib.neo_hip_fft_plan_create(4, 0, 0, 0, ctypes.byref(h)) == neo._native.NEO_HIP_EINVAL
     assert lib.neo_hip_upols_create(1, 500, 3, 0, ctypes.byref(h)) == neo._native.NEO_HIP_EINVAL
     assert lib.neo_hip_upols_create(0, 512, 3, 0, ctypes.byref(h)) == neo._native.NEO_HIP_EINVAL
+    assert lib.neo_hip_upols_join_background(None, None) == neo._native.NEO_HIP_EINVAL
+    assert lib.neo_hip_upols_get_far_form(None, None) == neo._native.NEO_HIP_EINVAL
     assert lib.neo_hip_fft_max_order() == 27
     assert lib.neo_hip_version() >= 100
     with pytest.raises(neo._native.NeoHipError):

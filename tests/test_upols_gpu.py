@@ -773,6 +773,38 @@ def test_far_recomputed_vs_oracle(neo_gpu, oracle, G, method, B, P, C):
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 1900 + P + G, opts) <= TOL
 
 
+@pytest.mark.parametrize("G", [1, 4])
+def test_join_background(neo_gpu, oracle, G):
+    """neo_hip_upols_join_background: after it, an event on the caller's stream completes only
+    when every background slice launch issued so far has (step groups); a no-op with G = 1. The
+    outputs are complete in stream order either way, and the handle steps on afterwards."""
+    torch = pytest.importorskip("torch")
+    B, P, C, nb = 64, 420, 2, 300
+    ir = np.stack([oracle.noise(1600 + c, B * P) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    sig = np.stack([oracle.noise(1610 + c, B * nb) for c in range(C)])
+    ref = oracle.dense_convolve(sig, parts)
+    conv = neo_gpu.UpolsConvolver(C, B, P, options={"step_group": G})
+    assert conv.step_group() == G
+    conv.filter(parts)
+    conv.set_batch(False)
+    s = torch.cuda.Stream()
+    t = torch.from_numpy(sig).cuda()
+    torch.cuda.synchronize()
+    half = nb // 2
+    conv.process_blocks_ptr(t.data_ptr(), t.data_ptr(), B * nb, half, s.cuda_stream)
+    conv.join_background(s.cuda_stream)
+    e = torch.cuda.Event()
+    e.record(s)
+    e.synchronize()
+    conv.process_blocks_ptr(t.data_ptr() + 4 * B * half, t.data_ptr() + 4 * B * half, B * nb, nb - half,
+                            s.cuda_stream)
+    conv.join_background(s.cuda_stream)
+    s.synchronize()
+    assert peak_err(t.cpu().numpy(), ref) <= TOL
+    conv.close()
+
+
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_step_groups_equal_one_launch(neo_gpu, oracle, G):
     """The same sums in the same order as the one-launch step. Not bit-identical: the step
