@@ -158,12 +158,32 @@ def code_tag() -> str:
     return h.hexdigest()[:12]
 
 
-def load_pmc_traffic(workload: str, kernel: str = ""):
+def pmc_workload(workload: str, C: int):
+    """The workload whose PMC summary measured this rank's shape (C channels of `workload`'s
+    B and L), or None: at N GPUs a strong-scaled c5full rank runs 2048 / N channels, so N = 8
+    reads c5's (256-channel) summary, and N = 2 / 4 (no summary of that shape) report no
+    traffic rather than the 2048-channel figure."""
+    if workload not in WORKLOADS:
+        return workload
+    _, B, L = WORKLOADS[workload]
+    for w in (workload, *WORKLOADS):
+        if WORKLOADS[w] == (C, B, L):
+            return w
+    return None
+
+
+def _pmc_sfx(workload, suffix: str):
+    return None if workload is None else workload + suffix
+
+
+def load_pmc_traffic(workload, kernel: str = ""):
     """HBM bytes per launch (per step for the streaming parts) of `kernel` from a committed
     rocprofv3 --pmc summary (tools/pmc_summary.py) for `workload` measured on THIS code
-    (same code_tag), or None."""
+    (same code_tag), or None (also for workload None: no summary of the rank's shape)."""
     import glob
 
+    if workload is None:
+        return None
     tag = code_tag()
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
         try:
@@ -509,7 +529,7 @@ def run_upols(args, world, rank, local):
     plain = {"value": samples / el_plain / 1e6, "ms_per_step": el_plain * 1e3 / args.steps,
              "kernel": f"k_upols_step<{B}>", "kernel_avg_ms": det_plain[0], "algorithmic_bytes_per_launch": bytes_plain,
              "achieved_gbs": gbs_plain, "frac": gbs_plain / PEAK_HBM_GBS,
-             "traffic": load_pmc_traffic(args.workload + "_plain", "k_upols_step")}
+             "traffic": load_pmc_traffic(_pmc_sfx(pmc_workload(args.workload, C), "_plain"), "k_upols_step")}
     if levels:
         conv.set_ahead(True)
     warm()
@@ -568,7 +588,7 @@ def run_upols(args, world, rank, local):
                     % ("/".join(map(str, plan["T"])), plan["nseg"]),
                     "ms_per_step": step_ms, "share_of_step": 1.0, "algorithmic_bytes_per_step": by,
                     "bytes_by_role": roles, "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS,
-                    "traffic": load_pmc_traffic(args.workload, "k_lvl_step")}]
+                    "traffic": load_pmc_traffic(pmc_workload(args.workload, C), "k_lvl_step")}]
         dom = kernels[0]
         roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": dom["frac"], "traffic": dom["traffic"],
@@ -594,7 +614,7 @@ def run_upols(args, world, rank, local):
             g = b / (ms * 1e-3) / 1e9
             kernels.append({"kernel": kname, "ms_per_launch": ms, "launches_per_step": 1.0 / per,
                             "algorithmic_bytes_per_launch": b, "achieved_gbs_alone": g,
-                            "traffic": load_pmc_traffic(f"{args.workload}_{kname.split('<')[0]}", kname.split("<")[0]),
+                            "traffic": load_pmc_traffic(_pmc_sfx(pmc_workload(args.workload, C), "_" + kname.split('<')[0]), kname.split("<")[0]),
                             "note": "launch time measured while the other kernel runs beside it (shared HBM), so "
                                     "bytes / launch time understates the kernel; the step pair is the roofline unit"})
         kernels[0]["bytes_by_role"] = {"toeplitz": G * roles["toeplitz"], "far": G * roles["far"]}
@@ -720,7 +740,7 @@ def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world, C_total):
     mac_avg_ms = max_over_ranks(mac_ms / max(launches, 1), world)
     bytes_pass = C * 16 * P * B  # filter + FDL streamed once per pass of T blocks
     gbs = bytes_pass / (mac_avg_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.workload + "_offline", "k_batch_mac")
+    traffic = load_pmc_traffic(_pmc_sfx(pmc_workload(args.workload, C), "_offline"), "k_batch_mac")
     return {"value": C_total * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": T,
             "traffic": traffic, "traffic_over_algorithmic": traffic / bytes_pass if traffic else None,
             "ms_per_block": elapsed * 1e3 / nb, "splits": splits, "kernel": f"k_batch_mac<{B},{T},1>",

@@ -70,3 +70,17 @@ def test_workloads_match_baseline_configs():
     assert bench.WORKLOADS["c4"] == (256, 256, 480000)
     assert bench.WORKLOADS["c3"] == (1, 512, 96000)
     assert bench.STRONG == {"c5full"}
+
+
+def test_pmc_summary_follows_rank_shape():
+    """The PMC traffic a rank reports is the summary of its own shape: a strong-scaled c5full
+    rank at N = 8 runs c5's 256 channels, at N = 2 / 4 no summary of its shape exists."""
+    for world, want in ((1, "c5full"), (2, None), (4, None), (8, "c5")):
+        C, total = bench.rank_channels("c5full", world, 0)
+        assert total == 2048 and C == 2048 // world
+        assert bench.pmc_workload("c5full", C) == want
+    assert bench.pmc_workload("c4", 256) == "c4"
+    assert bench.pmc_workload("c5", 256) == "c5"
+    assert bench.pmc_workload("c2", 0) == "c2"
+    assert bench.load_pmc_traffic(None) is None
+    assert bench._pmc_sfx(None, "_plain") is None and bench._pmc_sfx("c5", "_plain") == "c5_plain"
