@@ -135,6 +135,18 @@ def barrier(world):
         dist.barrier()
 
 
+def gather_over_ranks(x: float, world: int) -> list:
+    """x of every rank, in rank order (gloo all_gather; [x] at world 1)."""
+    if world == 1:
+        return [x]
+    import torch
+    import torch.distributed as dist
+
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(out, torch.tensor([x], dtype=torch.float64))
+    return [float(t.item()) for t in out]
+
+
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
@@ -505,7 +517,18 @@ def run_upols(args, world, rank, local):
         torch.cuda.synchronize()
         gpu_ms[tag] = max_over_ranks(e0.elapsed_time(e1) / args.steps, world)
         gpu_ms[tag + "_host_launch_ms"] = (t3 - t2) * 1e3
+        gpu_ms[tag + "_per_rank_ms"] = [v * 1e3 / args.steps for v in gather_over_ranks(t1 - t0, world)]
         return max_over_ranks(t1 - t0, world)
+
+    def wall_region(n):
+        """n steps timed like the headline (barrier + sync on both sides, max over ranks): seconds"""
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        feed.run(n)
+        torch.cuda.synchronize()
+        barrier(world)
+        return max_over_ranks(time.perf_counter() - t0, world)
 
     def instrumented():
         """max(steps, 64) more steps with HIP events the C-ABI records on the launch stream
@@ -566,6 +589,10 @@ def run_upols(args, world, rank, local):
     torch.cuda.synchronize()
     conv.set_timing(False)
     st = np.array(conv.step_times())
+    # steady state: one whole far window (128 steps = 32 step groups: every group's background
+    # launch once, whatever their sizes), timed like the headline
+    n_steady = 128
+    el_steady = wall_region(n_steady)
     latency = {"steps": int(st.size), "mean_ms": float(st.mean()), "p50_ms": float(np.percentile(st, 50)),
                "p99_ms": float(np.percentile(st, 99)), "max_ms": float(st.max()),
                "max_over_mean": float(st.max() / st.mean()),
@@ -644,6 +671,37 @@ def run_upols(args, world, rank, local):
                 "frac": gbs_plain / PEAK_HBM_GBS, "traffic": plain["traffic"], "kernel": plain["kernel"],
                 "kernel_avg_ms": det_plain[0], "steps_per_launch": 1, "algorithmic_bytes_per_launch": bytes_plain,
                 "d2d_copy_gbs": copy_ceiling_gbs(dev)}
+    step_bytes = roof["algorithmic_bytes_per_launch"]
+    steady = {"steps": n_steady, "value": C_total * B * n_steady / el_steady / 1e6, "unit": "Msamples/s",
+              "ms_per_step": el_steady * 1e3 / n_steady,
+              "achieved": step_bytes / (el_steady / n_steady) / 1e9, "unit_achieved": "GB/s",
+              "frac": step_bytes / (el_steady / n_steady) / 1e9 / PEAK_HBM_GBS,
+              "value_over_headline": (args.steps / elapsed) / (n_steady / el_steady),
+              "note": "one whole far window (128 steps, every step group's background launch once), wall clock "
+                      "with barrier + sync on both sides like the headline; frac on the headline's bytes per step"}
+    ir_change = None
+    if levels:
+        # IR change (DenseConvolution.cpp:78-108: normalize_impulse + uniform_partition + filter per
+        # channel): set_impulse on a device-resident IR, then the first block after it, which
+        # primes the levels (far segment spectra and window 0 of every level)
+        g2 = torch.Generator(device=dev).manual_seed(1008 + rank)
+        ir2 = torch.rand((C, L), generator=g2, device=dev).mul_(2).sub_(1)
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        conv.set_impulse(ir2, normalize=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        feed.run(1)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        del ir2
+        ir_change = {"set_impulse_ms": max_over_ranks((t1 - t0) * 1e3, world),
+                     "first_block_ms": max_over_ranks((t2 - t1) * 1e3, world),
+                     "total_ms": max_over_ranks((t2 - t0) * 1e3, world),
+                     "note": "device-resident IR [C][L]: normalize (sequential-float energy, min over channels), "
+                             "partition r2c, then the first streaming block (far segment spectra + level priming); "
+                             "max over ranks"}
     offline = run_upols_offline(args, conv, C, B, P, x, y, nx * B, stream, world, C_total)
     host_io = None
     if not args.no_host_io:
@@ -678,6 +736,7 @@ def run_upols(args, world, rank, local):
         "ms_per_step": elapsed * 1e3 / args.steps,
         "gpu_ms_per_step": gpu_ms.get("levels" if levels else "plain"),  # HIP events around the same steps
         "host_launch_ms": gpu_ms.get(("levels" if levels else "plain") + "_host_launch_ms"),  # t0 -> all steps enqueued
+        "per_rank_ms": gpu_ms.get(("levels" if levels else "plain") + "_per_rank_ms"),  # each rank's wall ms per step
         "higher_is_better": True,
         "scaling": "strong" if args.workload in STRONG else "weak",
         "vs_baseline": None,
@@ -695,6 +754,8 @@ def run_upols(args, world, rank, local):
                                  if levels else "plain step"),
                    "parallelism": f"channel-shard x{world} (no collective)"},
         "roofline": roof,
+        "steady": steady,
+        "ir_change": ir_change,
         "latency": latency,
         "parity": parity,
         "per_block_step": plain,
@@ -887,7 +948,7 @@ def main():
             res["c2_fft"] = {"value": f["value"], "unit": f["unit"], "ms_per_step": f["ms_per_step"],
                              "metric": f["metric"], "roofline": f["roofline"]}
     if rank == 0:
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:  # rank 0, after every timed region (N > 1 too: the other ranks wait)
             C, B, L = WORKLOADS.get(args.workload, (0, 0, 0))
             res["cpu_baseline"] = (cpu_baseline_fft(args.cpu_threads) if args.workload == "c2"
                                    else cpu_baseline_upols(C, B, L, args.cpu_threads))

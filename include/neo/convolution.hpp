@@ -355,32 +355,93 @@ namespace detail {
 struct group_deleter {
     void operator()(neo_hip_upols_group* g) const noexcept { neo_hip_upols_group_destroy(g); }
 };
-
-/// the process-wide group of single-channel convolvers of one shape (neo_hip_upols_group_*)
-inline auto acquire_group(std::size_t block, std::size_t partitions, method m, int device)
-    -> std::shared_ptr<neo_hip_upols_group>
-{
-    static std::mutex mu;
-    static std::map<std::array<std::size_t, 4>, std::weak_ptr<neo_hip_upols_group>> groups;
-    std::lock_guard<std::mutex> lk{mu};
-    auto const key = std::array<std::size_t, 4>{block, partitions, std::size_t(m == method::upola), std::size_t(device)};
-    if (auto g = groups[key].lock()) return g;
-    neo_hip_upols_group* raw = nullptr;
-    neo::hip::check(neo_hip_upols_group_create(int(block), int(partitions), m == method::upola ? 1 : 0, device, &raw));
-    auto g = std::shared_ptr<neo_hip_upols_group>(raw, group_deleter{});
-    groups[key] = g;
-    return g;
-}
 }  // namespace detail
 
+/// The convolvers of ONE owner (one plugin instance: DenseConvolution's
+/// std::vector<upols_convolver>, DenseConvolution.hpp:35), grouped per shape
+/// (neo_hip_upols_group_*): grouped_upols_convolver instances whose filter() runs inside a
+/// scope() of this object join its group of their shape; instances outside any scope run alone.
+/// register_buffer() names host memory the owner keeps allocated (its frame buffer) until
+/// unregister_all(): only convolvers called on such buffers are stepped together.
+class convolver_group {
+public:
+    convolver_group() = default;
+    convolver_group(convolver_group const&) = delete;
+    auto operator=(convolver_group const&) -> convolver_group& = delete;
+
+    /// RAII: convolvers whose filter() runs on this thread while the scope lives join `g`
+    class scope_guard {
+    public:
+        explicit scope_guard(convolver_group& g) noexcept : _prev{current()} { current() = &g; }
+        ~scope_guard() { current() = _prev; }
+        scope_guard(scope_guard const&) = delete;
+        auto operator=(scope_guard const&) -> scope_guard& = delete;
+
+    private:
+        convolver_group* _prev;
+    };
+    [[nodiscard]] auto scope() -> scope_guard { return scope_guard{*this}; }
+
+    /// [ptr, ptr + samples) stays allocated until unregister_all() (cheap to repeat per frame)
+    auto register_buffer(float const* ptr, std::size_t samples) -> void
+    {
+        std::lock_guard<std::mutex> lk{_mu};
+        auto const r = std::pair<float const*, std::size_t>{ptr, samples};
+        if (std::find(_ranges.begin(), _ranges.end(), r) == _ranges.end()) _ranges.push_back(r);
+        for (auto& [key, g] : _groups)
+            neo::hip::check(neo_hip_upols_group_register(g.get(), ptr, std::int64_t(samples * sizeof(float))));
+    }
+    /// before the registered memory is freed or reallocated (e.g. at prepare())
+    auto unregister_all() -> void
+    {
+        std::lock_guard<std::mutex> lk{_mu};
+        _ranges.clear();
+        for (auto& [key, g] : _groups) neo::hip::check(neo_hip_upols_group_unregister(g.get(), nullptr));
+    }
+
+    /// the group of one shape (created on first use, with the ranges registered so far)
+    auto acquire(std::size_t block, std::size_t partitions, method m, int device) -> std::shared_ptr<neo_hip_upols_group>
+    {
+        std::lock_guard<std::mutex> lk{_mu};
+        auto const key = std::array<std::size_t, 4>{block, partitions, std::size_t(m == method::upola), std::size_t(device)};
+        if (auto it = _groups.find(key); it != _groups.end()) return it->second;
+        auto g = make_group(block, partitions, m, device);
+        for (auto const& [p, n] : _ranges)
+            neo::hip::check(neo_hip_upols_group_register(g.get(), p, std::int64_t(n * sizeof(float))));
+        _groups.emplace(key, g);
+        return g;
+    }
+
+    static auto make_group(std::size_t block, std::size_t partitions, method m, int device)
+        -> std::shared_ptr<neo_hip_upols_group>
+    {
+        neo_hip_upols_group* raw = nullptr;
+        neo::hip::check(
+            neo_hip_upols_group_create(int(block), int(partitions), m == method::upola ? 1 : 0, device, &raw));
+        return std::shared_ptr<neo_hip_upols_group>(raw, detail::group_deleter{});
+    }
+
+    /// the group scope active on this thread, or null
+    static auto current() noexcept -> convolver_group*&
+    {
+        thread_local convolver_group* cur = nullptr;
+        return cur;
+    }
+
+private:
+    std::mutex _mu;
+    std::map<std::array<std::size_t, 4>, std::shared_ptr<neo_hip_upols_group>> _groups;
+    std::vector<std::pair<float const*, std::size_t>> _ranges;
+};
+
 /// Single-channel drop-in for upols_convolver<complex<float>> (uniform_partitioned_convolver.hpp:13-65)
-/// whose instances of one shape form a group (neo_hip_upols_group_*, include/neo_hip.h): in the
-/// plugin's frame pattern (DenseConvolution.cpp:62-74: every instance called once per frame on a
-/// buffer of its own) a frame of all instances is ONE launch instead of one launch and one wait
-/// per instance; each instance's outputs are its own sequential convolver's in any pattern. A
-/// coalesced frame's first call reads the other instances' buffers of the previous frame: they
-/// must stay valid while the instances live. upols_convolver is this type when
-/// NEO_HIP_CONVOLVER_GROUPS is defined.
+/// that joins the convolver_group whose scope() is active when its filter() runs (else it runs
+/// alone): in the plugin's frame pattern (DenseConvolution.cpp:62-74: every instance called once
+/// per frame on a buffer of its own, inside the owner's registered frame buffer) a frame of all
+/// instances is ONE launch instead of one launch and one wait per instance; each instance's
+/// outputs are its own sequential convolver's in any pattern. upols_convolver / upola_convolver
+/// are this type when NEO_HIP_CONVOLVER_GROUPS is defined (the split_* forms are not: the
+/// plugin's Convolution.hpp:61 runs them on the host's own output buffer).
 template<typename Complex, method M = method::upols>
 struct grouped_upols_convolver {
     static_assert(std::same_as<Complex, std::complex<float>>);
@@ -389,13 +450,15 @@ struct grouped_upols_convolver {
 
     grouped_upols_convolver() = default;
     grouped_upols_convolver(grouped_upols_convolver&& o) noexcept
-        : _g{std::move(o._g)}, _id{std::exchange(o._id, -1)}, _B{o._B}, _P{o._P}, _block{std::move(o._block)}
+        : _g{std::move(o._g)}, _owner{o._owner}, _id{std::exchange(o._id, -1)}, _B{o._B}, _P{o._P},
+          _block{std::move(o._block)}
     {}
     auto operator=(grouped_upols_convolver&& o) noexcept -> grouped_upols_convolver&
     {
         if (this != &o) {
             leave();
             _g = std::move(o._g);
+            _owner = o._owner;
             _id = std::exchange(o._id, -1);
             _B = o._B;
             _P = o._P;
@@ -413,9 +476,12 @@ struct grouped_upols_convolver {
         std::vector<Complex> h(P * bins);
         for (std::size_t p = 0; p < P; ++p)
             for (std::size_t k = 0; k < bins; ++k) h[p * bins + k] = Complex(neo::hip::detail::at(filter, p, k));
-        if (!_g || _P != P || _B != bins - 1) {
+        auto* owner = convolver_group::current();
+        if (!_g || _P != P || _B != bins - 1 || owner != _owner) {
             leave();
-            _g = detail::acquire_group(bins - 1, P, M, neo::hip::detail::default_device());
+            auto const dev = neo::hip::detail::default_device();
+            _g = owner ? owner->acquire(bins - 1, P, M, dev) : convolver_group::make_group(bins - 1, P, M, dev);
+            _owner = owner;
             neo::hip::check(neo_hip_upols_group_join(_g.get(), &_id));
             _B = bins - 1;
             _P = P;
@@ -445,10 +511,12 @@ private:
     {
         if (_g && _id >= 0) (void)neo_hip_upols_group_leave(_g.get(), _id);
         _g.reset();
+        _owner = nullptr;
         _id = -1;
     }
 
     std::shared_ptr<neo_hip_upols_group> _g;
+    convolver_group* _owner = nullptr;
     int _id = -1;
     std::size_t _B = 0, _P = 0;
     std::vector<float> _block;
@@ -524,14 +592,14 @@ template<typename Complex>
 using upols_convolver = grouped_upols_convolver<Complex>;
 
 template<typename Complex>
-using split_upols_convolver = grouped_upols_convolver<Complex>;
+using split_upols_convolver = hip_upols_convolver<Complex>;
 
 /// dense_convolver.hpp:23-24, 32-35 (overlap-add stage, same FDL MAC)
 template<typename Complex>
 using upola_convolver = grouped_upols_convolver<Complex, method::upola>;
 
 template<typename Complex>
-using split_upola_convolver = grouped_upols_convolver<Complex, method::upola>;
+using split_upola_convolver = hip_upols_convolver<Complex, method::upola>;
 #else
 template<typename Complex>
 using upols_convolver = hip_upols_convolver<Complex>;

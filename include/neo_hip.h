@@ -236,14 +236,16 @@ NEO_HIP_API int neo_hip_upols_multi_reset(neo_hip_upols_multi* m);
  * Members are C independent one-channel upols / upola convolvers of one shape, each with its
  * own filter and state, as the plugin's std::vector<upols_convolver> (DenseConvolution.hpp:35)
  * holds them; process(member, io) is that member's operator()(block): one block of B samples,
- * host memory, in place, complete on return. While the callers follow the plugin's frame
- * pattern (every member called once per frame on a buffer of its own that it reuses), the
- * group steps every member in ONE launch at a frame's first call, from the blocks in the other
- * members' buffers, and later calls only verify their block (a different block re-runs that
+ * host memory, in place, complete on return. A group belongs to ONE owner (one plugin
+ * instance's convolvers; C++: neo::convolution::convolver_group). While the callers follow the
+ * plugin's frame pattern (every member called once per frame on a buffer of its own that it
+ * reuses) AND every member's buffer lies in a range the owner registered, the group steps every
+ * member in ONE launch at a frame's first call, from the blocks in the other members'
+ * registered buffers, and later calls only verify their block (a different block re-runs that
  * member's block step alone); any other pattern runs each member on a handle of its own. Either
- * way each member's outputs are those of its own sequential convolver. NOTE: a coalesced frame's
- * first call READS the buffers the other members passed in the previous frame: they must stay
- * valid while the group lives (the plugin's channel buffers do). method 0 upols, 1 upola. */
+ * way each member's outputs are those of its own sequential convolver (up to float summation
+ * order after a mode switch, which re-primes the streaming levels). The group never reads a
+ * buffer outside the registered ranges. method 0 upols, 1 upola. */
 typedef struct neo_hip_upols_group neo_hip_upols_group;
 NEO_HIP_API int neo_hip_upols_group_create(int block, int partitions, int method, int device, neo_hip_upols_group** g);
 NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g);
@@ -253,6 +255,14 @@ NEO_HIP_API int neo_hip_upols_group_leave(neo_hip_upols_group* g, int member);
 NEO_HIP_API int neo_hip_upols_group_set_filter(neo_hip_upols_group* g, int member, const void* filter, int is_device);
 NEO_HIP_API int neo_hip_upols_group_process(neo_hip_upols_group* g, int member, float* io);
 NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int member);
+/* register [ptr, ptr + bytes) of host memory the owner keeps allocated until it unregisters it
+ * (e.g. the plugin's frame buffer, ConstantOverlapAdd.hpp:34, between two prepare() calls):
+ * only members whose buffers lie in a registered range are stepped ahead of their call.
+ * Registering a range again is a no-op (cheap enough per frame). unregister(ptr) removes the
+ * range starting at ptr, unregister(NULL) every range; the group then stops reading them
+ * before the call returns (a coalesced group splits at its next frame). */
+NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void* ptr, int64_t bytes);
+NEO_HIP_API int neo_hip_upols_group_unregister(neo_hip_upols_group* g, const void* ptr);
 /* coalesced now; one-launch frame steps, member calls, block re-runs, mode switches so far */
 NEO_HIP_API int neo_hip_upols_group_stats(neo_hip_upols_group* g, int* coalesced, int64_t* frame_steps, int64_t* calls,
                                           int64_t* redos, int64_t* switches);

@@ -14,7 +14,11 @@
 //   coalesced mode    the first call of a frame (the leader) steps ALL members in one launch: its
 //                     own block, and for every other member the contents of the buffer it passed
 //                     in the previous frame (speculation: the plugin's AudioBlock channels are
-//                     filled before the loop over the convolvers). A later member's call compares
+//                     filled before the loop over the convolvers). The leader reads ONLY buffers
+//                     the group's owner registered (neo_hip_upols_group_register: the owner
+//                     promises they stay allocated until it unregisters them), never a caller
+//                     pointer it was merely handed once: a member whose buffer is not (or no
+//                     longer) registered keeps the group in independent mode. A later member's call compares
 //                     its block with the block speculated for it: equal -> its output is already
 //                     computed; different -> its channel's block step runs again with the real
 //                     block (previous block restored: the step's other roles never read the
@@ -22,10 +26,14 @@
 //                     for bit). A member called twice before the others (or joining, leaving,
 //                     changing its filter) ends coalescing: the states move back into one-channel
 //                     handles (a speculatively stepped member one block back) before the call.
-// So every output equals the instance's own sequential step; the launch count per frame drops
-// from one per channel to one while the caller keeps the plugin's call pattern. Handles of a
-// group force the shared handle's code-path choices (far window group, Toeplitz window parts),
-// so both modes compute the same sums in the same order.
+// So every output is the instance's own sequential step; the launch count per frame drops from
+// one per channel to one while the caller keeps the plugin's call pattern. Every handle of a
+// group (the members' own and the shared one) uses the code-path choices of the shared handle
+// over the live members (far window group, Toeplitz window parts, step group; re-applied when
+// the live count changes), so both modes run the same arithmetic. A mode switch re-primes the
+// streaming levels at that block, so the far level's 128-block windows may start elsewhere than
+// in an uninterrupted run: outputs then differ from it in float summation order only (tests:
+// bit for bit before the far level contributes, against the oracle over long runs).
 #include "upols_handle.hpp"
 
 #include <algorithm>
@@ -43,6 +51,7 @@ struct member {
     bool filtered = false;
     int64_t steps = 0;             // blocks processed since the filter was set
     const float* io_last = nullptr;
+    neo_hip_upols_opts opts{};     // the options its own handle was made with
     const float* io_prev = nullptr;  // the buffer of the frame before (coalescing needs stable buffers)
     bool pending = false;          // coalesced: stepped by the frame's leader, call not yet seen
     bool seen = false;             // independent: called in the frame being observed
@@ -57,6 +66,7 @@ struct neo_hip_upols_group {
     bool coalesced = false;
     neo_hip_upols* shared = nullptr;
     std::vector<int> slot_member;     // shared handle channel -> member
+    std::vector<std::pair<uintptr_t, uintptr_t>> reg;  // owner-registered host ranges [lo, hi) the leader may read
     float* in_pin = nullptr;          // mapped pinned [C][B]: the frame's input blocks
     float* out_pin = nullptr;         // mapped pinned [C][B]: the frame's output blocks
     float* in_dev = nullptr;          // their device addresses
@@ -119,8 +129,48 @@ void free_shared(group_t* g)
 int make_own(group_t* g, member& x, int C)
 {
     if (x.own) return NEO_HIP_OK;
+    x.opts = group_opts(g, C);
+    return neo_hip_upols_create_ex(1, g->B, g->P, g->device, g->method, &x.opts, &x.own);
+}
+
+bool same_opts(const neo_hip_upols_opts& a, const neo_hip_upols_opts& b)
+{
+    return a.far_group == b.far_group && a.toep_split == b.toep_split && a.step_group == b.step_group;
+}
+
+// independent mode, after the live count changed: every member's own handle re-made with the
+// options of the new count (state copied: filter rows, FDL ring, previous block, ring row)
+int reoption(group_t* g)
+{
+    const int C = live_count(g);
     const neo_hip_upols_opts o = group_opts(g, C);
-    return neo_hip_upols_create_ex(1, g->B, g->P, g->device, g->method, &o, &x.own);
+    for (auto& x : g->m) {
+        if (!x.live || !x.own || same_opts(x.opts, o)) continue;
+        neo_hip_upols* old = x.own;
+        x.own = nullptr;
+        int rc = make_own(g, x, C);
+        if (!rc) rc = copy_channel(x.own, 0, old, 0, old->prev, g->stream);
+        if (!rc && hipStreamSynchronize(g->stream) != hipSuccess) rc = fail(NEO_HIP_ERUNTIME, "group stream sync failed");
+        if (rc) {
+            if (x.own) neo_hip_upols_destroy(x.own);
+            x.own = old;
+            return rc;
+        }
+        x.own->wpos = old->wpos;
+        x.own->batch = false;
+        neo_hip::lvl_filter_changed(x.own);
+        neo_hip_upols_destroy(old);
+    }
+    return NEO_HIP_OK;
+}
+
+// the B samples at p lie in a range the owner registered
+bool registered(const group_t* g, const float* p)
+{
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + size_t(g->B) * sizeof(float);
+    for (const auto& r : g->reg)
+        if (lo >= r.first && hi <= r.second) return true;
+    return false;
 }
 
 // independent -> coalesced: every live member's state into one shared handle
@@ -218,7 +268,7 @@ int call_independent(group_t* g, int i, float* io)
     std::vector<const float*> ptrs;
     for (auto& y : g->m) {
         if (!y.live) continue;
-        ok = ok && y.filtered && y.steps == x.steps && y.io_last && y.io_last == y.io_prev;
+        ok = ok && y.filtered && y.steps == x.steps && y.io_last && y.io_last == y.io_prev && registered(g, y.io_last);
         ptrs.push_back(y.io_last);
         y.seen = false;
     }
@@ -263,7 +313,14 @@ int call_coalesced(group_t* g, int i, float* io)
         if (rc) return rc;
         return call_independent(g, i, io);
     }
-    // the frame's leader: every member's block (its own, the others' buffers of the last frame)
+    // the frame's leader: every member's block (its own, the others' buffers of the last frame,
+    // read only while the owner keeps them registered)
+    for (const auto& y : g->m)
+        if (y.live && &y != &x && !registered(g, y.io_last)) {
+            int rc = split(g);
+            if (rc) return rc;
+            return call_independent(g, i, io);
+        }
     for (const auto& y : g->m)
         if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
     NEO_HIP_CHECK(hipMemcpyAsync(g->prev_bak, sh->prev, size_t(sh->C) * bb, hipMemcpyDeviceToDevice, g->stream));
@@ -323,6 +380,10 @@ NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
     return NEO_HIP_OK;
 }
 
+// every entry point takes the group's lock before it looks at a member (a join on another
+// thread may grow the member vector)
+static bool live_member(const group_t* g, int id) { return id >= 0 && id < int(g->m.size()) && g->m[size_t(id)].live; }
+
 NEO_HIP_API int neo_hip_upols_group_join(neo_hip_upols_group* g, int* id)
 {
     if (!g || !id) return fail(NEO_HIP_EINVAL, "null group or id");
@@ -336,20 +397,27 @@ NEO_HIP_API int neo_hip_upols_group_join(neo_hip_upols_group* g, int* id)
     if (i == g->m.size()) g->m.emplace_back();
     g->m[i] = member{};
     g->m[i].live = true;
-    const int rc = make_own(g, g->m[i], live_count(g));
+    int rc = make_own(g, g->m[i], live_count(g));
+    if (!rc) rc = reoption(g);
     if (rc) {
-        g->m[i].live = false;
+        if (g->m[i].own) neo_hip_upols_destroy(g->m[i].own);
+        g->m[i] = member{};
         return rc;
     }
+    for (auto& y : g->m) y.seen = false;
+    g->nseen = 0;
+    g->good_frames = 0;
     *id = int(i);
     return NEO_HIP_OK;
 }
 
 NEO_HIP_API int neo_hip_upols_group_leave(neo_hip_upols_group* g, int id)
 {
-    if (!g || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live) return fail(NEO_HIP_EINVAL, "no such member");
+    if (!g) return fail(NEO_HIP_EINVAL, "null group");
     std::lock_guard<std::mutex> lk(g->mu);
+    if (!live_member(g, id)) return fail(NEO_HIP_EINVAL, "no such member");
     neo_hip::device_guard dg(g->device);
+    if (dg.rc) return dg.rc;
     if (g->coalesced)
         if (int rc = split(g)) return rc;
     member& x = g->m[size_t(id)];
@@ -358,14 +426,14 @@ NEO_HIP_API int neo_hip_upols_group_leave(neo_hip_upols_group* g, int id)
     for (auto& y : g->m) y.seen = false;
     g->nseen = 0;
     g->good_frames = 0;
-    return NEO_HIP_OK;
+    return reoption(g);
 }
 
 NEO_HIP_API int neo_hip_upols_group_set_filter(neo_hip_upols_group* g, int id, const void* filter, int is_device)
 {
-    if (!g || !filter || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live)
-        return fail(NEO_HIP_EINVAL, "no such member or null filter");
+    if (!g || !filter) return fail(NEO_HIP_EINVAL, "null group or filter");
     std::lock_guard<std::mutex> lk(g->mu);
+    if (!live_member(g, id)) return fail(NEO_HIP_EINVAL, "no such member");
     neo_hip::device_guard dg(g->device);
     if (dg.rc) return dg.rc;
     if (g->coalesced)
@@ -384,9 +452,9 @@ NEO_HIP_API int neo_hip_upols_group_set_filter(neo_hip_upols_group* g, int id, c
 
 NEO_HIP_API int neo_hip_upols_group_process(neo_hip_upols_group* g, int id, float* io)
 {
-    if (!g || !io || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live)
-        return fail(NEO_HIP_EINVAL, "no such member or null block");
+    if (!g || !io) return fail(NEO_HIP_EINVAL, "null group or block");
     std::lock_guard<std::mutex> lk(g->mu);
+    if (!live_member(g, id)) return fail(NEO_HIP_EINVAL, "no such member");
     neo_hip::device_guard dg(g->device);
     if (dg.rc) return dg.rc;
     ++g->stat_calls;
@@ -395,14 +463,40 @@ NEO_HIP_API int neo_hip_upols_group_process(neo_hip_upols_group* g, int id, floa
 
 NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int id)
 {
-    if (!g || id < 0 || id >= int(g->m.size()) || !g->m[size_t(id)].live) return fail(NEO_HIP_EINVAL, "no such member");
+    if (!g) return fail(NEO_HIP_EINVAL, "null group");
     std::lock_guard<std::mutex> lk(g->mu);
+    if (!live_member(g, id)) return fail(NEO_HIP_EINVAL, "no such member");
     neo_hip::device_guard dg(g->device);
+    if (dg.rc) return dg.rc;
     if (g->coalesced)
         if (int rc = split(g)) return rc;
     member& x = g->m[size_t(id)];
     if (int rc = neo_hip_upols_reset(x.own)) return rc;
     x.steps = 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void* ptr, int64_t bytes)
+{
+    if (!g || !ptr || bytes <= 0) return fail(NEO_HIP_EINVAL, "null group or empty range");
+    std::lock_guard<std::mutex> lk(g->mu);
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + uint64_t(bytes);
+    for (const auto& r : g->reg)
+        if (r.first == lo && r.second == hi) return NEO_HIP_OK;  // already registered (a per-frame call is cheap)
+    g->reg.emplace_back(lo, hi);
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_unregister(neo_hip_upols_group* g, const void* ptr)
+{
+    if (!g) return fail(NEO_HIP_EINVAL, "null group");
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!ptr) {
+        g->reg.clear();
+        return NEO_HIP_OK;
+    }
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
+    g->reg.erase(std::remove_if(g->reg.begin(), g->reg.end(), [lo](const auto& r) { return r.first == lo; }), g->reg.end());
     return NEO_HIP_OK;
 }
 

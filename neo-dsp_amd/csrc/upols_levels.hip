@@ -1348,10 +1348,17 @@ constexpr int block_lds() { return (B + upols_cfg<B>::LL + upols_cfg<B>::TW1 + u
 // step groups: the block role of one step (the caller's stream) and the slice of the 4-block
 // Toeplitz level where G = 4 (toep_role<4>: no LDS); the block's LDS only -- more workgroups
 // resident per CU than the step kernel's 53.8 KB tile allows
+#ifndef NEO_BLOCK_PRIO
+#define NEO_BLOCK_PRIO 0
+#endif
+#ifndef NEO_BLOCK_WPE
+#define NEO_BLOCK_WPE 1
+#endif
 template<int B, bool OLA>
-__global__ __launch_bounds__(lstep_cfg<B>::WG) void k_lvl_block(slice_args a)
+__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(NEO_BLOCK_WPE))) void k_lvl_block(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[block_lds<B>()];
+    if constexpr (NEO_BLOCK_PRIO > 0) __builtin_amdgcn_s_setprio(NEO_BLOCK_PRIO);
     (void)lvl_roles<B, OLA, 2, 1>(a, smem);
 }
 
@@ -1655,9 +1662,13 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
                                                                                   dim3(lstep_cfg<BB>::WG), 0, s, a))
         }
     } else if (part == 2) {
-        if (raw) hipLaunchKernelGGL((k_lvl_slices<1>), dim3(grid), dim3(256), 0, s, a);
-        else if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(grid), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_lvl_slices<kFarKMax>), dim3(grid), dim3(256), 0, s, a);
+#ifndef NEO_BG_LDS_PAD
+#define NEO_BG_LDS_PAD 0
+#endif
+        const unsigned pad = NEO_BG_LDS_PAD;
+        if (raw) hipLaunchKernelGGL((k_lvl_slices<1>), dim3(grid), dim3(256), pad, s, a);
+        else if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(grid), dim3(256), pad, s, a);
+        else hipLaunchKernelGGL((k_lvl_slices<kFarKMax>), dim3(grid), dim3(256), pad, s, a);
     } else {
 #define NEO_LVL(OL, KM)                                                                                        \
     NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, OL, KM>), dim3(grid), \

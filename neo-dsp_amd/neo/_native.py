@@ -91,6 +91,8 @@ SIGNATURES = {
     "neo_hip_upols_group_process": (_i, [_vp, _i, _vp]),
     "neo_hip_upols_group_reset": (_i, [_vp, _i]),
     "neo_hip_upols_group_stats": (_i, [_vp, ctypes.POINTER(_i)] + [ctypes.POINTER(_i64)] * 4),
+    "neo_hip_upols_group_register": (_i, [_vp, _vp, _i64]),
+    "neo_hip_upols_group_unregister": (_i, [_vp, _vp]),
     "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
     "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),
     "neo_hip_normalize_impulse": (_i, [_vp, _i, _i64, _i, _i]),

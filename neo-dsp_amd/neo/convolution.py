@@ -551,8 +551,10 @@ class UpolsGroup:
     """Single-channel convolvers of one shape stepped together (neo_hip_upols_group_*): members
     join(), take a filter [P][B+1] each and process one host block [B] per call, in place; while
     the calls follow the plugin's frame pattern (DenseConvolution.cpp:62-74: every member once
-    per frame, each on a buffer of its own) a frame is ONE launch, else each member runs on a
-    handle of its own; outputs are each member's own sequential convolver's either way."""
+    per frame, each on a buffer of its own) and every member's buffer is registered with the
+    group (register(): the owner keeps it allocated until unregister()), a frame is ONE launch,
+    else each member runs on a handle of its own; outputs are each member's own sequential
+    convolver's either way (up to float summation order after a mode switch)."""
 
     def __init__(self, block_size: int, partitions: int, method: str = "upols", device: int = 0):
         methods = {"upols": 0, "upola": 1}
@@ -587,6 +589,25 @@ class UpolsGroup:
 
     def reset(self, member: int) -> None:
         _native.check(_native.load().neo_hip_upols_group_reset(self._h, int(member)))
+
+    def register(self, buffer: np.ndarray) -> None:
+        """the group may read `buffer` (host memory the caller keeps alive until unregister)"""
+        if not isinstance(buffer, np.ndarray) or not buffer.flags.c_contiguous:
+            raise TypeError("register takes a C-contiguous numpy array")
+        self._keep = getattr(self, "_keep", {})
+        self._keep[buffer.ctypes.data] = buffer  # keeps the registered array alive on the Python side too
+        _native.check(_native.load().neo_hip_upols_group_register(self._h, ctypes.c_void_p(buffer.ctypes.data),
+                                                                  int(buffer.nbytes)))
+
+    def unregister(self, buffer=None) -> None:
+        """stop reading `buffer` (None: every registered range)"""
+        ptr = None if buffer is None else buffer.ctypes.data
+        _native.check(_native.load().neo_hip_upols_group_unregister(self._h, ctypes.c_void_p(ptr)))
+        keep = getattr(self, "_keep", {})
+        if ptr is None:
+            keep.clear()
+        else:
+            keep.pop(ptr, None)
 
     def stats(self) -> dict:
         c = ctypes.c_int()

@@ -1,9 +1,11 @@
 """Groups of single-channel convolvers (neo_hip_upols_group_*, upols_group.hip): the plugin's
 std::vector<upols_convolver> called channel by channel per frame
 (extra/plugin/src/dsp/DenseConvolution.hpp:35, DenseConvolution.cpp:62-74). Every member's
-outputs must equal its own sequential convolver's bit for bit (the group forces the shared
-handle's code-path choices on every handle), whatever the call pattern; in the plugin's
-pattern a frame is one launch."""
+outputs must equal its own sequential convolver's (every handle of the group uses the shared
+handle's code-path choices): bit for bit while the far level contributes nothing yet, and within
+the oracle's bar over long runs (a mode switch re-primes the levels, so the far windows may be
+aligned elsewhere); in the plugin's pattern, with the members' buffers registered by their
+owner, a frame is one launch. The group never reads a buffer that is not registered."""
 import numpy as np
 import pytest
 
@@ -33,6 +35,8 @@ def test_group_frames_equal_multichannel(neo_gpu, oracle, method):
     C, B, L, nf = 16, 128, 128 * 300, 40
     g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 1100, method)
     bufs = [np.zeros(B, np.float32) for _ in range(C)]
+    for b in bufs:
+        g.register(b)
     x = np.stack([oracle.noise(1200 + c, B * nf) for c in range(C)])
     for f in range(nf):
         blk = np.ascontiguousarray(x[:, f * B:(f + 1) * B])
@@ -68,6 +72,8 @@ def test_group_pattern_breaks_split(neo_gpu, oracle):
         s.filter(parts[c][None])
         singles.append(s)
     bufs = [np.zeros(B, np.float32) for _ in range(C)]
+    for b in bufs:
+        g.register(b)
     rng = np.random.default_rng(5)
 
     def call(c, blk):
@@ -119,3 +125,123 @@ def g_far(neo_gpu, C, B, P):
 
 def g_split(C, B):
     return 2 if C * (B // 16) < 256 else 1
+
+
+def test_group_unregistered_buffers_never_read(neo_gpu, oracle):
+    """The plugin's pattern on buffers the owner did NOT register: the group never coalesces
+    (it would have to read them at the next frame's first call). Registered, it coalesces; the
+    owner then frees the buffers and allocates new ones (a prepare() with another block size
+    would): after unregister the group stops reading the old ones at once (the next frame's
+    leader splits), re-coalesces on the new registered buffers, and every output stays its
+    own convolver's."""
+    C, B, L = 8, 128, 128 * 100
+    g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 1500)
+    rng = np.random.default_rng(9)
+
+    def frame(bufs):
+        blk = (rng.random((C, B), dtype=np.float32) - 0.5)
+        expect = ref(blk.copy())
+        for c in range(C):
+            bufs[c][:] = blk[c]
+        for c in range(C):
+            g(ids[c], bufs[c])
+        assert np.array_equal(np.stack(bufs), expect)
+
+    bufs = [np.zeros(B, np.float32) for _ in range(C)]
+    for _ in range(6):
+        frame(bufs)
+    assert not g.stats()["coalesced"] and g.stats()["frame_steps"] == 0
+    for b in bufs:
+        g.register(b)
+    for _ in range(4):
+        frame(bufs)
+    assert g.stats()["coalesced"]
+    n0 = g.stats()["frame_steps"]
+    g.unregister(None)
+    del bufs  # freed (no reference left on our side either)
+    bufs = [np.full(B, np.nan, np.float32) for _ in range(C)]  # new allocations
+    for b in bufs:
+        g.register(b)
+    frame(bufs)  # leader: neighbours' last buffers unregistered -> split, independent
+    st = g.stats()
+    assert not st["coalesced"] and st["frame_steps"] == n0
+    for _ in range(4):
+        frame(bufs)
+    assert g.stats()["coalesced"]
+
+
+def test_group_step_groups_late_blocks_and_split(neo_gpu, oracle):
+    """A shape with step groups (64 members x B = 512: 2048 16-column units, G = 4, the block
+    of a redo runs k_lvl_block): members whose blocks change after the frame's first call
+    (redos) and a member called twice (split mid-frame, one member stepped back a block),
+    against independent one-channel convolvers with the group's code-path choices."""
+    C, B, L = 64, 512, 512 * 100
+    g, ids, parts, _ = _setup(neo_gpu, oracle, C, B, L, 1600)
+    P = parts.shape[1]
+    probe = neo_gpu.UpolsConvolver(C, B, P)
+    opts = {"far_group": probe.far_group(), "toep_split": g_split(C, B), "step_group": probe.step_group()}
+    assert opts["step_group"] == 4
+    probe.close()
+    singles = []
+    for c in range(C):
+        s = neo_gpu.UpolsConvolver(1, B, P, options=opts)
+        s.filter(parts[c][None])
+        singles.append(s)
+    bufs = [np.zeros(B, np.float32) for _ in range(C)]
+    for b in bufs:
+        g.register(b)
+    rng = np.random.default_rng(11)
+    for f in range(14):
+        blk = rng.random((C, B), dtype=np.float32) - 0.5
+        late = {3, 40} if f in (6, 9) else set()
+        for c in range(C):
+            bufs[c][:] = 0.0 if c in late else blk[c]
+        order = list(range(C))
+        if f == 11:  # member 7 twice before the others: the group splits mid-frame
+            order = [0, 7, 7] + [c for c in range(1, C) if c != 7]
+        seen = set()
+        for c in order:
+            if c in late:
+                bufs[c][:] = blk[c]
+            if c in seen:  # the second call of a member: a new block
+                bufs[c][:] = rng.random(B, dtype=np.float32) - 0.5
+            e = bufs[c][None].copy()
+            g(ids[c], bufs[c])
+            singles[c](e)
+            assert np.allclose(bufs[c], e[0], rtol=0, atol=1e-5 * max(1e-3, float(np.abs(e).max()))), (f, c)
+            seen.add(c)
+        if f == 8:
+            st = g.stats()
+            assert st["coalesced"] and st["redos"] >= 2, st
+    assert g.stats()["switches"] >= 2
+
+
+def test_group_long_run_vs_oracle(neo_gpu, oracle):
+    """Far level contributing (P = 600 > 256 partitions) over 700 frames with mode switches (new
+    filters for every member at frame 350: the group splits, then re-coalesces with its levels
+    re-primed at another block): every member's output against the oracle's dense_convolve of its
+    own input, each run from its filter on (a filter restarts the state,
+    uniform_partitioned_convolver::filter)."""
+    C, B, P, nf = 4, 128, 600, 700
+    L = B * P
+    g, ids, parts, _ = _setup(neo_gpu, oracle, C, B, L, 1700)
+    bufs = [np.zeros(B, np.float32) for _ in range(C)]
+    for b in bufs:
+        g.register(b)
+    x = np.stack([oracle.noise(1800 + c, B * nf) for c in range(C)])
+    y = np.zeros_like(x)
+    for f in range(nf):
+        if f == 350:
+            for c in range(C):
+                g.filter(ids[c], parts[c])  # every member restarts
+        for c in range(C):
+            bufs[c][:] = x[c, f * B:(f + 1) * B]
+        for c in range(C):
+            g(ids[c], bufs[c])
+            y[c, f * B:(f + 1) * B] = bufs[c]
+    assert g.stats()["switches"] >= 3
+    for lo, hi in ((0, 350), (350, nf)):
+        ref = oracle.dense_convolve(np.ascontiguousarray(x[:, lo * B:hi * B]), parts)
+        got = y[:, lo * B:hi * B]
+        err = np.abs(got - ref).max() / np.abs(ref).max()
+        assert err <= 1e-5, (lo, err)
