@@ -333,7 +333,9 @@ def algorithmic_bytes(C, B, P, plan, G=1, far_k=0, far_form=1):
                entries; phase 1 takes K windows per pass over the nseg - 1 older row-pair and
                segment spectra (1/K per window), and 2b segments 1 .. j of window j of a group
                (K - 1 spectrum pairs per window on average): 256 (4 + 2 (nseg - 1) / K + K - 1)
-               + 128 values per window, K = far_group(nseg, units) (upols_levels.hip).
+               + 128 values per window, K = far_group(nseg, units) (upols_levels.hip); plus phase
+               1's partial sums, 256 values per column and window written and read back by
+               phase 2 (included in "far", also reported alone as "far_partial_sums").
                far_form 2 (recomputed every window, far2r_role): per column and window the
                (nseg + 1) 128 FDL rows of the segments' row pairs, the P - 256 filter rows of the
                band and the 128 field rows.
@@ -349,9 +351,13 @@ def algorithmic_bytes(C, B, P, plan, G=1, far_k=0, far_form=1):
     # step groups: phase 2 keeps the fresh spectrum in registers (far2c_role), 3 instead of 4
     fresh = 4 if G == 1 else 3
     far = C * B / 128 * 8 * (256 * (fresh + 2 * (ns - 1) / K + K - 1) + 128) if ns else 0.0
+    # phase 1's partial sums: 256 values per column and window written by phase 1 and read back
+    # by phase 2 (the two phases' hand-off; none in the recomputed form)
+    partials = C * B / 128 * 8 * 2 * 256 if ns else 0.0
     if ns and far_form == 2:
         far = C * B / 128 * 8 * ((ns + 1) * 128 + (P - 256) + 128)
-    out = {"block": block, "toeplitz": toep, "far": far}
+        partials = 0.0
+    out = {"block": block, "toeplitz": toep, "far": far + partials, "far_partial_sums": partials}
     if G > 1:
         out["toeplitz_block"] = toep_block
     return out
@@ -608,7 +614,7 @@ def run_upols(args, world, rank, local):
         # time of the timed steps where that is smaller (with timing events on it the stream's
         # launches slow down; at one channel the event run is host-bound)
         step_ms = min(gpu_ms["levels"], elapsed * 1e3 / args.steps)
-        by = sum(roles.values())
+        by = sum(v for k, v in roles.items() if k != "far_partial_sums")
         gbs = by / (step_ms * 1e-3) / 1e9
         name = f"k_lvl_step<{B}>"
         kernels = [{"kernel": name + " (block, Toeplitz T = %s, far %d segments)"
@@ -702,6 +708,7 @@ def run_upols(args, world, rank, local):
                      "note": "device-resident IR [C][L]: normalize (sequential-float energy, min over channels), "
                              "partition r2c, then the first streaming block (far segment spectra + level priming); "
                              "max over ranks"}
+    latency_mode = run_latency_mode(args, conv, feed, C, B, world, C_total) if levels else None
     offline = run_upols_offline(args, conv, C, B, P, x, y, nx * B, stream, world, C_total)
     host_io = None
     if not args.no_host_io:
@@ -756,6 +763,7 @@ def run_upols(args, world, rank, local):
         "roofline": roof,
         "steady": steady,
         "ir_change": ir_change,
+        "latency_mode": latency_mode,
         "latency": latency,
         "parity": parity,
         "per_block_step": plain,
@@ -767,6 +775,47 @@ def run_upols(args, world, rank, local):
     if args.workload == "c3":
         res["roofline"]["note"] = "working set L2/MALL-resident: effective GB/s, launch-latency bound"
     return res
+
+
+def run_latency_mode(args, conv, feed, C, B, world, C_total):
+    """The latency mode (neo_hip_upols_set_persistent: one persistent kernel steps every block,
+    each call synchronous) on the same convolver and input, for the shapes it takes (C3): the
+    host round trip per block (one call, complete on return), the same number of steps as the
+    headline back to back (wall clock), and the GPU time per step (record read -> done, on the
+    GPU clock). None where the shape is not latency-bound (the handle refuses it)."""
+    import numpy as np
+
+    try:
+        conv.set_persistent(True)
+    except RuntimeError as e:
+        return {"available": False, "reason": str(e).split(": ", 1)[-1]}
+    t_warm = time.perf_counter()
+    while time.perf_counter() - t_warm < WARM_SECONDS:
+        feed.run(16)  # synchronous calls: no device sync while the persistent kernel is resident
+    rt = []
+    for _ in range(400):
+        t0 = time.perf_counter()
+        feed.run(1)
+        rt.append(time.perf_counter() - t0)
+    st = np.array(conv.persist_step_times())
+    barrier(world)
+    t0 = time.perf_counter()
+    feed.run(args.steps)
+    el = max_over_ranks(time.perf_counter() - t0, world)
+    info = conv.persistent_info()
+    conv.set_persistent(False)
+    rt = np.array(rt) * 1e6
+    return {"available": True, "value": C_total * B * args.steps / el / 1e6, "unit": "Msamples/s",
+            "ms_per_step": el * 1e3 / args.steps,
+            "host_roundtrip_p50_us": max_over_ranks(float(np.percentile(rt, 50)), world),
+            "host_roundtrip_p99_us": max_over_ranks(float(np.percentile(rt, 99)), world),
+            "host_roundtrip_mean_us": max_over_ranks(float(rt.mean()), world),
+            "gpu_step_p50_us": float(np.percentile(st, 50)) if st.size else None,
+            "gpu_step_p99_us": float(np.percentile(st, 99)) if st.size else None,
+            "gpu_steps_sampled": int(st.size), "persistent_launches": info["launches"],
+            "note": "neo_hip_upols_set_persistent: round trip = one synchronous call per block (device-resident "
+                    "blocks), 400 calls; value = --steps calls back to back (pipelined records, wall clock); "
+                    "gpu_step = record read -> completion signal on the GPU clock (last 63 steps)"}
 
 
 def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world, C_total):

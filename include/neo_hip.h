@@ -185,6 +185,22 @@ NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* pha
  * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries); the automatic
  * choice of far_level. */
 NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, int* T, int* a, int* b, int* nseg);
+/* Latency mode for latency-bound shapes (few channels, filters up to 256 partitions, blocks up
+ * to 512; C3): ONE persistent kernel per handle steps every block. A call writes the block's
+ * record to a mailbox in mapped host memory and spins until the kernel reports the block done:
+ * no launch and no stream wait per block, and the Toeplitz levels' slices run beside the
+ * caller's next block instead of before it. Every process call is then SYNCHRONOUS (complete
+ * on return; the stream argument is not used) and device inputs must be ready when it is made.
+ * The kernel leaves after idle_ms without a block (the next call relaunches it) and whenever a
+ * setup call (set_filter, set_impulse, reset, set_ahead, set_persistent(0), destroy) runs.
+ * Outputs equal the normal streaming step's (the same sums; the levels re-prime on entry and
+ * exit, bit for bit). Not available: EINVAL names the reason. */
+NEO_HIP_API int neo_hip_upols_set_persistent(neo_hip_upols* h, int enable, double idle_ms);
+/* requested, kernel resident now, persistent launches so far */
+NEO_HIP_API int neo_hip_upols_get_persistent(neo_hip_upols* h, int* enabled, int* running, int64_t* launches);
+/* GPU time of the last min(63, cap) latency-mode steps, oldest first, in us: from the kernel
+ * reading the block's record to its completion signal (both on the GPU clock) */
+NEO_HIP_API int neo_hip_upols_persist_step_times(neo_hip_upols* h, double* us, int64_t cap, int64_t* count);
 /* windows per far phase-1 pass the handle runs (neo_hip_upols_opts.far_group or the automatic
  * choice); 0 without a far transform level */
 NEO_HIP_API int neo_hip_upols_get_far_group(neo_hip_upols* h, int* windows);

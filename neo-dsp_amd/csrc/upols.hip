@@ -393,6 +393,11 @@ int reset_state(upols_t* h, hipStream_t s)
 void destroy(upols_t* h)
 {
     if (!h) return;
+    (void)persist_stop(h);
+    if (h->ps_stream) (void)hipStreamDestroy(h->ps_stream);
+    if (h->ps_mb) (void)hipHostFree(h->ps_mb);
+    (void)hipFree(h->ps_flags);
+    (void)hipFree(h->ps_tl);
     for (auto& g : h->events)
         for (auto& e : g.e) (void)hipEventDestroy(e);
     (void)hipFree(h->H);  // the FDL shares H's allocation (rows [nrows, 2 nrows))
@@ -414,6 +419,7 @@ void destroy(upols_t* h)
 
 int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
+    if (h->persist) return persist_process(h, in, ld_in, out, ld_out, 1);  // synchronous: s is not used
     if (h->ahead) return launch_levels(h, in, ld_in, out, ld_out, s);
     if (int rc = lvl_join(h, s)) return rc;
     upols_t::ev_group* ev = nullptr;
@@ -483,6 +489,10 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
     const int T = h->batch ? batch_blocks(h) : 1;
     const bool a16 = !((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) &&
                      !((ld_in | ld_out) & 3);
+    if (h->persist) {  // latency mode: every block through the persistent kernel, complete on return
+        if (n % B || !a16) return fail(NEO_HIP_EINVAL, "latency mode: whole 16-byte aligned blocks");
+        return persist_process(h, in, ld_in, out, ld_out, n / B);
+    }
     if (!h->v2) {
         if (n % B) return fail(NEO_HIP_EINVAL, "upols/upola convolvers take whole blocks (%lld samples, block %d)",
                                (long long)n, B);
@@ -683,6 +693,7 @@ NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h)
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     device_guard g(h->device);
+    if (int rc = persist_stop(h)) return rc;
     NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
     int rc = reset_state(h, h->stream);
     if (rc) return rc;
@@ -695,6 +706,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
     if (!h || !filter) return fail(NEO_HIP_EINVAL, "null handle or filter");
     device_guard g(h->device);
     if (g.rc) return g.rc;
+    if (int rc = persist_stop(h)) return rc;
     NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
     const int64_t rows = int64_t(h->C) * h->P;
     const size_t bytes = size_t(rows) * size_t(h->B + 1) * sizeof(cf);
@@ -722,6 +734,7 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
                     (long long)partitions_for(length, h->B), h->P);
     device_guard g(h->device);
     if (g.rc) return g.rc;
+    if (int rc = persist_stop(h)) return rc;
     NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
     const size_t bytes = size_t(h->C) * size_t(length) * sizeof(float);
     float* d = nullptr;
@@ -852,8 +865,59 @@ NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable)
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     if (enable && h->v2) return fail(NEO_HIP_EINVAL, "streaming levels are for whole-block upols / upola handles");
     if (enable && h->B > 1024) return fail(NEO_HIP_EINVAL, "streaming levels take blocks up to 1024");
+    device_guard g(h->device);
+    if (int rc = persist_stop(h)) return rc;
+    if (!enable) h->persist = false;  // the latency mode runs the levels
     h->ahead = enable != 0;
     h->lv_n = -1;  // the FDL is complete at any block boundary: the next step primes the levels
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_set_persistent(neo_hip_upols* h, int enable, double idle_ms)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    if (enable) {
+        if (const char* why = persist_ineligible(h)) return fail(NEO_HIP_EINVAL, "latency mode: %s", why);
+        if (!(idle_ms > 0.0 && idle_ms <= 10000.0)) return fail(NEO_HIP_EINVAL, "idle_ms must be in (0, 10000]");
+        NEO_HIP_CHECK(hipDeviceSynchronize());  // steps queued on any stream come first
+        if (int rc = lvl_join(h, h->stream)) return rc;
+        NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->ps_idle_ms = idle_ms;
+        h->persist = true;
+        h->ps_valid = false;  // the persistent schedule primes the levels at its first block
+        return NEO_HIP_OK;
+    }
+    h->persist = false;
+    return persist_stop(h);
+}
+
+NEO_HIP_API int neo_hip_upols_get_persistent(neo_hip_upols* h, int* enabled, int* running, int64_t* launches)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    if (enabled) *enabled = h->persist;
+    if (running) *running = h->ps_running && h->ps_mb && __atomic_load_n(&h->ps_mb->alive, __ATOMIC_ACQUIRE);
+    if (launches) *launches = h->ps_launches;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_persist_step_times(neo_hip_upols* h, double* us, int64_t cap, int64_t* count)
+{
+    if (!h || (cap > 0 && !us)) return fail(NEO_HIP_EINVAL, "null handle or output");
+    if (count) *count = 0;
+    if (!h->ps_tl || h->lv_n <= h->ps_n0 || !h->ps_valid) return NEO_HIP_OK;
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    std::vector<unsigned long long> tl(2 * kPsRing);
+    NEO_HIP_CHECK(hipMemcpy(tl.data(), h->ps_tl, tl.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    // the last min(kPsRing - 1, steps of this launch) steps, oldest first
+    const int64_t last = h->lv_n - 1, k = std::min<int64_t>({int64_t(kPsRing) - 1, last - h->ps_n0 + 1, cap});
+    for (int64_t i = 0; i < k; ++i) {
+        const int64_t n = last - k + 1 + i, slot = n % kPsRing;
+        us[i] = double(tl[size_t(2 * slot + 1)] - tl[size_t(2 * slot)]) * 1e-2;  // 100 MHz ticks -> us
+    }
+    if (count) *count = k;
     return NEO_HIP_OK;
 }
 

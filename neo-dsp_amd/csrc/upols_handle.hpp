@@ -27,6 +27,25 @@ constexpr int kFarT = 128;   // far level: blocks per window (256-point partitio
 constexpr int kFarA = 256;   // far level: first partition (2 kFarT)
 constexpr int kFarRing = 2 * kFarA;  // far level: FDL ring rows needed (a slice reads back 383 blocks)
 
+// Latency mode (neo_hip_upols_set_persistent, upols_levels.hip): one persistent kernel per handle
+// polls a mailbox in mapped host memory. Step n's record (device addresses of its input and
+// output blocks) goes to slot n mod kPsRing; both words carry the slot's lap tag in their low 4
+// bits (the blocks are 16-B aligned), so a record read while the host rewrites it shows two
+// different tags and is read again.
+constexpr int kPsRing = 64;
+__host__ __device__ inline uint64_t ps_tag(int64_t n) { return uint64_t((n / kPsRing) % 15 + 1); }
+struct persist_rec {
+    uint64_t in, out;
+};
+struct persist_mb {
+    persist_rec rec[kPsRing];
+    int64_t done;   // kernel -> host: steps completed (n + 1 of the last one)
+    int32_t stop;   // host -> kernel: leave
+    int32_t alive;  // kernel -> host: 0 once the kernel leaves (stop, idle timeout, error)
+    int32_t err;    // kernel -> host: a wait passed its deadline
+    int32_t pad;
+};
+
 struct level_plan {
     int a0 = 1;                      // the block step takes partitions [0, a0)
     int n = 0;                       // Toeplitz levels
@@ -109,6 +128,20 @@ struct neo_hip_upols {
     double part_ms[4] = {};        // drained event time per part (see neo_hip_upols_timing_detail)
     int64_t part_n[4] = {};
     std::vector<float> group_ms;   // whole-group durations, in order (neo_hip_upols_step_times)
+    // latency mode (neo_hip_upols_set_persistent): a persistent step kernel on ps_stream
+    bool persist = false;          // requested
+    bool ps_running = false;       // a persistent kernel was launched and not yet joined
+    bool ps_valid = false;         // the level slabs follow the persistent schedule (relaunch without priming)
+    hipStream_t ps_stream = nullptr;
+    neo_hip::persist_mb* ps_mb = nullptr;      // mapped pinned mailbox (host address)
+    neo_hip::persist_mb* ps_mb_dev = nullptr;  // its device address
+    int64_t* ps_flags = nullptr;               // device: blk_done, quit, arrive, sl_done[]
+    unsigned long long* ps_tl = nullptr;       // device: per ring slot {record seen, done} (wall clock, 100 MHz)
+    int ps_nslices = 0;                        // slice workgroups of the persistent kernel
+    int64_t ps_ld_in = 0, ps_ld_out = 0;       // channel strides of the running kernel
+    int64_t ps_n0 = 0;                         // first step of the running kernel
+    int64_t ps_launches = 0;                   // persistent launches so far (idle timeouts relaunch)
+    double ps_idle_ms = 50.0;                  // the kernel leaves after this long without a block
 };
 
 
@@ -190,6 +223,12 @@ int launch_block_only(upols_t* h, int64_t n, int w, int c, const float* in, floa
 int far_group_for(int C, int B, int P);
 int toep_split_for(int C, int B);
 int step_group_for(int C, int B, int P);
+// latency mode: whole blocks through the persistent kernel, synchronous (upols_levels.hip)
+int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t nblocks);
+// stop the persistent kernel (if any) and leave the levels to re-prime on the next normal step
+int persist_stop(upols_t* h);
+// why a handle cannot run the latency mode (nullptr: it can)
+const char* persist_ineligible(const upols_t* h);
 // order everything enqueued on the background stream (step-group slices) before later work on s;
 // every path that writes the FDL ring or the level buffers other than a streaming step calls it
 int lvl_join(upols_t* h, hipStream_t s);

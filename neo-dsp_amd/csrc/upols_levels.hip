@@ -26,7 +26,9 @@
 #include "upols_handle.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -2033,6 +2035,373 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     if ((rc = timing_mark(ev, 1, s))) return rc;
     h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
     h->lv_n = n + 1;
+    return NEO_HIP_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Latency mode (neo_hip_upols_set_persistent): ONE persistent kernel per handle runs every step
+// of a latency-bound shape (few channels, no far level, one launch per step otherwise: C3). The
+// host writes step n's record (its blocks' device addresses) to the mapped mailbox and spins on
+// mb->done; no launch, no stream wait. Workgroups by role, fixed for the launch:
+//   block    one per channel: waits for the slices of step n - 2 (agent acquire, issued before
+//            the record arrives), polls the record, runs block_role, publishes (system-scope
+//            release: the output and the FDL row), and the last of them signals the host
+//   slices   per Toeplitz level: part j = n mod T (j < T - 1) of the NEXT window in T - 1 parts
+//            (step groups' schedule: a window's slabs are complete two steps before its first
+//            block, so a block never waits for the slices of the step before), after block
+//            n - 1 published (agent acquire), then publish (agent release) and sl_done = n
+// Every wait has a deadline (mb->err, then every workgroup leaves); the block workgroups leave
+// after ps_idle_ms without a record, and the host relaunches at the next block.
+struct persist_args {
+    slice_args base;                // handle constants (H, FDL, ring, strides, prev, twiddles, a0)
+    cf* slab[kLvToep];
+    int T[kLvToep], A[kLvToep], Bd[kLvToep], JH[kLvToep], UPW[kLvToep], U[kLvToep];
+    int wg0[kLvToep + 1];           // slice workgroups of level l: [wg0[l], wg0[l + 1])
+    int nlev, nblk;
+    int64_t n0;                     // first step of this launch (levels primed at step 0)
+    int w0;                         // its ring row
+    persist_mb* mb;                 // the mapped mailbox (device address)
+    int64_t* flags;                 // [0] blk_done, [1] quit, [2] arrive, [3 + s] sl_done of slice workgroup s
+    unsigned long long* tl;         // [kPsRing][2] record seen / done
+    long long idle_ticks, dead_ticks;
+};
+
+__device__ __forceinline__ int64_t ps_ld(const int64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ps_st(int64_t* p, int64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ps_ring_row(const persist_args& pa, int64_t n)
+{
+    const int64_t r = (int64_t(pa.w0) + (n - pa.n0)) % pa.base.ring;
+    return int(r < 0 ? r + pa.base.ring : r);
+}
+
+// thread 0: wait until cond() (quit and the deadline checked every round); false = leave
+template<class F>
+__device__ __forceinline__ bool ps_wait(const persist_args& pa, F cond)
+{
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+        if (cond()) return true;
+        if (ps_ld(pa.flags + 1)) return false;
+        if ((long long)(wall_clock64() - t0) > pa.dead_ticks) {
+            __hip_atomic_store(&pa.mb->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ps_st(pa.flags + 1, 1);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+__device__ __forceinline__ void ps_acquire()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template<int B, bool OLA>
+__device__ __forceinline__ void persist_block(const persist_args& pa, int c, char* smem)
+{
+    __shared__ uint64_t io[2];
+    __shared__ int go;
+    const int nsl = pa.wg0[pa.nlev];
+    for (int64_t n = pa.n0;; ++n) {
+        if (threadIdx.x == 0) {
+            // the window's slabs: every slice workgroup past step n - 2
+            bool ok = ps_wait(pa, [&] {
+                for (int s = 0; s < nsl; ++s)
+                    if (ps_ld(pa.flags + 3 + s) < n - 2) return false;
+                return true;
+            });
+            if (ok) ps_acquire();
+            // the record of step n (both words tagged with its lap), the host's stop, the idle limit
+            const int slot = int(n % kPsRing);
+            const uint64_t tag = ps_tag(n);
+            const unsigned long long t0 = wall_clock64();
+            while (ok) {
+                const uint64_t r0 = __hip_atomic_load(&pa.mb->rec[slot].in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t r1 = __hip_atomic_load(&pa.mb->rec[slot].out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((r0 & 15) == tag && (r1 & 15) == tag) {
+                    io[0] = r0 & ~uint64_t(15);
+                    io[1] = r1 & ~uint64_t(15);
+                    __hip_atomic_store(pa.tl + 2 * slot, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                if (__hip_atomic_load(&pa.mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) || ps_ld(pa.flags + 1) ||
+                    (long long)(wall_clock64() - t0) > pa.idle_ticks) {
+                    ok = false;
+                    ps_st(pa.flags + 1, 1);
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            go = ok;
+        }
+        __syncthreads();
+        if (!go) break;
+        slice_args a = pa.base;
+        a.in = reinterpret_cast<const float*>(io[0]);
+        a.out = reinterpret_cast<float*>(io[1]);
+        a.w = ps_ring_row(pa, n);
+        a.nsl = pa.nlev;
+        a.ff = nullptr;
+#pragma unroll
+        for (int l = 0; l < kLvToep; ++l) {  // static indices: the slice_args stay in registers
+            if (l < pa.nlev) {
+                const int T = pa.T[l];
+                a.sl[l] = pa.slab[l] + (((n / T) & 1) * a.C * T + n % T) * a.B;
+                a.scs[l] = int64_t(T) * a.B;
+            }
+        }
+        block_role<B, OLA>(a, c, smem);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the output reaches the host's view
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int64_t prev = __hip_atomic_fetch_add(pa.flags + 2, int64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == (n - pa.n0 + 1) * pa.nblk - 1) {  // the last channel of step n
+                ps_st(pa.flags + 0, n);
+                __hip_atomic_store(pa.tl + 2 * (n % kPsRing) + 1, wall_clock64(), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&pa.mb->done, n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    if (threadIdx.x == 0 && c == 0) __hip_atomic_store(&pa.mb->alive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void persist_slices(const persist_args& pa, int s, char* smem)
+{
+    __shared__ int go;
+    int l = 0;
+    while (l + 1 < pa.nlev && s >= pa.wg0[l + 1]) ++l;
+    const int i = s - pa.wg0[l], T = pa.T[l], U = pa.U[l], UPW = pa.UPW[l];
+    for (int64_t n = pa.n0 - 1;; ++n) {
+        if (threadIdx.x == 0) {
+            // FDL rows up to block n - 1 (the relaunch's first round redoes step n0 - 1: rows of
+            // earlier launches, ordered by the kernel boundary)
+            bool ok = n < pa.n0 || ps_wait(pa, [&] { return ps_ld(pa.flags + 0) >= n - 1; });
+            if (ok && n >= pa.n0) ps_acquire();
+            go = ok;
+        }
+        __syncthreads();
+        if (!go) break;
+        const int64_t cur = n / T;
+        const int j = int(n % T);
+        if (n >= 0 && j < T - 1) {
+            const int u0 = int(int64_t(j) * U / (T - 1)), u1 = int(int64_t(j + 1) * U / (T - 1));
+            const int nwg = (u1 - u0 + UPW - 1) / UPW;
+            if (i < nwg) {
+                slice_args a = pa.base;
+                a.nblk = 0;
+                a.ntp = l + 1;
+                toep_arg ta{};
+                ta.slab = pa.slab[l] + ((cur + 1) & 1) * int64_t(a.C) * T * a.B;
+                ta.T = T;
+                ta.a = pa.A[l];
+                ta.b = pa.Bd[l];
+                int tw = int((int64_t(ps_ring_row(pa, n)) + (cur + 1) * T - n) % a.ring);
+                ta.tw = tw < 0 ? tw + a.ring : tw;
+                ta.u0 = u0;
+                ta.u1 = u1;
+                ta.nwg = nwg;
+                ta.jh = pa.JH[l];
+#pragma unroll
+                for (int L = 0; L < kLvToep; ++L) {  // static indices
+                    if (L < l) a.tp[L].nwg = 0;
+                    if (L == l) a.tp[L] = ta;
+                }
+                int bid = i;
+                if (!toep_level<0>(a, bid, smem) && !toep_level<1>(a, bid, smem) && !toep_level<2>(a, bid, smem))
+                    (void)toep_level<3>(a, bid, smem);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ps_st(pa.flags + 3 + s, n);
+        }
+    }
+}
+
+template<int B, bool OLA>
+__global__ __launch_bounds__(256) void k_lvl_persist(persist_args pa)
+{
+    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
+    if (int(blockIdx.x) < pa.nblk) persist_block<B, OLA>(pa, int(blockIdx.x), smem);
+    else persist_slices(pa, int(blockIdx.x) - pa.nblk, smem);
+}
+
+const char* persist_ineligible(const upols_t* h)
+{
+    if (!h->ahead) return "the latency mode runs the streaming levels (from 64 partitions)";
+    if (h->v2) return "upola_convolver_v2 takes sub-block input";
+    if (h->lv.nseg || (h->lv.n && h->lv.T[h->lv.n - 1] == kBigT)) return "a filter of more than 256 partitions (far level)";
+    if (h->C > 16) return "more than 16 channels (the latency mode is for latency-bound shapes)";
+    if (h->B > 512) return "blocks above 512 samples";
+    return nullptr;
+}
+
+// the slice workgroups of level l: the most any part of its T - 1 needs
+static int persist_level_wgs(const upols_t* h, int l, int& U, int& UPW, int& JH)
+{
+    const int T = h->lv.T[l];
+    toep_geom(h, T, JH, UPW);
+    U = int(toep_units(h, T));
+    int most = 0;
+    for (int j = 0; j + 1 < T; ++j) {
+        const int u0 = int(int64_t(j) * U / (T - 1)), u1 = int(int64_t(j + 1) * U / (T - 1));
+        most = std::max(most, (u1 - u0 + UPW - 1) / UPW);
+    }
+    return most;
+}
+
+static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
+{
+    if (!h->ps_stream) {
+        NEO_HIP_CHECK(hipStreamCreateWithFlags(&h->ps_stream, hipStreamNonBlocking));
+        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->ps_mb), sizeof(persist_mb),
+                                    hipHostMallocMapped | hipHostMallocCoherent));
+        NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->ps_mb_dev), h->ps_mb, 0));
+        std::memset(h->ps_mb, 0, sizeof(persist_mb));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_tl), 2 * kPsRing * sizeof(unsigned long long)));
+        NEO_HIP_CHECK(hipMemset(h->ps_tl, 0, 2 * kPsRing * sizeof(unsigned long long)));
+    }
+    if (int rc = lvl_buffers(h)) return rc;
+    if (!h->ps_valid || h->lv_n < 0) {  // window 0 of every level, from this block on
+        if (int rc = lvl_join(h, h->ps_stream)) return rc;
+        h->lv_n = -1;
+        if (int rc = lvl_prime(h, h->ps_stream)) return rc;
+        h->lv_n = 0;
+        h->ps_valid = true;
+    }
+    persist_args pa{};
+    pa.base = base_args(h);
+    pa.base.prev = h->prev;
+    pa.base.twg = h->tw;
+    pa.base.a0 = h->lv.a0;
+    pa.base.ld_in = ld_in;
+    pa.base.ld_out = ld_out;
+    pa.nlev = h->lv.n;
+    pa.nblk = h->C;
+    pa.wg0[0] = 0;
+    for (int l = 0; l < h->lv.n; ++l) {
+        pa.slab[l] = h->lv_slab[l];
+        pa.T[l] = h->lv.T[l];
+        pa.A[l] = h->lv.a[l];
+        pa.Bd[l] = h->lv.b[l];
+        pa.wg0[l + 1] = pa.wg0[l] + persist_level_wgs(h, l, pa.U[l], pa.UPW[l], pa.JH[l]);
+    }
+    const int nsl = pa.wg0[h->lv.n];
+    if (h->ps_nslices < nsl || !h->ps_flags) {
+        (void)hipFree(h->ps_flags);
+        h->ps_flags = nullptr;
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_flags), size_t(3 + nsl) * sizeof(int64_t)));
+        h->ps_nslices = nsl;
+    }
+    pa.n0 = h->lv_n;
+    pa.w0 = h->wpos;
+    pa.mb = h->ps_mb_dev;
+    pa.flags = h->ps_flags;
+    pa.tl = h->ps_tl;
+    pa.idle_ticks = (long long)(h->ps_idle_ms * 1e5);  // wall_clock64: 100 MHz
+    pa.dead_ticks = 200000000LL;                        // 2 s: a wait that long is a fault, not a schedule
+    std::vector<int64_t> init(size_t(3 + nsl), pa.n0 - 2);
+    init[0] = pa.n0 - 1;
+    init[1] = 0;
+    init[2] = 0;
+    NEO_HIP_CHECK(hipMemcpyAsync(h->ps_flags, init.data(), init.size() * sizeof(int64_t), hipMemcpyHostToDevice,
+                                 h->ps_stream));
+    NEO_HIP_CHECK(hipStreamSynchronize(h->ps_stream));  // the prime and the flags before the first record
+    h->ps_mb->stop = 0;
+    h->ps_mb->err = 0;
+    h->ps_mb->done = pa.n0;
+    h->ps_mb->alive = 1;
+    const unsigned grid = unsigned(h->C + nsl);
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 512) hipLaunchKernelGGL((k_lvl_persist<BB, true>), dim3(grid),
+                                                                              dim3(256), 0, h->ps_stream, pa))
+    } else {
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 512) hipLaunchKernelGGL((k_lvl_persist<BB, false>), dim3(grid),
+                                                                              dim3(256), 0, h->ps_stream, pa))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    h->ps_running = true;
+    h->ps_ld_in = ld_in;
+    h->ps_ld_out = ld_out;
+    h->ps_n0 = pa.n0;
+    ++h->ps_launches;
+    return NEO_HIP_OK;
+}
+
+// the running kernel (if any) leaves; ps_valid stays: a relaunch continues the schedule
+static int persist_join(upols_t* h)
+{
+    if (!h->ps_running) return NEO_HIP_OK;
+    __atomic_store_n(&h->ps_mb->stop, 1, __ATOMIC_SEQ_CST);
+    const hipError_t e = hipStreamSynchronize(h->ps_stream);
+    h->ps_running = false;
+    if (e != hipSuccess) return fail(NEO_HIP_ERUNTIME, "persistent kernel: %s", hipGetErrorString(e));
+    if (__atomic_load_n(&h->ps_mb->err, __ATOMIC_SEQ_CST))
+        return fail(NEO_HIP_ERUNTIME, "persistent kernel: a wait passed its deadline");
+    return NEO_HIP_OK;
+}
+
+int persist_stop(upols_t* h)
+{
+    const int rc = persist_join(h);
+    if (h->ps_valid) {
+        h->ps_valid = false;
+        h->lv_n = -1;  // the normal schedule re-primes the levels
+    }
+    return rc;
+}
+
+int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t nblocks)
+{
+    if (const char* why = persist_ineligible(h)) return fail(NEO_HIP_EINVAL, "latency mode: %s", why);
+    if (h->C > 1 && (ld_in != h->ps_ld_in || ld_out != h->ps_ld_out) && h->ps_running)
+        if (int rc = persist_join(h)) return rc;  // another channel stride: relaunch with it
+    persist_mb* mb = h->ps_mb;
+    if (h->ps_running && !__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE))
+        if (int rc = persist_join(h)) return rc;  // left after its idle limit (or failed)
+    if (!h->ps_running)
+        if (int rc = persist_launch(h, ld_in, ld_out)) return rc;
+    const int B = h->B;
+    for (int64_t k = 0; k < nblocks; ++k) {
+        const int64_t n = h->lv_n;
+        while (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) < n - (kPsRing - 2)) {  // a free slot
+            if (!__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE)) {
+                const int rc = persist_join(h);
+                return rc ? rc : fail(NEO_HIP_ERUNTIME, "persistent kernel left");
+            }
+        }
+        const uint64_t tag = ps_tag(n);
+        persist_rec& r = mb->rec[n % kPsRing];
+        __atomic_store_n(&r.in, reinterpret_cast<uint64_t>(in + k * B) | tag, __ATOMIC_RELEASE);
+        __atomic_store_n(&r.out, reinterpret_cast<uint64_t>(out + k * B) | tag, __ATOMIC_RELEASE);
+        h->lv_n = n + 1;
+        h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
+    }
+    // complete on return (the block's deadline: spin, do not yield); the kernel's own waits give
+    // up after 2 s, so a host wait past 5 s means the kernel is not running at all
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0; __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) < h->lv_n; ++it) {
+        if (!__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) && __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) < h->lv_n) {
+            const int rc = persist_join(h);
+            return rc ? rc : fail(NEO_HIP_ERUNTIME, "persistent kernel left before step %lld", (long long)h->lv_n);
+        }
+        if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+            __atomic_store_n(&mb->stop, 1, __ATOMIC_SEQ_CST);
+            return fail(NEO_HIP_ERUNTIME, "persistent kernel: no progress for 5 s");
+        }
+    }
     return NEO_HIP_OK;
 }
 

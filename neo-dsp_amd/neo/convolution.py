@@ -301,6 +301,24 @@ class UpolsConvolver:
         slice launches of the step groups issued so far (device-side; no host wait)."""
         _native.check(_native.load().neo_hip_upols_join_background(self._h, ctypes.c_void_p(stream)))
 
+    def set_persistent(self, enable: bool, idle_ms: float = 50.0) -> None:
+        """Latency mode (neo_hip_upols_set_persistent): one persistent kernel steps every block;
+        every process call is then synchronous (complete on return, the stream is not used).
+        Raises for shapes it does not take (more than 256 partitions, 16 channels, B > 512)."""
+        _native.check(_native.load().neo_hip_upols_set_persistent(self._h, int(bool(enable)), float(idle_ms)))
+
+    def persistent_info(self) -> dict:
+        e, r, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+        _native.check(_native.load().neo_hip_upols_get_persistent(self._h, ctypes.byref(e), ctypes.byref(r),
+                                                                   ctypes.byref(n)))
+        return {"enabled": bool(e.value), "running": bool(r.value), "launches": n.value}
+
+    def persist_step_times(self, cap: int = 63):
+        """GPU time (us) of the last latency-mode steps, oldest first: record read -> done signal."""
+        buf, n = (ctypes.c_double * cap)(), ctypes.c_int64()
+        _native.check(_native.load().neo_hip_upols_persist_step_times(self._h, buf, cap, ctypes.byref(n)))
+        return list(buf[: n.value])
+
     # -- instrumentation ------------------------------------------------------
     def set_timing(self, enable, every: int = 1) -> None:
         """HIP events around every `every`-th MAC launch while enabled (bench instrumentation)."""

@@ -25,6 +25,7 @@ def count_step_bytes(C, B, P, nseg, G, K, form):
     else:
         fresh = 4 if G == 1 else 3
         far = (256 * (fresh + 2 * (nseg - 1) / K + K - 1) + 128) * row / 128
+        far += 2 * 256 * row / 128  # phase 1's partial sums: written, read back by phase 2
     return block, lv, far
 
 
@@ -46,11 +47,17 @@ def test_algorithmic_bytes_by_role(C, B, P, nseg, G, K, form):
 
 
 def test_headline_byte_totals():
-    """the per-step totals DESIGN.md quotes: c5full 605.6 MB (K = 3), the C5 shard 77.1 MB, C4 45.9 MB"""
-    tot = lambda *a: sum(bench.algorithmic_bytes(*a).values()) / 1e6
-    assert tot(2048, 512, 938, dict(PLAN, nseg=6), 4, 3, 1) == pytest.approx(605.6, abs=0.05)
-    assert tot(256, 512, 938, dict(PLAN, nseg=6), 4, 2, 1) == pytest.approx(77.1, abs=0.05)
-    assert tot(256, 256, 1875, dict(PLAN, nseg=13), 4, 2, 1) == pytest.approx(45.9, abs=0.05)
+    """the per-step totals DESIGN.md quotes, far partial sums included: c5full 639.2 MB (K = 3), the
+    C5 shard 81.3 MB, C4 48.0 MB (605.6 / 77.1 / 45.9 without them, round 3's count)"""
+    def tot(*a):
+        r = bench.algorithmic_bytes(*a)
+        return sum(v for k, v in r.items() if k != "far_partial_sums") / 1e6, r["far_partial_sums"] / 1e6
+    for args, full, partials in (((2048, 512, 938, dict(PLAN, nseg=6), 4, 3, 1), 639.2, 33.6),
+                                 ((256, 512, 938, dict(PLAN, nseg=6), 4, 2, 1), 81.3, 4.2),
+                                 ((256, 256, 1875, dict(PLAN, nseg=13), 4, 2, 1), 48.0, 2.1)):
+        t, p = tot(*args)
+        assert t == pytest.approx(full, abs=0.05) and p == pytest.approx(partials, abs=0.05)
+        assert t - p == pytest.approx({639.2: 605.6, 81.3: 77.1, 48.0: 45.9}[full], abs=0.05)
 
 
 def test_far_group_rule():

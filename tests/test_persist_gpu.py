@@ -1,0 +1,158 @@
+"""Latency mode (neo_hip_upols_set_persistent, upols_levels.hip k_lvl_persist): one persistent
+kernel per handle steps every block of a latency-bound shape (the reference's benchmark shape,
+extra/benchmark/src/convolution.cpp:34-44: one channel, one call per block). Outputs must equal
+the oracle's dense_convolve (uniform_partitioned_convolver.hpp:47-65) and the normal streaming
+step's bit for bit; the mode survives idle timeouts (relaunch) and hands back to the normal
+schedule (re-prime) when switched off."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from conftest import peak_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _pair(neo_gpu, oracle, C, B, P, seed, method="upols"):
+    ir = np.stack([oracle.noise(seed + c, B * P) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    convs = []
+    for _ in range(2):
+        c = neo_gpu.UpolsConvolver(C, B, P, method=method)
+        c.filter(parts)
+        c.set_batch(False)
+        convs.append(c)
+    return convs, parts
+
+
+def _run(conv, x, B, torch, per_call=1):
+    """x [C][N] through conv, per_call blocks per process call, device-resident, in place"""
+    t = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    torch.cuda.synchronize()
+    nb = x.shape[1] // B
+    stream = torch.cuda.current_stream().cuda_stream
+    for i in range(0, nb, per_call):
+        k = min(per_call, nb - i)
+        conv.process_blocks_ptr(t.data_ptr() + 4 * i * B, t.data_ptr() + 4 * i * B, x.shape[1], k, stream)
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def test_c3_latency_mode_golden_and_oracle(neo_gpu, oracle):
+    """configs[2] at its exact shape (B = 512, L = 96000, P = 188, 1 channel): the golden
+    fixture's 200 blocks one call per block, then 640 blocks of fresh noise against the oracle
+    and against the normal streaming step (bit for bit)."""
+    torch = pytest.importorskip("torch")
+    g = np.load(os.path.join(GOLD, "upols_b512_l96000_seed7.npz"))
+    B = 512
+    P = neo_gpu.num_partitions(g["ir"].shape[-1], B)
+    conv = neo_gpu.UpolsConvolver(1, B, P)
+    conv.set_impulse(np.atleast_2d(g["ir"]), normalize=True)
+    conv.set_batch(False)
+    conv.set_persistent(True)
+    assert conv.persistent_info()["enabled"]
+    sig = np.atleast_2d(g["signal"]).astype(np.float32)
+    nb = sig.shape[1] // B
+    got = _run(conv, sig[:, : nb * B], B, torch)
+    out = np.atleast_2d(g["out"])[:, : nb * B]
+    assert peak_err(got, out) <= TOL
+    assert np.abs(got - out).max() <= 1e-5
+    info = conv.persistent_info()
+    assert info["launches"] >= 1 and info["running"], info
+    st = conv.persist_step_times()
+    assert len(st) == 63 and all(0 < s < 1000 for s in st), st[:4]
+    # fresh noise vs the oracle and vs the normal step
+    conv.reset()
+    conv.set_persistent(True)
+    nb2 = 640
+    x = np.stack([oracle.noise(4243, B * nb2)])
+    irn = oracle.normalize_impulse(np.atleast_2d(g["ir"]).astype(np.float32))
+    ref = oracle.dense_convolve(x, oracle.uniform_partition(irn, B))
+    got = _run(conv, x, B, torch, per_call=4)
+    assert peak_err(got, ref) <= TOL
+    normal = neo_gpu.UpolsConvolver(1, B, P)
+    normal.set_impulse(np.atleast_2d(g["ir"]), normalize=True)
+    normal.set_batch(False)
+    assert np.array_equal(got, _run(normal, x, B, torch))
+    conv.close()
+    normal.close()
+
+
+@pytest.mark.parametrize("method,C,B,P", [("upols", 4, 256, 100), ("upola", 3, 128, 240), ("upols", 16, 64, 200)])
+def test_latency_mode_channels_methods(neo_gpu, oracle, method, C, B, P):
+    """several channels (one block workgroup each, the last to finish signals), OLA, small
+    blocks: oracle (the OLS restatement for upols; for upola the same bit-equality with the
+    normal step, which the streaming tests pin to the oracle) and the normal step bit for bit."""
+    torch = pytest.importorskip("torch")
+    (pc, nc), parts = _pair(neo_gpu, oracle, C, B, P, 5000 + C, method)
+    pc.set_persistent(True)
+    nb = 3 * P // 2 + 37
+    x = np.stack([oracle.noise(5100 + c, B * nb) for c in range(C)])
+    got = _run(pc, x, B, torch, per_call=3)
+    assert np.array_equal(got, _run(nc, x, B, torch))
+    if method == "upols":
+        assert peak_err(got, oracle.dense_convolve(x, parts)) <= TOL
+
+
+def test_latency_mode_idle_relaunch_and_handback(neo_gpu, oracle):
+    """idle_ms = 5: the kernel leaves between bursts and the next call relaunches it (state
+    kept); switched off mid-stream, the normal schedule re-primes and continues; both stay
+    bit-equal to a handle that never left the normal step."""
+    torch = pytest.importorskip("torch")
+    C, B, P = 2, 256, 150
+    (pc, nc), parts = _pair(neo_gpu, oracle, C, B, P, 5300)
+    pc.set_persistent(True, idle_ms=5.0)
+    nb = 400
+    x = np.stack([oracle.noise(5400 + c, B * nb) for c in range(C)])
+    t = torch.from_numpy(x.copy()).cuda()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    for i in range(nb):
+        if i in (100, 101, 250):
+            time.sleep(0.03)  # past the idle limit
+        if i == 300:
+            pc.set_persistent(False)  # hand back: the normal step re-primes
+        pc.process_blocks_ptr(t.data_ptr() + 4 * i * B, t.data_ptr() + 4 * i * B, x.shape[1], 1, stream)
+    torch.cuda.synchronize()
+    got = t.cpu().numpy()
+    assert pc.persistent_info()["launches"] >= 4
+    assert np.array_equal(got, _run(nc, x, B, torch))
+    assert peak_err(got, oracle.dense_convolve(x, parts)) <= TOL
+
+
+def test_latency_mode_host_buffers(neo_gpu, oracle):
+    """the plugin's call (neo_hip_upols_process on a host block, in place) in latency mode:
+    page-locked (read and written in place by the kernel) and pageable (the handle's staging)."""
+    torch = pytest.importorskip("torch")
+    C, B, P = 1, 512, 188
+    (pc, nc), parts = _pair(neo_gpu, oracle, C, B, P, 5500)
+    pc.set_persistent(True)
+    nb = 300
+    x = np.stack([oracle.noise(5600, B * nb)])
+    pinned = torch.empty((C, B), dtype=torch.float32).pin_memory().numpy()
+    y = np.empty_like(x)
+    for i in range(nb):
+        blk = x[:, i * B:(i + 1) * B]
+        if i % 2:
+            pinned[:] = blk
+            pc(pinned)
+            y[:, i * B:(i + 1) * B] = pinned
+        else:
+            b = blk.copy()
+            pc(b)
+            y[:, i * B:(i + 1) * B] = b
+    assert np.array_equal(y, _run(nc, x, B, torch))
+
+
+def test_latency_mode_rejects_other_shapes(neo_gpu):
+    """far level (> 256 partitions), more than 16 channels, B > 512, sub-block v2: EINVAL"""
+    for args, kw in (((1, 512, 300), {}), ((32, 128, 100), {}), ((1, 1024, 100), {}),
+                     ((1, 256, 100), {"method": "upola_v2"})):
+        c = neo_gpu.UpolsConvolver(*args, **kw)
+        with pytest.raises(RuntimeError, match="latency mode"):
+            c.set_persistent(True)
+        c.close()
