@@ -439,6 +439,28 @@ def host_io_times(conv, C, B, nblocks, kind, seed=0):
     return dt
 
 
+def group_frames(C, frames, B, L):
+    """tests/cpp/bench_group (C++, NEO_HIP_CONVOLVER_GROUPS): the plugin's processFrame over C
+    single-channel convolvers of one owner-registered frame buffer (one launch per frame once
+    coalesced), and the dense_convolve<Convolver> harness pattern (one shared scratch block: one
+    launch and one host wait per channel-block). Host memory, PCIe-inclusive; None if the binary
+    cannot be built here."""
+    import subprocess
+
+    cpp = os.path.join(REPO, "tests", "cpp")
+    exe = os.path.join(cpp, "bin", "bench_group")
+    try:
+        subprocess.run(["make", "-s", "-C", cpp, "bin/bench_group"], check=True, capture_output=True, timeout=300)
+        r = subprocess.run([exe, str(C), str(frames), str(B), str(L)], capture_output=True, text=True, timeout=600)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except (OSError, subprocess.SubprocessError, ValueError, IndexError) as e:
+        return {"error": str(e)[:200]}
+    d["note"] = ("tests/cpp/bench_group: per frame = C calls of upols_convolver::operator() on the owner's "
+                 "registered frame buffer (DenseConvolution.cpp:62-74); shared_scratch = the "
+                 "dense_convolve<Convolver> harness (DenseConvolution.hpp:56-67), per channel-block")
+    return d
+
+
 def host_io_summary(dt, C, B):
     import numpy as np
 
@@ -728,6 +750,11 @@ def run_upols(args, world, rank, local):
         for kind in ("pinned", "pageable"):
             host_io[f"c5_{kind}"] = host_io_summary(host_io_times(c5, cs, B, 200, kind), cs, B)
         c5.close()
+        del c5
+        torch.cuda.empty_cache()
+        # the plugin's std::vector<upols_convolver> (group-backed alias, C++) at 256 and 2048 channels
+        for cs_, nf_ in ((256, 64), (2048, 16)):
+            host_io[f"group_{cs_}"] = group_frames(cs_, nf_, B, L)
     weak = None
     if world > 1 and args.workload in STRONG and not args.no_weak:
         conv.close()

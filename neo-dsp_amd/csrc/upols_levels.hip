@@ -2061,7 +2061,7 @@ struct persist_args {
     int64_t n0;                     // first step of this launch (levels primed at step 0)
     int w0;                         // its ring row
     persist_mb* mb;                 // the mapped mailbox (device address)
-    int64_t* flags;                 // [0] blk_done, [1] quit, [2] arrive, [3 + s] sl_done of slice workgroup s
+    int64_t* flags;                 // blk_done, quit, arrivals, records, sl_done (kPsFlag*)
     unsigned long long* tl;         // [kPsRing][2] record seen / done
     long long idle_ticks, dead_ticks;
 };
@@ -2103,6 +2103,14 @@ __device__ __forceinline__ void ps_acquire()
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// device flags of the persistent kernel (int64 words): blk_done, quit, the per-step arrival
+// counters of the block workgroups (a ring: a channel may run up to three steps ahead of another),
+// the last step whose record block workgroup 0 handed on and those records (a ring), then
+// sl_done per slice workgroup
+constexpr int kPsArr = 8;
+constexpr int kPsFlagArrive = 2, kPsFlagGo = kPsFlagArrive + kPsArr, kPsFlagIo = kPsFlagGo + 1;
+constexpr int kPsFlagSlices = kPsFlagIo + 2 * kPsArr;
+
 template<int B, bool OLA>
 __device__ __forceinline__ void persist_block(const persist_args& pa, int c, char* smem)
 {
@@ -2114,29 +2122,47 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
             // the window's slabs: every slice workgroup past step n - 2
             bool ok = ps_wait(pa, [&] {
                 for (int s = 0; s < nsl; ++s)
-                    if (ps_ld(pa.flags + 3 + s) < n - 2) return false;
+                    if (ps_ld(pa.flags + kPsFlagSlices + s) < n - 2) return false;
                 return true;
             });
             if (ok) ps_acquire();
-            // the record of step n (both words tagged with its lap), the host's stop, the idle limit
             const int slot = int(n % kPsRing);
-            const uint64_t tag = ps_tag(n);
-            const unsigned long long t0 = wall_clock64();
-            while (ok) {
-                const uint64_t r0 = __hip_atomic_load(&pa.mb->rec[slot].in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const uint64_t r1 = __hip_atomic_load(&pa.mb->rec[slot].out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if ((r0 & 15) == tag && (r1 & 15) == tag) {
-                    io[0] = r0 & ~uint64_t(15);
-                    io[1] = r1 & ~uint64_t(15);
-                    __hip_atomic_store(pa.tl + 2 * slot, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
+            if (c == 0) {
+                // the record of step n (both words tagged with its lap), the host's stop, the idle
+                // limit; workgroup 0 alone decides, the other channels take the record from it
+                const uint64_t tag = ps_tag(n);
+                const unsigned long long t0 = wall_clock64();
+                while (ok) {
+                    const uint64_t r0 = __hip_atomic_load(&pa.mb->rec[slot].in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    const uint64_t r1 = __hip_atomic_load(&pa.mb->rec[slot].out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if ((r0 & 15) == tag && (r1 & 15) == tag) {
+                        io[0] = r0 & ~uint64_t(15);
+                        io[1] = r1 & ~uint64_t(15);
+                        __hip_atomic_store(pa.tl + 2 * slot, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if (pa.nblk > 1) {
+                            int64_t* r = pa.flags + kPsFlagIo + 2 * (n % kPsArr);
+                            ps_st(r, int64_t(io[0]));
+                            ps_st(r + 1, int64_t(io[1]));
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                            ps_st(pa.flags + kPsFlagGo, n);
+                        }
+                        break;
+                    }
+                    if (__hip_atomic_load(&pa.mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                        ps_ld(pa.flags + 1) || (long long)(wall_clock64() - t0) > pa.idle_ticks) {
+                        ok = false;
+                        ps_st(pa.flags + 1, 1);
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                if (__hip_atomic_load(&pa.mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) || ps_ld(pa.flags + 1) ||
-                    (long long)(wall_clock64() - t0) > pa.idle_ticks) {
-                    ok = false;
-                    ps_st(pa.flags + 1, 1);
+            } else if (ok) {
+                ok = ps_wait(pa, [&] { return ps_ld(pa.flags + kPsFlagGo) >= n; });
+                if (ok) {
+                    ps_acquire();
+                    const int64_t* r = pa.flags + kPsFlagIo + 2 * (n % kPsArr);
+                    io[0] = uint64_t(ps_ld(r));
+                    io[1] = uint64_t(ps_ld(r + 1));
                 }
-                __builtin_amdgcn_s_sleep(1);
             }
             go = ok;
         }
@@ -2162,8 +2188,10 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the output reaches the host's view
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int64_t prev = __hip_atomic_fetch_add(pa.flags + 2, int64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev == (n - pa.n0 + 1) * pa.nblk - 1) {  // the last channel of step n
+            int64_t* arr = pa.flags + kPsFlagArrive + n % kPsArr;
+            const int64_t prev = __hip_atomic_fetch_add(arr, int64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == pa.nblk - 1) {  // the last channel of step n
+                ps_st(arr, 0);          // free for step n + kPsArr (no channel gets there before blk_done moves on)
                 ps_st(pa.flags + 0, n);
                 __hip_atomic_store(pa.tl + 2 * (n % kPsRing) + 1, wall_clock64(), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2225,7 +2253,7 @@ __device__ __forceinline__ void persist_slices(const persist_args& pa, int s, ch
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            ps_st(pa.flags + 3 + s, n);
+            ps_st(pa.flags + kPsFlagSlices + s, n);
         }
     }
 }
@@ -2302,7 +2330,7 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     if (h->ps_nslices < nsl || !h->ps_flags) {
         (void)hipFree(h->ps_flags);
         h->ps_flags = nullptr;
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_flags), size_t(3 + nsl) * sizeof(int64_t)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_flags), size_t(kPsFlagSlices + nsl) * sizeof(int64_t)));
         h->ps_nslices = nsl;
     }
     pa.n0 = h->lv_n;
@@ -2312,10 +2340,10 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     pa.tl = h->ps_tl;
     pa.idle_ticks = (long long)(h->ps_idle_ms * 1e5);  // wall_clock64: 100 MHz
     pa.dead_ticks = 200000000LL;                        // 2 s: a wait that long is a fault, not a schedule
-    std::vector<int64_t> init(size_t(3 + nsl), pa.n0 - 2);
-    init[0] = pa.n0 - 1;
-    init[1] = 0;
-    init[2] = 0;
+    std::vector<int64_t> init(size_t(kPsFlagSlices + nsl), 0);  // quit, arrivals, records: 0
+    init[0] = pa.n0 - 1;                                          // blk_done
+    init[kPsFlagGo] = pa.n0 - 1;
+    for (int k = 0; k < nsl; ++k) init[size_t(kPsFlagSlices + k)] = pa.n0 - 2;  // sl_done
     NEO_HIP_CHECK(hipMemcpyAsync(h->ps_flags, init.data(), init.size() * sizeof(int64_t), hipMemcpyHostToDevice,
                                  h->ps_stream));
     NEO_HIP_CHECK(hipStreamSynchronize(h->ps_stream));  // the prime and the flags before the first record
@@ -2368,11 +2396,11 @@ int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int6
     if (const char* why = persist_ineligible(h)) return fail(NEO_HIP_EINVAL, "latency mode: %s", why);
     if (h->C > 1 && (ld_in != h->ps_ld_in || ld_out != h->ps_ld_out) && h->ps_running)
         if (int rc = persist_join(h)) return rc;  // another channel stride: relaunch with it
-    persist_mb* mb = h->ps_mb;
-    if (h->ps_running && !__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE))
+    if (h->ps_running && !__atomic_load_n(&h->ps_mb->alive, __ATOMIC_ACQUIRE))
         if (int rc = persist_join(h)) return rc;  // left after its idle limit (or failed)
     if (!h->ps_running)
         if (int rc = persist_launch(h, ld_in, ld_out)) return rc;
+    persist_mb* mb = h->ps_mb;  // allocated by the first launch
     const int B = h->B;
     for (int64_t k = 0; k < nblocks; ++k) {
         const int64_t n = h->lv_n;
