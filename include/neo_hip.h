@@ -53,6 +53,9 @@ typedef struct neo_hip_fft_plan neo_hip_fft_plan;
 typedef struct neo_hip_upols neo_hip_upols;
 
 /* -- library ------------------------------------------------------------ */
+/* ABI version of this header. neo_hip_upols_opts grows with it (0.1.0: 6 ints; 0.2.0: the 10
+ * below), so a caller checks neo_hip_version() == NEO_HIP_VERSION before passing one. */
+#define NEO_HIP_VERSION 200 /* 0.2.0 */
 NEO_HIP_API const char* neo_hip_last_error(void);
 NEO_HIP_API int neo_hip_version(void);
 NEO_HIP_API int neo_hip_device_count(int* count);
@@ -193,8 +196,8 @@ NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, 
  * on return; the stream argument is not used) and device inputs must be ready when it is made.
  * The kernel leaves after idle_ms without a block (the next call relaunches it) and whenever a
  * setup call (set_filter, set_impulse, reset, set_ahead, set_persistent(0), destroy) runs.
- * Outputs equal the normal streaming step's (the same sums; the levels re-prime on entry and
- * exit, bit for bit). Not available: EINVAL names the reason. */
+ * Outputs equal the normal streaming step's to float rounding (the same sums in the same order;
+ * the levels re-prime on entry and exit). Not available: EINVAL names the reason. */
 NEO_HIP_API int neo_hip_upols_set_persistent(neo_hip_upols* h, int enable, double idle_ms);
 /* requested, kernel resident now, persistent launches so far */
 NEO_HIP_API int neo_hip_upols_get_persistent(neo_hip_upols* h, int* enabled, int* running, int64_t* launches);

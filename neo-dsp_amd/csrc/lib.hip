@@ -13,7 +13,7 @@ extern "C" {
 
 NEO_HIP_API const char* neo_hip_last_error(void) { return neo_hip::last_error_slot().c_str(); }
 
-NEO_HIP_API int neo_hip_version(void) { return 100; /* 0.1.0 */ }
+NEO_HIP_API int neo_hip_version(void) { return NEO_HIP_VERSION; }
 
 NEO_HIP_API int neo_hip_device_count(int* count)
 {

@@ -120,7 +120,16 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
 // E = 4 keeps the fused kernel inside its 64-VGPR budget (T = B/E <= 256 lanes).
 // WS = true: run by one wave (T <= 64 lanes), no workgroup barriers.
 // JOINED = true: X already holds the joined c2r input Z[k] (c2r_join applied by the caller).
-template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256), bool WS = false, bool JOINED = false>
+// WT = true: the output block is stored write-through at system scope (the latency mode hands it
+// to the host after s_waitcnt alone, no L2 write-back on its path)
+__device__ __forceinline__ void st_out(cf* p, cf v, bool wt)
+{
+    if (wt) __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else *p = v;
+}
+
+template<int B, bool OLA, int E = (B / 4 <= 256 ? 4 : B / 256), bool WS = false, bool JOINED = false, bool WT = false>
 __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, float* out_c, float* ovl_c, int tid)
 {
     using K = upols_cfg<B>;
@@ -152,7 +161,7 @@ __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, flo
             for (int m = 0; m < E / 2; ++m) {
                 const int n = tid + m * T;
                 const cf old = ov[n];
-                o[n] = {v[m].x * scale + old.x, v[m].y * scale + old.y};
+                st_out(o + n, cf{v[m].x * scale + old.x, v[m].y * scale + old.y}, WT);
             }
 #pragma unroll
             for (int m = E / 2; m < E; ++m) {
@@ -163,7 +172,7 @@ __device__ __forceinline__ void c2r_tail(const cf* X, cf* fft, const cf* tw, flo
 #pragma unroll
             for (int m = E / 2; m < E; ++m) {  // window samples [B, 2B): z[n], n >= B/2
                 const int n = tid + m * T;
-                o[n - B / 2] = {v[m].x * scale, v[m].y * scale};
+                st_out(o + n - B / 2, cf{v[m].x * scale, v[m].y * scale}, WT);
             }
         }
     }

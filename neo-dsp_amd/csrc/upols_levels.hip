@@ -46,6 +46,18 @@ namespace neo_hip {
     do {               \
     } while (0)
 #endif
+// latency-mode probe builds (NEO_PS_PROBE): thread 0 stamps point i of the block role into a.tl
+#ifdef NEO_PS_PROBE
+#define NEO_PS_MARK(a, i)                                                                              \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && (a).tl)                                                                \
+            static_cast<unsigned long long*>((a).tl)[i] = wall_clock64(); /* plain: no wait added */  \
+    } while (0)
+#else
+#define NEO_PS_MARK(a, i) \
+    do {                  \
+    } while (0)
+#endif
 
 
 // ---------------------------------------------------------------------------------------
@@ -226,7 +238,7 @@ __device__ __forceinline__ void cmac(cf& y, cf h, cf x, bool bin0)
     }
 }
 
-template<int B, bool OLA>
+template<int B, bool OLA, bool WT = false>
 __device__ __forceinline__ void block_role(const slice_args& a, int c, char* smem)
 {
     using K = upols_cfg<B>;
@@ -252,11 +264,19 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
         if (tid < TW) {
             const cf* pz = reinterpret_cast<const cf*>(prev_c);
             const cf* iz = reinterpret_cast<const cf*>(in_c);
+            // WT (latency mode): the caller's block read at system scope, past every cache (another
+            // kernel or the host may have rewritten it since this persistent kernel last read there)
+            auto in_ld = [&](int i) {
+                if constexpr (WT)
+                    return __builtin_bit_cast(cf, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(iz + i),
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                else return iz[i];
+            };
 #pragma unroll
             for (int m = 0; m < EW; ++m) {
                 const int n = tid + m * TW;
-                if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
-                else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+                if constexpr (OLA) v[m] = n < B / 2 ? in_ld(n) : cf{0.f, 0.f};
+                else v[m] = n < B / 2 ? pz[n] : in_ld(n - B / 2);
             }
         }
     }
@@ -299,7 +319,9 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
         }
         twr.store(tw, tid);
         wave_sync();
+        NEO_PS_MARK(a, 1);  // wave 0 issued its loads and stored the previous block
         stockham<B, EW, -1, 1, true>(v, fft, tw, tid, tid < TW);
+        NEO_PS_MARK(a, 2);  // r2c done (the window's loads had landed)
         if (tid < TW) {
 #pragma unroll
             for (int m = 0; m < EW; ++m) fft[lpad(tid + m * TW)] = v[m];
@@ -327,6 +349,7 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
     }
     __syncthreads();
     NEO_TL_MARK(a);
+    NEO_PS_MARK(a, 3);  // every pair lane's loads landed
     if (pair) {
         // bin pair (k0, k1): r2c split, FDL row w, Y = rest + H0 X, c2r join; w(B - k) = -conj(w(k))
         const cf wa = k0 == 0 ? cf{1.f, 0.f} : twiddle<2 * B, -1>(tw + K::TW1, k0);
@@ -343,7 +366,9 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
         X[k1] = c2r_join_w<B>(yb, k0 == 0 ? yb : ya, cf{wb.x, -wb.y}, k1);
     }
     __syncthreads();
-    if (tid < 64) c2r_tail<B, OLA, EW, true, true>(X, fft, tw, a.out + int64_t(c) * a.ld_out, prev_c, tid);
+    NEO_PS_MARK(a, 4);  // joined spectrum in LDS
+    if (tid < 64) c2r_tail<B, OLA, EW, true, true, WT>(X, fft, tw, a.out + int64_t(c) * a.ld_out, prev_c, tid);
+    NEO_PS_MARK(a, 5);  // output stores issued
 }
 
 // buffer loads / stores: 32-bit lane offsets, uniform offsets in SGPRs (fewer VGPRs than
@@ -2055,7 +2080,7 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
 struct persist_args {
     slice_args base;                // handle constants (H, FDL, ring, strides, prev, twiddles, a0)
     cf* slab[kLvToep];
-    int T[kLvToep], A[kLvToep], Bd[kLvToep], JH[kLvToep], UPW[kLvToep], U[kLvToep];
+    int T[kLvToep], LT[kLvToep], A[kLvToep], Bd[kLvToep], JH[kLvToep], UPW[kLvToep], U[kLvToep];  // LT = log2 T
     int wg0[kLvToep + 1];           // slice workgroups of level l: [wg0[l], wg0[l + 1])
     int nlev, nblk;
     int64_t n0;                     // first step of this launch (levels primed at step 0)
@@ -2108,7 +2133,8 @@ __device__ __forceinline__ void ps_acquire()
 // the last step whose record block workgroup 0 handed on and those records (a ring), then
 // sl_done per slice workgroup
 constexpr int kPsArr = 8;
-constexpr int kPsFlagArrive = 2, kPsFlagGo = kPsFlagArrive + kPsArr, kPsFlagIo = kPsFlagGo + 1;
+constexpr int kPsFlagArrive = 2, kPsFlagArriveFdl = kPsFlagArrive + kPsArr, kPsFlagGo = kPsFlagArriveFdl + kPsArr;
+constexpr int kPsFlagIo = kPsFlagGo + 1;
 constexpr int kPsFlagSlices = kPsFlagIo + 2 * kPsArr;
 
 template<int B, bool OLA>
@@ -2117,7 +2143,22 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
     __shared__ uint64_t io[2];
     __shared__ int go;
     const int nsl = pa.wg0[pa.nlev];
-    for (int64_t n = pa.n0;; ++n) {
+    unsigned long long t_seen = 0;  // thread 0: when the record of the step was read (stored with its done time)
+    int w = pa.w0;                  // ring row of step n
+    for (int64_t n = pa.n0;; ++n, w = w + 1 == pa.base.ring ? 0 : w + 1) {
+        // the step's arguments but its blocks, while thread 0 waits (T are powers of two)
+        slice_args a = pa.base;
+        a.w = w;
+        a.nsl = pa.nlev;
+        a.ff = nullptr;
+#pragma unroll
+        for (int l = 0; l < kLvToep; ++l) {  // static indices: the slice_args stay in registers
+            if (l < pa.nlev) {
+                const int T = pa.T[l];
+                a.sl[l] = pa.slab[l] + (((n >> pa.LT[l]) & 1) * a.C * T + (n & (T - 1))) * a.B;
+                a.scs[l] = int64_t(T) * a.B;
+            }
+        }
         if (threadIdx.x == 0) {
             // the window's slabs: every slice workgroup past step n - 2
             bool ok = ps_wait(pa, [&] {
@@ -2125,20 +2166,23 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
                     if (ps_ld(pa.flags + kPsFlagSlices + s) < n - 2) return false;
                 return true;
             });
-            if (ok) ps_acquire();
+            // a window of some level starts (every level's T is a multiple of the first's): its slab
+            // rows were written by other workgroups since this CU last read that buffer
+            if (ok && (n == pa.n0 || (n & (pa.T[0] - 1)) == 0)) ps_acquire();
             const int slot = int(n % kPsRing);
             if (c == 0) {
-                // the record of step n (both words tagged with its lap), the host's stop, the idle
-                // limit; workgroup 0 alone decides, the other channels take the record from it
+                // the record of step n (both words tagged with its lap); the host's stop, quit and
+                // the idle limit checked every 16th poll; workgroup 0 alone decides, the other
+                // channels take the record from it
                 const uint64_t tag = ps_tag(n);
                 const unsigned long long t0 = wall_clock64();
-                while (ok) {
+                for (unsigned it = 0; ok; ++it) {
                     const uint64_t r0 = __hip_atomic_load(&pa.mb->rec[slot].in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     const uint64_t r1 = __hip_atomic_load(&pa.mb->rec[slot].out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if ((r0 & 15) == tag && (r1 & 15) == tag) {
                         io[0] = r0 & ~uint64_t(15);
                         io[1] = r1 & ~uint64_t(15);
-                        __hip_atomic_store(pa.tl + 2 * slot, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        t_seen = wall_clock64();
                         if (pa.nblk > 1) {
                             int64_t* r = pa.flags + kPsFlagIo + 2 * (n % kPsArr);
                             ps_st(r, int64_t(io[0]));
@@ -2148,12 +2192,12 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
                         }
                         break;
                     }
-                    if (__hip_atomic_load(&pa.mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                        ps_ld(pa.flags + 1) || (long long)(wall_clock64() - t0) > pa.idle_ticks) {
+                    if ((it & 15) == 15 &&
+                        (__hip_atomic_load(&pa.mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                         ps_ld(pa.flags + 1) || (long long)(wall_clock64() - t0) > pa.idle_ticks)) {
                         ok = false;
                         ps_st(pa.flags + 1, 1);
                     }
-                    __builtin_amdgcn_s_sleep(1);
                 }
             } else if (ok) {
                 ok = ps_wait(pa, [&] { return ps_ld(pa.flags + kPsFlagGo) >= n; });
@@ -2168,34 +2212,32 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
         }
         __syncthreads();
         if (!go) break;
-        slice_args a = pa.base;
         a.in = reinterpret_cast<const float*>(io[0]);
         a.out = reinterpret_cast<float*>(io[1]);
-        a.w = ps_ring_row(pa, n);
-        a.nsl = pa.nlev;
-        a.ff = nullptr;
-#pragma unroll
-        for (int l = 0; l < kLvToep; ++l) {  // static indices: the slice_args stay in registers
-            if (l < pa.nlev) {
-                const int T = pa.T[l];
-                a.sl[l] = pa.slab[l] + (((n / T) & 1) * a.C * T + n % T) * a.B;
-                a.scs[l] = int64_t(T) * a.B;
-            }
-        }
-        block_role<B, OLA>(a, c, smem);
+#ifdef NEO_PS_PROBE
+        a.tl = pa.tl + 2 * kPsRing + 8 * (n % kPsRing);  // probe records [kPsRing][8] after the step times
+        NEO_PS_MARK(a, 0);
+#endif
+        block_role<B, OLA, true>(a, c, smem);  // the output block write-through (system scope)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the output reaches the host's view
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // 1. the output: its write-through stores are complete, so the host may read it now
             int64_t* arr = pa.flags + kPsFlagArrive + n % kPsArr;
-            const int64_t prev = __hip_atomic_fetch_add(arr, int64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev == pa.nblk - 1) {  // the last channel of step n
-                ps_st(arr, 0);          // free for step n + kPsArr (no channel gets there before blk_done moves on)
-                ps_st(pa.flags + 0, n);
-                __hip_atomic_store(pa.tl + 2 * (n % kPsRing) + 1, wall_clock64(), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            if (__hip_atomic_fetch_add(arr, int64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pa.nblk - 1) {
+                ps_st(arr, 0);  // free for step n + kPsArr (no channel gets there before blk_done moves on)
+                const unsigned long long t_done = wall_clock64();
                 __hip_atomic_store(&pa.mb->done, n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                pa.tl[2 * (n % kPsRing) + 1] = t_done;  // plain: written back by the release below
+            }
+            if (c == 0) pa.tl[2 * (n % kPsRing)] = t_seen;  // workgroup 0 read the record
+            // 2. the FDL row for the slice workgroups (off the host's path): agent release, blk_done
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            int64_t* arf = pa.flags + kPsFlagArriveFdl + n % kPsArr;
+            if (__hip_atomic_fetch_add(arf, int64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pa.nblk - 1) {
+                ps_st(arf, 0);
+                ps_st(pa.flags + 0, n);
             }
         }
     }
@@ -2298,8 +2340,8 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
                                     hipHostMallocMapped | hipHostMallocCoherent));
         NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->ps_mb_dev), h->ps_mb, 0));
         std::memset(h->ps_mb, 0, sizeof(persist_mb));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_tl), 2 * kPsRing * sizeof(unsigned long long)));
-        NEO_HIP_CHECK(hipMemset(h->ps_tl, 0, 2 * kPsRing * sizeof(unsigned long long)));
+        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_tl), 10 * kPsRing * sizeof(unsigned long long)));
+        NEO_HIP_CHECK(hipMemset(h->ps_tl, 0, 10 * kPsRing * sizeof(unsigned long long)));
     }
     if (int rc = lvl_buffers(h)) return rc;
     if (!h->ps_valid || h->lv_n < 0) {  // window 0 of every level, from this block on
@@ -2322,6 +2364,7 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     for (int l = 0; l < h->lv.n; ++l) {
         pa.slab[l] = h->lv_slab[l];
         pa.T[l] = h->lv.T[l];
+        pa.LT[l] = __builtin_ctz(unsigned(h->lv.T[l]));
         pa.A[l] = h->lv.a[l];
         pa.Bd[l] = h->lv.b[l];
         pa.wg0[l + 1] = pa.wg0[l] + persist_level_wgs(h, l, pa.U[l], pa.UPW[l], pa.JH[l]);
@@ -2484,6 +2527,17 @@ extern "C" NEO_HIP_API int neo_hip_upols_join_background(neo_hip_upols* h, void*
     if (g.rc) return g.rc;
     return neo_hip::lvl_join(h, static_cast<hipStream_t>(stream));
 }
+
+#ifdef NEO_PS_PROBE
+// diagnostic builds only (not in include/neo_hip.h): the latency mode's per-step probe records,
+// [kPsRing][2] {seen, done} then [kPsRing][8] block-role points (wall clock, 100 MHz)
+extern "C" NEO_HIP_API int neo_hip_diag_persist_probe(neo_hip_upols* h, unsigned long long* out)
+{
+    if (!h || !h->ps_tl) return neo_hip::fail(NEO_HIP_EINVAL, "no latency-mode records");
+    NEO_HIP_CHECK(hipMemcpy(out, h->ps_tl, 10 * neo_hip::kPsRing * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return NEO_HIP_OK;
+}
+#endif
 
 #ifdef NEO_TIMELINE
 // diagnostic builds only (not in include/neo_hip.h): copy the last step launch's per-workgroup

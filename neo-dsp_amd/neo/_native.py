@@ -108,6 +108,7 @@ SIGNATURES = {
     "neo_hip_stft_f64": (_i, [_vp, _i, _i64, _i, _i, _i, _vp, _vp, _i, _i]),
 }
 
+ABI_VERSION = 200  # include/neo_hip.h NEO_HIP_VERSION
 _lib = None
 _lock = threading.Lock()
 
@@ -138,6 +139,9 @@ def load(path: str = LIB_PATH):
                     f"{path} not found: build the HIP library first (make -C neo-dsp_amd); "
                     "there is no CPU fallback")
             lib = ctypes.CDLL(path)
+            lib.neo_hip_version.restype = ctypes.c_int
+            if lib.neo_hip_version() != ABI_VERSION:  # neo_hip_upols_opts' layout is tied to it
+                raise ImportError(f"{path}: ABI version {lib.neo_hip_version()}, these bindings need {ABI_VERSION}")
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)
                 fn.restype = res

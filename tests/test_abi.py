@@ -50,7 +50,9 @@ def test_host_validation_without_gpu():
     assert lib.neo_hip_upols_join_background(None, None) == neo._native.NEO_HIP_EINVAL
     assert lib.neo_hip_upols_get_far_form(None, None) == neo._native.NEO_HIP_EINVAL
     assert lib.neo_hip_fft_max_order() == 27
-    assert lib.neo_hip_version() >= 100
+    hdr = open(os.path.join(REPO, "include", "neo_hip.h")).read()
+    assert lib.neo_hip_version() == int(re.search(r"#define NEO_HIP_VERSION (\d+)", hdr).group(1))
+    assert neo._native.ABI_VERSION == lib.neo_hip_version()
     with pytest.raises(neo._native.NeoHipError):
         neo.fft.FFTPlan(0, 28)
 
