@@ -2036,8 +2036,11 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
         // previous background launch finished. So one cross-stream wait per 2 G steps each way
         // (each costs the waiting queue ~10 us of idle time on MI355X, kernel traces).
         const bool odd = (n / G) & 1;
+#ifndef NEO_NO_XWAIT
+#define NEO_NO_XWAIT 0  // diagnostic builds (timing only, outputs wrong): 1 drops both cross-stream waits
+#endif
         if (primed) NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the priming launches
-        if (odd || primed) NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
+        if ((odd && !NEO_NO_XWAIT) || primed) NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
         slice_args b = base_args(h);
         slice_part(h, n, h->wpos, b);
         upols_t::ev_group* eb = nullptr;  // timed when it launches (the first group after a window start may be empty)
@@ -2051,7 +2054,7 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
             NEO_HIP_CHECK(hipEventRecord(h->ev_sl[0], h->bg));  // due at the next even group's block
         } else {
             NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the blocks before n: the next odd group's launch
-            if (!primed) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_sl[0], 0));
+            if (!primed && !NEO_NO_XWAIT) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_sl[0], 0));
         }
     }
     upols_t::ev_group* ev = nullptr;  // the step's (block's) launch alone
