@@ -188,6 +188,12 @@ NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* pha
  * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries); the automatic
  * choice of far_level. */
 NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, int* T, int* a, int* b, int* nseg);
+/* Paced background work (step groups only; a no-op with one launch per block): the step group's
+ * background launch is issued in G pieces, one per call, and every block waits for the piece of
+ * the call before it, so no call waits for more than one piece of background work: the host round
+ * trip per block is even (p99 near p50) instead of one call in 2 G paying for two groups' launches.
+ * Same outputs; costs a cross-stream wait per call. The levels re-prime when it changes. */
+NEO_HIP_API int neo_hip_upols_set_paced(neo_hip_upols* h, int enable);
 /* Latency mode for latency-bound shapes (few channels, filters up to 256 partitions, blocks up
  * to 512; C3): ONE persistent kernel per handle steps every block. A call writes the block's
  * record to a mailbox in mapped host memory and spins until the kernel reports the block done:

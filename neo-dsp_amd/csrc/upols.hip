@@ -873,6 +873,19 @@ NEO_HIP_API int neo_hip_upols_set_ahead(neo_hip_upols* h, int enable)
     return NEO_HIP_OK;
 }
 
+NEO_HIP_API int neo_hip_upols_set_paced(neo_hip_upols* h, int enable)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    device_guard g(h->device);
+    if (g.rc) return g.rc;
+    if (bool(enable) == h->paced) return NEO_HIP_OK;
+    if (int rc = lvl_join(h, h->stream)) return rc;
+    NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
+    h->paced = enable != 0;
+    h->lv_n = -1;  // the levels re-prime: no group is half issued in the other form
+    return NEO_HIP_OK;
+}
+
 NEO_HIP_API int neo_hip_upols_set_persistent(neo_hip_upols* h, int enable, double idle_ms)
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");

@@ -255,7 +255,7 @@ int call_independent(group_t* g, int i, float* io)
         g->nseen = 0;
         g->good_frames = 0;
     }
-    int rc = neo_hip_upols_process(x.own, io, 0, nullptr);
+    int rc = neo_hip_upols_process(x.own, io, 0, g->stream);  // the group's one stream for every member
     if (rc) return rc;
     ++x.steps;
     x.io_prev = x.io_last;

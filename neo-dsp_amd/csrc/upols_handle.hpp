@@ -97,6 +97,9 @@ struct neo_hip_upols {
     int sg = 1;
     hipStream_t bg = nullptr;
     hipEvent_t ev_blk = nullptr, ev_sl[2] = {}, ev_join = nullptr;
+    bool paced = false;            // neo_hip_upols_set_paced: the group's background launch in G per-call pieces
+    bool pace_prev = false;        // a piece was issued at the previous call (its event ev_pc[(n - 1) & 1])
+    hipEvent_t ev_pc[2] = {};
     bool bg_busy = false;  // slices enqueued on bg since the last join
     int64_t bg_launches = 0;
     float* tail = nullptr;  // batched OLA tails [C][T][B]

@@ -194,6 +194,7 @@ struct slice_args {
     cf* f2acc;    // as f1acc
     cf* f3ff;     // 2b's target far window [C][128][B]
     void* tl;     // timeline builds (NEO_TIMELINE): per-workgroup records of the launch
+    int bid0;     // paced background pieces: the first workgroup of the launch this piece runs
 };
 
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
@@ -1285,7 +1286,7 @@ constexpr int step_wpe() { return B > 512 ? 2 : (KMAX == 1 ? NEO_RAW_WPE : NEO_S
 template<int B, bool OLA, int KMAX, int PART = 0>
 __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
 {
-    int bid = int(blockIdx.x);
+    int bid = int(blockIdx.x) + a.bid0;
     auto far2b = [&]() {
         if (bid >= a.f3nwg) {
             bid -= a.f3nwg;
@@ -1573,7 +1574,7 @@ void lvl_free(upols_t* h)
         (void)hipStreamSynchronize(h->bg);
         (void)hipStreamDestroy(h->bg);
         h->bg = nullptr;
-        for (hipEvent_t* e : {&h->ev_blk, &h->ev_sl[0], &h->ev_sl[1], &h->ev_join}) {
+        for (hipEvent_t* e : {&h->ev_blk, &h->ev_sl[0], &h->ev_sl[1], &h->ev_join, &h->ev_pc[0], &h->ev_pc[1]}) {
             (void)hipEventDestroy(*e);
             *e = nullptr;
         }
@@ -1662,10 +1663,16 @@ static unsigned launch_grid(const slice_args& a)
 }
 
 // kernel of a launch: part 0 the step kernel (every role), 1 the block alone, 2 the slices alone
-static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStream_t s, int part = 0)
+static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStream_t s, int part = 0,
+                              int piece = 0, int pieces = 1)
 {
     slice_args a = a_in;
-    const unsigned grid = launch_grid(a);
+    unsigned grid = launch_grid(a);
+    if (pieces > 1) {  // workgroups [piece grid / pieces, (piece + 1) grid / pieces) of the launch
+        const unsigned g0 = unsigned(uint64_t(grid) * piece / pieces), g1 = unsigned(uint64_t(grid) * (piece + 1) / pieces);
+        a.bid0 = int(g0);
+        grid = g1 - g0;
+    }
     if (!grid) return NEO_HIP_OK;
 #ifdef NEO_TIMELINE
     if (int64_t(grid) > g_tl_cap) {
@@ -2001,7 +2008,7 @@ static int group_streams(upols_t* h)
     lo = 0;
 #endif
     NEO_HIP_CHECK(hipStreamCreateWithPriority(&h->bg, hipStreamNonBlocking, lo));  // lo: the least urgent
-    for (hipEvent_t* e : {&h->ev_blk, &h->ev_sl[0], &h->ev_sl[1], &h->ev_join})
+    for (hipEvent_t* e : {&h->ev_blk, &h->ev_sl[0], &h->ev_sl[1], &h->ev_join, &h->ev_pc[0], &h->ev_pc[1]})
         NEO_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     return NEO_HIP_OK;
 }
@@ -2022,13 +2029,38 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     if (primed) {
         if ((rc = lvl_prime(h, s))) return rc;
         h->lv_n = 0;
+        h->pace_prev = false;
     }
     const int64_t n = h->lv_n;
     const int G = h->sg;
     slice_args a = base_args(h);
     block_part(h, n, h->wpos, 0, h->C, in, ld_in, out, ld_out, a);
     block_levels(h, n, h->wpos, a);
-    if (G > 1 && n % G == 0) {
+    if (G > 1 && h->paced) {
+        // Paced (neo_hip_upols_set_paced): the group's background launch in G pieces, piece k at
+        // the group's call k (workgroups [k W / G, (k + 1) W / G) of the same launch: its
+        // workgroups are independent), and every block waits for the piece of the call before it.
+        // Then no block waits for more than one piece of background work (the last piece of a
+        // group is the call before the next group's first block): every call costs about the
+        // same, at the price of a cross-stream wait per call (the real-time caller's view).
+        const int k = int(n % G);
+        const int64_t n0 = n - k;
+        const int w0 = ring_add(h->wpos, -k, h->ring);
+        const bool odd = (n0 / G) & 1;
+        if (k == 0) {
+            if (primed) NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the priming launches
+            if (odd || primed) NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
+            if (!odd) NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the blocks before n: the next odd group
+        }
+        slice_args b = base_args(h);
+        slice_part(h, n0, w0, b);
+        if ((rc = launch_step_kernel(h, b, h->bg, 2, k, G))) return rc;
+        h->bg_busy = true;
+        if (k == G - 1) ++h->bg_launches;
+        NEO_HIP_CHECK(hipEventRecord(h->ev_pc[n & 1], h->bg));
+        if (h->pace_prev) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_pc[(n - 1) & 1], 0));
+        h->pace_prev = true;
+    } else if (G > 1 && n % G == 0) {
         // Every background level has T >= 2 G, so its windows (and the far level's) start at
         // multiples of 2 G: a background launch at an odd group (n = G mod 2 G) needs the blocks
         // before n - G, one at an even group only those before n - 2 G (its predecessor on bg

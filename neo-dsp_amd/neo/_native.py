@@ -67,6 +67,7 @@ SIGNATURES = {
     "neo_hip_upols_get_far_group": (_i, [_vp, ctypes.POINTER(_i)]),
     "neo_hip_upols_get_step_group": (_i, [_vp, ctypes.POINTER(_i)]),
     "neo_hip_upols_join_background": (_i, [_vp, _vp]),
+    "neo_hip_upols_set_paced": (_i, [_vp, _i]),
     "neo_hip_upols_set_persistent": (_i, [_vp, _i, ctypes.c_double]),
     "neo_hip_upols_get_persistent": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i64)]),
     "neo_hip_upols_persist_step_times": (_i, [_vp, ctypes.POINTER(ctypes.c_double), _i64, ctypes.POINTER(_i64)]),

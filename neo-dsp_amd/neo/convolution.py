@@ -301,6 +301,11 @@ class UpolsConvolver:
         slice launches of the step groups issued so far (device-side; no host wait)."""
         _native.check(_native.load().neo_hip_upols_join_background(self._h, ctypes.c_void_p(stream)))
 
+    def set_paced(self, enable: bool) -> None:
+        """Step groups' background launch in one piece per call, each block waiting for the piece
+        of the call before it (neo_hip_upols_set_paced): an even host round trip per block."""
+        _native.check(_native.load().neo_hip_upols_set_paced(self._h, int(bool(enable))))
+
     def set_persistent(self, enable: bool, idle_ms: float = 50.0) -> None:
         """Latency mode (neo_hip_upols_set_persistent): one persistent kernel steps every block;
         every process call is then synchronous (complete on return, the stream is not used).
