@@ -513,6 +513,14 @@ def run_upols(args, world, rank, local):
         while time.perf_counter() - t_warm < WARM_SECONDS:  # untimed
             feed.run(64)
             torch.cuda.synchronize()
+        # end the warm-up on a step-group boundary: a timed region then starts with its group's
+        # background launch, as every group does in steady state (starting k calls into a group,
+        # the region would open with k blocks and no background work beside them, then still
+        # hold the same number of background launches)
+        G_, ph = conv.step_group(), conv.ahead_info()[1]  # ph: the next step's position in its far window
+        if G_ > 1 and ph % G_:
+            feed.run(G_ - ph % G_)
+            torch.cuda.synchronize()
 
     gpu_ms = {}
 

@@ -1,9 +1,10 @@
 """Paced background work (neo_hip_upols_set_paced): a step group's background launch issued as G
 per-call pieces (workgroup ranges of the same launch) with every block waiting for the piece of
 the call before it. The same kernels compute the same sums, so the outputs equal the unpaced
-step groups' bit for bit; pinned to the oracle (uniform_partitioned_convolver.hpp:47-65) too.
-The shape has step groups (128 channels x B = 512: 4096 16-column units, G = 4) and a far level
-(P = 600: two segments), 700 blocks (five far windows), switched on and off mid-stream."""
+step groups' bit for bit (until a switch re-primes the levels: the far level's windows then start
+elsewhere, float summation order); pinned to the oracle (uniform_partitioned_convolver.hpp:47-65)
+throughout. The shape has step groups (128 channels x B = 512: 4096 16-column units, G = 4) and a
+far level (P = 600), 700 blocks (five far windows), switched off and on again mid-stream."""
 import numpy as np
 import pytest
 
@@ -39,7 +40,8 @@ def test_paced_equals_step_groups(neo_gpu, oracle):
         conv.join_background(None)
         torch.cuda.synchronize()
         outs.append(t.cpu().numpy())
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0][:, :300 * B], outs[1][:, :300 * B])
+    assert peak_err(outs[0], outs[1]) <= 1e-6
     chans = [0, 77, 127]
     ref = oracle.dense_convolve(x.cpu().numpy()[chans], parts[chans])
     assert peak_err(outs[0][chans], ref) <= 1e-5
