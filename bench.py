@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-fft", action="store_true", help="skip the c2_fft sub-object of UPOLS runs")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the affinity mask's CPUs, at most 16")
     ap.add_argument("--no-host-io", action="store_true", help="skip the host_io sub-object")
+    ap.add_argument("--no-paced", action="store_true",
+                    help="skip latency.paced (its per-call background pieces would mix into kernel-level profiles)")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the secondary weak-scaling object")
     ap.add_argument("--far-group", type=int, default=0,
                     help="neo_hip_upols_opts.far_group: 0 auto, 1..4 windows per far phase-1 pass")
@@ -626,7 +628,7 @@ def run_upols(args, world, rank, local):
     conv.set_timing(False)
     st = np.array(conv.step_times())
     paced = None
-    if levels and G > 1:
+    if levels and G > 1 and not args.no_paced:
         # the same round trip with the background work paced (neo_hip_upols_set_paced: one piece of
         # the group's launch per call, each block after the piece of the call before): even calls
         conv.set_paced(True)

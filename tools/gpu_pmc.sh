@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 for W in c5full c5 c4 c2; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${W}_${C}_$TAG -o run -- \
-      python3 $R/bench.py --workload $W --steps 32 --warmup 2 --no-cpu-baseline --no-parity --no-fft --no-host-io \
+      python3 $R/bench.py --workload $W --steps 32 --warmup 2 --no-cpu-baseline --no-parity --no-fft --no-paced --no-host-io \
       > $O/pmc_${W}_${C}_$TAG.log 2>&1 || exit $?
   done
 done

@@ -27,10 +27,10 @@ timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 fi
 [ "$PART" = "1" ] && { echo "round part 1 exit=0"; exit 0; }
 cd /tmp && export TMPDIR=/tmp && \
-NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5full_$TAG -o run -- python3 $R/bench.py --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5full_$TAG.log 2>&1 && \
-NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$TAG -o run -- python3 $R/bench.py --workload c5 --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft > $O/prof_c5_$TAG.log 2>&1 && \
+NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5full_$TAG -o run -- python3 $R/bench.py --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft --no-paced > $O/prof_c5full_$TAG.log 2>&1 && \
+NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$TAG -o run -- python3 $R/bench.py --workload c5 --steps 64 --warmup 5 --no-cpu-baseline --no-parity --no-fft --no-paced > $O/prof_c5_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2_$TAG -o run -- python3 $R/bench.py --workload c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_c2_$TAG.log 2>&1 && \
-NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- python3 $R/bench.py --workload c4 --steps 128 --no-cpu-baseline --no-parity --no-fft > $O/prof_c4_$TAG.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$TAG -o run -- python3 $R/bench.py --workload c3 --steps 256 --no-cpu-baseline --no-parity --no-fft > $O/prof_c3_$TAG.log 2>&1 && \
+NEO_BENCH_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- python3 $R/bench.py --workload c4 --steps 128 --no-cpu-baseline --no-parity --no-fft --no-paced > $O/prof_c4_$TAG.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$TAG -o run -- python3 $R/bench.py --workload c3 --steps 256 --no-cpu-baseline --no-parity --no-fft --no-paced > $O/prof_c3_$TAG.log 2>&1 && \
 cd $R && bash tools/gpu_pmc.sh $TAG && bash tools/gpu_calib.sh $TAG
 echo "round exit=$?"

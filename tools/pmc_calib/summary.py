@@ -16,7 +16,7 @@ def per_kernel(path):
     acc = {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            name = row["Kernel_Name"].split("(")[0]
+            name = row["Kernel_Name"].replace("float __vector(2)", "v2f").replace("float __vector(4)", "v4f").split("(")[0]
             acc.setdefault(name, []).append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
