@@ -390,6 +390,18 @@ __device__ __forceinline__ void buf_st(cf v, __amdgpu_buffer_rsrc_t r, int voff,
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, 0);
 }
 
+// Toeplitz levels' filter rows: nontemporal (the default) or, NEO_H_POLICY 1, the default cache
+// policy for the levels whose band ends by partition 64 (diagnostic A/B: the small bands' filter
+// rows, re-read every T steps, may stay in the Infinity Cache at the 256-channel shapes)
+#ifndef NEO_H_POLICY
+#define NEO_H_POLICY 0
+#endif
+__device__ __forceinline__ cf ld_h(const cf* p, int band_end)
+{
+    if (NEO_H_POLICY && band_end <= 64) return *p;
+    return ld_nt(p);
+}
+
 // v + v of the lane D = 16 / 32 apart (v_permlane16_swap / v_permlane32_swap, gfx950): the
 // swap of v with itself leaves v and its partner in the two halves of the pair, whose sum is
 // the same float sum in every lane as v + __shfl_xor(v, D)
@@ -483,7 +495,7 @@ __device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& 
                 xr[i] = ld_nt(Xc + int64_t(r) * sa.pstride);
             }
 #pragma unroll
-            for (int m = 0; m < NPL; ++m) hm[m] = pa + m < ta.b ? ld_nt(Hc + int64_t(pa + m) * sa.pstride) : cf{0.f, 0.f};
+            for (int m = 0; m < NPL; ++m) hm[m] = pa + m < ta.b ? ld_h(Hc + int64_t(pa + m) * sa.pstride, ta.b) : cf{0.f, 0.f};
 #pragma unroll
             for (int m = 0; m < NPL; ++m) {
                 const pk_coef h(hm[m], k == 0);
@@ -633,7 +645,7 @@ __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_a
 #pragma unroll
         for (int i = 0; i < G::NH; ++i) {
             const int m = q + G::NQ * i;
-            if (live && m < nb) hv[i] = ld_nt(Hc + int64_t(ta.a + m) * sa.pstride);
+            if (live && m < nb) hv[i] = ld_h(Hc + int64_t(ta.a + m) * sa.pstride, ta.b);
         }
 #pragma unroll
         for (int i = 0; i < G::NXL; ++i) {
