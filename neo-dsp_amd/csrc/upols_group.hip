@@ -72,6 +72,8 @@ struct neo_hip_upols_group {
     float* in_dev = nullptr;          // their device addresses
     float* out_dev = nullptr;
     float* prev_bak = nullptr;        // device [C][B]: the previous blocks before the frame's step
+    float* stage_pin = nullptr;       // independent mode: one member's block, mapped pinned
+    float* stage_dev = nullptr;
     int64_t step_n = 0;               // the frame step's level index and FDL ring row (for redos)
     int step_w = 0;
     int npending = 0;
@@ -255,7 +257,18 @@ int call_independent(group_t* g, int i, float* io)
         g->nseen = 0;
         g->good_frames = 0;
     }
-    int rc = neo_hip_upols_process(x.own, io, 0, g->stream);  // the group's one stream for every member
+    // the block through the group's own mapped staging, on the group's stream: no per-call
+    // pointer query of the caller's buffer, no per-member stream or staging
+    if (!g->stage_pin) {
+        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->stage_pin), size_t(g->B) * sizeof(float),
+                                    hipHostMallocMapped | hipHostMallocCoherent));
+        NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g->stage_dev), g->stage_pin, 0));
+    }
+    const size_t bb = size_t(g->B) * sizeof(float);
+    std::memcpy(g->stage_pin, io, bb);
+    int rc = neo_hip_upols_process_device(x.own, g->stage_dev, g->B, g->stage_dev, g->B, g->stream);
+    if (!rc) rc = neo_hip::spin_sync(g->stream);
+    if (!rc) std::memcpy(io, g->stage_pin, bb);
     if (rc) return rc;
     ++x.steps;
     x.io_prev = x.io_last;
@@ -375,6 +388,7 @@ NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
     free_shared(g);
     for (auto& x : g->m)
         if (x.own) neo_hip_upols_destroy(x.own);
+    if (g->stage_pin) (void)hipHostFree(g->stage_pin);
     (void)hipStreamDestroy(g->stream);
     delete g;
     return NEO_HIP_OK;
