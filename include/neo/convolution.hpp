@@ -199,6 +199,14 @@ struct upols_multichannel {
         neo::hip::check_or_abort(neo_hip_upols_process_samples(_h.get(), io, n, io, n, n, 0, nullptr));
     }
     auto reset() -> void { neo::hip::check(neo_hip_upols_reset(_h.get())); }
+    /// latency mode (neo_hip_upols_set_persistent): one resident kernel steps every block; every
+    /// call completes on return (shapes up to 16 channels, 256 partitions, B <= 512; throws otherwise)
+    auto latency_mode(bool on, double idle_ms = 50.0) -> void
+    {
+        neo::hip::check(neo_hip_upols_set_persistent(_h.get(), on ? 1 : 0, idle_ms));
+    }
+    /// paced background work (neo_hip_upols_set_paced): an even cost per call with step groups
+    auto paced(bool on) -> void { neo::hip::check(neo_hip_upols_set_paced(_h.get(), on ? 1 : 0)); }
 
     [[nodiscard]] auto channels() const noexcept { return _C; }
     [[nodiscard]] auto block_size() const noexcept { return _B; }
@@ -284,10 +292,21 @@ struct hip_upols_convolver {
         std::vector<Complex> h(P * bins);
         for (std::size_t p = 0; p < P; ++p)
             for (std::size_t k = 0; k < bins; ++k) h[p * bins + k] = Complex(neo::hip::detail::at(filter, p, k));
-        if (!_impl || _impl->partitions() != P || _impl->block_size() != bins - 1)
+        if (!_impl || _impl->partitions() != P || _impl->block_size() != bins - 1) {
             _impl = std::make_unique<upols_multichannel>(1, bins - 1, P, neo::hip::detail::default_device(), M);
+            if (_latency) _impl->latency_mode(true, _idle_ms);
+        }
         _impl->filter(h.data());
         _block.resize(bins - 1);
+    }
+
+    /// latency mode for this instance (upols_multichannel::latency_mode), kept across filter()
+    /// calls; applied at the next filter() when no filter was set yet
+    auto latency_mode(bool on, double idle_ms = 50.0) -> void
+    {
+        _latency = on;
+        _idle_ms = idle_ms;
+        if (_impl) _impl->latency_mode(on, idle_ms);
     }
 
     template<typename Vec>
@@ -306,6 +325,8 @@ struct hip_upols_convolver {
 private:
     std::unique_ptr<upols_multichannel> _impl;
     std::vector<float> _block;
+    bool _latency = false;
+    double _idle_ms = 50.0;
 };
 
 /// Single-channel drop-in for upola_convolver_v2<complex<float>> (dense_convolver.hpp:28,

@@ -389,6 +389,47 @@ static void test_overlap_stage()
     REQUIRE(max_abs_diff(x, ref) <= 1e-5 * peak);
 }
 
+// the latency mode (one resident kernel, synchronous calls) through the single-channel drop-in
+// at the reference benchmark's shape (B = 512, 2 s IR: P = 188), against the oracle's dense
+// convolution of the same blocks; the multichannel object's paced step groups against the unpaced
+static void test_latency_mode_and_paced()
+{
+    std::size_t const B = 512, L = 96000, nb = 300;
+    auto ir = rnoise(31, L);
+    oracle_normalize_impulse(ir.data(), 1, L);
+    auto const P = std::size_t(oracle_num_partitions(L, B));
+    std::vector<float> parts(P * (B + 1) * 2);
+    oracle_uniform_partition(ir.data(), 1, L, B, parts.data());
+    auto const signal = rnoise(32, B * nb);
+    std::vector<float> ref(signal.size());
+    oracle_dense_convolve(signal.data(), ref.data(), parts.data(), 1, signal.size(), P, B, 1);
+    neo::convolution::upols_convolver<cf> conv;
+    conv.latency_mode(true);
+    conv.filter(neo::hip::make_matrix_view(reinterpret_cast<cf*>(parts.data()), P, B + 1));
+    auto out = signal;
+    for (std::size_t i = 0; i < out.size(); i += B) conv(neo::hip::make_view(out.data() + i, B));
+    double peak = 0;
+    for (float r : ref) peak = std::max(peak, double(std::abs(r)));
+    REQUIRE(max_abs_diff(out, ref) <= 1e-5 * peak);
+    // step groups (128 channels x B = 512), paced vs not: the same kernels, bit for bit
+    std::size_t const C = 128, P2 = 100, n2 = 40;
+    std::vector<cf> h2(C * P2 * (B + 1));
+    for (std::size_t i = 0; i < h2.size(); ++i)
+        h2[i] = cf{float((i * 7919) % 1000) * 1e-4f, float((i * 104729) % 1000) * 1e-4f};
+    neo::convolution::upols_multichannel a{C, B, P2}, b{C, B, P2};
+    a.filter(h2.data());
+    b.filter(h2.data());
+    a.paced(true);
+    bool same = true;
+    for (std::size_t f = 0; f < n2; ++f) {
+        auto xa = rnoise(40 + f, C * B), xb = xa;
+        a(xa.data());
+        b(xb.data());
+        same = same && xa == xb;
+    }
+    REQUIRE(same);
+}
+
 int main()
 {
     test_fdl_index();
@@ -410,6 +451,7 @@ int main()
     test_stft();
     test_overlap_stage<neo::convolution::overlap_save<cf>, 0>();
     test_overlap_stage<neo::convolution::overlap_add<cf>, 1>();
+    test_latency_mode_and_paced();
     std::printf(failures ? "FAILED (%d)\n" : "all C++ API tests passed\n", failures);
     return failures ? 1 : 0;
 }
