@@ -27,13 +27,12 @@
 //                     changing its filter) ends coalescing: the states move back into one-channel
 //                     handles (a speculatively stepped member one block back) before the call.
 // So every output is the instance's own sequential step; the launch count per frame drops from
-// one per channel to one while the caller keeps the plugin's call pattern. Every handle of a
-// group (the members' own and the shared one) uses the code-path choices of the shared handle
-// over the live members (far window group, Toeplitz window parts, step group; re-applied when
-// the live count changes), so both modes run the same arithmetic. A mode switch re-primes the
-// streaming levels at that block, so the far level's 128-block windows may start elsewhere than
-// in an uninterrupted run: outputs then differ from it in float summation order only (tests:
-// bit for bit before the far level contributes, against the oracle over long runs).
+// one per channel to one while the caller keeps the plugin's call pattern. Each handle takes the
+// code-path choices of its own shape (a member alone: one channel, one launch per block; the
+// shared handle: its channel count's step groups, far window group, Toeplitz window parts), and a
+// mode switch re-primes the streaming levels at that block: outputs equal a standalone
+// single-channel convolver's up to float summation order (tests: bit for bit where the levels
+// whose order depends on the shape do not contribute yet, against the oracle over long runs).
 #include "upols_handle.hpp"
 
 #include <algorithm>
@@ -51,7 +50,6 @@ struct member {
     bool filtered = false;
     int64_t steps = 0;             // blocks processed since the filter was set
     const float* io_last = nullptr;
-    neo_hip_upols_opts opts{};     // the options its own handle was made with
     const float* io_prev = nullptr;  // the buffer of the frame before (coalescing needs stable buffers)
     bool pending = false;          // coalesced: stepped by the frame's leader, call not yet seen
     bool seen = false;             // independent: called in the frame being observed
@@ -72,6 +70,8 @@ struct neo_hip_upols_group {
     float* in_dev = nullptr;          // their device addresses
     float* out_dev = nullptr;
     float* prev_bak = nullptr;        // device [C][B]: the previous blocks before the frame's step
+    float* stage_pin = nullptr;       // independent mode: one member's block, mapped pinned
+    float* stage_dev = nullptr;
     int64_t step_n = 0;               // the frame step's level index and FDL ring row (for redos)
     int step_w = 0;
     int npending = 0;
@@ -88,17 +88,6 @@ int live_count(const group_t* g)
     int n = 0;
     for (const auto& x : g->m) n += x.live;
     return n;
-}
-
-// the code-path choices every handle of the group uses: those of the shared handle over the
-// live members (the far window group and the Toeplitz window parts depend on the channel count)
-neo_hip_upols_opts group_opts(const group_t* g, int C)
-{
-    neo_hip_upols_opts o{-1, 0, 0, 0, -1, -1, 0, 0, 0};
-    o.far_group = neo_hip::far_group_for(C, g->B, g->P);
-    o.toep_split = neo_hip::toep_split_for(C, g->B);
-    o.step_group = neo_hip::step_group_for(C, g->B, g->P);
-    return o;
 }
 
 // one channel's state (filter rows, FDL ring, previous block) from (src, cs) to (dst, cd); both
@@ -126,42 +115,10 @@ void free_shared(group_t* g)
     g->slot_member.clear();
 }
 
-int make_own(group_t* g, member& x, int C)
+int make_own(group_t* g, member& x)
 {
     if (x.own) return NEO_HIP_OK;
-    x.opts = group_opts(g, C);
-    return neo_hip_upols_create_ex(1, g->B, g->P, g->device, g->method, &x.opts, &x.own);
-}
-
-bool same_opts(const neo_hip_upols_opts& a, const neo_hip_upols_opts& b)
-{
-    return a.far_group == b.far_group && a.toep_split == b.toep_split && a.step_group == b.step_group;
-}
-
-// independent mode, after the live count changed: every member's own handle re-made with the
-// options of the new count (state copied: filter rows, FDL ring, previous block, ring row)
-int reoption(group_t* g)
-{
-    const int C = live_count(g);
-    const neo_hip_upols_opts o = group_opts(g, C);
-    for (auto& x : g->m) {
-        if (!x.live || !x.own || same_opts(x.opts, o)) continue;
-        neo_hip_upols* old = x.own;
-        x.own = nullptr;
-        int rc = make_own(g, x, C);
-        if (!rc) rc = copy_channel(x.own, 0, old, 0, old->prev, g->stream);
-        if (!rc && hipStreamSynchronize(g->stream) != hipSuccess) rc = fail(NEO_HIP_ERUNTIME, "group stream sync failed");
-        if (rc) {
-            if (x.own) neo_hip_upols_destroy(x.own);
-            x.own = old;
-            return rc;
-        }
-        x.own->wpos = old->wpos;
-        x.own->batch = false;
-        neo_hip::lvl_filter_changed(x.own);
-        neo_hip_upols_destroy(old);
-    }
-    return NEO_HIP_OK;
+    return neo_hip_upols_create_ex(1, g->B, g->P, g->device, g->method, nullptr, &x.own);
 }
 
 // the B samples at p lie in a range the owner registered
@@ -177,8 +134,7 @@ bool registered(const group_t* g, const float* p)
 int coalesce(group_t* g)
 {
     const int C = live_count(g);
-    const neo_hip_upols_opts o = group_opts(g, C);
-    int rc = neo_hip_upols_create_ex(C, g->B, g->P, g->device, g->method, &o, &g->shared);
+    int rc = neo_hip_upols_create_ex(C, g->B, g->P, g->device, g->method, nullptr, &g->shared);
     if (rc) return rc;
     const size_t io = size_t(C) * size_t(g->B) * sizeof(float);
     NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->in_pin), io, hipHostMallocMapped | hipHostMallocCoherent));
@@ -219,10 +175,9 @@ int coalesce(group_t* g)
 int split(group_t* g)
 {
     neo_hip_upols* sh = g->shared;
-    const int C = live_count(g);
     for (auto& x : g->m) {
         if (!x.live) continue;
-        int rc = make_own(g, x, C);
+        int rc = make_own(g, x);
         if (rc) return rc;
         const bool back = x.pending;
         if (x.slot >= 0) {
@@ -255,7 +210,18 @@ int call_independent(group_t* g, int i, float* io)
         g->nseen = 0;
         g->good_frames = 0;
     }
-    int rc = neo_hip_upols_process(x.own, io, 0, g->stream);  // the group's one stream for every member
+    // the block through the group's own mapped staging, on the group's stream: no per-call
+    // pointer query of the caller's buffer, no per-member stream or staging
+    if (!g->stage_pin) {
+        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->stage_pin), size_t(g->B) * sizeof(float),
+                                    hipHostMallocMapped | hipHostMallocCoherent));
+        NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g->stage_dev), g->stage_pin, 0));
+    }
+    const size_t bb = size_t(g->B) * sizeof(float);
+    std::memcpy(g->stage_pin, io, bb);
+    int rc = neo_hip_upols_process_device(x.own, g->stage_dev, g->B, g->stage_dev, g->B, g->stream);
+    if (!rc) rc = neo_hip::spin_sync(g->stream);
+    if (!rc) std::memcpy(io, g->stage_pin, bb);
     if (rc) return rc;
     ++x.steps;
     x.io_prev = x.io_last;
@@ -375,6 +341,7 @@ NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
     free_shared(g);
     for (auto& x : g->m)
         if (x.own) neo_hip_upols_destroy(x.own);
+    if (g->stage_pin) (void)hipHostFree(g->stage_pin);
     (void)hipStreamDestroy(g->stream);
     delete g;
     return NEO_HIP_OK;
@@ -397,8 +364,7 @@ NEO_HIP_API int neo_hip_upols_group_join(neo_hip_upols_group* g, int* id)
     if (i == g->m.size()) g->m.emplace_back();
     g->m[i] = member{};
     g->m[i].live = true;
-    int rc = make_own(g, g->m[i], live_count(g));
-    if (!rc) rc = reoption(g);
+    const int rc = make_own(g, g->m[i]);
     if (rc) {
         if (g->m[i].own) neo_hip_upols_destroy(g->m[i].own);
         g->m[i] = member{};
@@ -426,7 +392,7 @@ NEO_HIP_API int neo_hip_upols_group_leave(neo_hip_upols_group* g, int id)
     for (auto& y : g->m) y.seen = false;
     g->nseen = 0;
     g->good_frames = 0;
-    return reoption(g);
+    return NEO_HIP_OK;
 }
 
 NEO_HIP_API int neo_hip_upols_group_set_filter(neo_hip_upols_group* g, int id, const void* filter, int is_device)
