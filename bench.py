@@ -160,13 +160,21 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+# the translation units whose kernels the PMC passes measure (the streaming step, the plain and
+# batched steps, the FFT) and every shared header; host-only units (groups, multi-device shards,
+# setup, one-shot convolution, overlap stages, the library glue) do not change what they measured
+PMC_SOURCES = ("upols_levels.hip", "upols.hip", "upols_batch.hip", "fft.hip")
+
+
 def code_tag() -> str:
-    """Hash of the kernel sources: PMC summaries count only for the code they measured."""
+    """Hash of the measured kernels' sources: PMC summaries count only for the code they measured."""
     import glob
     import hashlib
 
     h = hashlib.sha1()
-    for path in sorted(glob.glob(os.path.join(REPO, "neo-dsp_amd", "csrc", "*.[hc]*"))):
+    csrc = os.path.join(REPO, "neo-dsp_amd", "csrc")
+    paths = sorted(glob.glob(os.path.join(csrc, "*.hpp"))) + [os.path.join(csrc, f) for f in PMC_SOURCES]
+    for path in paths:
         with open(path, "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:12]
