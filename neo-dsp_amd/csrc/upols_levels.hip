@@ -1947,7 +1947,7 @@ int lvl_join(upols_t* h, hipStream_t s)
 
 // First streaming step after a reset / filter change / batched pass (block t0 at ring row w):
 // window 0 of every level, starting at t0, computed whole (all units; the far level
-// transforms every segment: slice by slice, 2a of slice q beside 2b of slice q - 1).
+// transforms every segment: phase 1 and 2a in the levels' launch, 2b in a second one).
 static int lvl_prime(upols_t* h, hipStream_t s)
 {
     const level_plan& lp = h->lv;
@@ -1983,31 +1983,25 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         a.f2tw = w;
         a.f2comb = 2;
     }
+    if (lp.nseg && !h->far_raw) {  // far window 0: phase 1 and 2a of every unit beside the levels
+        const int U = int(far_units(h));
+        a.fnfresh = lp.nseg;  // every segment transformed
+        a.f1wn = 0;
+        far1_range(h, a, 0, U, 0, 0);  // zero partial sums (no stored segments)
+        a.f2u0 = 0;
+        a.f2nwg = U;
+        a.f2tw = w;
+        a.f2wn = 0;
+    }
     if (int rc = launch_step_kernel(h, a, s)) return rc;
     if (!lp.nseg || h->far_raw) return NEO_HIP_OK;
-    // far window 0, every segment transformed (fnfresh = nseg), in slices
-    const int64_t U = far_units(h);
-    const int ns = far_nslices(h);
-    for (int q = 0; q <= ns; ++q) {
-        slice_args f = base_args(h);
-        f.fnfresh = lp.nseg;
-        if (q < ns) {
-            f.f1wn = 0;
-            far1_range(h, f, far_u(U, q, ns), far_u(U, q + 1, ns), 0, 0);  // zero partial sums (no stored segments)
-            f.f2u0 = far_u(U, q, ns);
-            f.f2nwg = far_u(U, q + 1, ns) - f.f2u0;
-            f.f2tw = w;
-            f.f2wn = 0;
-        }
-        if (q >= 1) {
-            f.f3u0 = far_u(U, q - 1, ns);
-            f.f3nwg = far_u(U, q, ns) - f.f3u0;
-            f.f3wn = 0;
-            f.f3ff = h->fv_ff;
-        }
-        if (int rc = launch_step_kernel(h, f, s)) return rc;
-    }
-    return NEO_HIP_OK;
+    slice_args f = base_args(h);  // and 2b of every unit: two launches whatever the shape
+    f.fnfresh = lp.nseg;
+    f.f3u0 = 0;
+    f.f3nwg = int(far_units(h));
+    f.f3wn = 0;
+    f.f3ff = h->fv_ff;
+    return launch_step_kernel(h, f, s);
 }
 
 // background stream and events of the step groups (created on the first grouped step)

@@ -263,16 +263,10 @@ class Sim:
         if self.lp["nseg"] and self.raw:
             self.far2r(self.w, 0, 0, self.K)
         elif self.lp["nseg"]:
-            ns = self.lp["nseg"]
-            FS_ = self.ns
-            for q in range(FS_ + 1):  # launch q: phase 1 + 2a of slice q, 2b of slice q - 1
-                if q < FS_:
-                    k0, k1 = self.span(q)
-                    self.far1(0, k0, k1, ns)
-                    self.far2a(self.w, 0, k0, k1, ns)
-                if q >= 1:
-                    k0, k1 = self.span(q - 1)
-                    self.far2b(0, k0, k1, ns)
+            ns = self.lp["nseg"]  # phase 1 and 2a of every column, then 2b (two launches)
+            self.far1(0, 0, self.K, ns)
+            self.far2a(self.w, 0, 0, self.K, ns)
+            self.far2b(0, 0, self.K, ns)
         self.n = 0
 
     def step(self, x):
