@@ -188,6 +188,15 @@ NEO_HIP_API int neo_hip_upols_get_ahead(neo_hip_upols* h, int* enabled, int* pha
  * nseg far segments of 128 partitions from 256 (arrays of >= 5 entries); the automatic
  * choice of far_level. */
 NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, int* T, int* a, int* b, int* nseg);
+/* The step groups' background plan for (channels, block, partitions, step_group; 0 = automatic)
+ * with default options (no device needed; for tests): phi[l], the window offset of Toeplitz level
+ * l (its windows start at t0 + W T - phi: a level of 4 G <= T <= 32 blocks starts half a window
+ * later, so the groups where the levels skip fall apart); the cycle length in step groups; the unit
+ * cuts of every background level in level order, cycle / (T / G) windows of T / G cuts each, into
+ * cuts[cuts_cap] (*ncuts = how many there are); the predicted background bytes per step group of
+ * the cycle into loads[loads_cap]. uniform != 0: equal parts and no offsets (for comparison). */
+NEO_HIP_API int neo_hip_upols_part_plan(int channels, int block, int partitions, int step_group, int uniform, int* phi,
+                                        int* cycle, int* cuts, int cuts_cap, int* ncuts, double* loads, int loads_cap);
 /* Paced background work (step groups only; a no-op with one launch per block): the step group's
  * background launch is issued in G pieces, one per call, and every block waits for the piece of
  * the call before it, so no call waits for more than one piece of background work: the host round

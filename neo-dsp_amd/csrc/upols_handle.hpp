@@ -79,6 +79,12 @@ struct neo_hip_upols {
     int64_t lv_n = -1;              // blocks since the levels were primed (-1: prime at the next step)
     bool lv_ready = false;          // level buffers allocated
     neo_hip::cf* lv_slab[neo_hip::kLvToep] = {};  // Toeplitz level slabs [2][C][T][B]
+    // step groups (upols_levels.hip part_plan, set when the levels prime): per Toeplitz level the
+    // window offset phi (windows start at t0 + W T - phi) and the unit cuts of its background parts
+    // per window of a cycle of lv_cyc groups
+    int lv_phi[neo_hip::kLvToep] = {};
+    int lv_cyc = 1;
+    std::vector<int> lv_cut[neo_hip::kLvToep];
     neo_hip::cf* fv_hf = nullptr;   // far segment spectra [C][nseg][256][B]
     neo_hip::cf* fv_xf = nullptr;   // far FDL row-pair spectra, ring of nseg slots [C][nseg][256][B]
     neo_hip::cf* fv_ff = nullptr;   // far field [2][C][128][B]

@@ -1765,6 +1765,166 @@ static void far_raw_args(const upols_t* h, int64_t W, int q, int w, int64_t n, s
     a.f2comb = 2;
 }
 
+// Step groups: the background levels' window offsets and part sizes. A window's first group
+// carries none of its level's parts (they read the window's rows), so with every window starting at
+// a multiple of its length the groups at multiples of 8 (G = 4) had no Toeplitz work at all and
+// the odd ones all of the 8-block level's: background launches of 0.9 to 2.1 GB at c5full, and a
+// 20-step sample of the stream 5-8 % above or below the far window's mean. So a level of window
+// T >= 4 G (up to 32 blocks: its prime reads at most 16 rows further back) starts its windows half a
+// window later (phi = T / 2; still at even groups, which the events need), which puts the groups it
+// skips apart from every other level's (2 G: odd groups carry it, 4 G: skips 2 mod 4, 8 G: 4 mod 8,
+// the far level: 0 mod kFarT / G); and each window's units are cut into parts of unequal sizes so
+// that, over a cycle of groups (the far window, else the longest level window), every group's
+// background bytes come as close to equal as the slots allow: min-max water filling of one window
+// at a time against the rest (the far slices' bytes fixed), swept until it settles.
+static int part_phi(int T, int G, bool bg) { return bg && G > 1 && T >= 4 * G && T <= 32 ? T / 2 : 0; }
+
+struct part_level {
+    int T = 0, UPW = 1;
+    bool bg = false;
+    int64_t U = 0;
+    double wbytes = 0;  // bytes per window
+};
+
+// phi, cycle length (groups) and cuts [k][j] (k < cyc / (T / G) windows of the cycle, j <= T / G - 1)
+// per level; loads: the predicted background bytes per group of the cycle (null: not wanted)
+static void part_plan(const part_level* lv, int nl, int G, int64_t FU, int ns, double c1, double c2, bool far_raw,
+                      bool balance, int* phi, int& cyc, std::vector<int>* cut, std::vector<double>* loads)
+{
+    cyc = 1;
+    for (int l = 0; l < nl; ++l) {
+        phi[l] = balance ? part_phi(lv[l].T, G, lv[l].bg) : 0;
+        cut[l].clear();
+        if (lv[l].bg) cyc = std::max(cyc, lv[l].T / G);
+    }
+    if (ns) cyc = std::max(cyc, kFarT / G);
+    std::vector<double> load(size_t(cyc), 0.0);
+    if (ns) {  // the far slices (slice_part): equal units per slice
+        auto su = [&](int q) { return double(far_u(FU, q + 1, ns) - far_u(FU, q, ns)); };
+        for (int g = 0; g < cyc; ++g) {
+            if (far_raw) {
+                if (g >= 2 && g - 2 < ns) load[size_t(g)] += c2 * su(g - 2);
+            } else {
+                if (g >= 1 && g <= ns) load[size_t(g)] += c1 * su(g - 1);
+                if (g >= 2 && g - 2 < ns) load[size_t(g)] += c2 * su(g - 2);
+            }
+        }
+    }
+    struct win {
+        int l, np;
+        double c;
+        std::vector<int> grp;
+        std::vector<double> x;  // units per part
+    };
+    std::vector<win> ws;
+    for (int l = 0; l < nl; ++l) {
+        if (!lv[l].bg || lv[l].U <= 0) continue;
+        const int Tg = lv[l].T / G, np = Tg - 1, s = ((-phi[l] / G) % Tg + Tg) % Tg;
+        for (int k = 0; k < cyc / Tg; ++k) {
+            win w{l, np, lv[l].wbytes / double(lv[l].U), {}, std::vector<double>(size_t(np), double(lv[l].U) / np)};
+            for (int j = 1; j <= np; ++j) w.grp.push_back((s + k * Tg + j) % cyc);
+            for (int j = 0; j < np; ++j) load[size_t(w.grp[size_t(j)])] += w.c * w.x[size_t(j)];
+            ws.push_back(std::move(w));
+        }
+    }
+    std::vector<double> base;
+    for (int sweep = 0; sweep < (balance ? 64 : 0); ++sweep)
+        for (auto& w : ws) {
+            const int np = w.np;
+            base.assign(size_t(np), 0.0);
+            for (int j = 0; j < np; ++j) {
+                load[size_t(w.grp[size_t(j)])] -= w.c * w.x[size_t(j)];
+                base[size_t(j)] = load[size_t(w.grp[size_t(j)])];
+            }
+            // water level h: sum over parts of max(0, h - base) = the window's bytes
+            std::vector<double> sb(base);
+            std::sort(sb.begin(), sb.end());
+            const double total = w.c * double(lv[w.l].U);
+            double h = sb[0], acc = 0;
+            for (int i = 0; i < np; ++i) {
+                const double next = i + 1 < np ? sb[size_t(i + 1)] : 1e300;
+                const double need = (next - sb[size_t(i)]) * (i + 1);
+                if (acc + need >= total) {
+                    h = sb[size_t(i)] + (total - acc) / (i + 1);
+                    break;
+                }
+                acc += need;
+            }
+            for (int j = 0; j < np; ++j) {
+                w.x[size_t(j)] = std::max(0.0, h - base[size_t(j)]) / w.c;
+                load[size_t(w.grp[size_t(j)])] += w.c * w.x[size_t(j)];
+            }
+        }
+    for (int l = 0; l < nl; ++l)
+        if (lv[l].bg) cut[l].assign(size_t(cyc / (lv[l].T / G) * (lv[l].T / G)), 0);
+    std::vector<int> kcount(size_t(nl), 0);
+    for (const auto& w : ws) {  // cuts on workgroup multiples, the last at U
+        const int64_t U = lv[w.l].U, q = lv[w.l].UPW;
+        int* c = cut[w.l].data() + size_t(kcount[size_t(w.l)]++) * size_t(w.np + 1);
+        double cum = 0;
+        c[0] = 0;
+        for (int j = 1; j <= w.np; ++j) {
+            cum += w.x[size_t(j - 1)];
+            const int64_t r = j == w.np ? U : std::min<int64_t>(U, std::llround(cum / double(q)) * q);
+            c[j] = int(std::max<int64_t>(c[j - 1], r));
+        }
+    }
+    if (loads) {  // from the integer cuts
+        loads->assign(size_t(cyc), 0.0);
+        for (int g = 0; g < cyc; ++g) (*loads)[size_t(g)] = 0;
+        if (ns) {
+            auto su = [&](int q) { return double(far_u(FU, q + 1, ns) - far_u(FU, q, ns)); };
+            for (int g = 0; g < cyc; ++g) {
+                if (far_raw) {
+                    if (g >= 2 && g - 2 < ns) (*loads)[size_t(g)] += c2 * su(g - 2);
+                } else {
+                    if (g >= 1 && g <= ns) (*loads)[size_t(g)] += c1 * su(g - 1);
+                    if (g >= 2 && g - 2 < ns) (*loads)[size_t(g)] += c2 * su(g - 2);
+                }
+            }
+        }
+        std::fill(kcount.begin(), kcount.end(), 0);
+        for (const auto& w : ws) {
+            const int* c = cut[w.l].data() + size_t(kcount[size_t(w.l)]++) * size_t(w.np + 1);
+            for (int j = 1; j <= w.np; ++j) (*loads)[size_t(w.grp[size_t(j - 1)])] += w.c * double(c[j] - c[j - 1]);
+        }
+    }
+}
+
+static int64_t toep_units(const upols_t* h, int T);
+static bool block_level(const upols_t* h, int T);
+
+// the handle's plan (lvl_prime): levels, far slices and their bytes as bench.algorithmic_bytes
+// counts them
+static void plan_handle_parts(upols_t* h, std::vector<double>* loads = nullptr, bool balance = true)
+{
+    const level_plan& lp = h->lv;
+    part_level pl[kLvToep];
+    const double CB = double(h->C) * h->B;
+    for (int l = 0; l < lp.n; ++l) {
+        int JH, UPW;
+        toep_geom(h, lp.T[l], JH, UPW);
+        pl[l].T = lp.T[l];
+        pl[l].UPW = UPW;
+        pl[l].bg = h->sg > 1 && !h->persist && !block_level(h, lp.T[l]);  // latency mode: its own schedule
+        pl[l].U = toep_units(h, lp.T[l]);
+        pl[l].wbytes = CB * 8 * (2.0 * (lp.b[l] - lp.a[l]) + 2 * lp.T[l] - 1);
+    }
+    const int ns = h->sg > 1 && !h->persist && lp.nseg ? far_nslices(h) : 0;
+    const int64_t FU = far_units(h);
+    double c1 = 0, c2 = 0;  // bytes per far unit (16 columns) of phase 1 and 2 per window
+    if (ns) {
+        const int K = far_group(h), nseg = lp.nseg;
+        if (h->far_raw) {
+            c2 = 16.0 * 8 * ((nseg + 1) * 128.0 + (h->P - 256) + 128);
+        } else {
+            c1 = 16.0 * 8 * (256.0 * 2 * (nseg - 1) / K + 256);     // stored spectra, partial sums out
+            c2 = 16.0 * 8 * (256.0 * (3 + K - 1) + 128 + 256);       // fresh pair, products, field, sums in
+        }
+    }
+    part_plan(pl, lp.n, h->sg, FU, ns, c1, c2, h->far_raw, balance, h->lv_phi, h->lv_cyc, h->lv_cut, loads);
+}
+
 // The block role of step n (block t0 + n at FDL ring row w) for the channels [c0, c0 + nc): its
 // slab row of every Toeplitz level and its far-field row (windows finished in earlier launches)
 static void block_part(const upols_t* h, int64_t n, int w, int c0, int nc, const float* in, int64_t ld_in, float* out,
@@ -1784,7 +1944,8 @@ static void block_part(const upols_t* h, int64_t n, int w, int c0, int nc, const
     a.a0 = lp.a0;
     for (int l = 0; l < lp.n; ++l) {
         const int T = lp.T[l];
-        a.sl[a.nsl] = h->lv_slab[l] + ((n / T & 1) * C * T + n % T) * B;
+        const int64_t m = n + h->lv_phi[l];  // window m / T, its row m mod T
+        a.sl[a.nsl] = h->lv_slab[l] + ((m / T & 1) * C * T + m % T) * B;
         a.scs[a.nsl++] = int64_t(T) * B;
     }
     if (lp.nseg) {
@@ -1901,10 +2062,14 @@ static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
     const level_plan& lp = h->lv;
     const int G = h->sg;
     for (int l = 0; l < lp.n; ++l) {
-        const int T = lp.T[l];
+        const int T = lp.T[l], Tg = T / G;
         if (block_level(h, T)) continue;  // in the block launches
-        const int64_t j = (n0 % T) / G, np = T / G - 1, U = toep_units(h, T);
-        if (j >= 1) toep_slice(h, l, n0 / T + 1, (j - 1) * U / np, j * U / np, n0, w0, a);
+        const int64_t m0 = n0 + h->lv_phi[l], j = (m0 % T) / G, W = m0 / T;  // group j of window W
+        if (j < 1) continue;
+        const int64_t gw = (W * T - h->lv_phi[l]) / G, cyc = h->lv_cyc;  // window W's first group
+        const int k = int((gw % cyc + cyc) % cyc / Tg);
+        const int* cut = h->lv_cut[l].data() + size_t(k) * size_t(Tg);  // the window's cuts [0, Tg)
+        toep_slice(h, l, W + 1, cut[j - 1], cut[j], m0, w0, a);  // tw from m0: block t_{W+1} = (W + 1) T - phi
     }
     if (lp.nseg && h->far_raw) {  // recomputed: slice q - 2 of window W whole, at phase 2's time
         const int q = int(n0 % kFarT) / G;
@@ -1960,7 +2125,9 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         NEO_HIP_LAUNCH_CHECK();
         h->fv_dirty = false;
     }
-    slice_args a = base_args(h);
+    plan_handle_parts(h);  // window offsets and background part sizes (step groups)
+    slice_args a = base_args(h), f = base_args(h);  // f: the second launch (far 2b, offset windows 1)
+    bool f_any = false;
     for (int l = 0; l < lp.n; ++l) {
         int JH, UPW;
         toep_geom(h, lp.T[l], JH, UPW);
@@ -1970,10 +2137,18 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         ta.T = lp.T[l];
         ta.a = lp.a[l];
         ta.b = lp.b[l];
-        ta.tw = w;
+        ta.tw = ring_add(w, -h->lv_phi[l], h->ring);  // window 0 holds step 0: it began phi steps ago
         ta.u0 = 0;
         ta.u1 = C * (B / 16) * JH;
         ta.nwg = (ta.u1 + UPW - 1) / UPW;
+        if (h->lv_phi[l]) {  // and window 1 whole: its parts before step 0 never ran (the rest run again)
+            toep_arg& t1 = f.tp[l];
+            t1 = ta;
+            t1.slab = h->lv_slab[l] + size_t(C) * lp.T[l] * B;
+            t1.tw = ring_add(w, lp.T[l] - h->lv_phi[l], h->ring);
+            f.ntp = l + 1;
+            f_any = true;
+        }
     }
     if (lp.nseg && h->far_raw) {  // recomputed: window 0's field whole, every unit in the same launch
         a.f3u0 = 0;
@@ -1994,14 +2169,15 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         a.f2wn = 0;
     }
     if (int rc = launch_step_kernel(h, a, s)) return rc;
-    if (!lp.nseg || h->far_raw) return NEO_HIP_OK;
-    slice_args f = base_args(h);  // and 2b of every unit: two launches whatever the shape
-    f.fnfresh = lp.nseg;
-    f.f3u0 = 0;
-    f.f3nwg = int(far_units(h));
-    f.f3wn = 0;
-    f.f3ff = h->fv_ff;
-    return launch_step_kernel(h, f, s);
+    if (lp.nseg && !h->far_raw) {  // and 2b of every unit: two launches whatever the shape
+        f.fnfresh = lp.nseg;
+        f.f3u0 = 0;
+        f.f3nwg = int(far_units(h));
+        f.f3wn = 0;
+        f.f3ff = h->fv_ff;
+        f_any = true;
+    }
+    return f_any ? launch_step_kernel(h, f, s) : NEO_HIP_OK;
 }
 
 // background stream and events of the step groups (created on the first grouped step)
@@ -2535,6 +2711,41 @@ extern "C" NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int
         if (b) b[l] = lp.b[l];
     }
     if (nseg) *nseg = lp.nseg;
+    return NEO_HIP_OK;
+}
+
+// The step groups' background plan of a (channels, block, partitions) convolver with default
+// options and step group G (0: the automatic one), for tests (no device needed): phi[l] per
+// Toeplitz level; the cycle (groups); the cuts of every background level in level order, each
+// cycle / (T / G) windows of T / G cuts, into cuts[cuts_cap] (*ncuts written); the predicted
+// background bytes per group of the cycle into loads[loads_cap]; uniform != 0: equal parts and
+// no offsets (the plan step groups had before the balancing, for comparison).
+extern "C" NEO_HIP_API int neo_hip_upols_part_plan(int channels, int block, int partitions, int step_group, int uniform,
+                                                   int* phi, int* cycle, int* cuts, int cuts_cap, int* ncuts,
+                                                   double* loads, int loads_cap)
+{
+    if (channels < 1 || block < 16 || partitions < 1 || step_group < 0)
+        return neo_hip::fail(NEO_HIP_EINVAL, "part plan: bad shape");
+    neo_hip_upols h{};
+    h.C = channels;
+    h.B = block;
+    h.P = partitions;
+    neo_hip::plan_levels(partitions, h.lv);
+    h.sg = step_group ? step_group : neo_hip::step_group_for(channels, block, partitions);
+    std::vector<double> ld;
+    neo_hip::plan_handle_parts(&h, &ld, !uniform);
+    if (phi)
+        for (int l = 0; l < h.lv.n; ++l) phi[l] = h.lv_phi[l];
+    if (cycle) *cycle = h.lv_cyc;
+    int n = 0;
+    for (int l = 0; l < h.lv.n; ++l)
+        for (int v : h.lv_cut[l]) {
+            if (cuts && n < cuts_cap) cuts[n] = v;
+            ++n;
+        }
+    if (ncuts) *ncuts = n;
+    if (loads)
+        for (int g = 0; g < std::min(loads_cap, int(ld.size())); ++g) loads[g] = ld[size_t(g)];
     return NEO_HIP_OK;
 }
 

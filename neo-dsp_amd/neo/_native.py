@@ -64,6 +64,8 @@ SIGNATURES = {
     "neo_hip_upols_timing_detail": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "neo_hip_upols_step_times": (_i, [_vp, ctypes.POINTER(ctypes.c_double), _i64, ctypes.POINTER(_i64)]),
     "neo_hip_upols_level_plan": (_i, [_i] + [ctypes.POINTER(_i)] * 6),
+    "neo_hip_upols_part_plan": (_i, [_i] * 5 + [ctypes.POINTER(_i)] * 3 + [_i, ctypes.POINTER(_i),
+                                                                          ctypes.POINTER(ctypes.c_double), _i]),
     "neo_hip_upols_get_far_group": (_i, [_vp, ctypes.POINTER(_i)]),
     "neo_hip_upols_get_step_group": (_i, [_vp, ctypes.POINTER(_i)]),
     "neo_hip_upols_join_background": (_i, [_vp, _vp]),

@@ -74,6 +74,32 @@ def level_plan(partitions: int) -> dict:
     return {"a0": a0.value, "T": list(T[:n]), "a": list(a[:n]), "b": list(b[:n]), "nseg": ns.value}
 
 
+def part_plan(channels: int, block: int, partitions: int, step_group: int, uniform: bool = False) -> dict:
+    """The background plan of step groups of `step_group` blocks (neo_hip_upols_part_plan; no
+    device needed): per Toeplitz level the window offset phi, the cycle length in step groups,
+    per background level (T >= 2 step_group) the unit cuts of each window of the cycle
+    ({level: [[T / G cuts of window k], ...]}) and the predicted background bytes per step group
+    of the cycle; uniform: equal parts, no offsets."""
+    if step_group < 2:
+        raise ValueError("part_plan: step groups of >= 2 blocks")
+    L = _native.load()
+    lp = level_plan(partitions)
+    phi, cyc, nc = (ctypes.c_int * 8)(), ctypes.c_int(), ctypes.c_int()
+    loads = (ctypes.c_double * 512)()
+    args = (int(channels), int(block), int(partitions), int(step_group), int(uniform), phi, ctypes.byref(cyc))
+    _native.check(L.neo_hip_upols_part_plan(*args, None, 0, ctypes.byref(nc), loads, 512))
+    cuts = (ctypes.c_int * max(1, nc.value))()
+    _native.check(L.neo_hip_upols_part_plan(*args, cuts, nc.value, ctypes.byref(nc), loads, 512))
+    flat, out, i = list(cuts[:nc.value]), {}, 0
+    for l, T in enumerate(lp["T"]):
+        if T < 2 * step_group:
+            continue  # in the block launches
+        Tg = T // step_group
+        out[l] = [flat[i + k:i + k + Tg] for k in range(0, cyc.value, Tg)]
+        i += cyc.value
+    return {"phi": list(phi[:len(lp["T"])]), "cycle": cyc.value, "cuts": out, "loads": list(loads[:cyc.value])}
+
+
 def host_register(array: np.ndarray) -> np.ndarray:
     """Page-lock a host array in place (neo_hip_host_register) so that host-buffer calls
     (UpolsConvolver.__call__) read and write it over PCIe without staging; call

@@ -51,6 +51,11 @@ class Sim:
         self.raw = raw  # the recomputed far level (far2r_role: every segment from ring rows each window)
         self.ns = FS if sg == 1 else FT // sg - 2  # far slices per window (far_nslices)
         self.pending = []  # step groups: background launches [roles left, due block] in stream order
+        # step groups: a background level of window 4 sg <= T <= 32 starts its windows half a window
+        # later (part_phi), and a window's units are cut into its parts at arbitrary points (the
+        # library balances the groups' bytes; any cuts must give the same outputs: random here)
+        self.phi = [T // 2 if sg > 1 and 4 * sg <= T <= 32 else 0 for T in lp["T"]]
+        self.cuts = {}
         ns = lp["nseg"]
         self.P, self.K = H.shape
         # windows per phase-1 pass: the kernel's automatic choice for this many 16-column units
@@ -231,12 +236,14 @@ class Sim:
         for l, T in enumerate(lp["T"]):
             if T < 2 * G:
                 continue
-            U = K // 16 if K >= 16 else K
-            j, np_, W = (n0 % T) // G, T // G - 1, n0 // T + 1
+            m0 = n0 + self.phi[l]
+            j, np_, W = (m0 % T) // G, T // G - 1, m0 // T + 1  # part j of window W (the next one)
             if j >= 1:
-                k0, k1 = (j - 1) * U // np_ * K // U, j * U // np_ * K // U
+                if (l, W) not in self.cuts:
+                    self.cuts[(l, W)] = [0] + sorted(self.rng.integers(0, K + 1, size=np_ - 1).tolist()) + [K]
+                k0, k1 = self.cuts[(l, W)][j - 1], self.cuts[(l, W)][j]
                 if k1 > k0:
-                    out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1: self.toep(l, (w0 + W * T - n0) % R, k0, k1, W & 1))
+                    out.append(lambda l=l, T=T, W=W, k0=k0, k1=k1, m0=m0: self.toep(l, (w0 + W * T - m0) % R, k0, k1, W & 1))
         if lp["nseg"] and self.raw:
             q, W = (n0 % FT) // G, n0 // FT + 1
             if 2 <= q and q - 2 < self.ns:  # slice q - 2 of window W whole, at phase 2's time
@@ -258,8 +265,11 @@ class Sim:
 
     def prime(self):
         self.join()
-        for l in range(len(self.lp["T"])):
-            self.toep(l, self.w, 0, self.K, 0)
+        self.cuts = {}
+        for l, T in enumerate(self.lp["T"]):
+            self.toep(l, (self.w - self.phi[l]) % self.R, 0, self.K, 0)  # window 0 began phi steps ago
+            if self.phi[l]:  # and window 1 whole (its parts before step 0 never ran)
+                self.toep(l, (self.w + T - self.phi[l]) % self.R, 0, self.K, 1)
         if self.lp["nseg"] and self.raw:
             self.far2r(self.w, 0, 0, self.K)
         elif self.lp["nseg"]:
@@ -278,7 +288,8 @@ class Sim:
         def block_read():  # partitions 1..a0-1, the block's slabs and far field
             r = (self.H[1: lp["a0"]] * self.ring[(w - np.arange(1, lp["a0"])) % R]).sum(0)
             for l, T in enumerate(lp["T"]):
-                r = r + self.slab[l][(n // T) & 1, n % T]
+                m = n + self.phi[l]
+                r = r + self.slab[l][(m // T) & 1, m % T]
             if lp["nseg"]:
                 r = r + self.ff[(n // FT) & 1, n % FT]
             y[0] = r + self.H[0] * x
@@ -469,3 +480,35 @@ def test_level_schedule_far_recomputed(P, sg):
         ref = (H[:m] * X[t - np.arange(m)]).sum(0)
         worst = max(worst, float(np.abs(y - ref).max() / (np.abs(ref).max() + 1e-300)))
     assert worst < 1e-12, worst
+
+
+@pytest.mark.parametrize("C,B,P,G", [(2048, 512, 938, 4), (256, 512, 938, 4), (256, 256, 1875, 4), (64, 256, 700, 8),
+                                     (16, 64, 300, 2), (4, 256, 300, 4), (1, 512, 188, 4)])
+def test_part_plan_valid_and_balanced(C, B, P, G):
+    """The library's background plan (part_plan, upols_levels.hip): window offsets phi = T / 2 for
+    the background levels of 4 G <= T <= 32 (the replay above runs the same offsets with arbitrary
+    cuts); every window's cuts run 0 .. U in order; at the 256- and 2048-channel shapes every step
+    group of the far window carries 0.85-1.06 of the mean background bytes (before: an empty group
+    every 8), and any 5 consecutive groups (a 20-step sample) 0.87-1.05."""
+    import neo
+
+    lp = plan(P)
+    p = neo.convolution.part_plan(C, B, P, G)
+    for l, T in enumerate(lp["T"]):
+        assert p["phi"][l] == (T // 2 if 4 * G <= T <= 32 else 0)
+    for l, wins in p["cuts"].items():
+        T = lp["T"][l]
+        JH = (2 if C * (B // 16) < 256 else 1) if T == 32 else 1
+        U = C * (B // 16) * JH
+        assert len(wins) == p["cycle"] // (T // G)
+        for c in wins:
+            assert len(c) == T // G and c[0] == 0 and all(x <= y for x, y in zip(c, c[1:]))
+            assert c[-1] == U
+    if C >= 256:
+        ld = np.array(p["loads"])
+        m = ld.mean()
+        assert 0.85 * m <= ld.min() and ld.max() <= 1.06 * m, (ld.min() / m, ld.max() / m)
+        w5 = [ld[[(g + i) % len(ld) for i in range(5)]].mean() / m for g in range(len(ld))]
+        assert 0.87 <= min(w5) and max(w5) <= 1.05, (min(w5), max(w5))
+        u = np.array(neo.convolution.part_plan(C, B, P, G, uniform=True)["loads"])
+        assert u.min() < 0.1 * u.mean()  # the plan before: empty groups

@@ -891,9 +891,22 @@ def test_step_group_timing_detail(neo_gpu):
     torch.cuda.synchronize()
     conv.set_timing(False)
     parts = conv.timing_detail()
-    # 16 block launches; background launches at steps 0, 4, 8, 12, the first one empty (nothing of
-    # a window starting at step 0 is due yet: the levels primed it) and not timed
-    assert [n for _, n in parts] == [16, 3, 0, 0]
+    # 16 block launches; background launches at steps 0, 4, 8, 12 that carry work (an empty one
+    # is not launched, nor timed): from the plan (part_plan: window offsets and part cuts; slice_part)
+    pp = neo_gpu.convolution.part_plan(4, 256, 300, 4)
+    lp = neo_gpu.convolution.level_plan(300)
+    busy = 0
+    for g in range(4):
+        work = g >= 1 and lp["nseg"] > 0  # far phase 1 of slice g - 1 (and phase 2 from g = 2)
+        for l, wins in pp["cuts"].items():
+            T, phi = lp["T"][l], pp["phi"][l]
+            m0 = 4 * g + phi
+            j, Tg = (m0 % T) // 4, T // 4
+            gw = (m0 // T * T - phi) // 4  # the window's first group
+            c = wins[(gw % pp["cycle"]) // Tg]
+            work = work or (j >= 1 and c[j] > c[j - 1])
+        busy += work
+    assert [n for _, n in parts] == [16, busy, 0, 0]
     assert parts[0][0] > 0 and parts[1][0] > 0
     assert conv.step_group() == 4
     with pytest.raises(RuntimeError):
