@@ -85,6 +85,7 @@ struct neo_hip_upols {
     int lv_phi[neo_hip::kLvToep] = {};
     int lv_cyc = 1;
     std::vector<int> lv_cut[neo_hip::kLvToep];
+    std::vector<int> fv_cut;  // step groups: the far slices' first units (ns + 1 cuts; empty: equal slices)
     neo_hip::cf* fv_hf = nullptr;   // far segment spectra [C][nseg][256][B]
     neo_hip::cf* fv_xf = nullptr;   // far FDL row-pair spectra, ring of nseg slots [C][nseg][256][B]
     neo_hip::cf* fv_ff = nullptr;   // far field [2][C][128][B]

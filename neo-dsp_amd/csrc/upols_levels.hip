@@ -1740,25 +1740,29 @@ static int far_nslices(const upols_t* h) { return h->sg == 1 ? kFarT - 1 : kFarT
 
 static int far_u(int64_t U, int q, int ns) { return int(q * U / ns); }
 
+// the first unit of far slice q: step groups take the planned cuts (part_plan), G = 1 equal slices
+static int far_cut(const upols_t* h, int q)
+{
+    if (!h->fv_cut.empty()) return h->fv_cut[size_t(q)];
+    return far_u(int64_t(h->C) * (h->B / 16), q, h->sg == 1 ? kFarT - 1 : kFarT / h->sg - 2);
+}
+
 // far phase 1 for slice q of window W: the unit groups of class W mod K for the windows
 // W .. W + K - 1 (far1_mac); in the first windows after priming (W < K) the classes that have
 // not started, for window W alone
 static void far1_args(const upols_t* h, int64_t W, int q, slice_args& a)
 {
-    const int64_t U = far_units(h);
-    const int K = far_group(h), ns = far_nslices(h);
+    const int K = far_group(h);
     a.f1wn = int(W);
-    far1_range(h, a, far_u(U, q, ns), far_u(U, q + 1, ns), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
+    far1_range(h, a, far_cut(h, q), far_cut(h, q + 1), K == 1 ? 0 : (W < K ? 2 : 1), int(W % K));
 }
 
 // the recomputed far level's slice q of window W (far2r_role), issued at step n (block t0 + n at
 // ring row w): every unit of the slice computes the window's field from rows before t_W - 128
 static void far_raw_args(const upols_t* h, int64_t W, int q, int w, int64_t n, slice_args& a)
 {
-    const int64_t U = far_units(h);
-    const int ns = far_nslices(h);
-    a.f3u0 = far_u(U, q, ns);
-    a.f3nwg = far_u(U, q + 1, ns) - a.f3u0;
+    a.f3u0 = far_cut(h, q);
+    a.f3nwg = far_cut(h, q + 1) - a.f3u0;
     a.f3wn = int(W);
     a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
     a.f2tw = ring_add(w, W * kFarT - n, h->ring);
@@ -1786,10 +1790,12 @@ struct part_level {
     double wbytes = 0;  // bytes per window
 };
 
-// phi, cycle length (groups) and cuts [k][j] (k < cyc / (T / G) windows of the cycle, j <= T / G - 1)
-// per level; loads: the predicted background bytes per group of the cycle (null: not wanted)
+// phi, cycle length (groups), cuts [k][j] (k < cyc / (T / G) windows of the cycle, j <= T / G - 1)
+// per level and the far slices' unit cuts fcut[0 .. ns] (ns > 0); loads: the predicted background
+// bytes per group of the cycle (null: not wanted). balance = false: equal parts, no offsets.
 static void part_plan(const part_level* lv, int nl, int G, int64_t FU, int ns, double c1, double c2, bool far_raw,
-                      bool balance, int* phi, int& cyc, std::vector<int>* cut, std::vector<double>* loads)
+                      bool balance, int* phi, int& cyc, std::vector<int>* cut, std::vector<int>& fcut,
+                      std::vector<double>* loads)
 {
     cyc = 1;
     for (int l = 0; l < nl; ++l) {
@@ -1798,18 +1804,16 @@ static void part_plan(const part_level* lv, int nl, int G, int64_t FU, int ns, d
         if (lv[l].bg) cyc = std::max(cyc, lv[l].T / G);
     }
     if (ns) cyc = std::max(cyc, kFarT / G);
-    std::vector<double> load(size_t(cyc), 0.0);
-    if (ns) {  // the far slices (slice_part): equal units per slice
-        auto su = [&](int q) { return double(far_u(FU, q + 1, ns) - far_u(FU, q, ns)); };
-        for (int g = 0; g < cyc; ++g) {
-            if (far_raw) {
-                if (g >= 2 && g - 2 < ns) load[size_t(g)] += c2 * su(g - 2);
-            } else {
-                if (g >= 1 && g <= ns) load[size_t(g)] += c1 * su(g - 1);
-                if (g >= 2 && g - 2 < ns) load[size_t(g)] += c2 * su(g - 2);
-            }
+    // the far slices (slice_part): slice q's phase 1 at group q + 1, phase 2 at q + 2 (recomputed:
+    // all of it at q + 2), s[q] units each
+    std::vector<double> fs(size_t(ns), ns ? double(FU) / ns : 0.0), load(size_t(cyc), 0.0);
+    auto far_add = [&](std::vector<double>& L, const std::vector<double>& sq, double sign) {
+        for (int q = 0; q < ns; ++q) {
+            if (!far_raw) L[size_t(q + 1)] += sign * c1 * sq[size_t(q)];
+            L[size_t(q + 2)] += sign * c2 * sq[size_t(q)];
         }
-    }
+    };
+    far_add(load, fs, 1.0);
     struct win {
         int l, np;
         double c;
@@ -1819,42 +1823,71 @@ static void part_plan(const part_level* lv, int nl, int G, int64_t FU, int ns, d
     std::vector<win> ws;
     for (int l = 0; l < nl; ++l) {
         if (!lv[l].bg || lv[l].U <= 0) continue;
-        const int Tg = lv[l].T / G, np = Tg - 1, s = ((-phi[l] / G) % Tg + Tg) % Tg;
+        const int Tg = lv[l].T / G, np = Tg - 1, s0 = ((-phi[l] / G) % Tg + Tg) % Tg;
         for (int k = 0; k < cyc / Tg; ++k) {
             win w{l, np, lv[l].wbytes / double(lv[l].U), {}, std::vector<double>(size_t(np), double(lv[l].U) / np)};
-            for (int j = 1; j <= np; ++j) w.grp.push_back((s + k * Tg + j) % cyc);
+            for (int j = 1; j <= np; ++j) w.grp.push_back((s0 + k * Tg + j) % cyc);
             for (int j = 0; j < np; ++j) load[size_t(w.grp[size_t(j)])] += w.c * w.x[size_t(j)];
             ws.push_back(std::move(w));
         }
     }
-    std::vector<double> base;
-    for (int sweep = 0; sweep < (balance ? 64 : 0); ++sweep)
-        for (auto& w : ws) {
-            const int np = w.np;
-            base.assign(size_t(np), 0.0);
-            for (int j = 0; j < np; ++j) {
-                load[size_t(w.grp[size_t(j)])] -= w.c * w.x[size_t(j)];
-                base[size_t(j)] = load[size_t(w.grp[size_t(j)])];
-            }
-            // water level h: sum over parts of max(0, h - base) = the window's bytes
-            std::vector<double> sb(base);
-            std::sort(sb.begin(), sb.end());
-            const double total = w.c * double(lv[w.l].U);
-            double h = sb[0], acc = 0;
-            for (int i = 0; i < np; ++i) {
-                const double next = i + 1 < np ? sb[size_t(i + 1)] : 1e300;
-                const double need = (next - sb[size_t(i)]) * (i + 1);
-                if (acc + need >= total) {
-                    h = sb[size_t(i)] + (total - acc) / (i + 1);
-                    break;
+    std::vector<double> base, sb, grad, y;
+    for (int round = 0; round < (balance ? 4 : 0); ++round) {
+        // the Toeplitz windows, one at a time against the rest: min-max water filling
+        for (int sweep = 0; sweep < 32; ++sweep)
+            for (auto& w : ws) {
+                const int np = w.np;
+                base.assign(size_t(np), 0.0);
+                for (int j = 0; j < np; ++j) {
+                    load[size_t(w.grp[size_t(j)])] -= w.c * w.x[size_t(j)];
+                    base[size_t(j)] = load[size_t(w.grp[size_t(j)])];
                 }
-                acc += need;
+                sb = base;
+                std::sort(sb.begin(), sb.end());
+                const double total = w.c * double(lv[w.l].U);
+                double h = sb[0], acc = 0;  // water level: sum of max(0, h - base) = the window's bytes
+                for (int i = 0; i < np; ++i) {
+                    const double next = i + 1 < np ? sb[size_t(i + 1)] : 1e300;
+                    const double need = (next - sb[size_t(i)]) * (i + 1);
+                    if (acc + need >= total) {
+                        h = sb[size_t(i)] + (total - acc) / (i + 1);
+                        break;
+                    }
+                    acc += need;
+                }
+                for (int j = 0; j < np; ++j) {
+                    w.x[size_t(j)] = std::max(0.0, h - base[size_t(j)]) / w.c;
+                    load[size_t(w.grp[size_t(j)])] += w.c * w.x[size_t(j)];
+                }
             }
-            for (int j = 0; j < np; ++j) {
-                w.x[size_t(j)] = std::max(0.0, h - base[size_t(j)]) / w.c;
-                load[size_t(w.grp[size_t(j)])] += w.c * w.x[size_t(j)];
+        if (!ns) break;
+        // the far slices against the rest: least squares around the mean, projected gradient on
+        // {s >= 0, sum s = FU} (the min-max recurrence is unstable: phase 2 bytes > phase 1's)
+        double mean = 0;
+        for (double v : load) mean += v;
+        mean /= cyc;
+        const double eta = 1.0 / (2.0 * (c1 + c2) * (c1 + c2));
+        for (int it = 0; it < 400; ++it) {
+            grad.assign(size_t(ns), 0.0);
+            for (int q = 0; q < ns; ++q) {
+                if (!far_raw) grad[size_t(q)] += 2 * c1 * (load[size_t(q + 1)] - mean);
+                grad[size_t(q)] += 2 * c2 * (load[size_t(q + 2)] - mean);
             }
+            far_add(load, fs, -1.0);
+            y.resize(size_t(ns));
+            for (int q = 0; q < ns; ++q) y[size_t(q)] = fs[size_t(q)] - eta * grad[size_t(q)];
+            sb = y;  // projection onto the simplex: subtract tau, clip at 0
+            std::sort(sb.begin(), sb.end(), std::greater<double>());
+            double cs = 0, tau = 0;
+            for (int i = 0; i < ns; ++i) {
+                cs += sb[size_t(i)];
+                const double t = (cs - double(FU)) / (i + 1);
+                if (sb[size_t(i)] - t > 0) tau = t;
+            }
+            for (int q = 0; q < ns; ++q) fs[size_t(q)] = std::max(0.0, y[size_t(q)] - tau);
+            far_add(load, fs, 1.0);
         }
+    }
     for (int l = 0; l < nl; ++l)
         if (lv[l].bg) cut[l].assign(size_t(cyc / (lv[l].T / G) * (lv[l].T / G)), 0);
     std::vector<int> kcount(size_t(nl), 0);
@@ -1869,20 +1902,20 @@ static void part_plan(const part_level* lv, int nl, int G, int64_t FU, int ns, d
             c[j] = int(std::max<int64_t>(c[j - 1], r));
         }
     }
+    fcut.assign(ns ? size_t(ns + 1) : 0, 0);
+    if (ns) {
+        double cum = 0;
+        for (int q = 1; q <= ns; ++q) {
+            cum += fs[size_t(q - 1)];
+            const int64_t r = q == ns ? FU : std::min<int64_t>(FU, std::llround(cum));
+            fcut[size_t(q)] = int(std::max<int64_t>(fcut[size_t(q - 1)], r));
+        }
+    }
     if (loads) {  // from the integer cuts
         loads->assign(size_t(cyc), 0.0);
-        for (int g = 0; g < cyc; ++g) (*loads)[size_t(g)] = 0;
-        if (ns) {
-            auto su = [&](int q) { return double(far_u(FU, q + 1, ns) - far_u(FU, q, ns)); };
-            for (int g = 0; g < cyc; ++g) {
-                if (far_raw) {
-                    if (g >= 2 && g - 2 < ns) (*loads)[size_t(g)] += c2 * su(g - 2);
-                } else {
-                    if (g >= 1 && g <= ns) (*loads)[size_t(g)] += c1 * su(g - 1);
-                    if (g >= 2 && g - 2 < ns) (*loads)[size_t(g)] += c2 * su(g - 2);
-                }
-            }
-        }
+        std::vector<double> fi(static_cast<size_t>(ns));
+        for (int q = 0; q < ns; ++q) fi[size_t(q)] = double(fcut[size_t(q + 1)] - fcut[size_t(q)]);
+        far_add(*loads, fi, 1.0);
         std::fill(kcount.begin(), kcount.end(), 0);
         for (const auto& w : ws) {
             const int* c = cut[w.l].data() + size_t(kcount[size_t(w.l)]++) * size_t(w.np + 1);
@@ -1922,7 +1955,7 @@ static void plan_handle_parts(upols_t* h, std::vector<double>* loads = nullptr, 
             c2 = 16.0 * 8 * (256.0 * (3 + K - 1) + 128 + 256);       // fresh pair, products, field, sums in
         }
     }
-    part_plan(pl, lp.n, h->sg, FU, ns, c1, c2, h->far_raw, balance, h->lv_phi, h->lv_cyc, h->lv_cut, loads);
+    part_plan(pl, lp.n, h->sg, FU, ns, c1, c2, h->far_raw, balance, h->lv_phi, h->lv_cyc, h->lv_cut, h->fv_cut, loads);
 }
 
 // The block role of step n (block t0 + n at FDL ring row w) for the channels [c0, c0 + nc): its
@@ -2075,12 +2108,12 @@ static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
         const int q = int(n0 % kFarT) / G;
         if (q >= 2 && q - 2 < far_nslices(h)) far_raw_args(h, n0 / kFarT + 1, q - 2, w0, n0, a);
     } else if (lp.nseg) {
-        const int64_t U = far_units(h), W = n0 / kFarT + 1;
+        const int64_t W = n0 / kFarT + 1;
         const int q = int(n0 % kFarT) / G, ns = far_nslices(h);
         if (q >= 1 && q <= ns) far1_args(h, W, q - 1, a);  // phase 1 of slice q - 1
         if (q >= 2) {  // phase 2 of slice q - 2, 2a and 2b in one workgroup per unit (far2c_role)
-            a.f3u0 = far_u(U, q - 2, ns);
-            a.f3nwg = far_u(U, q - 1, ns) - a.f3u0;
+            a.f3u0 = far_cut(h, q - 2);
+            a.f3nwg = far_cut(h, q - 1) - a.f3u0;
             a.f3wn = int(W);
             a.f2grp = far_group(h) > 1;
             a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
