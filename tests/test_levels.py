@@ -496,7 +496,7 @@ def test_part_plan_valid_and_balanced(C, B, P, G):
     """The library's background plan (part_plan, upols_levels.hip): window offsets phi = T / 2 for
     the background levels of 4 G <= T <= 32 (the replay above runs the same offsets with arbitrary
     cuts); every window's cuts run 0 .. U in order; at the 256- and 2048-channel shapes every step
-    group of the far window carries 0.85-1.06 of the mean background bytes (before: an empty group
+    group of the far window carries 0.99-1.01 of the mean background bytes (before: an empty group
     every 8), and so any 5 consecutive groups (a 20-step sample)."""
     import neo
 
