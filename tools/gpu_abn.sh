@@ -15,7 +15,7 @@ for rep in $(seq 1 ${REPS:-2}); do
   for W in ${WL:-c4 c5 c5full}; do
     for L in ${LIBS:-main}; do
       if [ $L = main ]; then LIB=""; else LIB=$R/tools/ab/$L/libneo_hip.so; fi
-      NEO_HIP_LIBRARY=$LIB timeout -k 10 300 python bench.py --workload $W --steps 64 --warmup 5 --no-cpu-baseline \
+      NEO_HIP_LIBRARY=$LIB timeout -k 10 300 python bench.py --workload $W --steps ${STEPS:-64} --warmup 5 --no-cpu-baseline \
         --no-fft --no-offline --no-parity --no-host-io --no-paced > $O/ab_${T}_${W}_${L}_$rep.json 2> $O/ab_${T}_${W}_${L}_$rep.err || exit 1
       python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], round(d['value'],1), 'wall', round(d['ms_per_step']*1e3,2), 'gpu', round(d['gpu_ms_per_step']*1e3,2))" $O/ab_${T}_${W}_${L}_$rep.json $W $L
     done
