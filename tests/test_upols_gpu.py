@@ -749,8 +749,10 @@ def test_far_phase2_forms_vs_oracle(neo_gpu, oracle, f2, method, B, P, C, K):
     ("upola", 1024, 270, 1, 300, {}), ("upols", 32, 257, 2, 654, {"far_level": 1})])
 def test_step_groups_vs_oracle(neo_gpu, oracle, G, method, B, P, C, nb, opts):
     """Step groups (neo_hip_upols_opts.step_group = G): the block of every call alone on the
-    caller's stream, the level slices of G calls as one launch on the background stream, the far
-    level in kFarT / G - 1 slices per window; every band, the far window groups K = 2..4, the
+    caller's stream, the level slices of G calls as one launch on the background stream (the
+    levels of 4 G <= T <= 32 with their windows offset by T / 2, every window's parts and the far
+    level's kFarT / G - 2 slices cut where part_plan evens out the groups); every band, the far
+    window groups K = 2..4, the
     128-block Toeplitz level, several windows and ring wraparound; OLS and OLA
     (uniform_partitioned_convolver.hpp:47-65, fdl_index.hpp:23-36)."""
     assert _stream(neo_gpu, oracle, method, B, P, C, nb, 1300 + P, dict(opts, step_group=G)) <= TOL
