@@ -43,6 +43,7 @@ inline int fail(int code, const char* fmt, ...)
 // Scoped hipSetDevice that restores the caller's device.
 struct device_guard {
     int prev = -1;
+    bool changed = false;  // restore only what this guard changed (every entry point takes one)
     int rc = NEO_HIP_OK;
     explicit device_guard(int dev)
     {
@@ -51,12 +52,14 @@ struct device_guard {
             if (hipSetDevice(dev) != hipSuccess) {
                 (void)hipGetLastError();  // not sticky: a later launch check must not see it
                 rc = fail(NEO_HIP_ENODEV, "hipSetDevice(%d) failed", dev);
+            } else {
+                changed = true;
             }
         }
     }
     ~device_guard()
     {
-        if (prev >= 0) (void)hipSetDevice(prev);
+        if (changed && prev >= 0) (void)hipSetDevice(prev);
     }
 };
 
@@ -110,6 +113,25 @@ inline std::vector<C> make_split_table(int order, int lo_bits)
     }
     return t;
 }
+
+// dmem.hip: device memory for handle buffers, sub-allocated from cached per-device chunks (freeing
+// never synchronizes the device; free only memory no queued work still uses); twiddle tables
+// shared by every handle on a device, never freed
+int dalloc(void** out, size_t bytes);
+void dfree(void* p);
+template<class T>
+inline int dalloc(T** out, size_t bytes)
+{
+    void* v = nullptr;
+    const int rc = dalloc(&v, bytes);
+    *out = static_cast<T*>(v);
+    return rc;
+}
+int halloc(void** host, void** dev, size_t bytes);  // mapped page-locked host memory, pooled
+void hfree(void* host);
+int shared_stream(hipStream_t* out);  // one of four blocking streams per device, never destroyed
+int shared_tw(cf** out, int B);  // upload_tw's table for block B
+int shared_far_tw(cf** out);     // the 256-point forward table of the far level
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -139,7 +139,7 @@ int fft_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, R* 
     const int64_t N = int64_t(1) << order, bins = N / 2 + 1;
     if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
     hipStream_t s = nullptr;
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     int rc = NEO_HIP_OK;
     neo_hip_fft_plan *r2c = nullptr, *c2r = nullptr;
     R* rows = nullptr;
@@ -176,7 +176,6 @@ int fft_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, R* 
     neo_hip_fft_plan_destroy(c2r);
     (void)hipFree(rows);
     (void)hipFree(spec);
-    (void)hipStreamDestroy(s);
     return rc;
 }
 
@@ -190,7 +189,7 @@ int direct_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, 
     if (g.rc) return g.rc;
     if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());
     hipStream_t s = nullptr;
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     int rc = NEO_HIP_OK;
     {
         device_buffers<R> io;
@@ -207,7 +206,6 @@ int direct_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, 
             rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
         if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     }
-    (void)hipStreamDestroy(s);
     return rc;
 }
 
@@ -238,7 +236,7 @@ int stft_impl(const R* x, int channels, int64_t length, int frame, int transform
     if (g.rc) return g.rc;
     if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());
     hipStream_t s = nullptr;
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     int rc = NEO_HIP_OK;
     R *d_x = nullptr, *d_w = nullptr, *rows = nullptr;
     C* d_out = static_cast<C*>(out);
@@ -279,7 +277,6 @@ int stft_impl(const R* x, int channels, int64_t length, int frame, int transform
         (void)hipFree(d_x);
         (void)hipFree(d_out);
     }
-    (void)hipStreamDestroy(s);
     return rc;
 }
 

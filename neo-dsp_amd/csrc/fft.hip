@@ -422,7 +422,7 @@ void free_plan(plan_t* p)
     for (auto* s : p->d_scratch) (void)hipFree(s);
     (void)hipFree(p->d_in);
     (void)hipFree(p->d_out);
-    if (p->stream) (void)hipStreamDestroy(p->stream);
+    // p->stream is one of the device's shared streams (dmem.hip)
     delete p;
 }
 
@@ -540,8 +540,7 @@ NEO_HIP_API int neo_hip_fft_plan_create(int order, int64_t batch, int kind, int 
         free_plan(p);
         return code;
     };
-    if (hipStreamCreateWithFlags(&p->stream, hipStreamDefault) != hipSuccess)
-        return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
+    if (int rc = shared_stream(&p->stream)) return bail(rc);
     if (int rc = f64 ? setup_tables<cd>(p) : setup_tables<cf>(p)) return bail(rc);
     const size_t rs = f64 ? sizeof(double) : sizeof(float), cs = 2 * rs;
     const size_t cbytes = size_t(p->n) * cs, rbytes = size_t(p->n) * rs;

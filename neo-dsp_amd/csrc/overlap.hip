@@ -107,7 +107,7 @@ void destroy_overlap(neo_hip_overlap* h)
     (void)hipFree(h->ov);
     (void)hipFree(h->spec);
     (void)hipFree(h->io);
-    if (h->stream) (void)hipStreamDestroy(h->stream);
+    // h->stream is one of the device's shared streams (dmem.hip)
     delete h;
 }
 
@@ -188,7 +188,7 @@ NEO_HIP_API int neo_hip_overlap_create(int kind, int channels, int64_t block, in
     h->bins = h->n / 2 + 1;
     const size_t wb = size_t(channels) * size_t(h->n) * sizeof(float);
     int rc = NEO_HIP_OK;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamDefault) != hipSuccess) rc = fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed");
+    if (int rs = neo_hip::shared_stream(&h->stream)) rc = rs;
     if (!rc) rc = neo_hip_fft_plan_create(order, channels, NEO_HIP_R2C, h->device, &h->r2c);
     if (!rc) rc = neo_hip_fft_plan_create(order, channels, NEO_HIP_C2R, h->device, &h->c2r);
     if (!rc && (hipMalloc(reinterpret_cast<void**>(&h->win[0]), wb) != hipSuccess ||

@@ -372,6 +372,21 @@ __global__ __launch_bounds__(256) void k_upola2_piece(
 using namespace neo_hip;
 
 
+int neo_hip::setup_join(upols_t* h, bool device_input)
+{
+    if (h->used_many) {
+        NEO_HIP_CHECK(hipDeviceSynchronize());
+    } else {
+        for (int i = 0; i < h->n_used; ++i) NEO_HIP_CHECK(hipStreamSynchronize(h->used_s[i]));
+        if (device_input) NEO_HIP_CHECK(hipStreamSynchronize(nullptr));
+    }
+    h->n_used = 0;
+    h->used_many = false;
+    if (int rc = lvl_join(h, h->stream)) return rc;
+    NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
+    return NEO_HIP_OK;
+}
+
 namespace {
 
 int reset_state(upols_t* h, hipStream_t s)
@@ -395,30 +410,31 @@ void destroy(upols_t* h)
     if (!h) return;
     (void)persist_stop(h);
     if (h->ps_stream) (void)hipStreamDestroy(h->ps_stream);
-    if (h->ps_mb) (void)hipHostFree(h->ps_mb);
-    (void)hipFree(h->ps_flags);
-    (void)hipFree(h->ps_tl);
+    hfree(h->ps_mb);
+    dfree(h->ps_flags);
+    dfree(h->ps_tl);
     for (auto& g : h->events)
         for (auto& e : g.e) (void)hipEventDestroy(e);
-    (void)hipFree(h->H);  // the FDL shares H's allocation (rows [nrows, 2 nrows))
-    (void)hipFree(h->part);
-    (void)hipFree(h->prev);
-    (void)hipFree(h->arrivals);
-    (void)hipFree(h->window);
-    (void)hipFree(h->tmp);
-    (void)hipFree(h->tw);
-    if (h->io_host) (void)hipHostFree(h->io_host);  // h->io is its device mapping
-    (void)hipFree(h->samples_dev);
-    (void)hipFree(h->part_b);
-    (void)hipFree(h->tail);
-    lvl_free(h);
-    if (h->samples_host) (void)hipHostFree(h->samples_host);
-    if (h->stream) (void)hipStreamDestroy(h->stream);
-    delete h;
+    lvl_free(h);  // joins the background stream first
+    // device buffers back to the pool (dmem.hip): no device-wide synchronization; the caller
+    // joined every stream that used them
+    dfree(h->H);  // the FDL shares H's allocation (rows [nrows, 2 nrows))
+    dfree(h->part);
+    dfree(h->prev);
+    dfree(h->arrivals);
+    dfree(h->window);
+    dfree(h->tmp);
+    hfree(h->io_host);  // h->io is its device mapping
+    dfree(h->samples_dev);
+    dfree(h->part_b);
+    dfree(h->tail);
+    hfree(h->samples_host);
+    delete h;  // h->stream is shared (a group's, or one of the device's four: dmem.hip)
 }
 
 int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
+    note_stream(h, s);
     if (h->persist) return persist_process(h, in, ld_in, out, ld_out, 1);  // synchronous: s is not used
     if (h->ahead) return launch_levels(h, in, ld_in, out, ld_out, s);
     if (int rc = lvl_join(h, s)) return rc;
@@ -485,6 +501,7 @@ int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
 // (overlap_add_convolver.hpp:80-134) and run whole aligned blocks through launch_step.
 int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t n, hipStream_t s)
 {
+    note_stream(h, s);
     const int B = h->B;
     const int T = h->batch ? batch_blocks(h) : 1;
     const bool a16 = !((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) &&
@@ -538,7 +555,7 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
 
 namespace {
 int create_convolver(int channels, int block, int partitions, int device, bool ola, bool v2,
-                     const neo_hip_upols_opts* opt, neo_hip_upols** out)
+                     const neo_hip_upols_opts* opt, neo_hip_upols** out, hipStream_t borrow = nullptr)
 {
     if (!out) return fail(NEO_HIP_EINVAL, "handle pointer is null");
     const neo_hip_upols_opts o = opt ? *opt : neo_hip_upols_opts{-1, 0, 0, 0, -1, -1, 0, 0, 0, 0};
@@ -623,28 +640,38 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
         destroy(h);
         return code;
     };
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamDefault) != hipSuccess)
-        return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
+    // a group member runs its setup and host-I/O work on its group's stream (upols_group.hip),
+    // every other handle on one of its device's four shared streams (dmem.hip shared_stream: a
+    // stream of its own would cost ~4 ms to create and ~3 ms to destroy)
+    h->stream = borrow;
+    if (!borrow) {
+        if (int rc = shared_stream(&h->stream)) return bail(rc);
+    }
     // filter and FDL in ONE allocation (FDL = rows [nrows, 2 nrows)): the LDS-DMA batched MAC
     // reaches both of a channel through a single buffer descriptor
-    if (hipMalloc(reinterpret_cast<void**>(&h->H), 2 * nrows * rowbytes) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&h->part), size_t(channels) * h->S * rowbytes) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&h->prev), size_t(channels) * block * sizeof(float)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&h->arrivals), size_t(channels) * sizeof(int)) != hipSuccess ||
-        (v2 && (hipMalloc(reinterpret_cast<void**>(&h->window), size_t(channels) * 2 * block * sizeof(float)) !=
-                    hipSuccess ||
-                hipMalloc(reinterpret_cast<void**>(&h->tmp), size_t(channels) * rowbytes) != hipSuccess)))
+    if (dalloc(&h->H, 2 * nrows * rowbytes) || dalloc(&h->part, size_t(channels) * h->S * rowbytes) ||
+        dalloc(&h->prev, size_t(channels) * block * sizeof(float)) || dalloc(&h->arrivals, size_t(channels) * sizeof(int)) ||
+        (v2 && (dalloc(&h->window, size_t(channels) * 2 * block * sizeof(float)) ||
+                dalloc(&h->tmp, size_t(channels) * rowbytes))))
         return bail(fail(NEO_HIP_ENOMEM, "device allocation of %zu bytes failed", 2 * nrows * rowbytes));
     h->fdl = h->H + nrows * size_t(block);
-    int rc = upload_tw(&h->tw, block);
+    int rc = shared_tw(&h->tw, block);
     if (rc) return bail(rc);
-    if (hipMemset(h->H, 0, nrows * rowbytes) != hipSuccess) return bail(fail(NEO_HIP_ERUNTIME, "memset failed"));
+    // stream-ordered zeroing, one wait at the end (the caller's later work may run on any stream)
+    if (hipMemsetAsync(h->H, 0, nrows * rowbytes, h->stream) != hipSuccess)
+        return bail(fail(NEO_HIP_ERUNTIME, "memset failed"));
     if ((rc = reset_state(h, h->stream))) return bail(rc);
     if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(NEO_HIP_ERUNTIME, "sync failed"));
     *out = h;
     return NEO_HIP_OK;
 }
 }  // namespace
+
+int neo_hip::create_handle(int channels, int block, int partitions, int device, int method, hipStream_t stream,
+                           neo_hip_upols** out)
+{
+    return create_convolver(channels, block, partitions, device, method >= 1, method == 2, nullptr, out, stream);
+}
 
 extern "C" {
 
@@ -674,7 +701,8 @@ NEO_HIP_API int neo_hip_upols_destroy(neo_hip_upols* h)
 {
     if (!h) return NEO_HIP_OK;
     device_guard g(h->device);
-    (void)hipStreamSynchronize(h->stream);
+    (void)persist_stop(h);
+    (void)setup_join(h);
     destroy(h);
     return NEO_HIP_OK;
 }
@@ -694,7 +722,7 @@ NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h)
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     device_guard g(h->device);
     if (int rc = persist_stop(h)) return rc;
-    NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
+    if (int rc = setup_join(h)) return rc;  // after this handle's steps on any stream
     int rc = reset_state(h, h->stream);
     if (rc) return rc;
     NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
@@ -707,13 +735,13 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
     device_guard g(h->device);
     if (g.rc) return g.rc;
     if (int rc = persist_stop(h)) return rc;
-    NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
+    if (int rc = setup_join(h, is_device != 0)) return rc;  // after this handle's steps (and a device filter's producer)
     const int64_t rows = int64_t(h->C) * h->P;
     const size_t bytes = size_t(rows) * size_t(h->B + 1) * sizeof(cf);
     const cf* src = static_cast<const cf*>(filter);
     cf* tmp = nullptr;
     if (!is_device) {
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp), bytes));
+        if (int rc = dalloc(&tmp, bytes)) return rc;
         NEO_HIP_CHECK(hipMemcpyAsync(tmp, filter, bytes, hipMemcpyHostToDevice, h->stream));
         src = tmp;
     }
@@ -721,7 +749,7 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
     lvl_filter_changed(h);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
-    if (tmp) (void)hipFree(tmp);
+    dfree(tmp);  // the stream was joined above
     return rc;
 }
 
@@ -735,10 +763,10 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
     device_guard g(h->device);
     if (g.rc) return g.rc;
     if (int rc = persist_stop(h)) return rc;
-    NEO_HIP_CHECK(hipDeviceSynchronize());  // setup calls order after all prior work, any stream
+    if (int rc = setup_join(h, is_device != 0)) return rc;  // after this handle's steps (and a device IR's producer)
     const size_t bytes = size_t(h->C) * size_t(length) * sizeof(float);
     float* d = nullptr;
-    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), bytes));
+    if (int rc = dalloc(&d, bytes)) return rc;
     int rc = NEO_HIP_OK;
     if (hipMemcpyAsync(d, ir, bytes, is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream) !=
         hipSuccess)
@@ -748,7 +776,7 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
     lvl_filter_changed(h);
     if (!rc) rc = reset_state(h, h->stream);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
-    (void)hipFree(d);
+    dfree(d);
     return rc;
 }
 
@@ -794,9 +822,7 @@ NEO_HIP_API int neo_hip_upols_process(neo_hip_upols* h, float* io, int io_is_dev
     const bool staged = !dio || (reinterpret_cast<uintptr_t>(dio) & 15);
     if (staged) {
         if (!h->io_host) {
-            NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->io_host), bytes,
-                                        hipHostMallocMapped | hipHostMallocCoherent));
-            NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->io), h->io_host, 0));
+            if (int rc = halloc(reinterpret_cast<void**>(&h->io_host), reinterpret_cast<void**>(&h->io), bytes)) return rc;
         }
         std::memcpy(h->io_host, io, bytes);
         dio = h->io;
@@ -822,14 +848,15 @@ NEO_HIP_API int neo_hip_upols_process_samples(neo_hip_upols* h, const float* in,
     // host I/O: pinned staging (grown on demand), 1-D copies, synchronous like process()
     const size_t count = size_t(h->C) * size_t(num_samples);
     if (count > h->samples_cap) {
-        (void)hipFree(h->samples_dev);
-        if (h->samples_host) (void)hipHostFree(h->samples_host);
+        NEO_HIP_CHECK(hipStreamSynchronize(s));  // no queued work on the old staging
+        dfree(h->samples_dev);
+        hfree(h->samples_host);
         h->samples_dev = nullptr;
         h->samples_host = nullptr;
         h->samples_cap = 0;
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->samples_dev), count * sizeof(float)));
-        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->samples_host), count * sizeof(float),
-                                    hipHostMallocDefault));
+        if (int rc = dalloc(&h->samples_dev, count * sizeof(float))) return rc;
+        void* dmap = nullptr;  // not used: the samples go by DMA
+        if (int rc = halloc(reinterpret_cast<void**>(&h->samples_host), &dmap, count * sizeof(float))) return rc;
         h->samples_cap = count;
     }
     for (int c = 0; c < h->C; ++c)
@@ -879,6 +906,7 @@ NEO_HIP_API int neo_hip_upols_set_paced(neo_hip_upols* h, int enable)
     device_guard g(h->device);
     if (g.rc) return g.rc;
     if (bool(enable) == h->paced) return NEO_HIP_OK;
+    if (int rc = persist_stop(h)) return rc;  // a resident latency-mode kernel leaves first (lv_n restarts)
     if (int rc = lvl_join(h, h->stream)) return rc;
     NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
     h->paced = enable != 0;
@@ -894,9 +922,7 @@ NEO_HIP_API int neo_hip_upols_set_persistent(neo_hip_upols* h, int enable, doubl
     if (enable) {
         if (const char* why = persist_ineligible(h)) return fail(NEO_HIP_EINVAL, "latency mode: %s", why);
         if (!(idle_ms > 0.0 && idle_ms <= 10000.0)) return fail(NEO_HIP_EINVAL, "idle_ms must be in (0, 10000]");
-        NEO_HIP_CHECK(hipDeviceSynchronize());  // steps queued on any stream come first
-        if (int rc = lvl_join(h, h->stream)) return rc;
-        NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
+        if (int rc = setup_join(h)) return rc;  // this handle's steps queued on any stream come first
         h->ps_idle_ms = idle_ms;
         h->persist = true;
         h->ps_valid = false;  // the persistent schedule primes the levels at its first block

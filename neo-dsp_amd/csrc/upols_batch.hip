@@ -427,11 +427,9 @@ int launch_batch_mac(const upols_t* h, int T, hipStream_t s)
 static int batch_buffers(upols_t* h)
 {
     if (!h->part_b) {
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->part_b),
-                                size_t(h->C) * h->Sb * kMaxBatch * h->B * sizeof(cf)));
-        if (h->ola && hipMalloc(reinterpret_cast<void**>(&h->tail), size_t(h->C) * kMaxBatch * h->B * sizeof(float)) !=
-                          hipSuccess) {
-            (void)hipFree(h->part_b);
+        if (int rc = dalloc(&h->part_b, size_t(h->C) * h->Sb * kMaxBatch * h->B * sizeof(cf))) return rc;
+        if (h->ola && dalloc(&h->tail, size_t(h->C) * kMaxBatch * h->B * sizeof(float))) {
+            dfree(h->part_b);
             h->part_b = nullptr;
             return fail(NEO_HIP_ENOMEM, "batched OLA tail allocation failed");
         }

@@ -40,6 +40,38 @@
 #include <mutex>
 #include <vector>
 
+#ifdef NEO_GROUP_PROBE  // diagnostic builds (tools/build_variant.sh): where a coalesced frame's time goes
+#include <chrono>
+#include <cstdio>
+namespace {
+struct group_probe {
+    // leader: copy in, prev backup, launch, wait, copy out; member: compare, copy out, redo;
+    // whole call (coalesced); per-sample medians
+    static constexpr int K = 9;
+    std::vector<double> v[K];
+    ~group_probe()
+    {
+        const char* names[K] = {"lead_copy_in", "lead_prev_backup", "lead_launch", "lead_wait", "lead_copy_out",
+                                "member_cmp", "member_copy", "member_redo", "call_total"};
+        std::fprintf(stderr, "{\"group_probe_us\": {");
+        for (int k = 0; k < K; ++k) {
+            auto& x = v[k];
+            std::sort(x.begin(), x.end());
+            const double med = x.empty() ? 0.0 : x[x.size() / 2], p90 = x.empty() ? 0.0 : x[x.size() * 9 / 10];
+            std::fprintf(stderr, "%s\"%s\": [%.3f, %.3f, %zu]", k ? ", " : "", names[k], med, p90, x.size());
+        }
+        std::fprintf(stderr, "}}\n");
+    }
+} g_probe;
+inline double probe_now() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+}  // namespace
+#define NEO_GP_T(v) const double v = probe_now()
+#define NEO_GP_ADD(k, t0) g_probe.v[k].push_back(probe_now() - (t0))
+#else
+#define NEO_GP_T(v)
+#define NEO_GP_ADD(k, t0)
+#endif
+
 namespace {
 using neo_hip::cf;
 using neo_hip::fail;
@@ -108,9 +140,9 @@ void free_shared(group_t* g)
 {
     if (g->shared) neo_hip_upols_destroy(g->shared);
     g->shared = nullptr;
-    if (g->in_pin) (void)hipHostFree(g->in_pin);
-    if (g->out_pin) (void)hipHostFree(g->out_pin);
-    (void)hipFree(g->prev_bak);
+    neo_hip::hfree(g->in_pin);
+    neo_hip::hfree(g->out_pin);
+    neo_hip::dfree(g->prev_bak);
     g->in_pin = g->out_pin = g->in_dev = g->out_dev = g->prev_bak = nullptr;
     g->slot_member.clear();
 }
@@ -118,7 +150,7 @@ void free_shared(group_t* g)
 int make_own(group_t* g, member& x)
 {
     if (x.own) return NEO_HIP_OK;
-    return neo_hip_upols_create_ex(1, g->B, g->P, g->device, g->method, nullptr, &x.own);
+    return neo_hip::create_handle(1, g->B, g->P, g->device, g->method, g->stream, &x.own);  // on the group's stream
 }
 
 // the B samples at p lie in a range the owner registered
@@ -134,14 +166,13 @@ bool registered(const group_t* g, const float* p)
 int coalesce(group_t* g)
 {
     const int C = live_count(g);
-    int rc = neo_hip_upols_create_ex(C, g->B, g->P, g->device, g->method, nullptr, &g->shared);
+    int rc = neo_hip::create_handle(C, g->B, g->P, g->device, g->method, g->stream, &g->shared);
     if (rc) return rc;
     const size_t io = size_t(C) * size_t(g->B) * sizeof(float);
-    NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->in_pin), io, hipHostMallocMapped | hipHostMallocCoherent));
-    NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->out_pin), io, hipHostMallocMapped | hipHostMallocCoherent));
-    NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g->in_dev), g->in_pin, 0));
-    NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g->out_dev), g->out_pin, 0));
-    NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&g->prev_bak), io));
+    if ((rc = neo_hip::halloc(reinterpret_cast<void**>(&g->in_pin), reinterpret_cast<void**>(&g->in_dev), io)) ||
+        (rc = neo_hip::halloc(reinterpret_cast<void**>(&g->out_pin), reinterpret_cast<void**>(&g->out_dev), io)) ||
+        (rc = neo_hip::dalloc(&g->prev_bak, io)))
+        return rc;
     neo_hip_upols* sh = g->shared;
     int c = 0, wpos = -1;
     for (int i = 0; i < int(g->m.size()); ++i) {
@@ -213,9 +244,9 @@ int call_independent(group_t* g, int i, float* io)
     // the block through the group's own mapped staging, on the group's stream: no per-call
     // pointer query of the caller's buffer, no per-member stream or staging
     if (!g->stage_pin) {
-        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->stage_pin), size_t(g->B) * sizeof(float),
-                                    hipHostMallocMapped | hipHostMallocCoherent));
-        NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g->stage_dev), g->stage_pin, 0));
+        if (int rc = neo_hip::halloc(reinterpret_cast<void**>(&g->stage_pin), reinterpret_cast<void**>(&g->stage_dev),
+                                     size_t(g->B) * sizeof(float)))
+            return rc;
     }
     const size_t bb = size_t(g->B) * sizeof(float);
     std::memcpy(g->stage_pin, io, bb);
@@ -250,6 +281,16 @@ int call_independent(group_t* g, int i, float* io)
     return NEO_HIP_OK;
 }
 
+// the output block of shared-handle channel `slot` into the CPU caches ahead of its member's call
+// (the plugin calls the members in order): the GPU wrote it to host memory over PCIe, so the
+// member's copy would otherwise stall on DRAM (0.3 us per 2 KB block on MI355X boxes)
+inline void prefetch_output(const group_t* g, int slot)
+{
+    if (slot >= int(g->slot_member.size())) return;
+    const char* p = reinterpret_cast<const char*>(g->out_pin + int64_t(slot) * g->B);
+    for (size_t k = 0; k < size_t(g->B) * sizeof(float); k += 64) __builtin_prefetch(p + k, 0, 3);
+}
+
 // coalesced mode: the leader's step over every member, or a later member's commit / redo
 int call_coalesced(group_t* g, int i, float* io)
 {
@@ -259,7 +300,10 @@ int call_coalesced(group_t* g, int i, float* io)
     if (x.pending) {
         float* spec_in = g->in_pin + int64_t(x.slot) * g->B;
         float* out = g->out_pin + int64_t(x.slot) * g->B;
-        if (std::memcmp(io, spec_in, bb) != 0) {  // the caller's block differs: this channel's step again
+        NEO_GP_T(tc);
+        const bool differs = std::memcmp(io, spec_in, bb) != 0;
+        NEO_GP_ADD(5, tc);
+        if (differs) {  // the caller's block differs: this channel's step again
             std::memcpy(spec_in, io, bb);
             NEO_HIP_CHECK(hipMemcpyAsync(sh->prev + int64_t(x.slot) * g->B, g->prev_bak + int64_t(x.slot) * g->B, bb,
                                          hipMemcpyDeviceToDevice, g->stream));
@@ -267,8 +311,12 @@ int call_coalesced(group_t* g, int i, float* io)
                                                 g->out_dev + int64_t(x.slot) * g->B, g->stream);
             if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
             ++g->stat_redos;
+            NEO_GP_ADD(7, tc);
         }
+        NEO_GP_T(tm);
         std::memcpy(io, out, bb);
+        NEO_GP_ADD(6, tm);
+        prefetch_output(g, x.slot + 2);
         x.pending = false;
         x.io_last = io;
         --g->npending;
@@ -287,15 +335,27 @@ int call_coalesced(group_t* g, int i, float* io)
             if (rc) return rc;
             return call_independent(g, i, io);
         }
+    NEO_GP_T(t0);
     for (const auto& y : g->m)
         if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
+    NEO_GP_ADD(0, t0);
+    NEO_GP_T(t1);
     NEO_HIP_CHECK(hipMemcpyAsync(g->prev_bak, sh->prev, size_t(sh->C) * bb, hipMemcpyDeviceToDevice, g->stream));
+    NEO_GP_ADD(1, t1);
+    NEO_GP_T(t2);
     g->step_w = sh->wpos;
     int rc = neo_hip::launch_levels(sh, g->in_dev, g->B, g->out_dev, g->B, g->stream);
+    NEO_GP_ADD(2, t2);
+    NEO_GP_T(t3);
     if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
+    NEO_GP_ADD(3, t3);
     g->step_n = sh->lv_n - 1;
     ++g->stat_steps;
+    NEO_GP_T(t4);
     std::memcpy(io, g->out_pin + int64_t(x.slot) * g->B, bb);
+    NEO_GP_ADD(4, t4);
+    prefetch_output(g, x.slot + 1);  // the next members' outputs, written over PCIe: not in any CPU cache
+    prefetch_output(g, x.slot + 2);
     x.io_last = io;
     for (auto& y : g->m) {
         if (!y.live) continue;
@@ -341,7 +401,7 @@ NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
     free_shared(g);
     for (auto& x : g->m)
         if (x.own) neo_hip_upols_destroy(x.own);
-    if (g->stage_pin) (void)hipHostFree(g->stage_pin);
+    neo_hip::hfree(g->stage_pin);
     (void)hipStreamDestroy(g->stream);
     delete g;
     return NEO_HIP_OK;
@@ -424,7 +484,10 @@ NEO_HIP_API int neo_hip_upols_group_process(neo_hip_upols_group* g, int id, floa
     neo_hip::device_guard dg(g->device);
     if (dg.rc) return dg.rc;
     ++g->stat_calls;
-    return g->coalesced ? call_coalesced(g, id, io) : call_independent(g, id, io);
+    NEO_GP_T(t0);
+    const int rc = g->coalesced ? call_coalesced(g, id, io) : call_independent(g, id, io);
+    if (g->coalesced) NEO_GP_ADD(8, t0);
+    return rc;
 }
 
 NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int id)

@@ -152,12 +152,31 @@ struct neo_hip_upols {
     int64_t ps_n0 = 0;                         // first step of the running kernel
     int64_t ps_launches = 0;                   // persistent launches so far (idle timeouts relaunch)
     double ps_idle_ms = 50.0;                  // the kernel leaves after this long without a block
+    // streams the step calls ran on since the last setup call (setup_join waits for these, not for
+    // the device: another handle's resident latency-mode kernel must not stall a setup call); a
+    // stream given to a step call must stay valid until the handle's next setup call or destroy
+    static constexpr int kUsedStreams = 4;
+    hipStream_t used_s[kUsedStreams] = {};
+    int n_used = 0;
+    bool used_many = false;  // more distinct streams than kUsedStreams: setup waits for the device
 };
 
 
 namespace neo_hip {
 
 using upols_t = neo_hip_upols;
+
+inline void note_stream(upols_t* h, hipStream_t s)
+{
+    for (int i = 0; i < h->n_used; ++i)
+        if (h->used_s[i] == s) return;
+    if (h->n_used < upols_t::kUsedStreams) h->used_s[h->n_used++] = s;
+    else h->used_many = true;
+}
+// order a setup call (filter change, reset, mode switch, destroy) after every step of this handle:
+// the streams its step calls ran on, its background stream, its own stream; device_input: also
+// after work on the null stream (a device-resident filter or impulse produced there)
+int setup_join(upols_t* h, bool device_input = false);
 
 inline bool valid_block(int b) { return b >= 16 && b <= 4096 && (b & (b - 1)) == 0; }
 
@@ -196,6 +215,10 @@ constexpr int batch_t(int B, int NB, int want)
 
 inline int batch_blocks(const upols_t* h) { return batch_t(h->B, h->bNB, h->bT); }
 
+// a handle with default options whose setup and host-I/O work runs on `stream` (a group's; not
+// destroyed with the handle) instead of one of the device's shared streams (upols.hip)
+int create_handle(int channels, int block, int partitions, int device, int method, hipStream_t stream,
+                  neo_hip_upols** out);
 // upols_batch.hip: T whole blocks in one pass over the filter and the FDL
 int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int T, hipStream_t s);
 // Timing (neo_hip_upols_set_timing): the next event group of nev events if this launch

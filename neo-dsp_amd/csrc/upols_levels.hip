@@ -1545,13 +1545,13 @@ static int lvl_buffers(upols_t* h)
     const size_t C = size_t(h->C), B = size_t(h->B);
     std::vector<void**> got;
     auto alloc = [&](void** p, size_t bytes) {
-        if (hipMalloc(p, bytes) != hipSuccess) return false;
+        if (dalloc(p, bytes) != NEO_HIP_OK) return false;
         got.push_back(p);
         return true;
     };
     auto undo = [&](const char* what, size_t bytes) {
         for (void** p : got) {
-            (void)hipFree(*p);
+            dfree(*p);
             *p = nullptr;
         }
         return fail(NEO_HIP_ENOMEM, "level pipeline: allocation of %s (%zu bytes) failed", what, bytes);
@@ -1570,10 +1570,7 @@ static int lvl_buffers(upols_t* h)
             if (!alloc(reinterpret_cast<void**>(&h->fv_acc), accb)) return undo("far partial sums", accb);
         }
         if (!alloc(reinterpret_cast<void**>(&h->fv_ff), ffb)) return undo("far field", ffb);
-        if (!alloc(reinterpret_cast<void**>(&h->fv_tw), kFN * sizeof(cf))) return undo("far twiddles", kFN * sizeof(cf));
-        const auto t = make_twiddle_table(kFN);
-        if (hipMemcpy(h->fv_tw, t.data(), kFN * sizeof(cf), hipMemcpyHostToDevice) != hipSuccess)
-            return undo("far twiddle upload", kFN * sizeof(cf));
+        if (shared_far_tw(&h->fv_tw) != NEO_HIP_OK) return undo("far twiddles", kFN * sizeof(cf));
         h->fv_dirty = true;
     }
     h->lv_ready = true;
@@ -1593,13 +1590,14 @@ void lvl_free(upols_t* h)
         h->bg_busy = false;
     }
     for (auto& p : h->lv_slab) {
-        (void)hipFree(p);
+        dfree(p);
         p = nullptr;
     }
-    for (cf** p : {&h->fv_hf, &h->fv_xf, &h->fv_ff, &h->fv_tw, &h->fv_acc}) {
-        (void)hipFree(*p);
+    for (cf** p : {&h->fv_hf, &h->fv_xf, &h->fv_ff, &h->fv_acc}) {
+        dfree(*p);
         *p = nullptr;
     }
+    h->fv_tw = nullptr;  // shared (shared_far_tw)
     h->lv_ready = false;
 }
 
@@ -2586,12 +2584,11 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
 {
     if (!h->ps_stream) {
         NEO_HIP_CHECK(hipStreamCreateWithFlags(&h->ps_stream, hipStreamNonBlocking));
-        NEO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->ps_mb), sizeof(persist_mb),
-                                    hipHostMallocMapped | hipHostMallocCoherent));
-        NEO_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->ps_mb_dev), h->ps_mb, 0));
+        if (int rc = halloc(reinterpret_cast<void**>(&h->ps_mb), reinterpret_cast<void**>(&h->ps_mb_dev), sizeof(persist_mb)))
+            return rc;
         std::memset(h->ps_mb, 0, sizeof(persist_mb));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_tl), 10 * kPsRing * sizeof(unsigned long long)));
-        NEO_HIP_CHECK(hipMemset(h->ps_tl, 0, 10 * kPsRing * sizeof(unsigned long long)));
+        if (int rc = dalloc(&h->ps_tl, 10 * kPsRing * sizeof(unsigned long long))) return rc;
+        NEO_HIP_CHECK(hipMemsetAsync(h->ps_tl, 0, 10 * kPsRing * sizeof(unsigned long long), h->ps_stream));
     }
     if (int rc = lvl_buffers(h)) return rc;
     if (!h->ps_valid || h->lv_n < 0) {  // window 0 of every level, from this block on
@@ -2621,9 +2618,9 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     }
     const int nsl = pa.wg0[h->lv.n];
     if (h->ps_nslices < nsl || !h->ps_flags) {
-        (void)hipFree(h->ps_flags);
+        dfree(h->ps_flags);
         h->ps_flags = nullptr;
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->ps_flags), size_t(kPsFlagSlices + nsl) * sizeof(int64_t)));
+        if (int rc = dalloc(&h->ps_flags, size_t(kPsFlagSlices + nsl) * sizeof(int64_t))) return rc;
         h->ps_nslices = nsl;
     }
     pa.n0 = h->lv_n;
@@ -2632,7 +2629,9 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     pa.flags = h->ps_flags;
     pa.tl = h->ps_tl;
     pa.idle_ticks = (long long)(h->ps_idle_ms * 1e5);  // wall_clock64: 100 MHz
-    pa.dead_ticks = 200000000LL;                        // 2 s: a wait that long is a fault, not a schedule
+    // 2 s past the idle limit: a wait that long is a fault, not a schedule (the slice and later
+    // block workgroups wait for the host's next record too, up to the idle limit)
+    pa.dead_ticks = pa.idle_ticks + 200000000LL;
     std::vector<int64_t> init(size_t(kPsFlagSlices + nsl), 0);  // quit, arrivals, records: 0
     init[0] = pa.n0 - 1;                                          // blk_done
     init[kPsFlagGo] = pa.n0 - 1;
@@ -2640,6 +2639,14 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     NEO_HIP_CHECK(hipMemcpyAsync(h->ps_flags, init.data(), init.size() * sizeof(int64_t), hipMemcpyHostToDevice,
                                  h->ps_stream));
     NEO_HIP_CHECK(hipStreamSynchronize(h->ps_stream));  // the prime and the flags before the first record
+    // no record of an earlier launch may match a step of this one: a restarted schedule (n0 = 0
+    // after a reset, filter change or mode toggle) reuses the lap tags of the run before, so every
+    // slot is cleared to tag 0, which no step carries (ps_tag is 1..15). The kernel is not running
+    // and the host writes step n0's record only after this.
+    for (auto& r : h->ps_mb->rec) {
+        __atomic_store_n(&r.in, uint64_t(0), __ATOMIC_RELAXED);
+        __atomic_store_n(&r.out, uint64_t(0), __ATOMIC_RELAXED);
+    }
     h->ps_mb->stop = 0;
     h->ps_mb->err = 0;
     h->ps_mb->done = pa.n0;
@@ -2661,16 +2668,35 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     return NEO_HIP_OK;
 }
 
-// the running kernel (if any) leaves; ps_valid stays: a relaunch continues the schedule
+// a step that was handed to the kernel may not have completed: the FDL ring and the level slabs
+// no longer follow the schedule, so the next call re-primes from its own block (persist_stop's
+// semantics) instead of continuing with a missing row
+static void persist_invalidate(upols_t* h)
+{
+    h->ps_valid = false;
+    h->lv_n = -1;
+}
+
+// the running kernel (if any) leaves; ps_valid stays: a relaunch continues the schedule (unless
+// the kernel failed)
 static int persist_join(upols_t* h)
 {
     if (!h->ps_running) return NEO_HIP_OK;
     __atomic_store_n(&h->ps_mb->stop, 1, __ATOMIC_SEQ_CST);
     const hipError_t e = hipStreamSynchronize(h->ps_stream);
     h->ps_running = false;
-    if (e != hipSuccess) return fail(NEO_HIP_ERUNTIME, "persistent kernel: %s", hipGetErrorString(e));
-    if (__atomic_load_n(&h->ps_mb->err, __ATOMIC_SEQ_CST))
+    if (e != hipSuccess) {
+        persist_invalidate(h);
+        return fail(NEO_HIP_ERUNTIME, "persistent kernel: %s", hipGetErrorString(e));
+    }
+    if (__atomic_load_n(&h->ps_mb->err, __ATOMIC_SEQ_CST)) {
+        persist_invalidate(h);
         return fail(NEO_HIP_ERUNTIME, "persistent kernel: a wait passed its deadline");
+    }
+    if (__atomic_load_n(&h->ps_mb->done, __ATOMIC_SEQ_CST) < h->lv_n) {
+        persist_invalidate(h);  // left (stop, idle limit) with records not yet stepped
+        return fail(NEO_HIP_ERUNTIME, "persistent kernel left before step %lld", (long long)h->lv_n - 1);
+    }
     return NEO_HIP_OK;
 }
 
@@ -2687,6 +2713,8 @@ int persist_stop(upols_t* h)
 int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t nblocks)
 {
     if (const char* why = persist_ineligible(h)) return fail(NEO_HIP_EINVAL, "latency mode: %s", why);
+    if (h->ps_running && (h->lv_n < 0 || !h->ps_valid))
+        if (int rc = persist_join(h)) return rc;  // the schedule restarts: relaunch after the prime
     if (h->C > 1 && (ld_in != h->ps_ld_in || ld_out != h->ps_ld_out) && h->ps_running)
         if (int rc = persist_join(h)) return rc;  // another channel stride: relaunch with it
     if (h->ps_running && !__atomic_load_n(&h->ps_mb->alive, __ATOMIC_ACQUIRE))
@@ -2720,6 +2748,7 @@ int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int6
         }
         if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
             __atomic_store_n(&mb->stop, 1, __ATOMIC_SEQ_CST);
+            persist_invalidate(h);  // the next call joins the kernel and re-primes
             return fail(NEO_HIP_ERUNTIME, "persistent kernel: no progress for 5 s");
         }
     }

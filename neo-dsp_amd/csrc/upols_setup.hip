@@ -225,7 +225,7 @@ NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t
     const size_t out_bytes = size_t(channels) * size_t(P) * size_t(block + 1) * sizeof(cf);
     hipStream_t s = nullptr;
     if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     cf* tw = nullptr;
     const float* d_ir = ir;
     float* tmp_in = nullptr;
@@ -248,7 +248,6 @@ NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t
         (void)hipFree(d_out);
     }
     (void)hipFree(tw);
-    (void)hipStreamDestroy(s);
     return rc;
 }
 
@@ -260,7 +259,7 @@ NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t lengt
     if (g.rc) return g.rc;
     hipStream_t s = nullptr;
     if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
-    NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     const size_t bytes = size_t(channels) * size_t(length) * sizeof(float);
     float* d = ir;
     int rc = NEO_HIP_OK;
@@ -274,7 +273,6 @@ NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t lengt
         rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     if (!is_device && d) (void)hipFree(d);
-    (void)hipStreamDestroy(s);
     return rc;
 }
 

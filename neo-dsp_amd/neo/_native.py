@@ -38,6 +38,8 @@ SIGNATURES = {
     "neo_hip_device_count": (_i, [ctypes.POINTER(_i)]),
     "neo_hip_host_register": (_i, [_vp, _i64]),
     "neo_hip_host_unregister": (_i, [_vp]),
+    "neo_hip_memory_trim": (_i, [_i]),
+    "neo_hip_memory_info": (_i, [_i, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "neo_hip_fft_max_order": (_i, []),
     "neo_hip_fft_plan_create": (_i, [_i, _i64, _i, _i, ctypes.POINTER(_vp)]),
     "neo_hip_fft_plan_destroy": (_i, [_vp]),

@@ -163,3 +163,59 @@ def test_latency_mode_rejects_other_shapes(neo_gpu):
         with pytest.raises(RuntimeError, match="latency mode"):
             c.set_persistent(True)
         c.close()
+
+
+@pytest.mark.parametrize("how", ["reset", "filter", "paced"])
+def test_latency_mode_restart_after_short_run(neo_gpu, oracle, how):
+    """A schedule that restarts before its first lap of the mailbox (10 one-block calls, then
+    reset / set_filter / a set_paced toggle, then 10 more): no record of the first run may be
+    taken for a step of the second (every step below 64 carries the same lap tag). The kernel
+    stays resident across the setup call (idle limit 3 s), so only the cleared mailbox keeps
+    the second run's steps apart. After reset / set_filter the second run equals the oracle on
+    its blocks alone; after the paced toggle (state kept) the whole 20 blocks do."""
+    torch = pytest.importorskip("torch")
+    C, B, P = 1, 256, 100
+    (pc, _), parts = _pair(neo_gpu, oracle, C, B, P, 5700)
+    pc.set_persistent(True, idle_ms=3000.0)
+    x = np.stack([oracle.noise(5800, B * 20)])
+    first = _run(pc, x[:, : 10 * B], B, torch)
+    assert peak_err(first, oracle.dense_convolve(x[:, : 10 * B], parts)) <= TOL
+    if how == "reset":
+        pc.reset()
+    elif how == "filter":
+        pc.filter(parts)
+    else:
+        pc.set_paced(True)
+    pc.set_persistent(True, idle_ms=3000.0)
+    second = _run(pc, x[:, 10 * B:], B, torch)
+    if how == "paced":
+        ref = oracle.dense_convolve(x, parts)[:, 10 * B:]
+    else:
+        ref = oracle.dense_convolve(x[:, 10 * B:], parts)
+    assert peak_err(second, ref) <= TOL
+    pc.set_persistent(False)
+    pc.close()
+
+
+def test_setup_call_does_not_wait_for_another_latency_kernel(neo_gpu, oracle):
+    """Two handles: A in latency mode with its kernel resident (idle limit 3 s); a filter change
+    and a reset on B return in well under that (setup calls join B's own streams, not the
+    device), and A keeps stepping correctly afterwards."""
+    torch = pytest.importorskip("torch")
+    C, B, P = 1, 256, 100
+    (pa, pb), parts = _pair(neo_gpu, oracle, C, B, P, 5900)
+    pa.set_persistent(True, idle_ms=3000.0)
+    x = np.stack([oracle.noise(6000, B * 8)])
+    first = _run(pa, x[:, : 4 * B], B, torch)
+    assert pa.persistent_info()["running"]
+    t0 = time.perf_counter()
+    pb.filter(parts)
+    pb.reset()
+    dt = time.perf_counter() - t0
+    assert dt < 1.0, f"setup on another handle waited {dt:.2f} s for the resident kernel"
+    second = _run(pa, x[:, 4 * B:], B, torch)
+    got = np.concatenate([first, second], axis=1)
+    assert peak_err(got, oracle.dense_convolve(x, parts)) <= TOL
+    pa.set_persistent(False)
+    pa.close()
+    pb.close()

@@ -286,14 +286,36 @@ def _full_size_streaming(neo_gpu, oracle, C, B, L, nb, seed, chans, far_group=No
     # one normalization factor over all channels (normalize_impulse.hpp:21-30)
     irh = oracle.normalize_impulse(ir.cpu().numpy())
     irc = {c: irh[c:c + 1].copy() for c in chans}
-    del ir, irh
+    del irh
+    tail = 128 * B  # the last far window (steady state, the ring wrapped many times)
+    x_in = x[:, -(P + 128) * B:].clone()  # the blocks the plain step needs for that window
     conv.process_blocks(x)
     torch.cuda.synchronize()
+    conv.close()
+    refs = {}
     for c in chans:
         ref = oracle.dense_convolve(xh[c], oracle.uniform_partition(irc[c], B))
+        refs[c] = ref[0, -tail:]
         assert peak_err(x[c].cpu().numpy(), ref[0]) <= TOL, c
-        # the last far window alone (steady state, ring wrapped many times)
-        assert peak_err(x[c, -128 * B:].cpu().numpy(), ref[0, -128 * B:]) <= TOL, c
+        assert peak_err(x[c, -tail:].cpu().numpy(), refs[c]) <= TOL, c
+    # EVERY channel over the last far window against the plain step (k_upols_step: one pass over
+    # all P partitions per block; test_random_ir_vs_oracle, and the sampled channels below), run on the same input: a
+    # fault confined to channels the oracle does not sample cannot pass. The plain handle starts
+    # from zero state P + 128 blocks before the end, so its last 128 blocks see exactly the
+    # streaming run's FDL contents (every partition covered by real rows).
+    plain = neo_gpu.UpolsConvolver(C, B, P, options={"levels": 0})
+    assert not plain.ahead_info()[0]
+    plain.set_impulse(ir, normalize=True)
+    plain.set_batch(False)
+    del ir
+    plain.process_blocks(x_in)
+    torch.cuda.synchronize()
+    plain.close()
+    for c in chans:
+        assert peak_err(x_in[c, -tail:].cpu().numpy(), refs[c]) <= TOL, c
+    a, b = x[:, -tail:], x_in[:, -tail:]
+    err = (torch.amax(torch.abs(a - b), dim=1) / torch.amax(torch.abs(b), dim=1)).cpu().numpy()
+    assert err.max() <= TOL, (int(err.argmax()), float(err.max()))
 
 
 @pytest.mark.parametrize("far_level,form", [(-1, 1), (2, 2)])
