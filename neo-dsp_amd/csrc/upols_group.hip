@@ -304,6 +304,8 @@ int call_coalesced(group_t* g, int i, float* io)
         const bool differs = std::memcmp(io, spec_in, bb) != 0;
         NEO_GP_ADD(5, tc);
         if (differs) {  // the caller's block differs: this channel's step again
+            neo_hip::device_guard dg(g->device);  // the commit path alone makes no HIP call
+            if (dg.rc) return dg.rc;
             std::memcpy(spec_in, io, bb);
             NEO_HIP_CHECK(hipMemcpyAsync(sh->prev + int64_t(x.slot) * g->B, g->prev_bak + int64_t(x.slot) * g->B, bb,
                                          hipMemcpyDeviceToDevice, g->stream));
@@ -481,10 +483,15 @@ NEO_HIP_API int neo_hip_upols_group_process(neo_hip_upols_group* g, int id, floa
     if (!g || !io) return fail(NEO_HIP_EINVAL, "null group or block");
     std::lock_guard<std::mutex> lk(g->mu);
     if (!live_member(g, id)) return fail(NEO_HIP_EINVAL, "no such member");
-    neo_hip::device_guard dg(g->device);
-    if (dg.rc) return dg.rc;
     ++g->stat_calls;
     NEO_GP_T(t0);
+    if (g->coalesced && g->m[size_t(id)].pending) {  // a member's commit: no device guard (no HIP call)
+        const int rc = call_coalesced(g, id, io);
+        NEO_GP_ADD(8, t0);
+        return rc;
+    }
+    neo_hip::device_guard dg(g->device);
+    if (dg.rc) return dg.rc;
     const int rc = g->coalesced ? call_coalesced(g, id, io) : call_independent(g, id, io);
     if (g->coalesced) NEO_GP_ADD(8, t0);
     return rc;

@@ -2583,7 +2583,14 @@ static int persist_level_wgs(const upols_t* h, int l, int& U, int& UPW, int& JH)
 static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
 {
     if (!h->ps_stream) {
-        NEO_HIP_CHECK(hipStreamCreateWithFlags(&h->ps_stream, hipStreamNonBlocking));
+        // the most urgent priority: such a stream gets a hardware queue of its own. At the default
+        // priority it shares one of the process's GPU_MAX_HW_QUEUES (4) with other streams, whose
+        // work then queues behind the resident kernel until it leaves (idle limit): measured on
+        // MI355X, the third new torch stream waited 1.4 s behind a 1.5 s idle limit
+        // (tools/dbg_hwq.py; none waited with this priority)
+        int lo = 0, hi = 0;
+        NEO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        NEO_HIP_CHECK(hipStreamCreateWithPriority(&h->ps_stream, hipStreamNonBlocking, hi));
         if (int rc = halloc(reinterpret_cast<void**>(&h->ps_mb), reinterpret_cast<void**>(&h->ps_mb_dev), sizeof(persist_mb)))
             return rc;
         std::memset(h->ps_mb, 0, sizeof(persist_mb));

@@ -1,7 +1,8 @@
 // bench_create.cpp — diagnostic: what a one-channel convolver costs to bring up, phase by phase
 // (the group's switch from one shared handle to a handle per member pays this per member):
 // create, set_filter, the first streaming step (level buffers allocated, far segment spectra,
-// priming), a later step, destroy; median and max over N handles created one after another.
+// priming), a later step, destroy; median and max over N handles created one after another,
+// after one untimed warm-up handle.
 //   bench_create <N> [block] [partitions]
 #include <neo_hip.h>
 
@@ -21,6 +22,17 @@ int main(int argc, char** argv)
               P = argc > 3 ? std::atoi(argv[3]) : 938;
     std::vector<float> filt(size_t(P) * (B + 1) * 2, 0.0f), blk(size_t(B), 0.5f);
     filt[0] = 1.0f;
+    {  // warm-up, untimed: the HIP runtime's initialization and the first load of every kernel's
+       // code object happen once per process, not per handle
+        neo_hip_upols* w = nullptr;
+        if (neo_hip_upols_create_ex(1, B, P, 0, 0, nullptr, &w) || neo_hip_upols_set_filter(w, filt.data(), 0) ||
+            neo_hip_upols_set_batch(w, 0) || neo_hip_upols_process(w, blk.data(), 0, nullptr) ||
+            neo_hip_upols_process(w, blk.data(), 0, nullptr)) {
+            std::printf("{\"error\": \"%s\"}\n", neo_hip_last_error());
+            return 1;
+        }
+        neo_hip_upols_destroy(w);
+    }
     std::vector<neo_hip_upols*> h(size_t(N), nullptr);
     const char* names[5] = {"create", "set_filter", "first_step", "later_step", "destroy"};
     std::vector<std::vector<double>> t(5);

@@ -47,7 +47,7 @@ def test_pool_reuse_and_drain(neo_gpu, oracle):
         for c in hs:
             y = np.empty_like(x)
             for t in range(nb):
-                blk = np.ascontiguousarray(x[:, t * B:(t + 1) * B])
+                blk = x[:, t * B:(t + 1) * B].copy()  # a view of a one-row array is contiguous: copy
                 c(blk)
                 y[:, t * B:(t + 1) * B] = blk
         outs.append(y)

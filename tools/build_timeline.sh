@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/../neo-dsp_amd"
 make -s -j8
-F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -fvisibility=hidden"
+F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -fvisibility=hidden -ffp-contract=on"
 D=../tools/ab/${TL_NAME:-tl}
 mkdir -p $D
 /opt/rocm/bin/hipcc $F -DNEO_TIMELINE "$@" -c csrc/upols_levels.hip -o $D/upols_levels.o

@@ -7,7 +7,7 @@ N=$1; shift
 S=${SRC:-upols_levels}
 cd "$(dirname "$0")/../neo-dsp_amd"
 make -s -j8
-F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -fvisibility=hidden"
+F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -fvisibility=hidden -ffp-contract=on"
 mkdir -p ../tools/ab/$N
 /opt/rocm/bin/hipcc $F "$@" -c csrc/$S.hip -o ../tools/ab/$N/$S.o
 objs=$(ls build/*.o | grep -v "/$S.o")
