@@ -635,27 +635,32 @@ def run_upols(args, world, rank, local):
     torch.cuda.synchronize()
     conv.set_timing(False)
     st = np.array(conv.step_times())
-    paced = None
+    paced = paced2 = None
     if levels and G > 1 and not args.no_paced:
-        # the same round trip with the background work paced (neo_hip_upols_set_paced: one piece of
-        # the group's launch per call, each block after the piece of the call before): even calls
-        conv.set_paced(True)
-        warm()
-        prt = []
-        for _ in range(200):
-            t0 = time.perf_counter()
-            feed.run(1)
-            sobj.synchronize()
-            prt.append(time.perf_counter() - t0)
-        prt = np.array(prt) * 1e6
-        el_p = wall_region(args.steps)
-        paced = {"host_roundtrip_p50_us": max_over_ranks(float(np.percentile(prt, 50)), world),
-                 "host_roundtrip_p99_us": max_over_ranks(float(np.percentile(prt, 99)), world),
-                 "host_roundtrip_mean_us": max_over_ranks(float(prt.mean()), world),
-                 "value": samples / el_p / 1e6, "ms_per_step": el_p * 1e3 / args.steps,
-                 "note": "neo_hip_upols_set_paced: round trip as above; value = the timed steps back to back"}
-        conv.set_paced(False)
-        warm()
+        # the same round trip with the background work paced (neo_hip_upols_set_paced: the group's
+        # launch in pieces, each block that issues one after the piece before it): even calls.
+        # mode 1: a piece per call; mode 2: two pieces per group
+        def paced_run(mode):
+            conv.set_paced(mode)
+            warm()
+            prt = []
+            for _ in range(200):
+                t0 = time.perf_counter()
+                feed.run(1)
+                sobj.synchronize()
+                prt.append(time.perf_counter() - t0)
+            prt = np.array(prt) * 1e6
+            el_p = wall_region(args.steps)
+            conv.set_paced(0)
+            warm()
+            return {"host_roundtrip_p50_us": max_over_ranks(float(np.percentile(prt, 50)), world),
+                    "host_roundtrip_p99_us": max_over_ranks(float(np.percentile(prt, 99)), world),
+                    "host_roundtrip_mean_us": max_over_ranks(float(prt.mean()), world),
+                    "value": samples / el_p / 1e6, "ms_per_step": el_p * 1e3 / args.steps,
+                    "note": f"neo_hip_upols_set_paced({mode}): round trip as above; value = the timed steps back "
+                            "to back"}
+        paced = paced_run(1)
+        paced2 = paced_run(2)
     # steady state: one whole far window (128 steps = 32 step groups: every group's background
     # launch once, whatever their sizes), timed like the headline
     n_steady = 128
@@ -664,7 +669,7 @@ def run_upols(args, world, rank, local):
                "p99_ms": float(np.percentile(st, 99)), "max_ms": float(st.max()),
                "max_over_mean": float(st.max() / st.mean()),
                "host_roundtrip_p50_us": rt_p50, "host_roundtrip_p99_us": rt_p99, "host_roundtrip_mean_us": rt_mean,
-               "host_roundtrip_msamples_s": C_total * B / rt_mean, "paced": paced,
+               "host_roundtrip_msamples_s": C_total * B / rt_mean, "paced": paced, "paced_two_pieces": paced2,
                "note": "p50/p99/max: GPU time per step (HIP events around every step, which add their own records); "
                        "host_roundtrip: 200 device-resident single-block calls, each followed by a host wait for its "
                        "output before the next call (max over ranks)"}

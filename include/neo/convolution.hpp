@@ -207,6 +207,8 @@ struct upols_multichannel {
     }
     /// paced background work (neo_hip_upols_set_paced): an even cost per call with step groups
     auto paced(bool on) -> void { neo::hip::check(neo_hip_upols_set_paced(_h.get(), on ? 1 : 0)); }
+    /// the same with the group's background launch in two pieces (two cross-stream waits per group)
+    auto paced_two_pieces() -> void { neo::hip::check(neo_hip_upols_set_paced(_h.get(), 2)); }
 
     [[nodiscard]] auto channels() const noexcept { return _C; }
     [[nodiscard]] auto block_size() const noexcept { return _B; }

@@ -203,11 +203,13 @@ NEO_HIP_API int neo_hip_upols_level_plan(int partitions, int* a0, int* nlevels, 
  * the cycle into loads[loads_cap]. uniform != 0: equal parts and no offsets (for comparison). */
 NEO_HIP_API int neo_hip_upols_part_plan(int channels, int block, int partitions, int step_group, int uniform, int* phi,
                                         int* cycle, int* cuts, int cuts_cap, int* ncuts, double* loads, int loads_cap);
-/* Paced background work (step groups only; a no-op with one launch per block): the step group's
- * background launch is issued in G pieces, one per call, and every block waits for the piece of
- * the call before it, so no call waits for more than one piece of background work: the host round
- * trip per block is even (p99 near p50) instead of one call in 2 G paying for two groups' launches.
- * Same outputs; costs a cross-stream wait per call. The levels re-prime when it changes. */
+/* Paced background work (step groups only; a no-op with one launch per block): enable = 1 issues
+ * the step group's background launch in G pieces, one per call, and every block waits for the
+ * piece of the call before it; enable = 2 issues it in two pieces, at the group's calls 0 and
+ * G / 2, and those calls' blocks wait for the piece before. Either way no call waits for more
+ * than one piece of background work, so the host round trip per block is even (p99 near p50)
+ * instead of one call in 2 G paying for two groups' launches. Same outputs; costs one
+ * cross-stream wait per piece. 0 = off. The levels re-prime when it changes. */
 NEO_HIP_API int neo_hip_upols_set_paced(neo_hip_upols* h, int enable);
 /* Latency mode for latency-bound shapes (few channels, filters up to 256 partitions, blocks up
  * to 512; C3): ONE persistent kernel per handle steps every block. A call writes the block's

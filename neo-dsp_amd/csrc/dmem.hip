@@ -230,9 +230,9 @@ int shared_stream(hipStream_t* out)
     NEO_HIP_CHECK(hipGetDevice(&d));
     std::lock_guard<std::mutex> lk(g_mu);
     pool& p = g_pools[d];
-    hipStream_t& s = p.streams[p.next_stream++ % 4];
-    if (!s) NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
-    *out = s;
+    if (!p.streams[0])  // all four at the first request: the later handles never pay for one
+        for (auto& s : p.streams) NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    *out = p.streams[p.next_stream++ % 4];
     return NEO_HIP_OK;
 }
 

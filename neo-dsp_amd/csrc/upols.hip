@@ -905,11 +905,12 @@ NEO_HIP_API int neo_hip_upols_set_paced(neo_hip_upols* h, int enable)
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     device_guard g(h->device);
     if (g.rc) return g.rc;
-    if (bool(enable) == h->paced) return NEO_HIP_OK;
+    if (enable < 0 || enable > 2) return fail(NEO_HIP_EINVAL, "paced: 0 off, 1 a piece per call, 2 two pieces per group");
+    if (enable == h->paced) return NEO_HIP_OK;
     if (int rc = persist_stop(h)) return rc;  // a resident latency-mode kernel leaves first (lv_n restarts)
     if (int rc = lvl_join(h, h->stream)) return rc;
     NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
-    h->paced = enable != 0;
+    h->paced = enable;
     h->lv_n = -1;  // the levels re-prime: no group is half issued in the other form
     return NEO_HIP_OK;
 }

@@ -47,12 +47,13 @@ namespace {
 struct group_probe {
     // leader: copy in, prev backup, launch, wait, copy out; member: compare, copy out, redo;
     // whole call (coalesced); per-sample medians
-    static constexpr int K = 9;
+    static constexpr int K = 13;
     std::vector<double> v[K];
     ~group_probe()
     {
         const char* names[K] = {"lead_copy_in", "lead_prev_backup", "lead_launch", "lead_wait", "lead_copy_out",
-                                "member_cmp", "member_copy", "member_redo", "call_total"};
+                                "member_cmp", "member_copy", "member_redo", "call_total", "split_members",
+                                "split_sync", "split_free_shared", "coalesce_total"};
         std::fprintf(stderr, "{\"group_probe_us\": {");
         for (int k = 0; k < K; ++k) {
             auto& x = v[k];
@@ -165,6 +166,7 @@ bool registered(const group_t* g, const float* p)
 // independent -> coalesced: every live member's state into one shared handle
 int coalesce(group_t* g)
 {
+    NEO_GP_T(tc0);
     const int C = live_count(g);
     int rc = neo_hip::create_handle(C, g->B, g->P, g->device, g->method, g->stream, &g->shared);
     if (rc) return rc;
@@ -197,6 +199,7 @@ int coalesce(group_t* g)
     g->coalesced = true;
     g->npending = 0;
     ++g->stat_switches;
+    NEO_GP_ADD(12, tc0);
     return NEO_HIP_OK;
 }
 
@@ -206,6 +209,7 @@ int coalesce(group_t* g)
 int split(group_t* g)
 {
     neo_hip_upols* sh = g->shared;
+    NEO_GP_T(ts0);
     for (auto& x : g->m) {
         if (!x.live) continue;
         int rc = make_own(g, x);
@@ -222,8 +226,13 @@ int split(group_t* g)
         x.slot = -1;
         x.seen = false;
     }
+    NEO_GP_ADD(9, ts0);
+    NEO_GP_T(ts1);
     NEO_HIP_CHECK(hipStreamSynchronize(g->stream));
+    NEO_GP_ADD(10, ts1);
+    NEO_GP_T(ts2);
     free_shared(g);
+    NEO_GP_ADD(11, ts2);
     g->coalesced = false;
     g->npending = 0;
     g->nseen = 0;

@@ -104,8 +104,10 @@ struct neo_hip_upols {
     int sg = 1;
     hipStream_t bg = nullptr;
     hipEvent_t ev_blk = nullptr, ev_sl[2] = {}, ev_join = nullptr;
-    bool paced = false;            // neo_hip_upols_set_paced: the group's background launch in G per-call pieces
-    bool pace_prev = false;        // a piece was issued at the previous call (its event ev_pc[(n - 1) & 1])
+    int paced = 0;                 // neo_hip_upols_set_paced: the group's background launch in G per-call pieces
+                                   // (1) or in two pieces, at the group's calls 0 and G / 2 (2)
+    bool pace_prev = false;        // a piece was issued before (its event ev_pc[(pace_seq - 1) & 1])
+    int64_t pace_seq = 0;          // pieces issued since the levels primed
     hipEvent_t ev_pc[2] = {};
     bool bg_busy = false;  // slices enqueued on bg since the last join
     int64_t bg_launches = 0;

@@ -2243,6 +2243,7 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
         if ((rc = lvl_prime(h, s))) return rc;
         h->lv_n = 0;
         h->pace_prev = false;
+        h->pace_seq = 0;
     }
     const int64_t n = h->lv_n;
     const int G = h->sg;
@@ -2250,12 +2251,15 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     block_part(h, n, h->wpos, 0, h->C, in, ld_in, out, ld_out, a);
     block_levels(h, n, h->wpos, a);
     if (G > 1 && h->paced) {
-        // Paced (neo_hip_upols_set_paced): the group's background launch in G pieces, piece k at
-        // the group's call k (workgroups [k W / G, (k + 1) W / G) of the same launch: its
-        // workgroups are independent), and every block waits for the piece of the call before it.
-        // Then no block waits for more than one piece of background work (the last piece of a
-        // group is the call before the next group's first block): every call costs about the
-        // same, at the price of a cross-stream wait per call (the real-time caller's view).
+        // Paced (neo_hip_upols_set_paced): the group's background launch in np pieces (np = G:
+        // one per call; np = 2: at the group's calls 0 and G / 2), piece j covering workgroups
+        // [j W / np, (j + 1) W / np) of the same launch (its workgroups are independent); the
+        // block of a call that issues a piece waits for the piece issued before it (for piece 0:
+        // the previous group's last piece, so the previous group is complete before the group's
+        // first block, as without pacing). No block waits for more than one piece of background
+        // work: every call costs about the same, at the price of np cross-stream waits per group
+        // (the real-time caller's view).
+        const int np = h->paced == 2 ? 2 : G, per = G / np;
         const int k = int(n % G);
         const int64_t n0 = n - k;
         const int w0 = ring_add(h->wpos, -k, h->ring);
@@ -2265,14 +2269,18 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
             if (odd || primed) NEO_HIP_CHECK(hipStreamWaitEvent(h->bg, h->ev_blk, 0));
             if (!odd) NEO_HIP_CHECK(hipEventRecord(h->ev_blk, s));  // the blocks before n: the next odd group
         }
-        slice_args b = base_args(h);
-        slice_part(h, n0, w0, b);
-        if ((rc = launch_step_kernel(h, b, h->bg, 2, k, G))) return rc;
-        h->bg_busy = true;
-        if (k == G - 1) ++h->bg_launches;
-        NEO_HIP_CHECK(hipEventRecord(h->ev_pc[n & 1], h->bg));
-        if (h->pace_prev) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_pc[(n - 1) & 1], 0));
-        h->pace_prev = true;
+        if (k % per == 0) {
+            const int j = k / per;
+            slice_args b = base_args(h);
+            slice_part(h, n0, w0, b);
+            if ((rc = launch_step_kernel(h, b, h->bg, 2, j, np))) return rc;
+            h->bg_busy = true;
+            if (j == np - 1) ++h->bg_launches;
+            NEO_HIP_CHECK(hipEventRecord(h->ev_pc[h->pace_seq & 1], h->bg));
+            if (h->pace_prev) NEO_HIP_CHECK(hipStreamWaitEvent(s, h->ev_pc[(h->pace_seq - 1) & 1], 0));
+            h->pace_prev = true;
+            ++h->pace_seq;
+        }
     } else if (G > 1 && n % G == 0) {
         // Every background level has T >= 2 G, so its windows (and the far level's) start at
         // multiples of 2 G: a background launch at an odd group (n = G mod 2 G) needs the blocks

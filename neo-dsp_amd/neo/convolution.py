@@ -327,10 +327,11 @@ class UpolsConvolver:
         slice launches of the step groups issued so far (device-side; no host wait)."""
         _native.check(_native.load().neo_hip_upols_join_background(self._h, ctypes.c_void_p(stream)))
 
-    def set_paced(self, enable: bool) -> None:
-        """Step groups' background launch in one piece per call, each block waiting for the piece
-        of the call before it (neo_hip_upols_set_paced): an even host round trip per block."""
-        _native.check(_native.load().neo_hip_upols_set_paced(self._h, int(bool(enable))))
+    def set_paced(self, enable) -> None:
+        """Step groups: issue the group's background launch in pieces, each block after the
+        piece before it (neo_hip_upols_set_paced): an even host round trip per block. True / 1:
+        a piece per call; 2: two pieces per group; False / 0: off."""
+        _native.check(_native.load().neo_hip_upols_set_paced(self._h, int(enable)))
 
     def set_persistent(self, enable: bool, idle_ms: float = 50.0) -> None:
         """Latency mode (neo_hip_upols_set_persistent): one persistent kernel steps every block;

@@ -1,6 +1,6 @@
 """Paced background work (neo_hip_upols_set_paced): a step group's background launch issued as G
-per-call pieces (workgroup ranges of the same launch) with every block waiting for the piece of
-the call before it. The same kernels compute the same sums, so the outputs equal the unpaced
+per-call pieces, or as two pieces per group (workgroup ranges of the same launch), with the block
+of each call that issues a piece waiting for the piece before it. The same kernels compute the same sums, so the outputs equal the unpaced
 step groups' bit for bit (until a switch re-primes the levels: the far level's windows then start
 elsewhere, float summation order); pinned to the oracle (uniform_partitioned_convolver.hpp:47-65)
 throughout. The shape has step groups (128 channels x B = 512: 4096 16-column units, G = 4) and a
@@ -13,7 +13,9 @@ from conftest import peak_err
 pytestmark = pytest.mark.gpu
 
 
-def test_paced_equals_step_groups(neo_gpu, oracle):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_paced_equals_step_groups(neo_gpu, oracle, mode):
+    """mode 1: a piece per call; mode 2: two pieces per group (calls 0 and G / 2)"""
     torch = pytest.importorskip("torch")
     C, B, P, nb = 128, 512, 600, 700
     ir = np.stack([oracle.noise(6100 + c, B * P) for c in range(C)])
@@ -26,7 +28,7 @@ def test_paced_equals_step_groups(neo_gpu, oracle):
         assert c.step_group() == 4
         convs.append(c)
     paced, plain = convs
-    paced.set_paced(True)
+    paced.set_paced(mode)
     x = torch.from_numpy(np.stack([oracle.noise(6300 + c, B * nb) for c in range(C)])).cuda()
     outs = []
     for conv in convs:
@@ -34,7 +36,7 @@ def test_paced_equals_step_groups(neo_gpu, oracle):
         torch.cuda.synchronize()
         for i in range(nb):
             if conv is paced and i in (300, 333):  # off, then on again: the levels re-prime each time
-                conv.set_paced(i == 333)
+                conv.set_paced(mode if i == 333 else 0)
             p = t.data_ptr() + 4 * i * B
             conv.process_blocks_ptr(p, p, nb * B, 1, 0)
         conv.join_background(None)
