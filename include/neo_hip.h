@@ -64,10 +64,10 @@ NEO_HIP_API int neo_hip_device_count(int* count);
  * instead of staging it. The caller keeps the range alive until neo_hip_host_unregister(p). */
 NEO_HIP_API int neo_hip_host_register(void* p, int64_t bytes);
 NEO_HIP_API int neo_hip_host_unregister(void* p);
-/* Handle buffers come from per-device chunks the library keeps mapped (256 MiB each; a request
- * above 64 MiB gets a chunk of its own, released when its handle is destroyed), so creating and
- * destroying convolvers never synchronizes the device. trim releases every chunk no handle uses;
- * info reports the bytes held and the bytes in use on a device. */
+/* Handle buffers come from per-device chunks the library keeps mapped (256 MiB, or a request's own
+ * size above 64 MiB), so creating and destroying convolvers never synchronizes the device. Empty
+ * chunks stay cached (up to a quarter of the device's memory) for later handles; trim returns
+ * every chunk no handle uses; info reports the bytes held and the bytes in use on a device. */
 NEO_HIP_API int neo_hip_memory_trim(int device);
 NEO_HIP_API int neo_hip_memory_info(int device, int64_t* reserved, int64_t* in_use);
 

@@ -5,11 +5,15 @@
 // switches between one shared handle and a handle per member). With hipMalloc / hipFree per
 // buffer that costs milliseconds per handle: hipFree waits for the whole device (every stream,
 // including another handle's resident latency-mode kernel). Here a handle's buffers come from
-// 256 MiB chunks per device (first fit, neighbours merged on free) that stay mapped: freeing is a
-// list operation, no device synchronization. The caller frees only memory no queued work uses
-// (handles join their streams first). Requests above 64 MiB (a multichannel handle's filter and
-// delay line) get a chunk of their own, returned to HIP when freed; at most two empty 256 MiB
-// chunks stay cached per device (neo_hip_memory_trim releases them).
+// chunks per device (first fit, neighbours merged on free) that stay mapped: freeing is a list
+// operation, no device synchronization. The caller frees only memory no queued work uses (handles
+// join their streams first). A new chunk is 256 MiB, or the request's size above 64 MiB (a
+// multichannel handle's filter and delay line). Empty chunks stay cached, up to a quarter of the
+// device's memory, and serve any later request that fits: a group switching from its shared
+// handle to a handle per member (upols_group.hip split) carves the members' buffers from the
+// shared handle's just-freed chunks instead of returning 48 GB to the driver and mapping 45 GB
+// anew. Before a new chunk for a request above 64 MiB is mapped, the cached empty chunks are
+// returned; neo_hip_memory_trim returns them on demand.
 //
 // Also the constant tables every handle of a block size shares (twiddles), uploaded once per
 // device and never freed.
@@ -28,7 +32,6 @@ namespace {
 constexpr size_t kAlign = 256;
 constexpr size_t kChunk = size_t(256) << 20;
 constexpr size_t kDedicated = size_t(64) << 20;
-constexpr int kKeepEmpty = 2;
 
 struct chunk {
     char* base = nullptr;
@@ -51,11 +54,25 @@ std::mutex g_mu;
 std::map<int, pool> g_pools;
 std::unordered_map<const void*, std::tuple<int, chunk*, size_t>> g_live;  // pointer -> device, chunk, bytes
 
-int empty_chunks(const pool& p)
+size_t empty_bytes(const pool& p)
 {
-    int n = 0;
-    for (const auto& c : p.chunks) n += !c->dedicated && c->used == 0;
+    size_t n = 0;
+    for (const auto& c : p.chunks) n += c->used == 0 ? c->size : 0;
     return n;
+}
+
+// empty chunks kept cached per device: a quarter of its memory
+size_t keep_bytes()
+{
+    static size_t keep = [] {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+            (void)hipGetLastError();
+            return size_t(1) << 30;
+        }
+        return tot / 4;
+    }();
+    return keep;
 }
 
 void release(pool& p, size_t i)
@@ -88,21 +105,23 @@ int dalloc(void** out, size_t bytes)
     const size_t n = (std::max<size_t>(bytes, 1) + kAlign - 1) / kAlign * kAlign;
     std::lock_guard<std::mutex> lk(g_mu);
     pool& p = g_pools[dev];
-    if (n <= kDedicated) {
-        for (auto& c : p.chunks)
-            if (!c->dedicated && take(*c, n, out)) {
-                g_live.emplace(*out, std::make_tuple(dev, c.get(), n));
-                return NEO_HIP_OK;
-            }
-    }
+    for (auto& c : p.chunks)
+        if (take(*c, n, out)) {
+            g_live.emplace(*out, std::make_tuple(dev, c.get(), n));
+            return NEO_HIP_OK;
+        }
+    auto release_empty = [&] {
+        for (size_t i = p.chunks.size(); i-- > 0;)
+            if (p.chunks[i]->used == 0) release(p, i);
+    };
+    if (n > kDedicated) release_empty();  // no cached chunk fits: give them back before mapping a big one
     auto c = std::make_unique<chunk>();
-    c->dedicated = n > kDedicated;
-    c->size = c->dedicated ? n : kChunk;
+    constexpr size_t k2m = size_t(2) << 20;
+    c->size = n > kDedicated ? (n + k2m - 1) / k2m * k2m : kChunk;
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->base), c->size);
     if (e != hipSuccess) {  // give the cached empty chunks back and try once more
         (void)hipGetLastError();
-        for (size_t i = p.chunks.size(); i-- > 0;)
-            if (!p.chunks[i]->dedicated && p.chunks[i]->used == 0) release(p, i);
+        release_empty();
         e = hipMalloc(reinterpret_cast<void**>(&c->base), c->size);
         if (e != hipSuccess) {
             (void)hipGetLastError();
@@ -142,9 +161,10 @@ void dfree(void* ptr)
     c->free.emplace(off, len);
     c->used -= n;
     if (c->used) return;
+    if (empty_bytes(p) <= keep_bytes()) return;  // cached for later requests of any size
     for (size_t i = 0; i < p.chunks.size(); ++i)
         if (p.chunks[i].get() == c) {
-            if (c->dedicated || empty_chunks(p) > kKeepEmpty) release(p, i);
+            release(p, i);
             break;
         }
 }

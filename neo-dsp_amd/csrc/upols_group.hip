@@ -37,6 +37,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -97,7 +98,11 @@ struct neo_hip_upols_group {
     bool coalesced = false;
     neo_hip_upols* shared = nullptr;
     std::vector<int> slot_member;     // shared handle channel -> member
-    std::vector<std::pair<uintptr_t, uintptr_t>> reg;  // owner-registered host ranges [lo, hi) the leader may read
+    struct range {
+        uintptr_t lo, hi;  // owner-registered host range [lo, hi) the leader may read
+        float* dev;        // its device mapping (page-locked by the group, or already by its owner), or null
+    };
+    std::vector<range> reg;
     float* in_pin = nullptr;          // mapped pinned [C][B]: the frame's input blocks
     float* out_pin = nullptr;         // mapped pinned [C][B]: the frame's output blocks
     float* in_dev = nullptr;          // their device addresses
@@ -159,7 +164,81 @@ bool registered(const group_t* g, const float* p)
 {
     const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + size_t(g->B) * sizeof(float);
     for (const auto& r : g->reg)
-        if (lo >= r.first && hi <= r.second) return true;
+        if (lo >= r.lo && hi <= r.hi) return true;
+    return false;
+}
+
+// Page-locked, device-mapped registered ranges, process-wide and counted (an owner registers its
+// frame buffer with the group of every shape it holds): the coalesced step reads the members'
+// blocks in place instead of the leader copying them (DenseConvolution.cpp:62-74: the frame's
+// channels are filled before the loop over the convolvers). hipHostRegister page-locks 4 MB in
+// ~33 us (tests/cpp/bench_hipcost), once per registration.
+struct pin_entry {
+    uintptr_t hi;
+    float* dev;
+    int refs;
+    bool ours;  // registered by us (else it was page-locked already: its owner unregisters it)
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, pin_entry> g_pins;
+
+float* pin_range(uintptr_t lo, uintptr_t hi)
+{
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (auto it = g_pins.find(lo); it != g_pins.end() && it->second.hi == hi) {
+        ++it->second.refs;
+        return it->second.dev;
+    }
+    pin_entry e{hi, nullptr, 1, false};
+    void* p = reinterpret_cast<void*>(lo);
+    if (hipHostRegister(p, size_t(hi - lo), hipHostRegisterMapped) == hipSuccess) {
+        e.ours = true;
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) e.dev = static_cast<float*>(d);
+        else (void)hipGetLastError();
+    } else {
+        (void)hipGetLastError();     // already page-locked (or not lockable): use its mapping, if any
+        e.dev = neo_hip::host_mapped(p);
+    }
+    if (!g_pins.count(lo)) g_pins.emplace(lo, e);
+    else if (e.ours) (void)hipHostUnregister(p);  // a different range at the same address: do not keep two
+    return e.dev;
+}
+
+void unpin_range(uintptr_t lo)
+{
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.find(lo);
+    if (it == g_pins.end() || --it->second.refs > 0) return;
+    if (it->second.ours) {
+        if (hipHostUnregister(reinterpret_cast<void*>(lo)) != hipSuccess) (void)hipGetLastError();
+    }
+    g_pins.erase(it);
+}
+
+// The leader's frame read in place: every live member's block (the leader's own io, the others'
+// buffers of the last frame) at p0 + slot * ld in ONE registered, device-mapped range, 16-byte
+// aligned. Then *in_dev / *ld describe it for the step kernel; false: the leader copies.
+bool inplace_frame(const group_t* g, const member& lead, const float* io, const float** in_dev, int64_t* ld)
+{
+    const int C = int(g->slot_member.size());
+    auto ptr = [&](int slot) {
+        const member& y = g->m[size_t(g->slot_member[size_t(slot)])];
+        return &y == &lead ? io : y.io_last;
+    };
+    const float* p0 = ptr(0);
+    const int64_t d = C > 1 ? ptr(1) - p0 : g->B;
+    if (d < g->B || (d & 3) || (reinterpret_cast<uintptr_t>(p0) & 15)) return false;
+    for (int s = 2; s < C; ++s)
+        if (ptr(s) != p0 + int64_t(s) * d) return false;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p0),
+                    hi = reinterpret_cast<uintptr_t>(p0 + int64_t(C - 1) * d + g->B);
+    for (const auto& r : g->reg)
+        if (r.dev && lo >= r.lo && hi <= r.hi) {
+            *in_dev = r.dev + (lo - r.lo) / sizeof(float);
+            *ld = d;
+            return true;
+        }
     return false;
 }
 
@@ -346,18 +425,28 @@ int call_coalesced(group_t* g, int i, float* io)
             if (rc) return rc;
             return call_independent(g, i, io);
         }
+    // the frame read in place (registered, page-locked, one stride): the step starts at once and
+    // the leader copies the blocks it reads (the members' comparisons) while it runs; else the
+    // leader copies them first into the mapped staging the step reads
+    const float* in_dev = g->in_dev;
+    int64_t ld_in = g->B;
+    const bool inplace = inplace_frame(g, x, io, &in_dev, &ld_in);
+    auto copy_in = [&] {
+        for (const auto& y : g->m)
+            if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
+    };
     NEO_GP_T(t0);
-    for (const auto& y : g->m)
-        if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
+    if (!inplace) copy_in();
     NEO_GP_ADD(0, t0);
     NEO_GP_T(t1);
     NEO_HIP_CHECK(hipMemcpyAsync(g->prev_bak, sh->prev, size_t(sh->C) * bb, hipMemcpyDeviceToDevice, g->stream));
     NEO_GP_ADD(1, t1);
     NEO_GP_T(t2);
     g->step_w = sh->wpos;
-    int rc = neo_hip::launch_levels(sh, g->in_dev, g->B, g->out_dev, g->B, g->stream);
+    int rc = neo_hip::launch_levels(sh, in_dev, ld_in, g->out_dev, g->B, g->stream);
     NEO_GP_ADD(2, t2);
     NEO_GP_T(t3);
+    if (inplace) copy_in();  // beside the step: both read the frame, which nothing writes during this call
     if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
     NEO_GP_ADD(3, t3);
     g->step_n = sh->lv_n - 1;
@@ -413,6 +502,7 @@ NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
     for (auto& x : g->m)
         if (x.own) neo_hip_upols_destroy(x.own);
     neo_hip::hfree(g->stage_pin);
+    for (const auto& r : g->reg) unpin_range(r.lo);
     (void)hipStreamDestroy(g->stream);
     delete g;
     return NEO_HIP_OK;
@@ -527,8 +617,10 @@ NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void*
     std::lock_guard<std::mutex> lk(g->mu);
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + uint64_t(bytes);
     for (const auto& r : g->reg)
-        if (r.first == lo && r.second == hi) return NEO_HIP_OK;  // already registered (a per-frame call is cheap)
-    g->reg.emplace_back(lo, hi);
+        if (r.lo == lo && r.hi == hi) return NEO_HIP_OK;  // already registered (a per-frame call is cheap)
+    neo_hip::device_guard dg(g->device);
+    if (dg.rc) return dg.rc;
+    g->reg.push_back({lo, hi, pin_range(lo, hi)});
     return NEO_HIP_OK;
 }
 
@@ -536,12 +628,13 @@ NEO_HIP_API int neo_hip_upols_group_unregister(neo_hip_upols_group* g, const voi
 {
     if (!g) return fail(NEO_HIP_EINVAL, "null group");
     std::lock_guard<std::mutex> lk(g->mu);
-    if (!ptr) {
-        g->reg.clear();
-        return NEO_HIP_OK;
-    }
+    // no kernel reads a range after this returns: every coalesced step and redo completed in its
+    // own call, and the next frame splits if a member's buffer is no longer registered
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
-    g->reg.erase(std::remove_if(g->reg.begin(), g->reg.end(), [lo](const auto& r) { return r.first == lo; }), g->reg.end());
+    auto gone = [&](const group_t::range& r) { return !ptr || r.lo == lo; };
+    for (const auto& r : g->reg)
+        if (gone(r)) unpin_range(r.lo);
+    g->reg.erase(std::remove_if(g->reg.begin(), g->reg.end(), gone), g->reg.end());
     return NEO_HIP_OK;
 }
 

@@ -247,7 +247,9 @@ inline int timing_mark(upols_t::ev_group* g, int i, hipStream_t s)
 
 // upols_levels.hip: one streaming block step (level slabs + the newest partitions) and 1/T
 // of every level's next window; the level plan; buffers; filter-change hook
-int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
+// (snap: also copy each channel's input block, as read, to snap [C][B])
+int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s,
+                  float* snap = nullptr);
 // far: -1 auto (= 1), 0 the big Toeplitz level, 1 the far level
 void plan_levels(int P, level_plan& lp, int far = -1);
 // the block role of streaming step n (FDL ring row w) again for channel c alone, with another

@@ -160,6 +160,8 @@ struct slice_args {
     float* out;
     int64_t ld_out;
     float* prev;
+    float* snap;            // not null: a copy of each channel's input block, [C][B] (upols_group.hip: the
+                            // frame the leader's launch read in place, for the later members' comparisons)
     const cf* twg;
     int w, a0;              // ring row of the block; partitions the block role MACs directly
     int nsl;
@@ -278,6 +280,18 @@ __device__ __forceinline__ void block_role(const slice_args& a, int c, char* sme
                 const int n = tid + m * TW;
                 if constexpr (OLA) v[m] = n < B / 2 ? in_ld(n) : cf{0.f, 0.f};
                 else v[m] = n < B / 2 ? pz[n] : in_ld(n - B / 2);
+            }
+            if (a.snap) {  // the input block as read (uniform per launch)
+                cf* sz = reinterpret_cast<cf*>(a.snap + int64_t(c) * B);
+#pragma unroll
+                for (int m = 0; m < EW; ++m) {
+                    const int n = tid + m * TW;
+                    if constexpr (OLA) {
+                        if (n < B / 2) sz[n] = v[m];
+                    } else {
+                        if (n >= B / 2) sz[n - B / 2] = v[m];
+                    }
+                }
             }
         }
     }
@@ -2233,7 +2247,7 @@ static int group_streams(upols_t* h)
 // the previous group's background launch (ev_sl). With one group of slack on each side neither
 // stream waits for the other in steady state. The background launch is issued when its group's
 // first call comes, so a block redone before that call (upols_group.hip) is the one it reads.
-int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
+int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s, float* snap)
 {
     int rc = lvl_buffers(h);
     if (rc) return rc;
@@ -2249,6 +2263,7 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     const int G = h->sg;
     slice_args a = base_args(h);
     block_part(h, n, h->wpos, 0, h->C, in, ld_in, out, ld_out, a);
+    a.snap = snap;
     block_levels(h, n, h->wpos, a);
     if (G > 1 && h->paced) {
         // Paced (neo_hip_upols_set_paced): the group's background launch in np pieces (np = G:
