@@ -583,6 +583,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     h->toep_jh = o.toep_split;
     h->f2mode = o.far_phase2;
     h->sg = o.step_group ? o.step_group : step_group_for(channels, block, partitions);
+    h->bg_pad = bg_pad_for(channels, block);
     // the far level's form: the stored spectra (phase 1 + 2) by default; recomputed every window
     // (far2r_role) on request -- fewer bytes (C5: 15 instead of 23 rows per column and step) but
     // 2 nseg + 1 transforms per unit and window: same-box A/B with step groups, stored vs

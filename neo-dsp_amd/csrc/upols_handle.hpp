@@ -102,6 +102,7 @@ struct neo_hip_upols {
     // caller's stream and the level slices of G steps as one launch on the handle's background
     // stream bg, one step group ahead (events ev_blk / ev_sl order the two; upols_levels.hip)
     int sg = 1;
+    int bg_pad = 0;  // dynamic LDS bytes of the slices launches (bg_pad_for): 1024 holds them to 2 workgroups per CU
     hipStream_t bg = nullptr;
     hipEvent_t ev_blk = nullptr, ev_sl[2] = {}, ev_join = nullptr;
     int paced = 0;                 // neo_hip_upols_set_paced: the group's background launch in G per-call pieces
@@ -260,6 +261,7 @@ int launch_block_only(upols_t* h, int64_t n, int w, int c, const float* in, floa
 int far_group_for(int C, int B, int P);
 int toep_split_for(int C, int B);
 int step_group_for(int C, int B, int P);
+int bg_pad_for(int C, int B);
 // latency mode: whole blocks through the persistent kernel, synchronous (upols_levels.hip)
 int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t nblocks);
 // stop the persistent kernel (if any) and leave the levels to re-prime on the next normal step

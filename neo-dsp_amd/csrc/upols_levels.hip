@@ -1379,6 +1379,25 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
     if (far2b()) return 1;
     if (far2a()) return 2;
     if (block()) return 3;
+#if NEO_ORDER == 3
+    // far phase 1's workgroups spread evenly among the Toeplitz levels' (dispatch in bid order:
+    // its HBM-bound loads beside the LDS tiles instead of a tail of their own)
+    {
+        int A = 0;
+#pragma unroll
+        for (int l = 0; l < kLvToep; ++l)
+            if (l < a.ntp) A += a.tp[l].nwg;
+        const int F = a.f1nwg, N = A + F;
+        if (F > 0 && bid < N) {
+            const int f0 = int(int64_t(bid) * F / N), f1 = int(int64_t(bid + 1) * F / N);
+            if (f1 > f0) {
+                bid = f0 + A;  // the far1 lambda below subtracts the Toeplitz workgroups first
+            } else {
+                bid -= f0;
+            }
+        }
+    }
+#endif
 #if NEO_ORDER != 2
     if (toep(L4{})) return 8;
     if (toep(L3{})) return 7;
@@ -1408,31 +1427,13 @@ constexpr int block_lds() { return (B + upols_cfg<B>::LL + upols_cfg<B>::TW1 + u
 #ifndef NEO_BLOCK_WPE
 #define NEO_BLOCK_WPE 1
 #endif
-template<int B, bool OLA>
-__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(NEO_BLOCK_WPE))) void k_lvl_block(slice_args a)
-{
-    __shared__ __attribute__((aligned(16))) char smem[block_lds<B>()];
-    if constexpr (NEO_BLOCK_PRIO > 0) __builtin_amdgcn_s_setprio(NEO_BLOCK_PRIO);
-    (void)lvl_roles<B, OLA, 2, 1>(a, smem);
-}
-
-// step groups: every role but the block for the slices of G steps (the background stream);
-// 256 lanes (the roles' geometry), the step kernel's register budget
-template<int KMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(slices_wpe<KMAX>()))) void k_lvl_slices(slice_args a)
-{
-    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
-    (void)lvl_roles<512, false, KMAX, 2>(a, smem);
-}
-
-template<int B, bool OLA, int KMAX>
-__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(step_wpe<B, KMAX>()))) void k_lvl_step(slice_args a)
-{
-    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
 #ifdef NEO_TIMELINE  // diagnostic builds: per-workgroup start / end (100 MHz clock) and role
+template<int WG, class F>
+__device__ __forceinline__ void tl_record(const slice_args& a, F roles)
+{
     const unsigned long long t0 = wall_clock64();
-    const int role = lvl_roles<B, OLA, KMAX>(a, smem);
-    if constexpr (lstep_cfg<B>::WG > 256) return;  // lanes past 256 leave the roles early: no final barrier
+    const int role = roles();
+    if constexpr (WG > 256) return;  // lanes past 256 leave the roles early: no final barrier
     __syncthreads();
     if (threadIdx.x == 0 && a.tl) {
         unsigned long long* r = static_cast<unsigned long long*>(a.tl) + 4 * int64_t(blockIdx.x);
@@ -1441,9 +1442,34 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
         const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15;  // HW_REG_XCC_ID
         r[2] = (unsigned long long)(role) | ((unsigned long long)(__smid()) << 32) | ((unsigned long long)(xcc) << 56);
     }
+}
+#define NEO_TL_ROLES(WG, EXPR) tl_record<WG>(a, [&] { return EXPR; })
 #else
-    (void)lvl_roles<B, OLA, KMAX>(a, smem);
+#define NEO_TL_ROLES(WG, EXPR) (void)(EXPR)
 #endif
+
+template<int B, bool OLA>
+__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(NEO_BLOCK_WPE))) void k_lvl_block(slice_args a)
+{
+    __shared__ __attribute__((aligned(16))) char smem[block_lds<B>()];
+    if constexpr (NEO_BLOCK_PRIO > 0) __builtin_amdgcn_s_setprio(NEO_BLOCK_PRIO);
+    NEO_TL_ROLES(lstep_cfg<B>::WG, (lvl_roles<B, OLA, 2, 1>(a, smem)));
+}
+
+// step groups: every role but the block for the slices of G steps (the background stream);
+// 256 lanes (the roles' geometry), the step kernel's register budget
+template<int KMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(slices_wpe<KMAX>()))) void k_lvl_slices(slice_args a)
+{
+    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
+    NEO_TL_ROLES(256, (lvl_roles<512, false, KMAX, 2>(a, smem)));
+}
+
+template<int B, bool OLA, int KMAX>
+__global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(step_wpe<B, KMAX>()))) void k_lvl_step(slice_args a)
+{
+    __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
+    NEO_TL_ROLES(lstep_cfg<B>::WG, (lvl_roles<B, OLA, KMAX>(a, smem)));
 }
 
 // Segment spectra (grid C x NSEG x B/16): hf[c][s][f][k] = DFT256 over r < 128 of
@@ -1635,6 +1661,8 @@ int toep_split_for(int C, int B) { return C * (B / 16) < 8 * 32 ? 2 : 1; }
 // block launch and the cross-stream waits cost more than the overlap gives: 0.0063 / 0.0083)
 constexpr int64_t kStepGroupUnits = 2048;
 
+int bg_pad_for(int C, int B) { return int64_t(C) * (B / 16) <= 4096 ? 1024 : 0; }
+
 int step_group_for(int C, int B, int P)
 {
     (void)P;
@@ -1675,8 +1703,8 @@ static slice_args base_args(const upols_t* h)
 
 #ifdef NEO_TIMELINE
 // diagnostic builds: the records of the last step-kernel launch of a handle
-static void* g_tl = nullptr;
-static int64_t g_tl_n = 0, g_tl_cap = 0;
+static void* g_tl_buf[3] = {};  // timeline records of the last launch of each part (0 step, 1 block, 2 slices)
+static int64_t g_tl_nn[3] = {}, g_tl_capp[3] = {};
 #endif
 
 static unsigned launch_grid(const slice_args& a)
@@ -1699,14 +1727,14 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
     }
     if (!grid) return NEO_HIP_OK;
 #ifdef NEO_TIMELINE
-    if (int64_t(grid) > g_tl_cap) {
-        (void)hipFree(g_tl);
-        g_tl_cap = int64_t(grid) * 2;
-        NEO_HIP_CHECK(hipMalloc(&g_tl, size_t(g_tl_cap) * 32));
-        NEO_HIP_CHECK(hipMemset(g_tl, 0, size_t(g_tl_cap) * 32));
+    if (int64_t(grid) > g_tl_capp[part]) {
+        (void)hipFree(g_tl_buf[part]);
+        g_tl_capp[part] = int64_t(grid) * 2;
+        NEO_HIP_CHECK(hipMalloc(&g_tl_buf[part], size_t(g_tl_capp[part]) * 32));
+        NEO_HIP_CHECK(hipMemset(g_tl_buf[part], 0, size_t(g_tl_capp[part]) * 32));
     }
-    a.tl = g_tl;
-    g_tl_n = grid;
+    a.tl = g_tl_buf[part];
+    g_tl_nn[part] = grid;
 #endif
     // pairs-only build where the window group is <= 2 (fewer VGPRs: every shape below
     // kFarGroupUnits), else the build for any group
@@ -1720,10 +1748,17 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
                                                                                   dim3(lstep_cfg<BB>::WG), 0, s, a))
         }
     } else if (part == 2) {
-#ifndef NEO_BG_LDS_PAD
-#define NEO_BG_LDS_PAD 0
-#endif
+        // 1 KB of dynamic LDS holds the slices kernel to two workgroups per CU (three by its 53.8 KB
+        // of static LDS and 149 VGPRs), leaving room for block workgroups beside it: where the
+        // chain of block launches bounds the step (C4: 256 ch x B = 256) they are no longer held
+        // back until slice workgroups end (same-box A/B, 128 steps, two repetitions: C4 10.95 /
+        // 10.97 -> 10.24 / 10.39 us per step, C5 15.9 / 15.7 -> 15.5 / 15.8, c5full 107.0 /
+        // 107.7 -> 115.3 / 114.3: only at the smaller shapes, bg_pad_for)
+#ifdef NEO_BG_LDS_PAD  // diagnostic builds: force the padding
         const unsigned pad = NEO_BG_LDS_PAD;
+#else
+        const unsigned pad = h->bg_pad;
+#endif
         if (raw) hipLaunchKernelGGL((k_lvl_slices<1>), dim3(grid), dim3(256), pad, s, a);
         else if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(grid), dim3(256), pad, s, a);
         else hipLaunchKernelGGL((k_lvl_slices<kFarKMax>), dim3(grid), dim3(256), pad, s, a);
@@ -2890,9 +2925,20 @@ extern "C" NEO_HIP_API int neo_hip_diag_persist_probe(neo_hip_upols* h, unsigned
 extern "C" NEO_HIP_API int neo_hip_diag_timeline(unsigned long long* out, int64_t cap, int64_t* count)
 {
     NEO_HIP_CHECK(hipDeviceSynchronize());
-    const int64_t n = std::min(cap, neo_hip::g_tl_n);
-    if (n > 0) NEO_HIP_CHECK(hipMemcpy(out, neo_hip::g_tl, size_t(n) * 32, hipMemcpyDeviceToHost));
-    if (count) *count = neo_hip::g_tl_n;
+    const int64_t n = std::min(cap, neo_hip::g_tl_nn[0]);
+    if (n > 0) NEO_HIP_CHECK(hipMemcpy(out, neo_hip::g_tl_buf[0], size_t(n) * 32, hipMemcpyDeviceToHost));
+    if (count) *count = neo_hip::g_tl_nn[0];
+    return NEO_HIP_OK;
+}
+
+// the same for the last launch of part 1 (step groups' block launch) or 2 (their slices launch)
+extern "C" NEO_HIP_API int neo_hip_diag_timeline_part(int part, unsigned long long* out, int64_t cap, int64_t* count)
+{
+    if (part < 0 || part > 2) return neo_hip::fail(NEO_HIP_EINVAL, "part");
+    NEO_HIP_CHECK(hipDeviceSynchronize());
+    const int64_t n = std::min(cap, neo_hip::g_tl_nn[part]);
+    if (n > 0) NEO_HIP_CHECK(hipMemcpy(out, neo_hip::g_tl_buf[part], size_t(n) * 32, hipMemcpyDeviceToHost));
+    if (count) *count = neo_hip::g_tl_nn[part];
     return NEO_HIP_OK;
 }
 #endif

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
+for w in c4 c5; do for p in 2 1; do
+  echo "== $w part $p"
+  NEO_HIP_LIBRARY=$PWD/tools/ab/tl/libneo_hip.so timeout -k 10 240 python tools/timeline.py --workload $w --steps 64 --part $p \
+    --json gpurun_out/tl5_${w}_p$p.json 2> gpurun_out/tl5_${w}_p$p.err || { tail -5 gpurun_out/tl5_${w}_p$p.err; exit 1; }
+done; done

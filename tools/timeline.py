@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--json", default="")
+    ap.add_argument("--part", type=int, default=0, help="0 the one-launch step, 1 the step groups' block launch, "
+                    "2 their slices launch (sampled once per step group)")
     args = ap.parse_args()
     import torch
     import bench
@@ -35,8 +37,9 @@ def main():
 
     C, B, L = bench.WORKLOADS[args.workload]
     lib = neo._native.load()
-    fn = lib.neo_hip_diag_timeline
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    fn0 = lib.neo_hip_diag_timeline_part
+    fn0.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    fn = lambda *xs: fn0(args.part, *xs)
     P = neo.num_partitions(L, B)
     conv = neo.UpolsConvolver(C, B, P)
     conv.set_batch(False)
@@ -54,8 +57,9 @@ def main():
     per = {}
     per_xcc = {}
     spans = []
+    per_sample = conv.step_group() if args.part == 2 else 1
     for _ in range(args.steps):
-        feed.run(1)
+        feed.run(per_sample)
         fn(buf.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(cnt))
         n = int(cnt.value)
         r = buf[:n].astype(np.int64)
