@@ -1560,12 +1560,11 @@ static int far_group(const upols_t* h)
 
 // far phase 1 over the slice units [u0, u1): mode 0 one window per group, 1 only the groups of
 // class cls (K windows each), 2 every group (class cls: K windows; classes not started: one)
-static void far1_range(const upols_t* h, slice_args& a, int u0, int u1, int mode, int cls)
+__host__ __device__ inline void far1_range_k(slice_args& a, int u0, int u1, int mode, int cls, int K, int fpl)
 {
-    const int K = far_group(h);
     a.f1u0 = u0;
     a.f1u1 = u1;
-    a.f1fpl = far1_fpl(h);
+    a.f1fpl = fpl;
     a.f1mode = mode;
     a.f1cls = cls;
     a.f1nwg = 0;
@@ -1574,7 +1573,39 @@ static void far1_range(const upols_t* h, slice_args& a, int u0, int u1, int mode
     a.f1g0 = mode == 1 ? ga + ((cls - ga % K) % K + K) % K : ga;
     a.f1gs = mode == 1 ? K : 1;
     const int ng = a.f1g0 > gb ? 0 : (gb - a.f1g0) / a.f1gs + 1;
-    a.f1nwg = ng * (kFN / (4 * a.f1fpl));
+    a.f1nwg = ng * (kFN / (4 * fpl));
+}
+
+static void far1_range(const upols_t* h, slice_args& a, int u0, int u1, int mode, int cls)
+{
+    far1_range_k(a, u0, u1, mode, cls, far_group(h), far1_fpl(h));
+}
+
+// Latency mode's far level (persist_far): the far work of step n (block t0 + n, ring row w) in the
+// one-launch schedule, with kFarT - 2 slices (one more step of slack: the field of window W is
+// complete two steps before its first block, as the Toeplitz slabs): phase 1 of slice q and phase 2
+// (far2c_role) of slice q - 1 of window W = n / kFarT + 1 at q = n mod kFarT
+__host__ __device__ inline void persist_far_args(slice_args& a, int64_t n, int w, int U, int K, int fpl, cf* ff)
+{
+    constexpr int ns = kFarT - 2;
+    const int64_t W = n / kFarT + 1;
+    const int q = int(n % kFarT);
+    a.f1nwg = a.f2nwg = a.f3nwg = 0;
+    if (q < ns) {
+        a.f1wn = int(W);
+        far1_range_k(a, int(int64_t(q) * U / ns), int(int64_t(q + 1) * U / ns), K == 1 ? 0 : (W < K ? 2 : 1),
+                     int(W % K), K, fpl);
+    }
+    if (q >= 1 && q <= ns) {
+        a.f3u0 = int(int64_t(q - 1) * U / ns);
+        a.f3nwg = int(int64_t(q) * U / ns) - a.f3u0;
+        a.f3wn = int(W);
+        a.f2grp = K > 1;
+        a.f3ff = ff + (W & 1) * int64_t(a.C) * kFarT * a.B;
+        const int64_t t = (int64_t(w) + W * kFarT - n) % a.ring;
+        a.f2tw = int(t < 0 ? t + a.ring : t);
+        a.f2comb = 1;
+    }
 }
 
 // device buffers of the level pipeline (allocated on the first streaming step), all or none
@@ -2389,6 +2420,9 @@ struct persist_args {
     int T[kLvToep], LT[kLvToep], A[kLvToep], Bd[kLvToep], JH[kLvToep], UPW[kLvToep], U[kLvToep];  // LT = log2 T
     int wg0[kLvToep + 1];           // slice workgroups of level l: [wg0[l], wg0[l + 1])
     int nlev, nblk;
+    int far, fU, fK, ffpl;          // far level (persist_far): on, units, window group, phase-1 f rows per lane
+    int wgf0, wgf1;                 // its workgroups: slice workgroups [wgf0, wgf1) (after the Toeplitz levels')
+    cf* ff;                         // far field [2][C][kFarT][B]
     int64_t n0;                     // first step of this launch (levels primed at step 0)
     int w0;                         // its ring row
     persist_mb* mb;                 // the mapped mailbox (device address)
@@ -2448,7 +2482,7 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
 {
     __shared__ uint64_t io[2];
     __shared__ int go;
-    const int nsl = pa.wg0[pa.nlev];
+    const int nsl = pa.wgf1;  // the Toeplitz levels' slice workgroups and the far level's
     unsigned long long t_seen = 0;  // thread 0: when the record of the step was read (stored with its done time)
     int w = pa.w0;                  // ring row of step n
     for (int64_t n = pa.n0;; ++n, w = w + 1 == pa.base.ring ? 0 : w + 1) {
@@ -2457,6 +2491,10 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
         a.w = w;
         a.nsl = pa.nlev;
         a.ff = nullptr;
+        if (pa.far) {  // this block's far-field row (window n / kFarT, complete two steps before)
+            a.ff = pa.ff + (((n / kFarT) & 1) * a.C * kFarT + n % kFarT) * a.B;
+            a.fcs = int64_t(kFarT) * a.B;
+        }
 #pragma unroll
         for (int l = 0; l < kLvToep; ++l) {  // static indices: the slice_args stay in registers
             if (l < pa.nlev) {
@@ -2606,19 +2644,67 @@ __device__ __forceinline__ void persist_slices(const persist_args& pa, int s, ch
     }
 }
 
+// far workgroup i of the far level (slice workgroup s): per step n, after block n - 1 published its
+// FDL row AND every far workgroup finished step n - 1 (phase 2 of slice q - 1 reads the partial sums
+// phase 1 wrote at step n - 1), the far work of step n (persist_far_args); then publish, sl_done = n
+__device__ __forceinline__ void persist_far(const persist_args& pa, int s, int i, char* smem)
+{
+    __shared__ int go;
+    for (int64_t n = pa.n0 - 1;; ++n) {
+        if (threadIdx.x == 0) {
+            // the relaunch's first round redoes step n0 - 1 (its inputs are an earlier launch's)
+            bool ok = n < pa.n0 || ps_wait(pa, [&] {
+                if (ps_ld(pa.flags + 0) < n - 1) return false;
+                for (int f = pa.wgf0; f < pa.wgf1; ++f)
+                    if (ps_ld(pa.flags + kPsFlagSlices + f) < n - 1) return false;
+                return true;
+            });
+            if (ok && n >= pa.n0) ps_acquire();
+            go = ok;
+        }
+        __syncthreads();
+        if (!go) break;
+        if (n >= 0) {
+            slice_args a = pa.base;
+            a.nblk = 0;
+            a.ntp = 0;
+            persist_far_args(a, n, ps_ring_row(pa, n), pa.fU, pa.fK, pa.ffpl, pa.ff);
+            int bid = i;
+            if (bid < a.f3nwg) {
+                far2c_role<2>(a, bid, smem);
+            } else if ((bid -= a.f3nwg) < a.f1nwg) {
+                if (a.f1fpl == 4) far1_role<4, 2>(a, bid);
+                else if (a.f1fpl == 2) far1_role<2, 2>(a, bid);
+                else far1_role<1, 2>(a, bid);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ps_st(pa.flags + kPsFlagSlices + s, n);
+        }
+    }
+}
+
 template<int B, bool OLA>
 __global__ __launch_bounds__(256) void k_lvl_persist(persist_args pa)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
-    if (int(blockIdx.x) < pa.nblk) persist_block<B, OLA>(pa, int(blockIdx.x), smem);
-    else persist_slices(pa, int(blockIdx.x) - pa.nblk, smem);
+    const int s = int(blockIdx.x) - pa.nblk;
+    if (s < 0) persist_block<B, OLA>(pa, int(blockIdx.x), smem);
+    else if (s < pa.wgf0) persist_slices(pa, s, smem);
+    else persist_far(pa, s, s - pa.wgf0, smem);
 }
 
 const char* persist_ineligible(const upols_t* h)
 {
     if (!h->ahead) return "the latency mode runs the streaming levels (from 64 partitions)";
     if (h->v2) return "upola_convolver_v2 takes sub-block input";
-    if (h->lv.nseg || (h->lv.n && h->lv.T[h->lv.n - 1] == kBigT)) return "a filter of more than 256 partitions (far level)";
+    if (h->lv.n && h->lv.T[h->lv.n - 1] == kBigT) return "the 128-block Toeplitz form of the far band (far_level 0)";
+    if (h->lv.nseg && h->far_raw) return "the recomputed far level (far_level 2)";
+    if (h->lv.nseg && far_group(h) > 2) return "a far window group above 2 (neo_hip_upols_opts.far_group)";
     if (h->C > 16) return "more than 16 channels (the latency mode is for latency-bound shapes)";
     if (h->B > 512) return "blocks above 512 samples";
     return nullptr;
@@ -2681,7 +2767,23 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
         pa.Bd[l] = h->lv.b[l];
         pa.wg0[l + 1] = pa.wg0[l] + persist_level_wgs(h, l, pa.U[l], pa.UPW[l], pa.JH[l]);
     }
-    const int nsl = pa.wg0[h->lv.n];
+    pa.wgf0 = pa.wgf1 = pa.wg0[h->lv.n];
+    if (h->lv.nseg) {  // the far level: as many workgroups as its busiest step needs (any window, any slice)
+        pa.far = 1;
+        pa.fU = int(far_units(h));
+        pa.fK = far_group(h);
+        pa.ffpl = far1_fpl(h);
+        pa.ff = h->fv_ff;
+        int most = 1;
+        for (int64_t W = 1; W <= 2 * pa.fK + 1; ++W)
+            for (int q = 0; q < kFarT; ++q) {
+                slice_args t = pa.base;
+                persist_far_args(t, (W - 1) * kFarT + q, 0, pa.fU, pa.fK, pa.ffpl, pa.ff);
+                most = std::max(most, t.f1nwg + t.f3nwg);
+            }
+        pa.wgf1 = pa.wgf0 + most;
+    }
+    const int nsl = pa.wgf1;
     if (h->ps_nslices < nsl || !h->ps_flags) {
         dfree(h->ps_flags);
         h->ps_flags = nullptr;

@@ -158,9 +158,10 @@ def test_latency_mode_host_buffers(neo_gpu, oracle):
 
 
 def test_latency_mode_rejects_other_shapes(neo_gpu):
-    """far level (> 256 partitions), more than 16 channels, B > 512, sub-block v2: EINVAL"""
-    for args, kw in (((1, 512, 300), {}), ((32, 128, 100), {}), ((1, 1024, 100), {}),
-                     ((1, 256, 100), {"method": "upola_v2"})):
+    """more than 16 channels, B > 512, sub-block v2, the far band as a 128-block Toeplitz level or
+    recomputed every window: EINVAL"""
+    for args, kw in (((32, 128, 100), {}), ((1, 1024, 100), {}), ((1, 256, 100), {"method": "upola_v2"}),
+                     ((1, 512, 300), {"options": {"far_level": 0}}), ((1, 512, 300), {"options": {"far_level": 2}})):
         c = neo_gpu.UpolsConvolver(*args, **kw)
         with pytest.raises(RuntimeError, match="latency mode"):
             c.set_persistent(True)
@@ -221,3 +222,64 @@ def test_setup_call_does_not_wait_for_another_latency_kernel(neo_gpu, oracle):
     pa.set_persistent(False)
     pa.close()
     pb.close()
+
+
+def _far_pair(neo_gpu, oracle, C, B, L, seed):
+    """a latency-mode handle and a normal one whose far phase 2 is the same one-workgroup-per-unit
+    form (far2c_role) the persistent kernel runs: the same sums in the same order"""
+    P = neo_gpu.num_partitions(L, B)
+    ir = np.stack([oracle.noise(seed + c, L) for c in range(C)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    pc = neo_gpu.UpolsConvolver(C, B, P)
+    nc = neo_gpu.UpolsConvolver(C, B, P, options={"far_phase2": 1})
+    for c in (pc, nc):
+        c.filter(parts)
+        c.set_batch(False)
+    assert pc.far_form() == 1
+    return pc, nc, parts
+
+
+def test_latency_mode_far_level_10s_ir(neo_gpu, oracle):
+    """The plugin's real-time case at the headline's IR (one channel, B = 512, L = 480000: P = 938,
+    six far segments): 640 one-block calls (five far windows: every segment meets real FDL rows,
+    the ring of 969 rows wraps) through the persistent kernel's far workgroups, against the oracle
+    (uniform_partitioned_convolver.hpp:47-65) and the normal step bit for bit."""
+    torch = pytest.importorskip("torch")
+    C, B, L, nb = 1, 512, 480000, 640
+    pc, nc, parts = _far_pair(neo_gpu, oracle, C, B, L, 6400)
+    pc.set_persistent(True)
+    x = np.stack([oracle.noise(6500, B * nb)])
+    got = _run(pc, x, B, torch)
+    assert pc.persistent_info()["launches"] >= 1
+    assert peak_err(got, oracle.dense_convolve(x, parts)) <= TOL
+    assert same_sums(got, _run(nc, x, B, torch))
+    pc.set_persistent(False)
+
+
+def test_latency_mode_far_level_channels_relaunch(neo_gpu, oracle):
+    """4 channels, B = 256, P = 600 (three far segments), idle limit 5 ms with pauses (relaunches
+    mid-window and at a far window's first block) and calls of 1 and 3 blocks: the oracle and the
+    normal step bit for bit."""
+    torch = pytest.importorskip("torch")
+    C, B, L = 4, 256, 600 * 256
+    pc, nc, parts = _far_pair(neo_gpu, oracle, C, B, L, 6600)
+    pc.set_persistent(True, idle_ms=5.0)
+    nb = 700
+    x = np.stack([oracle.noise(6700 + c, B * nb) for c in range(C)])
+    t = torch.from_numpy(x.copy()).cuda()
+    torch.cuda.current_stream().synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    i = 0
+    while i < nb:
+        if i in (130, 256, 257, 400):
+            time.sleep(0.03)  # past the idle limit: the next call relaunches
+        k = 3 if 300 <= i < 360 and i + 3 <= nb else 1
+        pc.process_blocks_ptr(t.data_ptr() + 4 * i * B, t.data_ptr() + 4 * i * B, x.shape[1], k, stream)
+        i += k
+    torch.cuda.current_stream().synchronize()
+    got = t.cpu().numpy()
+    assert pc.persistent_info()["launches"] >= 4
+    chans = [0, 3]
+    assert peak_err(got[chans], oracle.dense_convolve(x[chans], parts[chans])) <= TOL
+    assert same_sums(got, _run(nc, x, B, torch))
+    pc.set_persistent(False)
