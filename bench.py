@@ -58,6 +58,7 @@ WORKLOADS = {
     "c5": (256, 512, 480000),  # one GPU's shard of 2048 ch / 8 GPUs, B=512, IR 10 s @ 48 kHz
     "c4": (256, 256, 480000),  # 256 ch, B=256, IR 10 s @ 48 kHz
     "c3": (1, 512, 96000),     # 1 ch, B=512, IR 2 s @ 48 kHz
+    "c3long": (1, 512, 480000),  # 1 ch with the headline's 10 s IR (far level): the plugin's real-time case
 }
 STRONG = {"c5full"}  # workloads whose channel count is the whole job's, split over the ranks
 
