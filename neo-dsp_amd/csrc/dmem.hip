@@ -243,16 +243,21 @@ void hfree(void* host)
 // A blocking stream for a handle's own setup and host-I/O work, from a per-device set of four
 // (GPU_MAX_HW_QUEUES is 4: more streams only share those hardware queues): creating a stream
 // costs ~4 ms and destroying one ~3 ms on MI355X (tests/cpp/bench_hipcost), the whole budget of
-// a plugin's convolver bring-up. The four are created on first use and never destroyed.
+// a plugin's convolver bring-up. Never destroyed.
 int shared_stream(hipStream_t* out)
 {
     int d = 0;
     NEO_HIP_CHECK(hipGetDevice(&d));
     std::lock_guard<std::mutex> lk(g_mu);
     pool& p = g_pools[d];
-    if (!p.streams[0])  // all four at the first request: the later handles never pay for one
-        for (auto& s : p.streams) NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
-    *out = p.streams[p.next_stream++ % 4];
+    // each created when first handed out: creating all four at once took every hardware queue, and
+    // the first handle's background stream then shared one with its own stream, its host-buffer
+    // blocks queueing behind the background launches (same-box A/B, c5full host round trip p50 /
+    // p99: 181-195 / 259-263 us all at once, 132 / 157-166 created one by one, 131-133 / 156-161
+    // with a stream of its own per handle as in round 4; tools/gpu_hostio_ab.sh)
+    hipStream_t& s = p.streams[p.next_stream++ % 4];
+    if (!s) NEO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamDefault));
+    *out = s;
     return NEO_HIP_OK;
 }
 

@@ -643,10 +643,16 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     };
     // a group member runs its setup and host-I/O work on its group's stream (upols_group.hip),
     // every other handle on one of its device's four shared streams (dmem.hip shared_stream: a
-    // stream of its own would cost ~4 ms to create and ~3 ms to destroy)
+    // stream of its own would cost ~4 ms to create and ~3 ms to destroy; the first four handles on
+    // a device create them)
     h->stream = borrow;
     if (!borrow) {
+#ifdef NEO_OWN_STREAM  // diagnostic builds (A/B): a stream of its own per handle, as before round 5 (never destroyed)
+        if (hipStreamCreateWithFlags(&h->stream, hipStreamDefault) != hipSuccess)
+            return bail(fail(NEO_HIP_ERUNTIME, "hipStreamCreate failed"));
+#else
         if (int rc = shared_stream(&h->stream)) return bail(rc);
+#endif
     }
     // filter and FDL in ONE allocation (FDL = rows [nrows, 2 nrows)): the LDS-DMA batched MAC
     // reaches both of a channel through a single buffer descriptor
