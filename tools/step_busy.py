@@ -46,13 +46,37 @@ for s, e in sorted(b + sl):
     else:
         cur[1] = max(cur[1], e)
 busy += cur[1] - cur[0]
+# the whole marked region: every kernel in it (block and slices launches of this handle; the
+# marker kernels at its edges), clipped to the region, so a slices launch that began before the
+# first block or ends after the last one counts where it runs
+def union(ivs, lo_, hi_):
+    tot, c = 0, None
+    for s_, e_ in sorted((max(s_, lo_), min(e_, hi_)) for s_, e_ in ivs):
+        if e_ <= s_:
+            continue
+        if c is None or s_ > c[1]:
+            if c:
+                tot += c[1] - c[0]
+            c = [s_, e_]
+        else:
+            c[1] = max(c[1], e_)
+    return tot + (c[1] - c[0] if c else 0)
+reg = {}
+if region:
+    all_iv = [iv(r) for r in rows]
+    ours = [iv(r) for r in rows if "k_lvl_block" in r["Kernel_Name"] or "k_lvl_slices" in r["Kernel_Name"]]
+    reg = {"region_busy_us_per_step": union(ours, *region) / len(b) / 1e3,
+           "region_idle_us": (region[1] - region[0] - union(all_iv, *region)) / 1e3}
 out = {"trace": sys.argv[1], "timed_region_only": region is not None,
        "region_us": (region[1] - region[0]) / 1e3 if region else None, "block_grid": int(grid), "block_launches": len(b), "slice_launches": len(sl),
        "busy_ns": busy, "busy_us_per_step": busy / len(b) / 1e3,
        "block_avg_us": sum(e - s for s, e in b) / len(b) / 1e3,
        "slices_avg_us": sum(e - s for s, e in sl) / max(len(sl), 1) / 1e3,
-       "note": "union of block and slice launch intervals / block launches (idle gaps between host-synchronized "
-               "runs not counted)"}
+       **reg,
+       "note": "busy_us_per_step: union of the main block launches and the slices launches that start between the "
+               "first and the last of them / block launches (undercounts: a slices launch begun before the first "
+               "block is left out); region_busy_us_per_step: every block and slices interval clipped to the marked "
+               "region / block launches; region_idle_us: the region's time with no kernel at all"}
 if len(sys.argv) > 2:
     by = float(sys.argv[2])
     out["algorithmic_bytes_per_step"] = by
