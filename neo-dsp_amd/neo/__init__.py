@@ -8,7 +8,7 @@ from . import _native
 from . import convolution
 from . import fft
 from .convolution import (UpolsConvolver, UpolsMultiConvolver, convolve, dense_convolve, direct_convolve, fft_convolve,
-                          host_register, host_unregister, normalize_impulse, overlap_add, overlap_save, OverlapStage, UpolsGroup,
+                          host_register, host_unregister, memory_info, memory_trim, normalize_impulse, overlap_add, overlap_save, OverlapStage, UpolsGroup,
                           num_partitions, split_upola_convolver, split_upols_convolver, uniform_partition,
                           upola_convolver, upola_convolver_v2, upols_convolver)
 
@@ -33,6 +33,8 @@ __all__ = [
     "UpolsGroup",
     "host_register",
     "host_unregister",
+    "memory_info",
+    "memory_trim",
     "dense_convolve",
     "convolve",
     "fft_convolve",

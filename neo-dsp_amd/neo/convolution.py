@@ -114,6 +114,19 @@ def host_unregister(array: np.ndarray) -> None:
     _native.check(_native.load().neo_hip_host_unregister(_ptr(array)))
 
 
+def memory_info(device: int = 0) -> dict:
+    """Device memory the library holds for convolver handles on `device` (neo_hip_memory_info):
+    bytes reserved in its cached chunks and bytes in use by live handles."""
+    r, u = ctypes.c_int64(), ctypes.c_int64()
+    _native.check(_native.load().neo_hip_memory_info(device, ctypes.byref(r), ctypes.byref(u)))
+    return {"reserved": r.value, "in_use": u.value}
+
+
+def memory_trim(device: int = 0) -> None:
+    """Return every cached chunk no handle uses to the driver (neo_hip_memory_trim)."""
+    _native.check(_native.load().neo_hip_memory_trim(device))
+
+
 def uniform_partition(impulse_response, block_size: int, device: int = 0) -> np.ndarray:
     """[C][L] float32 -> [C][P][B+1] complex64: rfft_2B of each zero-padded B-sample partition."""
     ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))

@@ -59,6 +59,6 @@ def test_pool_reuse_and_drain(neo_gpu, oracle):
     assert np.array_equal(outs[0], outs[1])
     assert peak_err(outs[1], ref) <= 1e-5
     assert np.median(times) < 2e-3, f"median create {np.median(times) * 1e3:.2f} ms"
-    assert lib.neo_hip_memory_trim(0) == 0
-    r2, u2 = _info(lib)
-    assert u2 == u0 and r2 < r1
+    neo_gpu.memory_trim(0)
+    info = neo_gpu.memory_info(0)
+    assert info["in_use"] == u0 and info["reserved"] < r1
