@@ -99,8 +99,7 @@ struct neo_hip_upols_group {
     neo_hip_upols* shared = nullptr;
     std::vector<int> slot_member;     // shared handle channel -> member
     struct range {
-        uintptr_t lo, hi;  // owner-registered host range [lo, hi) the leader may read
-        float* dev;        // its device mapping (page-locked by the group, or already by its owner), or null
+        uintptr_t lo, hi;  // owner-registered host range [lo, hi) the leader may read (page-locked: pin_range)
     };
     std::vector<range> reg;
     float* in_pin = nullptr;          // mapped pinned [C][B]: the frame's input blocks
@@ -174,41 +173,30 @@ bool registered(const group_t* g, const float* p)
 // channels are filled before the loop over the convolvers). hipHostRegister page-locks 4 MB in
 // ~33 us (tests/cpp/bench_hipcost), once per registration.
 struct pin_entry {
-    uintptr_t hi;
-    float* dev;
     int refs;
     bool ours;  // registered by us (else it was page-locked already: its owner unregisters it)
 };
 std::mutex g_pin_mu;
-std::map<uintptr_t, pin_entry> g_pins;
+std::map<std::pair<uintptr_t, uintptr_t>, pin_entry> g_pins;  // [lo, hi) -> entry
 
-float* pin_range(uintptr_t lo, uintptr_t hi)
+void pin_range(uintptr_t lo, uintptr_t hi)
 {
     std::lock_guard<std::mutex> lk(g_pin_mu);
-    if (auto it = g_pins.find(lo); it != g_pins.end() && it->second.hi == hi) {
+    if (auto it = g_pins.find({lo, hi}); it != g_pins.end()) {
         ++it->second.refs;
-        return it->second.dev;
+        return;
     }
-    pin_entry e{hi, nullptr, 1, false};
+    pin_entry e{1, false};
     void* p = reinterpret_cast<void*>(lo);
-    if (hipHostRegister(p, size_t(hi - lo), hipHostRegisterMapped) == hipSuccess) {
-        e.ours = true;
-        void* d = nullptr;
-        if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) e.dev = static_cast<float*>(d);
-        else (void)hipGetLastError();
-    } else {
-        (void)hipGetLastError();     // already page-locked (or not lockable): use its mapping, if any
-        e.dev = neo_hip::host_mapped(p);
-    }
-    if (!g_pins.count(lo)) g_pins.emplace(lo, e);
-    else if (e.ours) (void)hipHostUnregister(p);  // a different range at the same address: do not keep two
-    return e.dev;
+    if (hipHostRegister(p, size_t(hi - lo), hipHostRegisterMapped) == hipSuccess) e.ours = true;
+    else (void)hipGetLastError();  // already page-locked (by its owner, or overlapping a range locked here)
+    g_pins.emplace(std::make_pair(lo, hi), e);
 }
 
-void unpin_range(uintptr_t lo)
+void unpin_range(uintptr_t lo, uintptr_t hi)
 {
     std::lock_guard<std::mutex> lk(g_pin_mu);
-    auto it = g_pins.find(lo);
+    auto it = g_pins.find({lo, hi});
     if (it == g_pins.end() || --it->second.refs > 0) return;
     if (it->second.ours) {
         if (hipHostUnregister(reinterpret_cast<void*>(lo)) != hipSuccess) (void)hipGetLastError();
@@ -234,8 +222,12 @@ bool inplace_frame(const group_t* g, const member& lead, const float* io, const 
     const uintptr_t lo = reinterpret_cast<uintptr_t>(p0),
                     hi = reinterpret_cast<uintptr_t>(p0 + int64_t(C - 1) * d + g->B);
     for (const auto& r : g->reg)
-        if (r.dev && lo >= r.lo && hi <= r.hi) {
-            *in_dev = r.dev + (lo - r.lo) / sizeof(float);
+        if (lo >= r.lo && hi <= r.hi) {
+            // its device mapping as of now (a range another registration page-locked may have been
+            // unlocked since); none: the leader copies
+            const float* dev = neo_hip::host_mapped(const_cast<float*>(p0));
+            if (!dev) return false;
+            *in_dev = dev;
             *ld = d;
             return true;
         }
@@ -502,7 +494,7 @@ NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
     for (auto& x : g->m)
         if (x.own) neo_hip_upols_destroy(x.own);
     neo_hip::hfree(g->stage_pin);
-    for (const auto& r : g->reg) unpin_range(r.lo);
+    for (const auto& r : g->reg) unpin_range(r.lo, r.hi);
     (void)hipStreamDestroy(g->stream);
     delete g;
     return NEO_HIP_OK;
@@ -620,7 +612,8 @@ NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void*
         if (r.lo == lo && r.hi == hi) return NEO_HIP_OK;  // already registered (a per-frame call is cheap)
     neo_hip::device_guard dg(g->device);
     if (dg.rc) return dg.rc;
-    g->reg.push_back({lo, hi, pin_range(lo, hi)});
+    pin_range(lo, hi);
+    g->reg.push_back({lo, hi});
     return NEO_HIP_OK;
 }
 
@@ -633,7 +626,7 @@ NEO_HIP_API int neo_hip_upols_group_unregister(neo_hip_upols_group* g, const voi
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
     auto gone = [&](const group_t::range& r) { return !ptr || r.lo == lo; };
     for (const auto& r : g->reg)
-        if (gone(r)) unpin_range(r.lo);
+        if (gone(r)) unpin_range(r.lo, r.hi);
     g->reg.erase(std::remove_if(g->reg.begin(), g->reg.end(), gone), g->reg.end());
     return NEO_HIP_OK;
 }
