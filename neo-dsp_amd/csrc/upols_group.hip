@@ -207,8 +207,7 @@ void unpin_range(uintptr_t lo, uintptr_t hi)
 // The leader's frame read in place: every live member's block (the leader's own io, the others'
 // buffers of the last frame) at p0 + slot * ld in ONE registered, device-mapped range, 16-byte
 // aligned. Then *in_dev / *ld describe it for the step kernel; false: the leader copies.
-bool inplace_frame(const group_t* g, const member& lead, const float* io, const float** in_dev, int64_t* ld,
-                   const float** host0)
+bool inplace_frame(const group_t* g, const member& lead, const float* io, const float** in_dev, int64_t* ld)
 {
     const int C = int(g->slot_member.size());
     auto ptr = [&](int slot) {
@@ -230,7 +229,6 @@ bool inplace_frame(const group_t* g, const member& lead, const float* io, const 
             if (!dev) return false;
             *in_dev = dev;
             *ld = d;
-            *host0 = p0;
             return true;
         }
     return false;
@@ -363,22 +361,6 @@ int call_independent(group_t* g, int i, float* io)
     return NEO_HIP_OK;
 }
 
-// A member's commit in one pass over its block: while io equals the block the frame's step read
-// (snap), io takes the output chunk by chunk; at the first chunk that differs the chunks already
-// replaced are restored from snap (they equaled it) and false is returned. n: samples, a multiple
-// of 16.
-inline bool commit_if_equal(float* io, const float* snap, const float* out, size_t n)
-{
-    for (size_t i = 0; i < n; i += 16) {
-        if (std::memcmp(io + i, snap + i, 64) != 0) {
-            std::memcpy(io, snap, i * sizeof(float));
-            return false;
-        }
-        std::memcpy(io + i, out + i, 64);
-    }
-    return true;
-}
-
 // the output block of shared-handle channel `slot` into the CPU caches ahead of its member's call
 // (the plugin calls the members in order): the GPU wrote it to host memory over PCIe, so the
 // member's copy would otherwise stall on DRAM (0.3 us per 2 KB block on MI355X boxes)
@@ -399,7 +381,7 @@ int call_coalesced(group_t* g, int i, float* io)
         float* spec_in = g->in_pin + int64_t(x.slot) * g->B;
         float* out = g->out_pin + int64_t(x.slot) * g->B;
         NEO_GP_T(tc);
-        const bool differs = !commit_if_equal(io, spec_in, out, size_t(g->B));  // one pass over io
+        const bool differs = std::memcmp(io, spec_in, bb) != 0;
         NEO_GP_ADD(5, tc);
         if (differs) {  // the caller's block differs: this channel's step again
             neo_hip::device_guard dg(g->device);  // the commit path alone makes no HIP call
@@ -411,9 +393,11 @@ int call_coalesced(group_t* g, int i, float* io)
                                                 g->out_dev + int64_t(x.slot) * g->B, g->stream);
             if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
             ++g->stat_redos;
-            std::memcpy(io, out, bb);
             NEO_GP_ADD(7, tc);
         }
+        NEO_GP_T(tm);
+        std::memcpy(io, out, bb);
+        NEO_GP_ADD(6, tm);
         prefetch_output(g, x.slot + 2);
         x.pending = false;
         x.io_last = io;
@@ -437,14 +421,9 @@ int call_coalesced(group_t* g, int i, float* io)
     // the leader copies the blocks it reads (the members' comparisons) while it runs; else the
     // leader copies them first into the mapped staging the step reads
     const float* in_dev = g->in_dev;
-    const float* host0 = nullptr;
     int64_t ld_in = g->B;
-    const bool inplace = inplace_frame(g, x, io, &in_dev, &ld_in, &host0);
+    const bool inplace = inplace_frame(g, x, io, &in_dev, &ld_in);
     auto copy_in = [&] {
-        if (inplace && ld_in == g->B) {  // the frame is [C][B] in slot order: one copy
-            std::memcpy(g->in_pin, host0, size_t(sh->C) * bb);
-            return;
-        }
         for (const auto& y : g->m)
             if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
     };
