@@ -59,6 +59,9 @@ WORKLOADS = {
     "c4": (256, 256, 480000),  # 256 ch, B=256, IR 10 s @ 48 kHz
     "c3": (1, 512, 96000),     # 1 ch, B=512, IR 2 s @ 48 kHz
     "c3long": (1, 512, 480000),  # 1 ch with the headline's 10 s IR (far level): the plugin's real-time case
+    # the reference benchmark's own shape (extra/benchmark/src/convolution.cpp:47-55, its longest
+    # IR): 1 ch, B=4096, IR 2^17 taps, P=32: the plain step (no streaming levels)
+    "ref4096": (1, 4096, 131072),
 }
 STRONG = {"c5full"}  # workloads whose channel count is the whole job's, split over the ranks
 
@@ -775,7 +778,7 @@ def run_upols(args, world, rank, local):
                      "note": "device-resident IR [C][L]: normalize (sequential-float energy, min over channels), "
                              "partition r2c, then the first streaming block (far segment spectra + level priming); "
                              "max over ranks"}
-    latency_mode = run_latency_mode(args, conv, feed, C, B, world, C_total) if levels else None
+    latency_mode = run_latency_mode(args, conv, feed, C, B, world, C_total)
     offline = run_upols_offline(args, conv, C, B, P, x, y, nx * B, stream, world, C_total)
     host_io = None
     if not args.no_host_io:
@@ -854,7 +857,8 @@ def run_latency_mode(args, conv, feed, C, B, world, C_total):
     each call synchronous) on the same convolver and input, for the shapes it takes (C3): the
     host round trip per block (one call, complete on return), the same number of steps as the
     headline back to back (wall clock), and the GPU time per step (record read -> done, on the
-    GPU clock). None where the shape is not latency-bound (the handle refuses it)."""
+    GPU clock). available False where the shape is not latency-bound (the handle refuses it).
+    Without the streaming levels (ref4096) it is the plain step's persistent kernel."""
     import numpy as np
 
     try:

@@ -211,16 +211,19 @@ NEO_HIP_API int neo_hip_upols_part_plan(int channels, int block, int partitions,
  * instead of one call in 2 G paying for two groups' launches. Same outputs; costs one
  * cross-stream wait per piece. 0 = off. The levels re-prime when it changes. */
 NEO_HIP_API int neo_hip_upols_set_paced(neo_hip_upols* h, int enable);
-/* Latency mode for latency-bound shapes (few channels, filters up to 256 partitions, blocks up
- * to 512; C3): ONE persistent kernel per handle steps every block. A call writes the block's
- * record to a mailbox in mapped host memory and spins until the kernel reports the block done:
- * no launch and no stream wait per block, and the Toeplitz levels' slices run beside the
- * caller's next block instead of before it. Every process call is then SYNCHRONOUS (complete
- * on return; the stream argument is not used) and device inputs must be ready when it is made.
- * The kernel leaves after idle_ms without a block (the next call relaunches it) and whenever a
- * setup call (set_filter, set_impulse, reset, set_ahead, set_persistent(0), destroy) runs.
- * Outputs equal the normal streaming step's to float rounding (the same sums in the same order;
- * the levels re-prime on entry and exit). Not available: EINVAL names the reason. */
+/* Latency mode for latency-bound shapes (up to 16 channels; C3, and the reference benchmark's
+ * one channel at B = 4096): ONE persistent kernel per handle steps every block. With the
+ * streaming levels (64 partitions and up, blocks up to 512, the far level included) it runs their
+ * block and slice roles, the Toeplitz levels' slices beside the caller's next block instead of
+ * before it; without them (fewer than 64 partitions, any block up to 4096) the plain fused step.
+ * A call writes the block's record to a mailbox in mapped host memory and spins until the kernel
+ * reports the block done: no launch and no stream wait per block. Every process call is then
+ * SYNCHRONOUS (complete on return; the stream argument is not used) and device inputs must be
+ * ready when it is made. The kernel leaves after idle_ms without a block (the next call
+ * relaunches it) and whenever a setup call (set_filter, set_impulse, reset, set_ahead,
+ * set_persistent(0), destroy) runs. Outputs equal the normal step's bit for bit (the same sums in
+ * the same order; the levels re-prime on entry and exit). Not available: EINVAL names the
+ * reason. */
 NEO_HIP_API int neo_hip_upols_set_persistent(neo_hip_upols* h, int enable, double idle_ms);
 /* requested, kernel resident now, persistent launches so far */
 NEO_HIP_API int neo_hip_upols_get_persistent(neo_hip_upols* h, int* enabled, int* running, int64_t* launches);

@@ -49,22 +49,35 @@ namespace neo_hip {
 // s = 0..S-1 and runs the c2r: one launch per block, deterministic results.
 // TAIL (upola_convolver_v2 sub-block pieces): no window / insert, partitions p >= 1 only
 // (overlap_add_convolver.hpp:96-108), slabs summed by k_upola2_piece.
-template<int B, bool FUSED, bool OLA, bool TAIL = false, int UNROLL = upols_cfg<B>::U>
-__global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
+// the LDS of one step workgroup (k_upols_step, k_plain_persist)
+template<int B>
+struct step_lds {
+    using K = upols_cfg<B>;
+    __attribute__((aligned(16))) cf xnew[B];  // new spectrum; later the summed spectrum
+    cf fft[K::LL];
+    cf tw[K::TW1 + K::TW2];
+    __attribute__((aligned(16))) float4 red[K::RPI > 1 ? 256 * 2 * K::VPT : 1];
+    int last;
+};
+
+// The step of workgroup (c, s): returns true in the workgroup that ran the channel's tail (FUSED:
+// the last split to arrive). WT (the latency mode's persistent plain step): the input block read
+// at system scope and the output stored write-through.
+template<int B, bool FUSED, bool OLA, bool TAIL, int UNROLL, bool WT = false>
+__device__ __forceinline__ bool upols_step_wg(step_lds<B>& L, int c, int s,
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, cf* __restrict__ part, int* __restrict__ arrivals,
     const cf* __restrict__ twg, int P, int ring, int S, int rows, int w, int64_t cstride, int64_t pstride, int pc)
 {
     using K = upols_cfg<B>;
     static_assert(!(TAIL && FUSED), "the v2 tail is summed by k_upola2_piece");
-    __shared__ __attribute__((aligned(16))) cf xnew[B];  // new spectrum; later the summed spectrum
-    __shared__ cf fft[K::LL];
-    __shared__ cf tw[K::TW1 + K::TW2];
-    __shared__ __attribute__((aligned(16))) float4 red[K::RPI > 1 ? 256 * 2 * K::VPT : 1];
-    __shared__ int last;
+    cf* xnew = L.xnew;
+    cf* fft = L.fft;
+    cf* tw = L.tw;
+    float4* red = L.red;
+    int& last = L.last;
 
     const int tid = threadIdx.x;
-    const int c = blockIdx.x / S, s = blockIdx.x - c * S;
     const int p0 = s * rows, p1 = min(P, p0 + rows);
     const int64_t crow = int64_t(c) * cstride;  // channel base in H / FDL (complex units); row p at + p * pstride
     const int64_t ps4 = pstride / 2;            // row stride in float4 units
@@ -72,7 +85,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
     if (!TAIL && s == 0) {
         const float* in_c = in + int64_t(c) * ld_in;
         float* prev_c = prev + int64_t(c) * B;
-        window_fft<B, OLA>(prev_c, in_c, fft, tw, tid, twg);
+        window_fft<B, OLA, (B / 8 <= 256 ? 8 : B / 256), WT>(prev_c, in_c, fft, tw, tid, twg);
         cf* row = fdl + crow + int64_t(w) * pstride;
         for (int k = tid; k < B; k += 256) {
             const cf x = r2c_split<B>(fft, tw + K::TW1, k);
@@ -81,7 +94,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
         }
         if constexpr (!OLA) {  // the window's second half becomes the next call's first half
             for (int i = tid; i < B / 4; i += 256)
-                reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
+                reinterpret_cast<float4*>(prev_c)[i] = ld4_in<WT>(reinterpret_cast<const float4*>(in_c) + i);
         }
         __syncthreads();
     }
@@ -176,8 +189,8 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
             }
         }
         __syncthreads();
-        c2r_tail<B, OLA>(xnew, fft, tw, out_c, prev + int64_t(c) * B, tid);
-        return;
+        c2r_tail<B, OLA, (B / 4 <= 256 ? 4 : B / 256), false, false, WT>(xnew, fft, tw, out_c, prev + int64_t(c) * B, tid);
+        return true;
     }
 
     // publish this split's slab
@@ -190,7 +203,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
             slab[q] = make_float4(b0.x, b0.y, b1.x, b1.y);
         }
     }
-    if constexpr (!FUSED) return;  // k_upols_finish sums the slabs in the next launch
+    if constexpr (!FUSED) return false;  // k_upols_finish sums the slabs in the next launch
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     __syncthreads();
     if (tid == 0) {
@@ -200,7 +213,7 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
         last = before == S - 1;
     }
     __syncthreads();
-    if (!last) return;  // uniform per workgroup
+    if (!last) return false;  // uniform per workgroup
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -231,7 +244,116 @@ __global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
         reinterpret_cast<float4*>(xnew)[q] = sum;
     }
     __syncthreads();
-    c2r_tail<B, OLA>(xnew, fft, tw, out_c, prev + int64_t(c) * B, tid);
+    c2r_tail<B, OLA, (B / 4 <= 256 ? 4 : B / 256), false, false, WT>(xnew, fft, tw, out_c, prev + int64_t(c) * B, tid);
+    return true;
+}
+
+template<int B, bool FUSED, bool OLA, bool TAIL = false, int UNROLL = upols_cfg<B>::U>
+__global__ __launch_bounds__(256, (B <= 1024 ? 8 : 2)) void k_upols_step(
+    const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
+    const cf* __restrict__ H, cf* __restrict__ fdl, cf* __restrict__ part, int* __restrict__ arrivals,
+    const cf* __restrict__ twg, int P, int ring, int S, int rows, int w, int64_t cstride, int64_t pstride, int pc)
+{
+    __shared__ step_lds<B> L;
+    const int c = blockIdx.x / S, s = blockIdx.x - c * S;
+    (void)upols_step_wg<B, FUSED, OLA, TAIL, UNROLL>(L, c, s, in, ld_in, out, ld_out, prev, H, fdl, part, arrivals, twg,
+                                                     P, ring, S, rows, w, cstride, pstride, pc);
+}
+
+// Latency mode of a handle without streaming levels (fewer than 64 partitions, or the levels off;
+// blocks up to 4096: the reference benchmark's shape, extra/benchmark/src/convolution.cpp:47-55):
+// the fused plain step's C x S workgroups stay resident across steps. Per step n every workgroup
+// waits for step n - 1 to be complete (blk_done: every channel's tail summed its slabs, reset its
+// split counter and wrote its output; split 0 wrote the FDL row and the previous block), takes the
+// record (workgroup 0 polls the mailbox, ps_record) and runs its split (upols_step_wg, the input
+// read and the output stored at system scope). The tail of each channel counts the channel in; the
+// last one tells the host (mb->done) and the workgroups (blk_done).
+struct plain_persist_args : persist_ctl {
+    const cf* H;
+    cf* fdl;
+    cf* part;
+    int* arrivals;
+    float* prev;
+    const cf* twg;
+    int64_t ld_in, ld_out, cstride, pstride;
+    int C, P, ring, S, rows, pc;
+};
+
+template<int B, bool OLA>
+__global__ __launch_bounds__(256) void k_plain_persist(plain_persist_args pa)
+{
+    __shared__ step_lds<B> L;
+    __shared__ uint64_t io[2];
+    __shared__ int go;
+    const int c = int(blockIdx.x) / pa.S, s = int(blockIdx.x) - c * pa.S;
+    const bool lead = blockIdx.x == 0;
+    unsigned long long t_seen = 0;  // thread 0 of workgroup 0: when the step's record was read
+    int w = pa.w0;                  // ring row of step n
+    for (int64_t n = pa.n0;; ++n, w = w + 1 == pa.ring ? 0 : w + 1) {
+        if (threadIdx.x == 0) {
+            bool ok = ps_wait(pa, [&] { return ps_ld(pa.flags + 0) >= n - 1; });
+            if (ok) ps_acquire();  // the slabs, FDL row and previous block of step n - 1 (other workgroups')
+            go = ps_record(pa, n, lead, gridDim.x > 1, ok, io, t_seen);
+        }
+        __syncthreads();
+        if (!go) break;
+        const bool tail = upols_step_wg<B, true, OLA, false, upols_cfg<B>::U, true>(
+            L, c, s, reinterpret_cast<const float*>(io[0]), pa.ld_in, reinterpret_cast<float*>(io[1]), pa.ld_out,
+            pa.prev, pa.H, pa.fdl, pa.part, pa.arrivals, pa.twg, pa.P, pa.ring, pa.S, pa.rows, w, pa.cstride,
+            pa.pstride, pa.pc);
+        if (tail) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the output's write-through stores complete
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                int64_t* arr = pa.flags + kPsFlagArrive + n % kPsArr;
+                if (__hip_atomic_fetch_add(arr, int64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pa.C - 1) {
+                    ps_st(arr, 0);  // free for step n + kPsArr
+                    const unsigned long long t_done = wall_clock64();
+                    __hip_atomic_store(&pa.mb->done, n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    pa.tl[2 * (n % kPsRing) + 1] = t_done;
+                    ps_acquire();  // the other channels' releases, passed on by the one below
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    ps_st(pa.flags + 0, n);
+                }
+            }
+        }
+        if (lead && threadIdx.x == 0) pa.tl[2 * (n % kPsRing)] = t_seen;
+    }
+    if (lead && threadIdx.x == 0) __hip_atomic_store(&pa.mb->alive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int plain_persist_launch(upols_t* h, const persist_ctl& ctl, int64_t ld_in, int64_t ld_out)
+{
+    if (h->C * h->S > 256) return fail(NEO_HIP_EINVAL, "latency mode: %d x %d plain step workgroups", h->C, h->S);
+    plain_persist_args pa{};
+    static_cast<persist_ctl&>(pa) = ctl;
+    pa.H = h->H;
+    pa.fdl = h->fdl;
+    pa.part = h->part;
+    pa.arrivals = h->arrivals;
+    pa.prev = h->prev;
+    pa.twg = h->tw;
+    pa.ld_in = ld_in;
+    pa.ld_out = ld_out;
+    pa.cstride = h->cstride;
+    pa.pstride = h->pstride;
+    pa.C = h->C;
+    pa.P = h->P;
+    pa.ring = h->ring;
+    pa.S = h->S;
+    pa.rows = h->rows;
+    pa.pc = h->pc;
+    const unsigned grid = unsigned(h->C) * unsigned(h->S);
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_plain_persist<BB, true>), dim3(grid), dim3(256), 0, h->ps_stream, pa))
+    } else {
+        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_plain_persist<BB, false>), dim3(grid), dim3(256), 0, h->ps_stream, pa))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    return NEO_HIP_OK;
 }
 
 // Unfused tail (one workgroup per channel): sum the S slabs in order, c2r, write.
@@ -612,7 +734,8 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     const int target = o.split_workgroups ? o.split_workgroups : 1024;
     // >= 8 rows per split keeps the slab sum short at small C; the one-launch (latency) form
     // takes >= 16 (C3: 12 splits, 9.6 vs 10.6 us per block with 24)
-    const int min_rows = h->fused ? 16 : 8;
+    // (an explicit workgroup target is taken as given)
+    const int min_rows = o.split_workgroups ? 1 : h->fused ? 16 : 8;
     int S = std::max(1, std::min({(target + channels - 1) / channels, (partitions + min_rows - 1) / min_rows, 64}));
     h->rows = (partitions + S - 1) / S;
     h->S = (partitions + h->rows - 1) / h->rows;

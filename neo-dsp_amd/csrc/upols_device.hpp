@@ -83,7 +83,27 @@ __device__ __forceinline__ cf finish(const acc4& a, bool bin0)
 // count (the MAC loop itself needs ~60 VGPRs; occupancy is what streams HBM).
 // OLS window = [previous block | new block] (overlap_save.hpp:90-95);
 // OLA window = [new block | zeros]          (overlap_add.hpp:84-86).
-template<int B, bool OLA, int E = (B / 8 <= 256 ? 8 : B / 256)>
+// WT: the input block read at system scope (a persistent kernel: the caller may have rewritten it
+// since this CU last read there)
+__device__ __forceinline__ cf ld_in_cf(const cf* p, bool wt)
+{
+    if (wt)
+        return __builtin_bit_cast(cf, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_SYSTEM));
+    return *p;
+}
+template<bool WT>
+__device__ __forceinline__ float4 ld4_in(const float4* p)
+{
+    if constexpr (WT) {
+        const cf a = ld_in_cf(reinterpret_cast<const cf*>(p), true), b = ld_in_cf(reinterpret_cast<const cf*>(p) + 1, true);
+        return make_float4(a.x, a.y, b.x, b.y);
+    } else {
+        return *p;
+    }
+}
+
+template<int B, bool OLA, int E = (B / 8 <= 256 ? 8 : B / 256), bool WT = false>
 __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_c, cf* fft, cf* tw1, int tid,
                                            const cf* __restrict__ twg = nullptr)
 {
@@ -100,8 +120,8 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int n = tid + m * T;
-            if constexpr (OLA) v[m] = n < B / 2 ? iz[n] : cf{0.f, 0.f};
-            else v[m] = n < B / 2 ? pz[n] : iz[n - B / 2];
+            if constexpr (OLA) v[m] = n < B / 2 ? ld_in_cf(iz + n, WT) : cf{0.f, 0.f};
+            else v[m] = n < B / 2 ? pz[n] : ld_in_cf(iz + n - B / 2, WT);
         }
     }
     if (twg) twr.store(tw1, tid);

@@ -46,6 +46,100 @@ struct persist_mb {
     int32_t pad;
 };
 
+// What both persistent kernels (k_lvl_persist, upols_levels.hip; k_plain_persist, upols.hip) share:
+// the mailbox, the device flags (kPsFlag*), the step times, the idle limit and the deadline.
+struct persist_ctl {
+    persist_mb* mb;                 // the mapped mailbox (device address)
+    int64_t* flags;                 // blk_done, quit, arrivals, records, sl_done (kPsFlag*)
+    unsigned long long* tl;         // [kPsRing][2] record seen / done
+    long long idle_ticks, dead_ticks;
+    int64_t n0;                     // first step of this launch
+    int w0;                         // its ring row
+};
+// device flags of the persistent kernels (int64 words): blk_done, quit, the per-step arrival
+// counters of the block workgroups (a ring: a channel may run up to three steps ahead of another),
+// the last step whose record block workgroup 0 handed on and those records (a ring), then
+// sl_done per slice workgroup
+constexpr int kPsArr = 8;
+constexpr int kPsFlagArrive = 2, kPsFlagArriveFdl = kPsFlagArrive + kPsArr, kPsFlagGo = kPsFlagArriveFdl + kPsArr;
+constexpr int kPsFlagIo = kPsFlagGo + 1;
+constexpr int kPsFlagSlices = kPsFlagIo + 2 * kPsArr;
+
+__device__ __forceinline__ int64_t ps_ld(const int64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ps_st(int64_t* p, int64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ps_acquire()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// thread 0: wait until cond() (quit and the deadline checked every round); false = leave
+template<class F>
+__device__ __forceinline__ bool ps_wait(const persist_ctl& pc, F cond)
+{
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+        if (cond()) return true;
+        if (ps_ld(pc.flags + 1)) return false;
+        if ((long long)(wall_clock64() - t0) > pc.dead_ticks) {
+            __hip_atomic_store(&pc.mb->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ps_st(pc.flags + 1, 1);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// thread 0 of a block workgroup, ok = its own waits passed: step n's record into io[2]. Workgroup 0
+// (lead) polls the mailbox slot (both words tagged with the step's lap; the host's stop, quit and
+// the idle limit checked every 16th poll) and, with more than one block workgroup (share), hands
+// the record on through the flags; the others wait for it there. false = leave.
+__device__ __forceinline__ bool ps_record(const persist_ctl& pc, int64_t n, bool lead, bool share, bool ok,
+                                          uint64_t* io, unsigned long long& t_seen)
+{
+    if (lead) {
+        const int slot = int(n % kPsRing);
+        const uint64_t tag = ps_tag(n);
+        const unsigned long long t0 = wall_clock64();
+        for (unsigned it = 0; ok; ++it) {
+            const uint64_t r0 = __hip_atomic_load(&pc.mb->rec[slot].in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t r1 = __hip_atomic_load(&pc.mb->rec[slot].out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((r0 & 15) == tag && (r1 & 15) == tag) {
+                io[0] = r0 & ~uint64_t(15);
+                io[1] = r1 & ~uint64_t(15);
+                t_seen = wall_clock64();
+                if (share) {
+                    int64_t* r = pc.flags + kPsFlagIo + 2 * (n % kPsArr);
+                    ps_st(r, int64_t(io[0]));
+                    ps_st(r + 1, int64_t(io[1]));
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    ps_st(pc.flags + kPsFlagGo, n);
+                }
+                return true;
+            }
+            if ((it & 15) == 15 &&
+                (__hip_atomic_load(&pc.mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) || ps_ld(pc.flags + 1) ||
+                 (long long)(wall_clock64() - t0) > pc.idle_ticks)) {
+                ps_st(pc.flags + 1, 1);
+                return false;
+            }
+        }
+        return false;
+    }
+    if (!ok || !ps_wait(pc, [&] { return ps_ld(pc.flags + kPsFlagGo) >= n; })) return false;
+    ps_acquire();
+    const int64_t* r = pc.flags + kPsFlagIo + 2 * (n % kPsArr);
+    io[0] = uint64_t(ps_ld(r));
+    io[1] = uint64_t(ps_ld(r + 1));
+    return true;
+}
+
 struct level_plan {
     int a0 = 1;                      // the block step takes partitions [0, a0)
     int n = 0;                       // Toeplitz levels
@@ -264,6 +358,9 @@ int step_group_for(int C, int B, int P);
 int bg_pad_for(int C, int B);
 // latency mode: whole blocks through the persistent kernel, synchronous (upols_levels.hip)
 int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t nblocks);
+// latency mode of a handle without streaming levels: the plain step's persistent kernel on
+// h->ps_stream (upols.hip), its control (mailbox, flags, first step) set up by the caller
+int plain_persist_launch(upols_t* h, const persist_ctl& ctl, int64_t ld_in, int64_t ld_out);
 // stop the persistent kernel (if any) and leave the levels to re-prime on the next normal step
 int persist_stop(upols_t* h);
 // why a handle cannot run the latency mode (nullptr: it can)

@@ -2414,7 +2414,9 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
 //            n - 1 published (agent acquire), then publish (agent release) and sl_done = n
 // Every wait has a deadline (mb->err, then every workgroup leaves); the block workgroups leave
 // after ps_idle_ms without a record, and the host relaunches at the next block.
-struct persist_args {
+// persist_ctl (upols_handle.hpp): the mailbox, flags, step times and limits; n0 = the launch's
+// first step (the levels primed at step 0)
+struct persist_args : persist_ctl {
     slice_args base;                // handle constants (H, FDL, ring, strides, prev, twiddles, a0)
     cf* slab[kLvToep];
     int T[kLvToep], LT[kLvToep], A[kLvToep], Bd[kLvToep], JH[kLvToep], UPW[kLvToep], U[kLvToep];  // LT = log2 T
@@ -2423,59 +2425,13 @@ struct persist_args {
     int far, fU, fK, ffpl;          // far level (persist_far): on, units, window group, phase-1 f rows per lane
     int wgf0, wgf1;                 // its workgroups: slice workgroups [wgf0, wgf1) (after the Toeplitz levels')
     cf* ff;                         // far field [2][C][kFarT][B]
-    int64_t n0;                     // first step of this launch (levels primed at step 0)
-    int w0;                         // its ring row
-    persist_mb* mb;                 // the mapped mailbox (device address)
-    int64_t* flags;                 // blk_done, quit, arrivals, records, sl_done (kPsFlag*)
-    unsigned long long* tl;         // [kPsRing][2] record seen / done
-    long long idle_ticks, dead_ticks;
 };
 
-__device__ __forceinline__ int64_t ps_ld(const int64_t* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void ps_st(int64_t* p, int64_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ int ps_ring_row(const persist_args& pa, int64_t n)
 {
     const int64_t r = (int64_t(pa.w0) + (n - pa.n0)) % pa.base.ring;
     return int(r < 0 ? r + pa.base.ring : r);
 }
-
-// thread 0: wait until cond() (quit and the deadline checked every round); false = leave
-template<class F>
-__device__ __forceinline__ bool ps_wait(const persist_args& pa, F cond)
-{
-    const unsigned long long t0 = wall_clock64();
-    for (;;) {
-        if (cond()) return true;
-        if (ps_ld(pa.flags + 1)) return false;
-        if ((long long)(wall_clock64() - t0) > pa.dead_ticks) {
-            __hip_atomic_store(&pa.mb->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            ps_st(pa.flags + 1, 1);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
-__device__ __forceinline__ void ps_acquire()
-{
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// device flags of the persistent kernel (int64 words): blk_done, quit, the per-step arrival
-// counters of the block workgroups (a ring: a channel may run up to three steps ahead of another),
-// the last step whose record block workgroup 0 handed on and those records (a ring), then
-// sl_done per slice workgroup
-constexpr int kPsArr = 8;
-constexpr int kPsFlagArrive = 2, kPsFlagArriveFdl = kPsFlagArrive + kPsArr, kPsFlagGo = kPsFlagArriveFdl + kPsArr;
-constexpr int kPsFlagIo = kPsFlagGo + 1;
-constexpr int kPsFlagSlices = kPsFlagIo + 2 * kPsArr;
 
 template<int B, bool OLA>
 __device__ __forceinline__ void persist_block(const persist_args& pa, int c, char* smem)
@@ -2513,45 +2469,7 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
             // a window of some level starts (every level's T is a multiple of the first's): its slab
             // rows were written by other workgroups since this CU last read that buffer
             if (ok && (n == pa.n0 || (n & (pa.T[0] - 1)) == 0)) ps_acquire();
-            const int slot = int(n % kPsRing);
-            if (c == 0) {
-                // the record of step n (both words tagged with its lap); the host's stop, quit and
-                // the idle limit checked every 16th poll; workgroup 0 alone decides, the other
-                // channels take the record from it
-                const uint64_t tag = ps_tag(n);
-                const unsigned long long t0 = wall_clock64();
-                for (unsigned it = 0; ok; ++it) {
-                    const uint64_t r0 = __hip_atomic_load(&pa.mb->rec[slot].in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    const uint64_t r1 = __hip_atomic_load(&pa.mb->rec[slot].out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if ((r0 & 15) == tag && (r1 & 15) == tag) {
-                        io[0] = r0 & ~uint64_t(15);
-                        io[1] = r1 & ~uint64_t(15);
-                        t_seen = wall_clock64();
-                        if (pa.nblk > 1) {
-                            int64_t* r = pa.flags + kPsFlagIo + 2 * (n % kPsArr);
-                            ps_st(r, int64_t(io[0]));
-                            ps_st(r + 1, int64_t(io[1]));
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                            ps_st(pa.flags + kPsFlagGo, n);
-                        }
-                        break;
-                    }
-                    if ((it & 15) == 15 &&
-                        (__hip_atomic_load(&pa.mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                         ps_ld(pa.flags + 1) || (long long)(wall_clock64() - t0) > pa.idle_ticks)) {
-                        ok = false;
-                        ps_st(pa.flags + 1, 1);
-                    }
-                }
-            } else if (ok) {
-                ok = ps_wait(pa, [&] { return ps_ld(pa.flags + kPsFlagGo) >= n; });
-                if (ok) {
-                    ps_acquire();
-                    const int64_t* r = pa.flags + kPsFlagIo + 2 * (n % kPsArr);
-                    io[0] = uint64_t(ps_ld(r));
-                    io[1] = uint64_t(ps_ld(r + 1));
-                }
-            }
+            ok = ps_record(pa, n, c == 0, pa.nblk > 1, ok, io, t_seen);
             go = ok;
         }
         __syncthreads();
@@ -2700,13 +2618,14 @@ __global__ __launch_bounds__(256) void k_lvl_persist(persist_args pa)
 
 const char* persist_ineligible(const upols_t* h)
 {
-    if (!h->ahead) return "the latency mode runs the streaming levels (from 64 partitions)";
     if (h->v2) return "upola_convolver_v2 takes sub-block input";
+    if (h->C > 16) return "more than 16 channels (the latency mode is for latency-bound shapes)";
+    if (!h->ahead)  // the plain step's workgroups, all resident (one per CU at B = 4096)
+        return h->C * h->S > 256 ? "the plain step's channels x splits above 256 workgroups" : nullptr;
     if (h->lv.n && h->lv.T[h->lv.n - 1] == kBigT) return "the 128-block Toeplitz form of the far band (far_level 0)";
     if (h->lv.nseg && h->far_raw) return "the recomputed far level (far_level 2)";
     if (h->lv.nseg && far_group(h) > 2) return "a far window group above 2 (neo_hip_upols_opts.far_group)";
-    if (h->C > 16) return "more than 16 channels (the latency mode is for latency-bound shapes)";
-    if (h->B > 512) return "blocks above 512 samples";
+    if (h->B > 512) return "blocks above 512 samples with the streaming levels";
     return nullptr;
 }
 
@@ -2724,23 +2643,10 @@ static int persist_level_wgs(const upols_t* h, int l, int& U, int& UPW, int& JH)
     return most;
 }
 
-static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
+// the levels' part of the latency mode's arguments (window 0 of every level primed first when
+// the schedule restarts)
+static int persist_levels(upols_t* h, persist_args& pa, int64_t ld_in, int64_t ld_out)
 {
-    if (!h->ps_stream) {
-        // the most urgent priority: such a stream gets a hardware queue of its own. At the default
-        // priority it shares one of the process's GPU_MAX_HW_QUEUES (4) with other streams, whose
-        // work then queues behind the resident kernel until it leaves (idle limit): measured on
-        // MI355X, the third new torch stream waited 1.4 s behind a 1.5 s idle limit
-        // (tools/dbg_hwq.py; none waited with this priority)
-        int lo = 0, hi = 0;
-        NEO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        NEO_HIP_CHECK(hipStreamCreateWithPriority(&h->ps_stream, hipStreamNonBlocking, hi));
-        if (int rc = halloc(reinterpret_cast<void**>(&h->ps_mb), reinterpret_cast<void**>(&h->ps_mb_dev), sizeof(persist_mb)))
-            return rc;
-        std::memset(h->ps_mb, 0, sizeof(persist_mb));
-        if (int rc = dalloc(&h->ps_tl, 10 * kPsRing * sizeof(unsigned long long))) return rc;
-        NEO_HIP_CHECK(hipMemsetAsync(h->ps_tl, 0, 10 * kPsRing * sizeof(unsigned long long), h->ps_stream));
-    }
     if (int rc = lvl_buffers(h)) return rc;
     if (!h->ps_valid || h->lv_n < 0) {  // window 0 of every level, from this block on
         if (int rc = lvl_join(h, h->ps_stream)) return rc;
@@ -2749,7 +2655,6 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
         h->lv_n = 0;
         h->ps_valid = true;
     }
-    persist_args pa{};
     pa.base = base_args(h);
     pa.base.prev = h->prev;
     pa.base.twg = h->tw;
@@ -2783,7 +2688,34 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
             }
         pa.wgf1 = pa.wgf0 + most;
     }
-    const int nsl = pa.wgf1;
+    return NEO_HIP_OK;
+}
+
+static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
+{
+    if (!h->ps_stream) {
+        // the most urgent priority: such a stream gets a hardware queue of its own. At the default
+        // priority it shares one of the process's GPU_MAX_HW_QUEUES (4) with other streams, whose
+        // work then queues behind the resident kernel until it leaves (idle limit): measured on
+        // MI355X, the third new torch stream waited 1.4 s behind a 1.5 s idle limit
+        // (tools/dbg_hwq.py; none waited with this priority)
+        int lo = 0, hi = 0;
+        NEO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        NEO_HIP_CHECK(hipStreamCreateWithPriority(&h->ps_stream, hipStreamNonBlocking, hi));
+        if (int rc = halloc(reinterpret_cast<void**>(&h->ps_mb), reinterpret_cast<void**>(&h->ps_mb_dev), sizeof(persist_mb)))
+            return rc;
+        std::memset(h->ps_mb, 0, sizeof(persist_mb));
+        if (int rc = dalloc(&h->ps_tl, 10 * kPsRing * sizeof(unsigned long long))) return rc;
+        NEO_HIP_CHECK(hipMemsetAsync(h->ps_tl, 0, 10 * kPsRing * sizeof(unsigned long long), h->ps_stream));
+    }
+    persist_args pa{};
+    if (h->ahead) {
+        if (int rc = persist_levels(h, pa, ld_in, ld_out)) return rc;
+    } else if (!h->ps_valid || h->lv_n < 0) {  // the plain step continues from the FDL ring: nothing to prime
+        h->lv_n = 0;
+        h->ps_valid = true;
+    }
+    const int nsl = h->ahead ? pa.wgf1 : 0;
     if (h->ps_nslices < nsl || !h->ps_flags) {
         dfree(h->ps_flags);
         h->ps_flags = nullptr;
@@ -2819,7 +2751,9 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     h->ps_mb->done = pa.n0;
     h->ps_mb->alive = 1;
     const unsigned grid = unsigned(h->C + nsl);
-    if (h->ola) {
+    if (!h->ahead) {
+        if (int rc = plain_persist_launch(h, pa, ld_in, ld_out)) return rc;
+    } else if (h->ola) {
         NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 512) hipLaunchKernelGGL((k_lvl_persist<BB, true>), dim3(grid),
                                                                               dim3(256), 0, h->ps_stream, pa))
     } else {

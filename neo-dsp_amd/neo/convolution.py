@@ -349,7 +349,9 @@ class UpolsConvolver:
     def set_persistent(self, enable: bool, idle_ms: float = 50.0) -> None:
         """Latency mode (neo_hip_upols_set_persistent): one persistent kernel steps every block;
         every process call is then synchronous (complete on return, the stream is not used).
-        Raises for shapes it does not take (more than 256 partitions, 16 channels, B > 512)."""
+        With the streaming levels it runs their block and slice roles (blocks up to 512); without
+        them (fewer than 64 partitions) the plain fused step, blocks up to 4096. Raises for shapes
+        it does not take (more than 16 channels, sub-block v2, B > 512 with the levels)."""
         _native.check(_native.load().neo_hip_upols_set_persistent(self._h, int(bool(enable)), float(idle_ms)))
 
     def persistent_info(self) -> dict:

@@ -1,5 +1,6 @@
-"""Latency mode (neo_hip_upols_set_persistent, upols_levels.hip k_lvl_persist): one persistent
-kernel per handle steps every block of a latency-bound shape (the reference's benchmark shape,
+"""Latency mode (neo_hip_upols_set_persistent, upols_levels.hip k_lvl_persist; upols.hip
+k_plain_persist for handles without streaming levels): one persistent kernel per handle steps
+every block of a latency-bound shape (the reference's benchmark shape,
 extra/benchmark/src/convolution.cpp:34-44: one channel, one call per block). Outputs must equal
 the oracle's dense_convolve (uniform_partitioned_convolver.hpp:47-65) and the normal streaming
 step's bit for bit: the same sums in the same order, and its block role, a separate code
@@ -158,7 +159,7 @@ def test_latency_mode_host_buffers(neo_gpu, oracle):
 
 
 def test_latency_mode_rejects_other_shapes(neo_gpu):
-    """more than 16 channels, B > 512, sub-block v2, the far band as a 128-block Toeplitz level or
+    """more than 16 channels, B > 512 with the streaming levels, sub-block v2, the far band as a 128-block Toeplitz level or
     recomputed every window: EINVAL"""
     for args, kw in (((32, 128, 100), {}), ((1, 1024, 100), {}), ((1, 256, 100), {"method": "upola_v2"}),
                      ((1, 512, 300), {"options": {"far_level": 0}}), ((1, 512, 300), {"options": {"far_level": 2}})):
@@ -283,3 +284,94 @@ def test_latency_mode_far_level_channels_relaunch(neo_gpu, oracle):
     assert peak_err(got[chans], oracle.dense_convolve(x[chans], parts[chans])) <= TOL
     assert same_sums(got, _run(nc, x, B, torch))
     pc.set_persistent(False)
+
+
+@pytest.mark.parametrize("L", [2 ** 11, 2 ** 14, 2 ** 17])
+def test_latency_mode_plain_step_b4096(neo_gpu, oracle, L):
+    """The reference benchmark's shape (extra/benchmark/src/convolution.cpp:47-55: one channel,
+    B = 4096, IR 2^11..2^17, one call per block): P = 1..32 partitions, no streaming levels, so the
+    plain fused step runs as the persistent kernel (k_plain_persist). Against the oracle and the
+    normal one-launch step bit for bit (the same workgroup body, upols_step_wg)."""
+    torch = pytest.importorskip("torch")
+    B = 4096
+    P = neo_gpu.num_partitions(L, B)
+    ir = np.stack([oracle.noise(7000 + L % 97, L)])
+    parts = oracle.uniform_partition(oracle.normalize_impulse(ir), B)
+    pc = neo_gpu.UpolsConvolver(1, B, P)
+    nc = neo_gpu.UpolsConvolver(1, B, P)
+    for c in (pc, nc):
+        c.filter(parts)
+        c.set_batch(False)
+    assert not pc.ahead_info()[0]
+    pc.set_persistent(True)
+    nb = P + 40
+    x = np.stack([oracle.noise(7100, B * nb)])
+    got = _run(pc, x, B, torch)
+    info = pc.persistent_info()
+    assert info["launches"] >= 1 and info["running"], info
+    st = pc.persist_step_times()
+    assert len(st) == min(63, nb) and all(0 < s < 1000 for s in st), st[:4]
+    assert peak_err(got, oracle.dense_convolve(x, parts)) <= TOL
+    assert same_sums(got, _run(nc, x, B, torch))
+    pc.set_persistent(False)
+    pc.close()
+    nc.close()
+
+
+@pytest.mark.parametrize("method,C,B,P", [("upols", 4, 512, 40), ("upola", 3, 256, 63), ("upols", 16, 64, 20),
+                                          ("upols", 2, 2048, 12)])
+def test_latency_mode_plain_step_channels_relaunch(neo_gpu, oracle, method, C, B, P):
+    """k_plain_persist with several channels (the last channel's tail signals), OLA, small and
+    large blocks; idle limit 5 ms with pauses (relaunches keep the FDL ring and write position),
+    calls of 1 and 3 blocks, switched off mid-stream (the normal step continues from the same
+    state): the normal step bit for bit, and the oracle for upols."""
+    torch = pytest.importorskip("torch")
+    (pc, nc), parts = _pair(neo_gpu, oracle, C, B, P, 7200 + C, method)
+    assert not pc.ahead_info()[0]
+    pc.set_persistent(True, idle_ms=5.0)
+    nb = 2 * P + 50
+    x = np.stack([oracle.noise(7300 + c, B * nb) for c in range(C)])
+    t = torch.from_numpy(x.copy()).cuda()
+    torch.cuda.current_stream().synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    i = 0
+    while i < nb:
+        if i in (P // 2, P + 33):
+            time.sleep(0.03)  # past the idle limit: the next call relaunches
+        if i == nb - 20:
+            pc.set_persistent(False)  # hand back to the normal step
+        k = 3 if P <= i < P + 30 and i + 3 <= nb else 1
+        pc.process_blocks_ptr(t.data_ptr() + 4 * i * B, t.data_ptr() + 4 * i * B, x.shape[1], k, stream)
+        i += k
+    torch.cuda.current_stream().synchronize()
+    got = t.cpu().numpy()
+    assert pc.persistent_info()["launches"] >= 3
+    assert same_sums(got, _run(nc, x, B, torch))
+    if method == "upols":
+        assert peak_err(got, oracle.dense_convolve(x, parts)) <= TOL
+
+
+def test_latency_mode_plain_step_host_buffers(neo_gpu, oracle):
+    """the plugin's call (neo_hip_upols_process on a host block, in place) at B = 4096, P = 32:
+    page-locked and pageable blocks through the plain persistent kernel, against the oracle."""
+    pytest.importorskip("torch")
+    import torch
+    C, B, P = 1, 4096, 32
+    (pc, nc), parts = _pair(neo_gpu, oracle, C, B, P, 7500)
+    pc.set_persistent(True)
+    nb = 60
+    x = np.stack([oracle.noise(7600, B * nb)])
+    pinned = torch.empty((C, B), dtype=torch.float32).pin_memory().numpy()
+    y = np.empty_like(x)
+    for i in range(nb):
+        blk = x[:, i * B:(i + 1) * B]
+        if i % 2:
+            pinned[:] = blk
+            pc(pinned)
+            y[:, i * B:(i + 1) * B] = pinned
+        else:
+            b = blk.copy()
+            pc(b)
+            y[:, i * B:(i + 1) * B] = b
+    assert peak_err(y, oracle.dense_convolve(x, parts)) <= TOL
+    assert same_sums(y, _run(nc, x, B, torch))
