@@ -113,7 +113,8 @@ NEO_HIP_API int neo_hip_upola2_create(int channels, int block, int partitions, i
  * can be exercised and timed on any shape. */
 typedef struct neo_hip_upols_opts {
     int fused;            /* plain step: -1 auto (one launch below 64 MiB of filter + FDL), 0 MAC + finish, 1 one launch */
-    int split_workgroups; /* plain step: 0 auto (1024 workgroups), else the workgroup target for its partition splits */
+    int split_workgroups; /* plain step: 0 auto (1024 workgroups, >= 8 or 16 partitions per split), else the
+                             workgroup target for its partition splits, taken as given (up to 64 per channel) */
     int batch_blocks;     /* batched passes: 0 auto (32), else blocks per pass (power of two, 2..32) */
     int batch_bins;       /* batched passes: 0 auto (1), else bins per lane vector (1 or 2) */
     int levels;           /* single-block steps: -1 auto (streaming levels from 64 partitions), 0 plain step, 1 levels */

@@ -49,6 +49,18 @@ namespace neo_hip {
 // s = 0..S-1 and runs the c2r: one launch per block, deterministic results.
 // TAIL (upola_convolver_v2 sub-block pieces): no window / insert, partitions p >= 1 only
 // (overlap_add_convolver.hpp:96-108), slabs summed by k_upola2_piece.
+// latency-mode probe builds (NEO_PS_PROBE): thread 0 stamps point i of the plain step into mk
+#ifdef NEO_PS_PROBE
+#define NEO_STEP_MARK(i)                                    \
+    do {                                                    \
+        if (mk && threadIdx.x == 0) mk[i] = wall_clock64(); \
+    } while (0)
+#else
+#define NEO_STEP_MARK(i) \
+    do {                 \
+    } while (0)
+#endif
+
 // the LDS of one step workgroup (k_upols_step, k_plain_persist)
 template<int B>
 struct step_lds {
@@ -67,8 +79,10 @@ template<int B, bool FUSED, bool OLA, bool TAIL, int UNROLL, bool WT = false>
 __device__ __forceinline__ bool upols_step_wg(step_lds<B>& L, int c, int s,
     const float* __restrict__ in, int64_t ld_in, float* __restrict__ out, int64_t ld_out, float* __restrict__ prev,
     const cf* __restrict__ H, cf* __restrict__ fdl, cf* __restrict__ part, int* __restrict__ arrivals,
-    const cf* __restrict__ twg, int P, int ring, int S, int rows, int w, int64_t cstride, int64_t pstride, int pc)
+    const cf* __restrict__ twg, int P, int ring, int S, int rows, int w, int64_t cstride, int64_t pstride, int pc,
+    unsigned long long* mk = nullptr)
 {
+    (void)mk;
     using K = upols_cfg<B>;
     static_assert(!(TAIL && FUSED), "the v2 tail is summed by k_upola2_piece");
     cf* xnew = L.xnew;
@@ -86,15 +100,16 @@ __device__ __forceinline__ bool upols_step_wg(step_lds<B>& L, int c, int s,
         const float* in_c = in + int64_t(c) * ld_in;
         float* prev_c = prev + int64_t(c) * B;
         window_fft<B, OLA, (B / 8 <= 256 ? 8 : B / 256), WT>(prev_c, in_c, fft, tw, tid, twg);
+        NEO_STEP_MARK(1);
         cf* row = fdl + crow + int64_t(w) * pstride;
         for (int k = tid; k < B; k += 256) {
             const cf x = r2c_split<B>(fft, tw + K::TW1, k);
             xnew[k] = x;
             row[k] = x;
         }
-        if constexpr (!OLA) {  // the window's second half becomes the next call's first half
+        if constexpr (!OLA && !WT) {  // the window's second half becomes the next call's first half (WT: window_fft)
             for (int i = tid; i < B / 4; i += 256)
-                reinterpret_cast<float4*>(prev_c)[i] = ld4_in<WT>(reinterpret_cast<const float4*>(in_c) + i);
+                reinterpret_cast<float4*>(prev_c)[i] = reinterpret_cast<const float4*>(in_c)[i];
         }
         __syncthreads();
     }
@@ -154,6 +169,7 @@ __device__ __forceinline__ bool upols_step_wg(step_lds<B>& L, int c, int s,
     const int pmid = min(p1, max(pstart, pc));
     if (pmid > pstart) mac_rows.template operator()<false>(pstart, pmid);
     if (p1 > pmid) mac_rows.template operator()<true>(pmid, p1);
+    if (s < 2) NEO_STEP_MARK(2 + s);  // MAC loop issued (its loads land at the first use below)
 
     if constexpr (K::RPI > 1) {
         // fold the row groups into group 0 (fixed order -> deterministic)
@@ -219,12 +235,47 @@ __device__ __forceinline__ bool upols_step_wg(step_lds<B>& L, int c, int s,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(arrivals + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next step
     }
+    NEO_STEP_MARK(4);  // the tail: every split arrived
     if (s != 0)
         for (int i = tid; i < K::TW1 + K::TW2; i += 256) tw[i] = twg[i];
     __syncthreads();
 
     // sum the S slabs in order s = 0..S-1, 8 loads in flight
     const float4* p4 = reinterpret_cast<const float4*>(part + int64_t(c) * S * B);
+    if constexpr (K::Q > 256) {
+        // B >= 1024: QI float4 per lane and slab; every lane's loads of SB slabs in flight at once
+        // (one trip to memory per SB slabs instead of one per float4: the latency-bound one-channel
+        // step at B = 4096), the same order per bin
+        constexpr int QI = K::Q / 256, SB = QI >= 8 ? 2 : 16 / QI;
+        float4 sum[QI];
+#pragma unroll
+        for (int i = 0; i < QI; ++i) sum[i] = p4[tid + i * 256];
+        int t = 1;
+        for (; t + SB - 1 < S; t += SB) {
+            float4 r[SB][QI];
+#pragma unroll
+            for (int u = 0; u < SB; ++u)
+#pragma unroll
+                for (int i = 0; i < QI; ++i) r[u][i] = p4[int64_t(t + u) * K::Q + tid + i * 256];
+#pragma unroll
+            for (int u = 0; u < SB; ++u)
+#pragma unroll
+                for (int i = 0; i < QI; ++i) {
+                    sum[i].x += r[u][i].x; sum[i].y += r[u][i].y; sum[i].z += r[u][i].z; sum[i].w += r[u][i].w;
+                }
+        }
+        for (; t < S; ++t) {
+            float4 r[QI];
+#pragma unroll
+            for (int i = 0; i < QI; ++i) r[i] = p4[int64_t(t) * K::Q + tid + i * 256];
+#pragma unroll
+            for (int i = 0; i < QI; ++i) {
+                sum[i].x += r[i].x; sum[i].y += r[i].y; sum[i].z += r[i].z; sum[i].w += r[i].w;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < QI; ++i) reinterpret_cast<float4*>(xnew)[tid + i * 256] = sum[i];
+    } else
     for (int q = tid; q < K::Q; q += 256) {
         float4 sum = p4[q];
         int t = 1;
@@ -244,7 +295,9 @@ __device__ __forceinline__ bool upols_step_wg(step_lds<B>& L, int c, int s,
         reinterpret_cast<float4*>(xnew)[q] = sum;
     }
     __syncthreads();
+    NEO_STEP_MARK(5);  // slabs summed
     c2r_tail<B, OLA, (B / 4 <= 256 ? 4 : B / 256), false, false, WT>(xnew, fft, tw, out_c, prev + int64_t(c) * B, tid);
+    NEO_STEP_MARK(6);  // output stores issued
     return true;
 }
 
@@ -297,10 +350,17 @@ __global__ __launch_bounds__(256) void k_plain_persist(plain_persist_args pa)
         }
         __syncthreads();
         if (!go) break;
-        const bool tail = upols_step_wg<B, true, OLA, false, upols_cfg<B>::U, true>(
+        // two rows in flight at B >= 2048 (one row is 8 or 16 float4 per lane: a trip to memory per row)
+        const bool tail = upols_step_wg<B, true, OLA, false, (upols_cfg<B>::VPT >= 4 ? 2 : upols_cfg<B>::U), true>(
             L, c, s, reinterpret_cast<const float*>(io[0]), pa.ld_in, reinterpret_cast<float*>(io[1]), pa.ld_out,
             pa.prev, pa.H, pa.fdl, pa.part, pa.arrivals, pa.twg, pa.P, pa.ring, pa.S, pa.rows, w, pa.cstride,
-            pa.pstride, pa.pc);
+            pa.pstride, pa.pc,
+#ifdef NEO_PS_PROBE
+            c == 0 ? pa.tl + 2 * kPsRing + 8 * (n % kPsRing) : nullptr
+#else
+            nullptr
+#endif
+        );
         if (tail) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the output's write-through stores complete
             __syncthreads();
@@ -735,7 +795,12 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     // >= 8 rows per split keeps the slab sum short at small C; the one-launch (latency) form
     // takes >= 16 (C3: 12 splits, 9.6 vs 10.6 us per block with 24)
     // (an explicit workgroup target is taken as given)
-    const int min_rows = o.split_workgroups ? 1 : h->fused ? 16 : 8;
+    // (an explicit workgroup target is taken as given); above B = 512 the one-launch form takes
+    // >= 8 rows: a split's rows stream through one CU (~130 GB/s), the tail sums the slabs alone.
+    // One channel, P = 32, us per step with 2 / 4 / 8 splits (normal; latency mode): B = 4096
+    // 25.1 / 22.6 / 22.3 (22.5 / 21.2 / 23.4), B = 2048 16.3 / 15.2 / 15.2 (12.8 / 11.9 / 12.4),
+    // B = 1024 12.5 / 12.2 / 12.7 (10.0 / 9.3 / 9.6) (tools/plain_split_sweep.py)
+    const int min_rows = o.split_workgroups ? 1 : h->fused ? (block > 512 ? 8 : 16) : 8;
     int S = std::max(1, std::min({(target + channels - 1) / channels, (partitions + min_rows - 1) / min_rows, 64}));
     h->rows = (partitions + S - 1) / S;
     h->S = (partitions + h->rows - 1) / h->rows;

@@ -84,7 +84,7 @@ __device__ __forceinline__ cf finish(const acc4& a, bool bin0)
 // OLS window = [previous block | new block] (overlap_save.hpp:90-95);
 // OLA window = [new block | zeros]          (overlap_add.hpp:84-86).
 // WT: the input block read at system scope (a persistent kernel: the caller may have rewritten it
-// since this CU last read there)
+// since this CU last read there); OLS: the previous block written here, from registers
 __device__ __forceinline__ cf ld_in_cf(const cf* p, bool wt)
 {
     if (wt)
@@ -125,6 +125,18 @@ __device__ __forceinline__ void window_fft(const float* prev_c, const float* in_
         }
     }
     if (twg) twr.store(tw1, tid);
+    if constexpr (WT && !OLA) {
+        // the window's second half becomes the next call's first half, stored from registers (a
+        // second system-scope read of the input would be another trip to memory): after every
+        // lane's loads of the first half have landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (active) {
+            cf* pw = const_cast<cf*>(reinterpret_cast<const cf*>(prev_c));
+#pragma unroll
+            for (int m = E / 2; m < E; ++m) pw[tid + m * T - B / 2] = v[m];
+        }
+    }
     __syncthreads();  // twiddles staged (here or by the caller)
     stockham<B, E, -1>(v, fft, tw1, tid, active);
     if (active) {

@@ -22,6 +22,7 @@ timeout -k 10 600 python bench.py --workload c2 --steps 20 --warmup 3 > $O/bench
 timeout -k 10 300 python bench.py --workload c4 --steps 128 --no-cpu-baseline --no-fft > $O/bench_c4_$TAG.json 2> $O/bench_c4_$TAG.err && \
 timeout -k 10 300 python bench.py --workload c3 --steps 256 --no-cpu-baseline --no-fft > $O/bench_c3_$TAG.json 2> $O/bench_c3_$TAG.err && \
 timeout -k 10 300 python bench.py --workload c3long --steps 256 --no-cpu-baseline --no-fft > $O/bench_c3long_$TAG.json 2> $O/bench_c3long_$TAG.err && \
+timeout -k 10 300 python bench.py --workload ref4096 --steps 256 --no-fft > $O/bench_ref4096_$TAG.json 2> $O/bench_ref4096_$TAG.err && \
 timeout -k 10 300 python bench.py --workload c5 --host-io --steps 200 > $O/bench_c5_hostio_$TAG.json 2> $O/bench_c5_hostio_$TAG.err && \
 timeout -k 10 300 tests/cpp/bin/bench_create 512 > $O/bench_create512_$TAG.json 2>&1 && \
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
