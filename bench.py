@@ -475,6 +475,28 @@ def group_frames(C, frames, B, L):
     return d
 
 
+def plugin_frames(C, frames, B, L, latency):
+    """tests/cpp/bench_plugin (C++): the plugin's own processing class, neo::Convolution
+    (extra/plugin/src/dsp/Convolution.hpp:60-63,112): std::vector<split_upols_convolver>, one call
+    per channel and block on the host's channel buffer, never grouped; normal mode (a launch and a
+    host wait per call) or latency mode (a resident kernel per channel). Host memory,
+    PCIe-inclusive; an error entry if the binary cannot be built here."""
+    import subprocess
+
+    cpp = os.path.join(REPO, "tests", "cpp")
+    exe = os.path.join(cpp, "bin", "bench_plugin")
+    try:
+        subprocess.run(["make", "-s", "-C", cpp, "bin/bench_plugin"], check=True, capture_output=True, timeout=300)
+        r = subprocess.run([exe, str(C), str(frames), str(B), str(L), "1" if latency else "0"], capture_output=True,
+                           text=True, timeout=600)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except (OSError, subprocess.SubprocessError, ValueError, IndexError) as e:
+        return {"error": str(e)[:200]}
+    d["note"] = ("tests/cpp/bench_plugin: per frame = C calls of split_upols_convolver::operator() in place on "
+                 "the channel buffers (Convolution.hpp:60-63), back to back")
+    return d
+
+
 def host_io_summary(dt, C, B):
     import numpy as np
 
@@ -803,6 +825,9 @@ def run_upols(args, world, rank, local):
         # the plugin's std::vector<upols_convolver> (group-backed alias, C++) at 256 and 2048 channels
         for cs_, nf_ in ((256, 64), (2048, 16)):
             host_io[f"group_{cs_}"] = group_frames(cs_, nf_, B, L)
+        # the plugin's processing class (stereo split_upols_convolver, 10 s IR), both modes
+        for lat in (False, True):
+            host_io["plugin_stereo" + ("_latency" if lat else "")] = plugin_frames(2, 400, B, L, lat)
     weak = None
     if world > 1 and args.workload in STRONG and not args.no_weak:
         conv.close()
