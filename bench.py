@@ -687,6 +687,37 @@ def run_upols(args, world, rank, local):
                             "to back"}
         paced = paced_run(1)
         paced2 = paced_run(2)
+    # the same round trip at a real-time cadence (default mode, no pacing): calls issued on a fixed
+    # clock instead of back to back -- the audio clock of a B-sample block at 48 kHz, and a period
+    # 1.25 x the timed step (the GPU 80 % loaded); a call that overruns its period starts the next
+    # one late, counted in "overruns"
+    def cadence_run(period, n):
+        crt = []
+        nxt = time.perf_counter()
+        over = 0
+        for _ in range(n):
+            while time.perf_counter() < nxt:
+                pass
+            t0 = time.perf_counter()
+            feed.run(1)
+            sobj.synchronize()
+            d = time.perf_counter() - t0
+            crt.append(d)
+            over += d > period
+            nxt = max(nxt + period, t0 + d)
+        crt = np.array(crt) * 1e6
+        return {"period_us": period * 1e6, "calls": n,
+                "host_roundtrip_p50_us": max_over_ranks(float(np.percentile(crt, 50)), world),
+                "host_roundtrip_p99_us": max_over_ranks(float(np.percentile(crt, 99)), world),
+                "host_roundtrip_max_us": max_over_ranks(float(crt.max()), world),
+                "overruns": int(max_over_ranks(float(over), world))}
+    cadence = None
+    if not args.no_paced:
+        warm()
+        cadence = {"audio_48k": cadence_run(B / 48000.0, 200), "load_80pct": cadence_run(1.25 * elapsed / args.steps, 400),
+                   "note": "default mode (no pacing): one call per period on the host's clock, each followed by a "
+                           "host wait for its output; audio_48k = a B-sample block's period at 48 kHz, load_80pct = "
+                           "1.25 x the headline's ms_per_step"}
     # steady state: one whole far window (128 steps = 32 step groups: every group's background
     # launch once, whatever their sizes), timed like the headline
     n_steady = 128
@@ -696,7 +727,8 @@ def run_upols(args, world, rank, local):
                "max_over_mean": float(st.max() / st.mean()),
                "host_roundtrip_p50_us": rt_p50, "host_roundtrip_p99_us": rt_p99, "host_roundtrip_mean_us": rt_mean,
                "host_roundtrip_msamples_s": C_total * B / rt_mean, "paced": paced, "paced_two_pieces": paced2,
-               "note": "p50/p99/max: GPU time per step (HIP events around every step, which add their own records); "
+               "cadence": cadence,
+               "note":"p50/p99/max: GPU time per step (HIP events around every step, which add their own records); "
                        "host_roundtrip: 200 device-resident single-block calls, each followed by a host wait for its "
                        "output before the next call (max over ranks)"}
 

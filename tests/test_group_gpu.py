@@ -246,3 +246,31 @@ def test_group_long_run_vs_oracle(neo_gpu, oracle):
         got = y[:, lo * B:hi * B]
         err = np.abs(got - ref).max() / np.abs(ref).max()
         assert err <= 1e-5, (lo, err)
+
+
+def test_group_large_frame_helper_snapshot(neo_gpu, oracle):
+    """A frame of >= 1 MiB read in place (one registered [C][B] buffer, the plugin's AudioBuffer):
+    the leader's snapshot of the members' blocks (their later comparisons) is copied by helper
+    threads while the step runs (copy_pool, upols_group.hip). 520 members, B = 512 (1.02 MiB),
+    P = 6 (only the block role's partitions contribute: a member alone and the shared handle sum
+    in the same order): every frame equals one 520-channel handle bit for bit, members whose block
+    changes after the frame's first call (one in every helper's part) run their block step again."""
+    C, B, L, nf = 520, 512, 512 * 6, 12
+    g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 1800)
+    frame = np.zeros((C, B), np.float32)
+    g.register(frame)
+    x = np.stack([oracle.noise(1900 + c, B * nf) for c in range(C)])
+    late = (5, 140, 300, 519)
+    for f in range(nf):
+        blk = np.ascontiguousarray(x[:, f * B:(f + 1) * B])
+        expect = ref(blk.copy())
+        frame[:] = blk
+        if f >= 8:  # coalesced by now: these members' blocks change after the leader's call
+            frame[list(late)] = 0.0
+        for c in range(C):
+            if f >= 8 and c in late:
+                frame[c] = blk[c]
+            g(ids[c], frame[c])
+        assert np.array_equal(frame, expect), f
+    st = g.stats()
+    assert st["coalesced"] and st["frame_steps"] == nf - 3 and st["redos"] == len(late) * 4, st
