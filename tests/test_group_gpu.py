@@ -248,14 +248,16 @@ def test_group_long_run_vs_oracle(neo_gpu, oracle):
         assert err <= 1e-5, (lo, err)
 
 
+
 def test_group_large_frame_helper_snapshot(neo_gpu, oracle):
     """A frame of >= 1 MiB read in place (one registered [C][B] buffer, the plugin's AudioBuffer):
     the leader's snapshot of the members' blocks (their later comparisons) is copied by helper
     threads while the step runs (copy_pool, upols_group.hip). 520 members, B = 512 (1.02 MiB),
-    P = 6 (only the block role's partitions contribute: a member alone and the shared handle sum
-    in the same order): every frame equals one 520-channel handle bit for bit, members whose block
-    changes after the frame's first call (one in every helper's part) run their block step again."""
-    C, B, L, nf = 520, 512, 512 * 6, 12
+    P = 100 (streaming levels, step groups): every frame against one 520-channel handle over the
+    same blocks (to float rounding: the group re-primes its levels when it coalesces); members
+    whose block changes after the frame's first call (one in every helper's part) run their block
+    step again."""
+    C, B, L, nf = 520, 512, 512 * 100, 14
     g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 1800)
     frame = np.zeros((C, B), np.float32)
     g.register(frame)
@@ -271,6 +273,7 @@ def test_group_large_frame_helper_snapshot(neo_gpu, oracle):
             if f >= 8 and c in late:
                 frame[c] = blk[c]
             g(ids[c], frame[c])
-        assert np.array_equal(frame, expect), f
+        err = np.abs(frame - expect).max(axis=1) / np.maximum(np.abs(expect).max(axis=1), 1e-3)
+        assert err.max() <= 1e-5, (f, int(err.argmax()), float(err.max()))
     st = g.stats()
-    assert st["coalesced"] and st["frame_steps"] == nf - 3 and st["redos"] == len(late) * 4, st
+    assert st["coalesced"] and st["frame_steps"] == nf - 3 and st["redos"] == len(late) * (nf - 8), st
