@@ -101,6 +101,9 @@ def parse():
                          "spectra, 2 transform recomputed every window")
     ap.add_argument("--far-phase2", type=int, default=0,
                     help="neo_hip_upols_opts.far_phase2 (G = 1): 0 auto, 1 one workgroup per unit, 2 two steps")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="single process: run rank 0's channel shard of an N-GPU strong-scaling job (the per-GPU "
+                         "shape the driver's N-GPU run gives each rank; diagnostic, never the headline)")
     ap.add_argument("--host-io", action="store_true",
                     help="time the host-buffer boundary (neo_hip_upols_process on pinned-staged host memory): "
                          "PCIe-inclusive, reported for DESIGN.md, never the headline value")
@@ -412,12 +415,18 @@ def spin_wait(local: int) -> None:
     hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
 
 
+SHARD_OF = 1  # --shard-of
+
+
 def rank_channels(workload: str, world: int, rank: int, strong: bool = None):
     """(channels of this rank, channels of the whole job): a strong workload's channels are
     split over the ranks (shard), the others are per GPU."""
     C, _, _ = WORKLOADS[workload]
     if strong is None:
         strong = workload in STRONG
+    if strong and world == 1 and SHARD_OF > 1:  # --shard-of: one rank's share, measured alone
+        lo, hi = shard(C, SHARD_OF, 0)
+        return hi - lo, hi - lo
     if strong:
         lo, hi = shard(C, world, rank)
         return hi - lo, C
@@ -884,7 +893,7 @@ def run_upols(args, world, rank, local):
         "config": {"workload": f"UPOLS {args.workload}: {C_total} channels in all, {C} on rank 0 of {world} GPU(s) "
                                f"({'split over the ranks' if args.workload in STRONG else 'per GPU'}), B={B}, "
                                f"L={L} taps (P={P}), one block per step",
-                   "channels_per_gpu": C, "channels_total": C_total, "block": B, "taps": L, "partitions": P,
+                   "channels_per_gpu": C, "channels_total": C_total, "shard_of": SHARD_OF, "block": B, "taps": L, "partitions": P,
                    "far_group": conv_far_group, "step_group": G,
                    "far_form": {0: "none", 1: "transform, stored spectra", 2: "transform recomputed every window",
                                 3: "128-block Toeplitz"}[conv_far_form],
@@ -1116,6 +1125,8 @@ def main():
     if args.cpu_threads <= 0:
         args.cpu_threads = cpu_threads()
     world, rank, local = dist_setup(args)
+    global SHARD_OF
+    SHARD_OF = args.shard_of if world == 1 else 1
     if args.workload == "c2":
         res = run_fft(args, world, rank, local)
     elif args.host_io:

@@ -105,6 +105,15 @@ def test_bench_strong_scaling_spans():
     assert bench.rank_channels("c5full", 2, 1) == (1024, 2048)
     assert bench.rank_channels("c5", 8, 3) == (256, 2048)  # per GPU: weak
     assert bench.rank_channels("c4", 2, 0) == (256, 512)
+    # --shard-of N (one process): rank 0's share of an N-GPU strong run, measured alone
+    try:
+        for n in (2, 4, 8):
+            bench.SHARD_OF = n
+            assert bench.rank_channels("c5full", 1, 0) == (2048 // n, 2048 // n)
+            assert bench.rank_channels("c5full", 2, 1) == (1024, 2048)  # never under torchrun
+            assert bench.rank_channels("c4", 1, 0) == (256, 256)  # per-GPU workloads unchanged
+    finally:
+        bench.SHARD_OF = 1
 
 
 def _bench_rank_worker(rank, world, port, q):
