@@ -36,14 +36,9 @@
 #include "upols_handle.hpp"
 
 #include <algorithm>
-#include <atomic>
-#include <condition_variable>
 #include <cstring>
-#include <functional>
 #include <map>
-#include <memory>
 #include <mutex>
-#include <thread>
 #include <vector>
 
 #ifdef NEO_GROUP_PROBE  // diagnostic builds (tools/build_variant.sh): where a coalesced frame's time goes
@@ -83,79 +78,6 @@ namespace {
 using neo_hip::cf;
 using neo_hip::fail;
 
-// Helper threads for the leader's snapshot of a large frame (the members' blocks copied into the
-// mapped staging while the step runs): one thread copies a 4 MB frame at ~24 GB/s, longer than the
-// step itself at 2048 channels. Parts 1..n of a job run on the helpers (asleep on a condition
-// variable between frames), part 0 on the caller; wait() spins until the helpers' parts are done.
-struct copy_pool {
-    std::vector<std::thread> th;
-    std::mutex mu;
-    std::condition_variable cv;
-    uint64_t gen = 0;
-    bool quit = false;
-    std::function<void(int)> job;
-    std::atomic<int> left{0};
-    explicit copy_pool(int n)
-    {
-        try {
-            for (int i = 0; i < n; ++i) th.emplace_back([this, i] { run(i + 1); });
-        } catch (...) {  // the threads made so far leave before the error goes on
-            stop();
-            throw;
-        }
-    }
-    ~copy_pool() { stop(); }
-    void stop()
-    {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            quit = true;
-        }
-        cv.notify_all();
-        for (auto& t : th) t.join();
-        th.clear();
-    }
-    int parts() const { return int(th.size()) + 1; }
-    void run(int part)
-    {
-        uint64_t seen = 0;
-        for (;;) {
-            std::function<void(int)> f;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return quit || gen != seen; });
-                if (quit) return;
-                seen = gen;
-                f = job;
-            }
-            f(part);
-            left.fetch_sub(1, std::memory_order_release);
-        }
-    }
-    // start f(1..n) on the helpers and run f(0) here
-    void start(std::function<void(int)> f)
-    {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            job = std::move(f);
-            left.store(int(th.size()), std::memory_order_relaxed);
-            ++gen;
-        }
-        cv.notify_all();
-        job(0);
-    }
-    void wait() const
-    {
-        while (left.load(std::memory_order_acquire) > 0) std::this_thread::yield();
-    }
-};
-// frames of at least this many bytes take the helpers (below, one thread's copy hides behind the step)
-constexpr size_t kCopyPoolBytes = size_t(1) << 20;
-#ifndef NEO_COPY_POOL_THREADS  // diagnostic builds (A/B): 0 = the leader copies alone
-#define NEO_COPY_POOL_THREADS 3
-#endif
-constexpr int kCopyPoolThreads = NEO_COPY_POOL_THREADS;
-
 struct member {
     bool live = false;
     neo_hip_upols* own = nullptr;  // independent mode: the member's one-channel handle
@@ -193,7 +115,6 @@ struct neo_hip_upols_group {
     int nseen = 0, good_frames = 0;
     int64_t stat_steps = 0, stat_calls = 0, stat_redos = 0, stat_switches = 0;
     hipStream_t stream = nullptr;
-    std::unique_ptr<copy_pool> pool;  // the leader's snapshot helpers (large frames; made on first use)
 };
 
 namespace {
@@ -506,24 +427,6 @@ int call_coalesced(group_t* g, int i, float* io)
         for (const auto& y : g->m)
             if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
     };
-    // beside the step, a large frame's snapshot in parts on the helper threads: part j copies
-    // members [j M / n, (j + 1) M / n) (the member vector is not resized during the call: the
-    // group's lock is held)
-    bool pooled = kCopyPoolThreads > 0 && inplace && g->m.size() * bb >= kCopyPoolBytes;
-    if (pooled && !g->pool) {
-        try {
-            g->pool = std::make_unique<copy_pool>(kCopyPoolThreads);
-        } catch (...) {  // no threads to be had: the leader copies alone
-            pooled = false;
-        }
-    }
-    auto copy_in_part = [g, &x, io, bb](int j) {
-        const size_t M = g->m.size(), n = size_t(g->pool->parts());
-        for (size_t k = M * size_t(j) / n; k < M * size_t(j + 1) / n; ++k) {
-            const member& y = g->m[k];
-            if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
-        }
-    };
     NEO_GP_T(t0);
     if (!inplace) copy_in();
     NEO_GP_ADD(0, t0);
@@ -535,12 +438,8 @@ int call_coalesced(group_t* g, int i, float* io)
     int rc = neo_hip::launch_levels(sh, in_dev, ld_in, g->out_dev, g->B, g->stream);
     NEO_GP_ADD(2, t2);
     NEO_GP_T(t3);
-    const bool helpers = pooled && !rc;
-    if (helpers) g->pool->start(copy_in_part);
-    else if (inplace) copy_in();  // beside the step: both read the frame, which nothing writes during this call
-    if (!rc) rc = neo_hip::spin_sync(g->stream);
-    if (helpers) g->pool->wait();  // before any return: the helpers read the frame and the member list
-    if (rc) return rc;
+    if (inplace) copy_in();  // beside the step: both read the frame, which nothing writes during this call
+    if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
     NEO_GP_ADD(3, t3);
     g->step_n = sh->lv_n - 1;
     ++g->stat_steps;
@@ -591,7 +490,6 @@ NEO_HIP_API int neo_hip_upols_group_destroy(neo_hip_upols_group* g)
     if (!g) return NEO_HIP_OK;
     neo_hip::device_guard dg(g->device);
     (void)hipStreamSynchronize(g->stream);
-    g->pool.reset();
     free_shared(g);
     for (auto& x : g->m)
         if (x.own) neo_hip_upols_destroy(x.own);

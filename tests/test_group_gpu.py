@@ -249,14 +249,12 @@ def test_group_long_run_vs_oracle(neo_gpu, oracle):
 
 
 
-def test_group_large_frame_helper_snapshot(neo_gpu, oracle):
+def test_group_large_frame_in_place(neo_gpu, oracle):
     """A frame of >= 1 MiB read in place (one registered [C][B] buffer, the plugin's AudioBuffer):
-    the leader's snapshot of the members' blocks (their later comparisons) is copied by helper
-    threads while the step runs (copy_pool, upols_group.hip). 520 members, B = 512 (1.02 MiB),
-    P = 100 (streaming levels, step groups): every frame against one 520-channel handle over the
-    same blocks (to float rounding: the group re-primes its levels when it coalesces); members
-    whose block changes after the frame's first call (one in every helper's part) run their block
-    step again."""
+    520 members, B = 512, P = 100 (streaming levels, step groups): every frame against one
+    520-channel handle over the same blocks (to float rounding: the group re-primes its levels
+    when it coalesces); members whose block changes after the frame's first call (spread over the
+    frame) run their block step again."""
     C, B, L, nf = 520, 512, 512 * 100, 14
     g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 1800)
     frame = np.zeros((C, B), np.float32)
