@@ -326,12 +326,12 @@ class Feed:
 
 def far_group(nseg: int, units: int) -> int:
     """Windows per far phase-1 pass, as upols_levels.hip far_group: round(sqrt(2 (nseg - 1)))
-    clamped to [2, 4] from 32768 16-column units (C * B / 16) on, else 2 (1 below two segments)."""
+    clamped to [2, 4] from 16384 16-column units (C * B / 16) on, else 2 (1 below two segments)."""
     import math
 
     if nseg < 2:
         return 1
-    if units < 32768:
+    if units < 16384:
         return 2
     return min(4, max(2, int(math.floor(math.sqrt(2.0 * (nseg - 1)) + 0.5))))
 

@@ -1532,8 +1532,10 @@ static int64_t far_units(const upols_t* h) { return int64_t(h->C) * (h->B / 16);
 // window and column, 2 (nseg - 1) / K + K - 1; but phase 2 takes up to K - 1 extra segments in
 // its one-workgroup-per-unit chain, which bounds the step where a step has few far units
 // (measured: K = 3 / 4 instead of 2 at 64 / 32 units per step, C5 / C4: 13 % / 25 % slower; at
-// 512, the 2048-channel headline: 3 % faster), so K = 2 below kFarGroupUnits units
-constexpr int64_t kFarGroupUnits = 32768;  // 256 units per step
+// 512, the 2048-channel headline: 3 % faster; round 5, the 4-GPU shard of the headline, 512
+// channels = 128 units per step: K = 3 2-3.5 % faster, tools/gpu_shard_sweep.sh), so K = 2 below
+// kFarGroupUnits units
+constexpr int64_t kFarGroupUnits = 16384;  // 128 units per step
 
 static int far_group_auto(int C, int B, int ns)
 {
@@ -2089,7 +2091,7 @@ static void toep_slice(const upols_t* h, int l, int64_t W, int64_t u0, int64_t u
 // step later). One workgroup reads the fresh spectrum back from registers instead of its slot,
 // fewer bytes; two halve the chain, which bounds the step where a step has few far units.
 // Step groups always run one (their background launches have a group of slack).
-constexpr int64_t kFarWholeUnits = 32768;  // 256 units per step, as kFarGroupUnits
+constexpr int64_t kFarWholeUnits = 32768;  // 256 units per step
 
 static bool far2_whole(const upols_t* h)
 {

@@ -61,9 +61,10 @@ def test_headline_byte_totals():
 
 
 def test_far_group_rule():
-    """bench.far_group restates upols_levels.hip far_group_auto: 2 below 32768 16-column units,
+    """bench.far_group restates upols_levels.hip far_group_auto: 2 below 16384 16-column units,
     round(sqrt(2 (nseg - 1))) in [2, 4] from there, 1 without two segments"""
     assert bench.far_group(6, 256 * 32) == 2
+    assert bench.far_group(6, 512 * 32) == 3  # the 4-GPU shard of the headline
     assert bench.far_group(6, 2048 * 32) == 3
     assert bench.far_group(13, 2048 * 32) == 4
     assert bench.far_group(1, 2048 * 32) == 1

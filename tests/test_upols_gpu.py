@@ -735,7 +735,7 @@ def test_far_level_steps_vs_oracle(neo_gpu, oracle, method, B, P, C, nb, far):
 @pytest.mark.parametrize("B,P,C", [(32, 700, 1), (32, 1100, 1), (64, 1000, 2)])
 def test_far_window_groups_vs_oracle(neo_gpu, oracle, method, K, B, P, C):
     """The far level's phase 1 over groups of K windows (neo_hip_upols_opts.far_group forces
-    K; by default only shapes of >= 32768 16-column units, the 2048-channel headline, run
+    K; by default only shapes of >= 16384 16-column units, the headline and its 2- and 4-GPU shards, run
     K = 3 / 4): far1_mac<FPL, K> for every K, phase 2's segments 1 .. j of window j of a
     group, the classes' staggered start after priming, and the two kernel builds (pairs
     only for K <= 2, any group for K > 2). nseg = 4 / 7 / 6 (FPL 4 / 2 / 2), >= 2P + 300
@@ -938,11 +938,11 @@ def test_step_group_timing_detail(neo_gpu):
 
 
 def test_far_group_defaults(neo_gpu):
-    """The automatic window group: 2 below 32768 16-column units (every shape but the
-    headline), round(sqrt(2 (nseg - 1))) from there (bench.far_group restates it)."""
+    """The automatic window group: 2 below 16384 16-column units (the 256-channel shapes),
+    round(sqrt(2 (nseg - 1))) from there (bench.far_group restates it)."""
     import bench
 
-    for C, B, P in [(4, 512, 938), (256, 512, 938), (256, 256, 1875), (1, 512, 188), (3, 64, 300)]:
+    for C, B, P in [(4, 512, 938), (256, 512, 938), (512, 512, 938), (256, 256, 1875), (1, 512, 188), (3, 64, 300)]:
         c = neo_gpu.UpolsConvolver(C, B, P, options={"far_level": 1})  # the stored form
         nseg = neo_gpu.convolution.level_plan(P)["nseg"]
         assert c.far_group() == (bench.far_group(nseg, C * B // 16) if nseg else 0), (C, B, P)
