@@ -119,6 +119,10 @@ inline std::vector<C> make_split_table(int order, int lo_bits)
 // shared by every handle on a device, never freed
 int dalloc(void** out, size_t bytes);
 void dfree(void* p);
+// persistent (latency-mode) workgroups running per device: reserve wgs if the total stays <= cap
+// (false: no room, nothing reserved); release them when the kernel is joined
+bool resident_admit(int device, int wgs, int cap);
+void resident_release(int device, int wgs);
 template<class T>
 inline int dalloc(T** out, size_t bytes)
 {
@@ -134,6 +138,46 @@ int shared_tw(cf** out, int B);  // upload_tw's table for block B
 int shared_far_tw(cf** out);     // the 256-point forward table of the far level
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// A device-resident input's producer, for the synchronous setup calls: the work enqueued on the
+// HIP null stream (torch's default stream) before the call. Joined with an event marker on the
+// null stream, which waits for the blocking streams' earlier work only; hipDeviceSynchronize (and
+// hipStreamSynchronize on the null stream) would also wait for every non-blocking stream, e.g.
+// another handle's resident latency-mode kernel, up to its idle limit. A producer on another
+// non-blocking stream is the caller's to join (the Python layer synchronizes torch's current
+// stream first). dmem.hip.
+int null_join();
+
+// The streams a handle's (or plan's) asynchronous calls ran on since its last join: a setup call
+// or a destroy waits for these, not for the device. A stream given to such a call stays valid
+// until then. On overflow the remembered streams are joined first (their work is then complete).
+struct stream_set {
+    static constexpr int kMax = 16;
+    hipStream_t s[kMax] = {};
+    int n = 0;
+    int note(hipStream_t x)
+    {
+        for (int i = 0; i < n; ++i)
+            if (s[i] == x) return NEO_HIP_OK;
+        if (n == kMax)
+            if (int rc = join()) return rc;
+        s[n++] = x;
+        return NEO_HIP_OK;
+    }
+    int join()
+    {
+        const int k = n;
+        n = 0;
+        for (int i = 0; i < k; ++i) {
+            if (!s[i]) {  // the null stream: its own work only (null_join)
+                if (int rc = null_join()) return rc;
+            } else {
+                NEO_HIP_CHECK(hipStreamSynchronize(s[i]));
+            }
+        }
+        return NEO_HIP_OK;
+    }
+};
 
 // The device address of page-locked host memory (hipHostMalloc, hipHostRegister with the
 // mapped flag, neo_hip_host_register), or nullptr for pageable memory (not an error).

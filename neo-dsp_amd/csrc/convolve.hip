@@ -98,9 +98,9 @@ struct device_buffers {
     R* tmp_out = nullptr;
     ~device_buffers()
     {
-        (void)hipFree(tmp_a);
-        (void)hipFree(tmp_b);
-        (void)hipFree(tmp_out);
+        dfree(tmp_a);  // pooled (dmem.hip): no device-wide wait; the caller joined its stream
+        dfree(tmp_b);
+        dfree(tmp_out);
     }
     int stage(const R* ha, int64_t n, const R* hb, int64_t m, R* hout, int is_device, hipStream_t s)
     {
@@ -110,9 +110,9 @@ struct device_buffers {
             out = hout;
             return NEO_HIP_OK;
         }
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_a), size_t(n) * sizeof(R)));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_b), size_t(m) * sizeof(R)));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp_out), size_t(n + m - 1) * sizeof(R)));
+        if (int rc = dalloc(&tmp_a, size_t(n) * sizeof(R))) return rc;
+        if (int rc = dalloc(&tmp_b, size_t(m) * sizeof(R))) return rc;
+        if (int rc = dalloc(&tmp_out, size_t(n + m - 1) * sizeof(R))) return rc;
         NEO_HIP_CHECK(hipMemcpyAsync(tmp_a, ha, size_t(n) * sizeof(R), hipMemcpyHostToDevice, s));
         NEO_HIP_CHECK(hipMemcpyAsync(tmp_b, hb, size_t(m) * sizeof(R), hipMemcpyHostToDevice, s));
         a = tmp_a;
@@ -137,7 +137,8 @@ int fft_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, R* 
     device_guard g(device);
     if (g.rc) return g.rc;
     const int64_t N = int64_t(1) << order, bins = N / 2 + 1;
-    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
+    if (is_device)
+        if (int rj = null_join()) return rj;  // after its producer (common.hpp: null_join)
     hipStream_t s = nullptr;
     if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     int rc = NEO_HIP_OK;
@@ -149,8 +150,7 @@ int fft_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, R* 
         rc = io.stage(signal, n, patch, m, out, is_device, s);
         if (!rc) rc = neo_hip_fft_plan_create(order, 2, NEO_HIP_R2C | f64, device, &r2c);
         if (!rc) rc = neo_hip_fft_plan_create(order, 1, NEO_HIP_C2R | f64, device, &c2r);
-        if (!rc && (hipMalloc(reinterpret_cast<void**>(&rows), size_t(2 * N) * sizeof(R)) != hipSuccess ||
-                    hipMalloc(reinterpret_cast<void**>(&spec), size_t(2 * bins) * sizeof(C)) != hipSuccess))
+        if (!rc && (dalloc(&rows, size_t(2 * N) * sizeof(R)) || dalloc(&spec, size_t(2 * bins) * sizeof(C))))
             rc = fail(NEO_HIP_ENOMEM, "convolution buffers");
         if (!rc) {
             hipLaunchKernelGGL((k_pad2<R>), dim3(grid_for(2 * N)), dim3(256), 0, s, io.a, n, io.b, m, rows, N);
@@ -174,8 +174,8 @@ int fft_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, R* 
     }
     neo_hip_fft_plan_destroy(r2c);
     neo_hip_fft_plan_destroy(c2r);
-    (void)hipFree(rows);
-    (void)hipFree(spec);
+    dfree(rows);
+    dfree(spec);
     return rc;
 }
 
@@ -187,7 +187,8 @@ int direct_convolve_impl(const R* signal, int64_t n, const R* patch, int64_t m, 
     if (!signal || !patch || !out) return fail(NEO_HIP_EINVAL, "null buffer");
     device_guard g(device);
     if (g.rc) return g.rc;
-    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());
+    if (is_device)
+        if (int rj = null_join()) return rj;  // after its producer (common.hpp: null_join)
     hipStream_t s = nullptr;
     if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     int rc = NEO_HIP_OK;
@@ -234,7 +235,8 @@ int stft_impl(const R* x, int channels, int64_t length, int frame, int transform
     const int64_t F = stft_frames(length, frame, overlap), rows_n = int64_t(channels) * F;
     device_guard g(device);
     if (g.rc) return g.rc;
-    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());
+    if (is_device)
+        if (int rj = null_join()) return rj;  // after its producer (common.hpp: null_join)
     hipStream_t s = nullptr;
     if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     int rc = NEO_HIP_OK;
@@ -248,10 +250,8 @@ int stft_impl(const R* x, int channels, int64_t length, int frame, int transform
         for (int64_t i = 0; i < N; ++i) hann[size_t(i)] = R(0.5) * (R(1) - std::cos(two_pi * R(i) / n1));
     }
     const size_t xbytes = size_t(channels) * size_t(length) * sizeof(R), obytes = size_t(rows_n * bins) * sizeof(C);
-    if (hipMalloc(reinterpret_cast<void**>(&rows), size_t(rows_n * N) * sizeof(R)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&d_w), size_t(N) * sizeof(R)) != hipSuccess ||
-        (!is_device && (hipMalloc(reinterpret_cast<void**>(&d_x), xbytes) != hipSuccess ||
-                        hipMalloc(reinterpret_cast<void**>(&d_out), obytes) != hipSuccess)))
+    if (dalloc(&rows, size_t(rows_n * N) * sizeof(R)) || dalloc(&d_w, size_t(N) * sizeof(R)) ||
+        (!is_device && (dalloc(&d_x, xbytes) || dalloc(&d_out, obytes))))
         rc = fail(NEO_HIP_ENOMEM, "stft buffers");
     const R* xin = is_device ? x : d_x;
     if (!rc && !is_device && hipMemcpyAsync(d_x, x, xbytes, hipMemcpyHostToDevice, s) != hipSuccess)
@@ -271,11 +271,11 @@ int stft_impl(const R* x, int channels, int64_t length, int frame, int transform
         rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     neo_hip_fft_plan_destroy(plan);
-    (void)hipFree(rows);
-    (void)hipFree(d_w);
+    dfree(rows);  // the stream was joined above
+    dfree(d_w);
     if (!is_device) {
-        (void)hipFree(d_x);
-        (void)hipFree(d_out);
+        dfree(d_x);
+        dfree(d_out);
     }
     return rc;
 }

@@ -19,6 +19,7 @@
 // device and never freed.
 #include "upols_handle.hpp"
 
+#include <atomic>
 #include <map>
 #include <memory>
 #include <tuple>
@@ -81,6 +82,27 @@ void release(pool& p, size_t i)
     p.chunks.erase(p.chunks.begin() + std::ptrdiff_t(i));
 }
 
+// chunks taken out of a pool under g_mu, returned to the driver after it is released: hipFree
+// waits for the device, and no other thread's allocation may wait on the lock meanwhile. Declared
+// before the lock_guard, so its destructor runs after the guard's.
+struct deferred_free {
+    std::vector<std::unique_ptr<chunk>> v;
+    void take(pool& p, size_t i)
+    {
+        v.push_back(std::move(p.chunks[i]));
+        p.chunks.erase(p.chunks.begin() + std::ptrdiff_t(i));
+    }
+    ~deferred_free()
+    {
+        for (auto& c : v) (void)hipFree(c->base);
+    }
+};
+
+// persistent (latency-mode) workgroups running per device (resident_admit): while a persistent
+// kernel runs, hipFree would wait for it (up to its idle limit, indefinitely while an audio
+// thread keeps feeding it), so dfree keeps empty chunks cached instead of returning them
+std::atomic<int> g_resident[64];
+
 bool take(chunk& c, size_t bytes, void** out)
 {
     for (auto it = c.free.begin(); it != c.free.end(); ++it) {
@@ -135,9 +157,25 @@ int dalloc(void** out, size_t bytes)
     return NEO_HIP_OK;
 }
 
+bool resident_admit(int device, int wgs, int cap)
+{
+    if (device < 0 || device >= 64) return false;
+    int cur = g_resident[device].load();
+    do {
+        if (cur + wgs > cap) return false;
+    } while (!g_resident[device].compare_exchange_weak(cur, cur + wgs));
+    return true;
+}
+
+void resident_release(int device, int wgs)
+{
+    if (device >= 0 && device < 64) g_resident[device].fetch_sub(wgs);
+}
+
 void dfree(void* ptr)
 {
     if (!ptr) return;
+    deferred_free doomed;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_live.find(ptr);
     if (it == g_live.end()) return;  // not ours: nothing to do (never hipFree a foreign pointer)
@@ -162,9 +200,10 @@ void dfree(void* ptr)
     c->used -= n;
     if (c->used) return;
     if (empty_bytes(p) <= keep_bytes()) return;  // cached for later requests of any size
+    if (dev >= 0 && dev < 64 && g_resident[dev].load()) return;  // no hipFree beside a resident kernel
     for (size_t i = 0; i < p.chunks.size(); ++i)
         if (p.chunks[i].get() == c) {
-            release(p, i);
+            doomed.take(p, i);  // hipFree after the lock is released
             break;
         }
 }
@@ -261,6 +300,18 @@ int shared_stream(hipStream_t* out)
     return NEO_HIP_OK;
 }
 
+int null_join()
+{
+    int d = 0;
+    NEO_HIP_CHECK(hipGetDevice(&d));
+    thread_local std::map<int, hipEvent_t> ev;  // one marker per thread and device, never destroyed
+    hipEvent_t& e = ev[d];
+    if (!e) NEO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    NEO_HIP_CHECK(hipEventRecord(e, nullptr));
+    NEO_HIP_CHECK(hipEventSynchronize(e));
+    return NEO_HIP_OK;
+}
+
 namespace {
 // a constant table shared by every handle on the current device (key: block size, or -1 for the
 // far level's), made by upload on first use
@@ -309,10 +360,11 @@ NEO_HIP_API int neo_hip_memory_trim(int device)
     if (g.rc) return g.rc;
     int dev = 0;
     NEO_HIP_CHECK(hipGetDevice(&dev));
+    neo_hip::deferred_free doomed;  // returned after the lock is released
     std::lock_guard<std::mutex> lk(neo_hip::g_mu);
     neo_hip::pool& p = neo_hip::g_pools[dev];
     for (size_t i = p.chunks.size(); i-- > 0;)
-        if (p.chunks[i]->used == 0) neo_hip::release(p, i);
+        if (p.chunks[i]->used == 0) doomed.take(p, i);
     return NEO_HIP_OK;
 }
 

@@ -306,6 +306,7 @@ struct neo_hip_fft_plan {
     void* d_in = nullptr;    // staging for neo_hip_fft_execute_host
     void* d_out = nullptr;
     size_t in_bytes = 0, out_bytes = 0;
+    neo_hip::stream_set used;  // streams the plan's executes ran on (destroy joins them, not the device)
 };
 
 namespace {
@@ -407,7 +408,7 @@ int run_c2c_global(const plan_t* p, int order, const C* in, C* out, int dir, hip
 template<class C>
 int upload(void** dst, const std::vector<C>& v)
 {
-    NEO_HIP_CHECK(hipMalloc(dst, v.size() * sizeof(C)));
+    if (int rc = dalloc(dst, v.size() * sizeof(C))) return rc;  // pooled (dmem.hip)
     NEO_HIP_CHECK(hipMemcpy(*dst, v.data(), v.size() * sizeof(C), hipMemcpyHostToDevice));
     return NEO_HIP_OK;
 }
@@ -415,13 +416,16 @@ int upload(void** dst, const std::vector<C>& v)
 void free_plan(plan_t* p)
 {
     if (!p) return;
-    (void)hipFree(p->d_tw);
-    (void)hipFree(p->d_split);
-    (void)hipFree(p->d_split2);
-    (void)hipFree(p->d_ptw);
-    for (auto* s : p->d_scratch) (void)hipFree(s);
-    (void)hipFree(p->d_in);
-    (void)hipFree(p->d_out);
+    // pooled (dmem.hip): freeing waits for nothing, so the plan's streams are joined first
+    (void)p->used.join();
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
+    dfree(p->d_tw);
+    dfree(p->d_split);
+    dfree(p->d_split2);
+    dfree(p->d_ptw);
+    for (auto* s : p->d_scratch) dfree(s);
+    dfree(p->d_in);
+    dfree(p->d_out);
     // p->stream is one of the device's shared streams (dmem.hip)
     delete p;
 }
@@ -456,7 +460,7 @@ int setup_tables(plan_t* p)
         const int64_t inner = int64_t(1) << io;
         const int nscratch = p->kind == NEO_HIP_C2C ? 2 : 3;
         for (int i = 0; i < nscratch; ++i)
-            if (hipMalloc(&p->d_scratch[i], size_t(inner * p->batch) * sizeof(C)) != hipSuccess)
+            if (dalloc(&p->d_scratch[i], size_t(inner * p->batch) * sizeof(C)))
                 return fail(NEO_HIP_ENOMEM, "scratch allocation failed");
         if (p->kind != NEO_HIP_C2C) {
             p->lo_bits2 = (io + 2) / 2;
@@ -567,6 +571,7 @@ NEO_HIP_API int neo_hip_fft_execute(neo_hip_fft_plan* p, const void* in, void* o
     device_guard g(p->device);
     if (g.rc) return g.rc;
     hipStream_t s = as_stream(stream);  // NULL = the HIP null stream (torch's default stream)
+    if (int rc = p->used.note(s)) return rc;
     return p->f64 ? execute<cd>(p, in, out, direction, s) : execute<cf>(p, in, out, direction, s);
 }
 
@@ -575,10 +580,8 @@ NEO_HIP_API int neo_hip_fft_execute_host(neo_hip_fft_plan* p, const void* in, vo
     if (!p || !in || !out) return fail(NEO_HIP_EINVAL, "null plan or buffer");
     device_guard g(p->device);
     if (g.rc) return g.rc;
-    if (!p->d_in) {
-        NEO_HIP_CHECK(hipMalloc(&p->d_in, p->in_bytes));
-        NEO_HIP_CHECK(hipMalloc(&p->d_out, p->out_bytes));
-    }
+    if ((!p->d_in && dalloc(&p->d_in, p->in_bytes)) || (!p->d_out && dalloc(&p->d_out, p->out_bytes)))
+        return fail(NEO_HIP_ENOMEM, "fft staging allocation failed");
     NEO_HIP_CHECK(hipMemcpyAsync(p->d_in, in, p->in_bytes, hipMemcpyHostToDevice, p->stream));
     int rc = neo_hip_fft_execute(p, p->d_in, p->d_out, direction, p->stream);
     if (rc) return rc;

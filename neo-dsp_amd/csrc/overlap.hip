@@ -92,6 +92,7 @@ struct neo_hip_overlap {
     float* ov = nullptr;       // [C][B] overlap_add tail
     neo_hip::cf* spec = nullptr;  // [C][bins] device spectrum (host-memory calls)
     float* io = nullptr;          // [C][B] device block (host-memory calls)
+    neo_hip::stream_set used;     // streams the device-memory calls ran on (reset and destroy join them)
 };
 
 namespace {
@@ -102,11 +103,11 @@ void destroy_overlap(neo_hip_overlap* h)
     if (!h) return;
     if (h->r2c) neo_hip_fft_plan_destroy(h->r2c);
     if (h->c2r) neo_hip_fft_plan_destroy(h->c2r);
-    for (float* w : h->win) (void)hipFree(w);
-    (void)hipFree(h->real);
-    (void)hipFree(h->ov);
-    (void)hipFree(h->spec);
-    (void)hipFree(h->io);
+    for (float* w : h->win) neo_hip::dfree(w);  // pooled (dmem.hip): no device-wide wait
+    neo_hip::dfree(h->real);
+    neo_hip::dfree(h->ov);
+    neo_hip::dfree(h->spec);
+    neo_hip::dfree(h->io);
     // h->stream is one of the device's shared streams (dmem.hip)
     delete h;
 }
@@ -191,11 +192,9 @@ NEO_HIP_API int neo_hip_overlap_create(int kind, int channels, int64_t block, in
     if (int rs = neo_hip::shared_stream(&h->stream)) rc = rs;
     if (!rc) rc = neo_hip_fft_plan_create(order, channels, NEO_HIP_R2C, h->device, &h->r2c);
     if (!rc) rc = neo_hip_fft_plan_create(order, channels, NEO_HIP_C2R, h->device, &h->c2r);
-    if (!rc && (hipMalloc(reinterpret_cast<void**>(&h->win[0]), wb) != hipSuccess ||
-                (kind == 0 && (hipMalloc(reinterpret_cast<void**>(&h->win[1]), wb) != hipSuccess ||
-                               hipMalloc(reinterpret_cast<void**>(&h->real), wb) != hipSuccess)) ||
-                (kind == 1 && hipMalloc(reinterpret_cast<void**>(&h->ov), size_t(channels) * size_t(block) * sizeof(float)) !=
-                                  hipSuccess)))
+    if (!rc && (neo_hip::dalloc(&h->win[0], wb) ||
+                (kind == 0 && (neo_hip::dalloc(&h->win[1], wb) || neo_hip::dalloc(&h->real, wb))) ||
+                (kind == 1 && neo_hip::dalloc(&h->ov, size_t(channels) * size_t(block) * sizeof(float)))))
         rc = fail(NEO_HIP_ENOMEM, "device allocation of the overlap stage failed");
     if (!rc) rc = reset_overlap(h);
     if (rc) {
@@ -210,6 +209,7 @@ NEO_HIP_API int neo_hip_overlap_destroy(neo_hip_overlap* h)
 {
     if (!h) return NEO_HIP_OK;
     neo_hip::device_guard g(h->device);
+    (void)h->used.join();  // this handle's calls on any stream, not the device
     (void)hipStreamSynchronize(h->stream);
     destroy_overlap(h);
     return NEO_HIP_OK;
@@ -229,7 +229,7 @@ NEO_HIP_API int neo_hip_overlap_reset(neo_hip_overlap* h)
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     neo_hip::device_guard g(h->device);
     if (g.rc) return g.rc;
-    NEO_HIP_CHECK(hipDeviceSynchronize());
+    if (int rc = h->used.join()) return rc;  // this handle's calls on any stream, not the device
     return reset_overlap(h);
 }
 
@@ -240,13 +240,14 @@ NEO_HIP_API int neo_hip_overlap_forward(neo_hip_overlap* h, const float* in, int
     if (ld_in < h->B) return fail(NEO_HIP_EINVAL, "leading dimension smaller than the block");
     neo_hip::device_guard g(h->device);
     if (g.rc) return g.rc;
-    if (is_device) return forward_dev(h, in, ld_in, spectrum, neo_hip::as_stream(stream));
+    if (is_device) {
+        if (int rc = h->used.note(neo_hip::as_stream(stream))) return rc;
+        return forward_dev(h, in, ld_in, spectrum, neo_hip::as_stream(stream));
+    }
     hipStream_t s = stream ? neo_hip::as_stream(stream) : h->stream;
     const size_t ib = size_t(h->C) * size_t(h->B) * sizeof(float), sb = size_t(h->C) * size_t(h->bins) * sizeof(neo_hip::cf);
-    if (!h->io) {
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->io), ib));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->spec), sb));
-    }
+    if ((!h->io && neo_hip::dalloc(&h->io, ib)) || (!h->spec && neo_hip::dalloc(&h->spec, sb)))
+        return fail(NEO_HIP_ENOMEM, "overlap stage staging");
     NEO_HIP_CHECK(hipMemcpy2DAsync(h->io, size_t(h->B) * sizeof(float), in, size_t(ld_in) * sizeof(float),
                                    size_t(h->B) * sizeof(float), size_t(h->C), hipMemcpyHostToDevice, s));
     if (int rc = forward_dev(h, h->io, h->B, h->spec, s)) return rc;
@@ -262,13 +263,14 @@ NEO_HIP_API int neo_hip_overlap_inverse(neo_hip_overlap* h, const void* spectrum
     if (ld_out < h->B) return fail(NEO_HIP_EINVAL, "leading dimension smaller than the block");
     neo_hip::device_guard g(h->device);
     if (g.rc) return g.rc;
-    if (is_device) return inverse_dev(h, spectrum, out, ld_out, neo_hip::as_stream(stream));
+    if (is_device) {
+        if (int rc = h->used.note(neo_hip::as_stream(stream))) return rc;
+        return inverse_dev(h, spectrum, out, ld_out, neo_hip::as_stream(stream));
+    }
     hipStream_t s = stream ? neo_hip::as_stream(stream) : h->stream;
     const size_t ib = size_t(h->C) * size_t(h->B) * sizeof(float), sb = size_t(h->C) * size_t(h->bins) * sizeof(neo_hip::cf);
-    if (!h->io) {
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->io), ib));
-        NEO_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->spec), sb));
-    }
+    if ((!h->io && neo_hip::dalloc(&h->io, ib)) || (!h->spec && neo_hip::dalloc(&h->spec, sb)))
+        return fail(NEO_HIP_ENOMEM, "overlap stage staging");
     NEO_HIP_CHECK(hipMemcpyAsync(h->spec, spectrum, sb, hipMemcpyHostToDevice, s));
     if (int rc = inverse_dev(h, h->spec, h->io, h->B, s)) return rc;
     NEO_HIP_CHECK(hipMemcpy2DAsync(out, size_t(ld_out) * sizeof(float), h->io, size_t(h->B) * sizeof(float),

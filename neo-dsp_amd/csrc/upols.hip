@@ -385,8 +385,9 @@ __global__ __launch_bounds__(256) void k_plain_persist(plain_persist_args pa)
     if (lead && threadIdx.x == 0) __hip_atomic_store(&pa.mb->alive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-int plain_persist_launch(upols_t* h, const persist_ctl& ctl, int64_t ld_in, int64_t ld_out)
+int plain_persist_launch(upols_t* h, const persist_ctl& ctl, int64_t ld_in, int64_t ld_out, bool* launched)
 {
+    *launched = false;
     if (h->C * h->S > 256) return fail(NEO_HIP_EINVAL, "latency mode: %d x %d plain step workgroups", h->C, h->S);
     plain_persist_args pa{};
     static_cast<persist_ctl&>(pa) = ctl;
@@ -407,11 +408,16 @@ int plain_persist_launch(upols_t* h, const persist_ctl& ctl, int64_t ld_in, int6
     pa.rows = h->rows;
     pa.pc = h->pc;
     const unsigned grid = unsigned(h->C) * unsigned(h->S);
+    bool room = false;
     if (h->ola) {
-        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_plain_persist<BB, true>), dim3(grid), dim3(256), 0, h->ps_stream, pa))
+        NEO_UPOLS_DISPATCH(h->B, room = persist_room(h, reinterpret_cast<const void*>(&k_plain_persist<BB, true>), int(grid));
+                           if (room) hipLaunchKernelGGL((k_plain_persist<BB, true>), dim3(grid), dim3(256), 0, h->ps_stream, pa))
     } else {
-        NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_plain_persist<BB, false>), dim3(grid), dim3(256), 0, h->ps_stream, pa))
+        NEO_UPOLS_DISPATCH(h->B, room = persist_room(h, reinterpret_cast<const void*>(&k_plain_persist<BB, false>), int(grid));
+                           if (room) hipLaunchKernelGGL((k_plain_persist<BB, false>), dim3(grid), dim3(256), 0, h->ps_stream, pa))
     }
+    if (!room) return NEO_HIP_OK;
+    *launched = true;
     NEO_HIP_LAUNCH_CHECK();
     return NEO_HIP_OK;
 }
@@ -556,14 +562,9 @@ using namespace neo_hip;
 
 int neo_hip::setup_join(upols_t* h, bool device_input)
 {
-    if (h->used_many) {
-        NEO_HIP_CHECK(hipDeviceSynchronize());
-    } else {
-        for (int i = 0; i < h->n_used; ++i) NEO_HIP_CHECK(hipStreamSynchronize(h->used_s[i]));
-        if (device_input) NEO_HIP_CHECK(hipStreamSynchronize(nullptr));
-    }
-    h->n_used = 0;
-    h->used_many = false;
+    if (int rc = h->used.join()) return rc;
+    if (device_input)
+        if (int rc = null_join()) return rc;
     if (int rc = lvl_join(h, h->stream)) return rc;
     NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
     return NEO_HIP_OK;
@@ -583,7 +584,8 @@ int reset_state(upols_t* h, hipStream_t s)
     }
     h->wpos = 0;
     h->in_pos = 0;
-    h->lv_n = -1;  // streaming levels re-prime at the next step
+    h->lv_n = -1;  // streaming levels re-prime at the next step (zeroing: lvl_prime)
+    h->fdl_zero = true;
     return NEO_HIP_OK;
 }
 
@@ -616,8 +618,15 @@ void destroy(upols_t* h)
 
 int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
 {
-    note_stream(h, s);
+    if (int rc = note_stream(h, s)) return rc;
     if (h->persist) return persist_process(h, in, ld_in, out, ld_out, 1);  // synchronous: s is not used
+    return launch_step_normal(h, in, ld_in, out, ld_out, s);
+}
+
+}  // namespace
+
+int neo_hip::launch_step_normal(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s)
+{
     if (h->ahead) return launch_levels(h, in, ld_in, out, ld_out, s);
     if (int rc = lvl_join(h, s)) return rc;
     upols_t::ev_group* ev = nullptr;
@@ -636,6 +645,7 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
     }
 #undef NEO_STEP
     NEO_HIP_LAUNCH_CHECK();
+    h->fdl_zero = false;
     if (int rc = timing_mark(ev, 1, s)) return rc;
     if (!h->fused) {
         if (h->ola) {
@@ -652,12 +662,15 @@ int launch_step(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t 
     return NEO_HIP_OK;
 }
 
+namespace {
+
 // One v2 piece of n samples at block position h->in_pos (n <= B - in_pos).
 int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int n, hipStream_t s)
 {
     const int sum_first = h->in_pos == 0;
     if (int rc = lvl_join(h, s)) return rc;
     h->lv_n = -1;
+    h->fdl_zero = false;
     if (sum_first) {  // tail MAC over partitions p >= 1 into the split slabs
         const unsigned grid = unsigned(h->C) * unsigned(h->S);
         NEO_UPOLS_DISPATCH(h->B, hipLaunchKernelGGL((k_upols_step<BB, false, true, true>), dim3(grid), dim3(256), 0, s,
@@ -683,7 +696,7 @@ int launch_piece(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
 // (overlap_add_convolver.hpp:80-134) and run whole aligned blocks through launch_step.
 int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t n, hipStream_t s)
 {
-    note_stream(h, s);
+    if (int rc = note_stream(h, s)) return rc;
     const int B = h->B;
     const int T = h->batch ? batch_blocks(h) : 1;
     const bool a16 = !((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) &&
@@ -865,7 +878,9 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
 int neo_hip::create_handle(int channels, int block, int partitions, int device, int method, hipStream_t stream,
                            neo_hip_upols** out)
 {
-    return create_convolver(channels, block, partitions, device, method >= 1, method == 2, nullptr, out, stream);
+    const int rc = create_convolver(channels, block, partitions, device, method >= 1, method == 2, nullptr, out, stream);
+    if (!rc) (*out)->grouped = true;
+    return rc;
 }
 
 extern "C" {
@@ -919,6 +934,7 @@ NEO_HIP_API int neo_hip_upols_reset(neo_hip_upols* h)
     if (int rc = persist_stop(h)) return rc;
     if (int rc = setup_join(h)) return rc;  // after this handle's steps on any stream
     int rc = reset_state(h, h->stream);
+    if (!rc) rc = lvl_setup_prime(h);  // the next call is an ordinary streaming step
     if (rc) return rc;
     NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
     return NEO_HIP_OK;
@@ -943,6 +959,9 @@ NEO_HIP_API int neo_hip_upols_set_filter(neo_hip_upols* h, const void* filter, i
     int rc = pack_filter(h, src, h->stream);
     lvl_filter_changed(h);
     if (!rc) rc = reset_state(h, h->stream);
+    // the reference's filter() rebuilds the convolver's state (uniform_partitioned_convolver.hpp:37-45)
+    // and its next call is an ordinary block step (:47-65): the levels' setup runs here, not there
+    if (!rc) rc = lvl_setup_prime(h);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     dfree(tmp);  // the stream was joined above
     return rc;
@@ -970,6 +989,9 @@ NEO_HIP_API int neo_hip_upols_set_impulse(neo_hip_upols* h, const float* ir, int
     if (!rc) rc = partition_device(d, h->C, length, h->B, true, h->H, h->tw, h->stream, h->cstride, h->pstride);
     lvl_filter_changed(h);
     if (!rc) rc = reset_state(h, h->stream);
+    // the reference's filter() rebuilds the convolver's state (uniform_partitioned_convolver.hpp:37-45)
+    // and its next call is an ordinary block step (:47-65): the levels' setup runs here, not there
+    if (!rc) rc = lvl_setup_prime(h);
     if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
     dfree(d);
     return rc;

@@ -445,6 +445,7 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     const unsigned gCT = unsigned(h->C) * unsigned(T);
     if (int rc = lvl_join(h, s)) return rc;  // step-group slices still reading the FDL ring
     h->lv_n = -1;  // a streaming step after this re-primes its level windows
+    h->fdl_zero = false;
     if (h->ola) {
         NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, true>), dim3(gCT), dim3(256), 0, s, in, ld_in,
                                                  h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))

@@ -138,6 +138,7 @@ int copy_channel(neo_hip_upols* dst, int cd, const neo_hip_upols* src, int cs, c
                                  hipMemcpyDeviceToDevice, s));
     NEO_HIP_CHECK(hipMemcpyAsync(dst->prev + int64_t(cd) * dst->B, prev_src + int64_t(cs) * src->B,
                                  size_t(src->B) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    dst->fdl_zero = false;  // a stepped ring: the next streaming step primes in full
     return NEO_HIP_OK;
 }
 
@@ -174,7 +175,9 @@ bool registered(const group_t* g, const float* p)
 // ~33 us (tests/cpp/bench_hipcost), once per registration.
 struct pin_entry {
     int refs;
-    bool ours;  // registered by us (else it was page-locked already: its owner unregisters it)
+    bool ours;      // registered by us (else it was page-locked already: its owner unregisters it)
+    bool borrowed;  // not ours and overlapping a range locked here: that range's last unregister
+                    // (another group, another thread) may unlock it while a step reads it in place
 };
 std::mutex g_pin_mu;
 std::map<std::pair<uintptr_t, uintptr_t>, pin_entry> g_pins;  // [lo, hi) -> entry
@@ -186,11 +189,25 @@ void pin_range(uintptr_t lo, uintptr_t hi)
         ++it->second.refs;
         return;
     }
-    pin_entry e{1, false};
+    pin_entry e{1, false, false};
     void* p = reinterpret_cast<void*>(lo);
-    if (hipHostRegister(p, size_t(hi - lo), hipHostRegisterMapped) == hipSuccess) e.ours = true;
-    else (void)hipGetLastError();  // already page-locked (by its owner, or overlapping a range locked here)
+    if (hipHostRegister(p, size_t(hi - lo), hipHostRegisterMapped) == hipSuccess) {
+        e.ours = true;
+    } else {
+        (void)hipGetLastError();  // already page-locked (by its owner, or overlapping a range locked here)
+        for (const auto& [k, v] : g_pins)
+            if (v.ours && k.first < hi && lo < k.second) e.borrowed = true;
+    }
     g_pins.emplace(std::make_pair(lo, hi), e);
+}
+
+// a registered range whose page lock lasts while its registration does (ours, or its owner's own
+// page-locked memory), so a step may read it in place
+bool pin_stable(uintptr_t lo, uintptr_t hi)
+{
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.find({lo, hi});
+    return it != g_pins.end() && !it->second.borrowed;
 }
 
 void unpin_range(uintptr_t lo, uintptr_t hi)
@@ -222,7 +239,7 @@ bool inplace_frame(const group_t* g, const member& lead, const float* io, const 
     const uintptr_t lo = reinterpret_cast<uintptr_t>(p0),
                     hi = reinterpret_cast<uintptr_t>(p0 + int64_t(C - 1) * d + g->B);
     for (const auto& r : g->reg)
-        if (lo >= r.lo && hi <= r.hi) {
+        if (lo >= r.lo && hi <= r.hi && pin_stable(r.lo, r.hi)) {
             // its device mapping as of now (a range another registration page-locked may have been
             // unlocked since); none: the leader copies
             const float* dev = neo_hip::host_mapped(const_cast<float*>(p0));

@@ -171,6 +171,9 @@ struct neo_hip_upols {
     bool ahead = false;
     neo_hip::level_plan lv;
     int64_t lv_n = -1;              // blocks since the levels were primed (-1: prime at the next step)
+    bool fdl_zero = false;          // FDL ring all zero, nothing stepped since (reset_state): every level
+                                    // window the prime computes is zero, so priming is zeroing
+    bool grouped = false;           // created by a convolver group (create_handle): no eager priming
     bool lv_ready = false;          // level buffers allocated
     neo_hip::cf* lv_slab[neo_hip::kLvToep] = {};  // Toeplitz level slabs [2][C][T][B]
     // step groups (upols_levels.hip part_plan, set when the levels prime): per Toeplitz level the
@@ -248,14 +251,13 @@ struct neo_hip_upols {
     int64_t ps_ld_in = 0, ps_ld_out = 0;       // channel strides of the running kernel
     int64_t ps_n0 = 0;                         // first step of the running kernel
     int64_t ps_launches = 0;                   // persistent launches so far (idle timeouts relaunch)
+    int ps_wgs = 0;                            // workgroups of the running kernel (resident_admit)
+    int64_t ps_fallbacks = 0;                  // calls run as normal steps: no room for the grid
     double ps_idle_ms = 50.0;                  // the kernel leaves after this long without a block
     // streams the step calls ran on since the last setup call (setup_join waits for these, not for
     // the device: another handle's resident latency-mode kernel must not stall a setup call); a
     // stream given to a step call must stay valid until the handle's next setup call or destroy
-    static constexpr int kUsedStreams = 4;
-    hipStream_t used_s[kUsedStreams] = {};
-    int n_used = 0;
-    bool used_many = false;  // more distinct streams than kUsedStreams: setup waits for the device
+    neo_hip::stream_set used;
 };
 
 
@@ -263,13 +265,7 @@ namespace neo_hip {
 
 using upols_t = neo_hip_upols;
 
-inline void note_stream(upols_t* h, hipStream_t s)
-{
-    for (int i = 0; i < h->n_used; ++i)
-        if (h->used_s[i] == s) return;
-    if (h->n_used < upols_t::kUsedStreams) h->used_s[h->n_used++] = s;
-    else h->used_many = true;
-}
+inline int note_stream(upols_t* h, hipStream_t s) { return h->used.note(s); }
 // order a setup call (filter change, reset, mode switch, destroy) after every step of this handle:
 // the streams its step calls ran on, its background stream, its own stream; device_input: also
 // after work on the null stream (a device-resident filter or impulse produced there)
@@ -360,7 +356,15 @@ int bg_pad_for(int C, int B);
 int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int64_t nblocks);
 // latency mode of a handle without streaming levels: the plain step's persistent kernel on
 // h->ps_stream (upols.hip), its control (mailbox, flags, first step) set up by the caller
-int plain_persist_launch(upols_t* h, const persist_ctl& ctl, int64_t ld_in, int64_t ld_out);
+// (no room for its grid beside the process's other persistent kernels: *launched false, nothing
+// enqueued, persist_room)
+int plain_persist_launch(upols_t* h, const persist_ctl& ctl, int64_t ld_in, int64_t ld_out, bool* launched);
+// room on the device for a persistent grid of `grid` workgroups of kernel f (256 lanes): all of them
+// resident at once beside the persistent kernels this process already runs there, within three
+// quarters of the device's slots for f (occupancy x CUs); reserved in h->ps_wgs on success
+bool persist_room(upols_t* h, const void* f, int grid);
+// the normal (non-persistent) block step (launch_step without the latency-mode branch)
+int launch_step_normal(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, hipStream_t s);
 // stop the persistent kernel (if any) and leave the levels to re-prime on the next normal step
 int persist_stop(upols_t* h);
 // why a handle cannot run the latency mode (nullptr: it can)
@@ -370,6 +374,10 @@ const char* persist_ineligible(const upols_t* h);
 int lvl_join(upols_t* h, hipStream_t s);
 void lvl_free(upols_t* h);
 void lvl_filter_changed(upols_t* h);
+// a setup call's last step (set_filter, set_impulse, reset; FDL just zeroed): the level buffers,
+// the far segment spectra and window 0 of every level, on h->stream, so the next call is an
+// ordinary streaming step (no-op without levels and for group handles)
+int lvl_setup_prime(upols_t* h);
 // upols_setup.hip: twiddles, uniform_partition and normalize_impulse on the device
 int upload_tw(cf** d, int B);
 int partition_device(const float* d_ir, int C, int64_t L, int B, bool packed, cf* out, const cf* tw, hipStream_t s,

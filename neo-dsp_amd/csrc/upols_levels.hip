@@ -2226,6 +2226,11 @@ int lvl_join(upols_t* h, hipStream_t s)
 // First streaming step after a reset / filter change / batched pass (block t0 at ring row w):
 // window 0 of every level, starting at t0, computed whole (all units; the far level
 // transforms every segment: phase 1 and 2a in the levels' launch, 2b in a second one).
+// After a reset or a filter change (fdl_zero) every FDL row before t0 is zero, and so is every
+// value the prime computes from them: Toeplitz windows 0 and 1 (slab[j] = sum over the band,
+// p >= 2T, of H[p] X[t_W + j - p]: rows before t0), the far window's row-pair spectra, partial
+// sums and field (rows t_W - 128 (q + 1) ... + 255 < t0). Then priming is zeroing the level
+// buffers (all of them: a superset of what the two launches write), a fraction of their time.
 static int lvl_prime(upols_t* h, hipStream_t s)
 {
     const level_plan& lp = h->lv;
@@ -2239,6 +2244,20 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         h->fv_dirty = false;
     }
     plan_handle_parts(h);  // window offsets and background part sizes (step groups)
+    if (h->fdl_zero) {
+        for (int l = 0; l < lp.n; ++l)
+            NEO_HIP_CHECK(hipMemsetAsync(h->lv_slab[l], 0, 2 * size_t(C) * lp.T[l] * B * sizeof(cf), s));
+        if (lp.nseg) {
+            if (!h->far_raw) {
+                const size_t spec = size_t(C) * size_t(lp.nseg) * kFN * B * sizeof(cf);
+                NEO_HIP_CHECK(hipMemsetAsync(h->fv_xf, 0, spec, s));
+                const size_t accb = size_t(far_group(h)) * size_t(far_units(h)) * kFN * 16 * sizeof(cf);
+                NEO_HIP_CHECK(hipMemsetAsync(h->fv_acc, 0, accb, s));
+            }
+            NEO_HIP_CHECK(hipMemsetAsync(h->fv_ff, 0, 2 * size_t(C) * kFarT * B * sizeof(cf), s));
+        }
+        return NEO_HIP_OK;
+    }
     slice_args a = base_args(h), f = base_args(h);  // f: the second launch (far 2b, offset windows 1)
     bool f_any = false;
     for (int l = 0; l < lp.n; ++l) {
@@ -2396,9 +2415,21 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     upols_t::ev_group* ev = nullptr;  // the step's (block's) launch alone
     if ((rc = timing_begin(h, 2, &ev)) || (rc = timing_mark(ev, 0, s))) return rc;
     if ((rc = launch_step_kernel(h, a, s, G > 1 ? 1 : 0))) return rc;
+    h->fdl_zero = false;
     if ((rc = timing_mark(ev, 1, s))) return rc;
     h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
     h->lv_n = n + 1;
+    return NEO_HIP_OK;
+}
+
+int lvl_setup_prime(upols_t* h)
+{
+    if (!h->ahead || h->grouped || h->lv_n >= 0) return NEO_HIP_OK;
+    if (int rc = lvl_buffers(h)) return rc;
+    if (int rc = lvl_prime(h, h->stream)) return rc;
+    h->lv_n = 0;
+    h->pace_prev = false;
+    h->pace_seq = 0;
     return NEO_HIP_OK;
 }
 
@@ -2650,7 +2681,9 @@ static int persist_level_wgs(const upols_t* h, int l, int& U, int& UPW, int& JH)
 static int persist_levels(upols_t* h, persist_args& pa, int64_t ld_in, int64_t ld_out)
 {
     if (int rc = lvl_buffers(h)) return rc;
-    if (!h->ps_valid || h->lv_n < 0) {  // window 0 of every level, from this block on
+    if (h->lv_n == 0 && h->fdl_zero) {  // primed by a setup call (lvl_setup_prime), nothing stepped since
+        h->ps_valid = true;
+    } else if (!h->ps_valid || h->lv_n < 0) {  // window 0 of every level, from this block on
         if (int rc = lvl_join(h, h->ps_stream)) return rc;
         h->lv_n = -1;
         if (int rc = lvl_prime(h, h->ps_stream)) return rc;
@@ -2691,6 +2724,19 @@ static int persist_levels(upols_t* h, persist_args& pa, int64_t ld_in, int64_t l
         pa.wgf1 = pa.wgf0 + most;
     }
     return NEO_HIP_OK;
+}
+
+bool persist_room(upols_t* h, const void* f, int grid)
+{
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (!resident_admit(h->device, grid, per_cu * cus * 3 / 4)) return false;
+    h->ps_wgs = grid;
+    return true;
 }
 
 static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
@@ -2753,16 +2799,29 @@ static int persist_launch(upols_t* h, int64_t ld_in, int64_t ld_out)
     h->ps_mb->done = pa.n0;
     h->ps_mb->alive = 1;
     const unsigned grid = unsigned(h->C + nsl);
+    bool launched = false;
     if (!h->ahead) {
-        if (int rc = plain_persist_launch(h, pa, ld_in, ld_out)) return rc;
+        if (int rc = plain_persist_launch(h, pa, ld_in, ld_out, &launched)) return rc;
     } else if (h->ola) {
-        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 512) hipLaunchKernelGGL((k_lvl_persist<BB, true>), dim3(grid),
-                                                                              dim3(256), 0, h->ps_stream, pa))
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 512) {
+            if ((launched = persist_room(h, reinterpret_cast<const void*>(&k_lvl_persist<BB, true>), int(grid))))
+                hipLaunchKernelGGL((k_lvl_persist<BB, true>), dim3(grid), dim3(256), 0, h->ps_stream, pa);
+        })
     } else {
-        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 512) hipLaunchKernelGGL((k_lvl_persist<BB, false>), dim3(grid),
-                                                                              dim3(256), 0, h->ps_stream, pa))
+        NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 512) {
+            if ((launched = persist_room(h, reinterpret_cast<const void*>(&k_lvl_persist<BB, false>), int(grid))))
+                hipLaunchKernelGGL((k_lvl_persist<BB, false>), dim3(grid), dim3(256), 0, h->ps_stream, pa);
+        })
     }
-    NEO_HIP_LAUNCH_CHECK();
+    if (!launched) {  // no room for every workgroup at once: the caller runs normal steps (persist_process)
+        h->ps_mb->alive = 0;
+        return NEO_HIP_OK;
+    }
+    if (hipGetLastError() != hipSuccess) {
+        resident_release(h->device, h->ps_wgs);
+        h->ps_wgs = 0;
+        return fail(NEO_HIP_ERUNTIME, "persistent kernel launch failed");
+    }
     h->ps_running = true;
     h->ps_ld_in = ld_in;
     h->ps_ld_out = ld_out;
@@ -2788,6 +2847,8 @@ static int persist_join(upols_t* h)
     __atomic_store_n(&h->ps_mb->stop, 1, __ATOMIC_SEQ_CST);
     const hipError_t e = hipStreamSynchronize(h->ps_stream);
     h->ps_running = false;
+    resident_release(h->device, h->ps_wgs);
+    h->ps_wgs = 0;
     if (e != hipSuccess) {
         persist_invalidate(h);
         return fail(NEO_HIP_ERUNTIME, "persistent kernel: %s", hipGetErrorString(e));
@@ -2822,8 +2883,19 @@ int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int6
         if (int rc = persist_join(h)) return rc;  // another channel stride: relaunch with it
     if (h->ps_running && !__atomic_load_n(&h->ps_mb->alive, __ATOMIC_ACQUIRE))
         if (int rc = persist_join(h)) return rc;  // left after its idle limit (or failed)
-    if (!h->ps_running)
+    if (!h->ps_running) {
         if (int rc = persist_launch(h, ld_in, ld_out)) return rc;
+        if (!h->ps_running) {
+            // no room on the device for the persistent grid (other persistent kernels of this
+            // process hold it): this call's blocks run as normal steps, complete on return; the
+            // schedules differ, so the levels re-prime (and again when a later call relaunches)
+            ++h->ps_fallbacks;
+            if (int rc = persist_stop(h)) return rc;
+            for (int64_t k = 0; k < nblocks; ++k)
+                if (int rc = launch_step_normal(h, in + k * h->B, ld_in, out + k * h->B, ld_out, h->stream)) return rc;
+            return spin_sync(h->stream);
+        }
+    }
     persist_mb* mb = h->ps_mb;  // allocated by the first launch
     const int B = h->B;
     for (int64_t k = 0; k < nblocks; ++k) {
@@ -2838,21 +2910,24 @@ int persist_process(upols_t* h, const float* in, int64_t ld_in, float* out, int6
         persist_rec& r = mb->rec[n % kPsRing];
         __atomic_store_n(&r.in, reinterpret_cast<uint64_t>(in + k * B) | tag, __ATOMIC_RELEASE);
         __atomic_store_n(&r.out, reinterpret_cast<uint64_t>(out + k * B) | tag, __ATOMIC_RELEASE);
+        h->fdl_zero = false;
         h->lv_n = n + 1;
         h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
     }
     // complete on return (the block's deadline: spin, do not yield); the kernel's own waits give
-    // up after 2 s, so a host wait past 5 s means the kernel is not running at all
+    // up 2 s past its idle limit (dead_ticks), so a host wait 3 s past it means the kernel is not
+    // running at all
     const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = std::chrono::duration<double, std::milli>(h->ps_idle_ms + 3000.0);
     for (unsigned it = 0; __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) < h->lv_n; ++it) {
         if (!__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) && __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) < h->lv_n) {
             const int rc = persist_join(h);
             return rc ? rc : fail(NEO_HIP_ERUNTIME, "persistent kernel left before step %lld", (long long)h->lv_n);
         }
-        if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > limit) {
             __atomic_store_n(&mb->stop, 1, __ATOMIC_SEQ_CST);
             persist_invalidate(h);  // the next call joins the kernel and re-primes
-            return fail(NEO_HIP_ERUNTIME, "persistent kernel: no progress for 5 s");
+            return fail(NEO_HIP_ERUNTIME, "persistent kernel: no progress for %.0f ms", limit.count());
         }
     }
     return NEO_HIP_OK;

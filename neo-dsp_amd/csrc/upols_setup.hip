@@ -224,16 +224,16 @@ NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t
     const size_t in_bytes = size_t(channels) * size_t(length) * sizeof(float);
     const size_t out_bytes = size_t(channels) * size_t(P) * size_t(block + 1) * sizeof(cf);
     hipStream_t s = nullptr;
-    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
+    if (is_device)
+        if (int rc = null_join()) return rc;  // after its producer (common.hpp: null_join)
     if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     cf* tw = nullptr;
     const float* d_ir = ir;
     float* tmp_in = nullptr;
     cf* d_out = static_cast<cf*>(out);
-    int rc = upload_tw(&tw, block);
-    if (!rc && !is_device) {
-        if (hipMalloc(reinterpret_cast<void**>(&tmp_in), in_bytes) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&d_out), out_bytes) != hipSuccess)
+    int rc = shared_tw(&tw, block);
+    if (!rc && !is_device) {  // pooled (dmem.hip): no hipMalloc / hipFree, which wait for the device
+        if (dalloc(&tmp_in, in_bytes) || dalloc(&d_out, out_bytes))
             rc = fail(NEO_HIP_ENOMEM, "allocation failed");
         else if (hipMemcpyAsync(tmp_in, ir, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
             rc = fail(NEO_HIP_ERUNTIME, "copy failed");
@@ -243,11 +243,10 @@ NEO_HIP_API int neo_hip_uniform_partition(const float* ir, int channels, int64_t
     if (!rc && !is_device && hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
-    if (!is_device) {
-        (void)hipFree(tmp_in);
-        (void)hipFree(d_out);
+    if (!is_device) {  // the stream was joined above
+        dfree(tmp_in);
+        dfree(d_out);
     }
-    (void)hipFree(tw);
     return rc;
 }
 
@@ -258,13 +257,14 @@ NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t lengt
     device_guard g(device);
     if (g.rc) return g.rc;
     hipStream_t s = nullptr;
-    if (is_device) NEO_HIP_CHECK(hipDeviceSynchronize());  // order after producers on any stream
+    if (is_device)
+        if (int rc = null_join()) return rc;  // after its producer (common.hpp: null_join)
     if (int rs = shared_stream(&s)) return rs;  // one of the device's four (dmem.hip)
     const size_t bytes = size_t(channels) * size_t(length) * sizeof(float);
     float* d = ir;
     int rc = NEO_HIP_OK;
     if (!is_device) {
-        if (hipMalloc(reinterpret_cast<void**>(&d), bytes) != hipSuccess) rc = fail(NEO_HIP_ENOMEM, "alloc failed");
+        if (dalloc(&d, bytes)) rc = fail(NEO_HIP_ENOMEM, "alloc failed");
         else if (hipMemcpyAsync(d, ir, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
             rc = fail(NEO_HIP_ERUNTIME, "copy failed");
     }
@@ -272,7 +272,7 @@ NEO_HIP_API int neo_hip_normalize_impulse(float* ir, int channels, int64_t lengt
     if (!rc && !is_device && hipMemcpyAsync(ir, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = fail(NEO_HIP_ERUNTIME, "copy back failed");
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(NEO_HIP_ERUNTIME, "sync failed");
-    if (!is_device && d) (void)hipFree(d);
+    if (!is_device) dfree(d);  // the stream was joined above
     return rc;
 }
 

@@ -53,6 +53,19 @@ def _ptr(a: np.ndarray) -> ctypes.c_void_p:
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _producer_join(t) -> None:
+    """A device tensor handed to a synchronous setup call (filter, impulse, normalize, partition)
+    is complete first: torch's current stream is its producer. The library orders such an input
+    after the null stream (torch's default stream) itself, with a marker event, never after the
+    whole device (a resident latency-mode kernel on another handle); a side stream
+    (`with torch.cuda.stream(s)`) is synchronized here, that stream alone."""
+    import torch
+
+    s = torch.cuda.current_stream(t.device)
+    if s.cuda_stream != 0:
+        s.synchronize()
+
+
 def num_partitions(length: int, block: int) -> int:
     """P = ceil(L / B) (stft.hpp:21-25 with overlap 0; clamped to 1 for L < B)."""
     p = ctypes.c_int64()
@@ -127,8 +140,22 @@ def memory_trim(device: int = 0) -> None:
     _native.check(_native.load().neo_hip_memory_trim(device))
 
 
-def uniform_partition(impulse_response, block_size: int, device: int = 0) -> np.ndarray:
-    """[C][L] float32 -> [C][P][B+1] complex64: rfft_2B of each zero-padded B-sample partition."""
+def uniform_partition(impulse_response, block_size: int, device: int = 0):
+    """[C][L] float32 -> [C][P][B+1] complex64: rfft_2B of each zero-padded B-sample partition.
+    A CUDA tensor gives a CUDA tensor on its device (no host copies)."""
+    if _is_torch(impulse_response) and impulse_response.is_cuda:
+        import torch
+
+        t = impulse_response
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise TypeError("uniform_partition takes a contiguous float32 tensor")
+        C, L = (1, t.shape[0]) if t.dim() == 1 else tuple(t.shape)
+        P = num_partitions(L, block_size)
+        out = torch.empty((C, P, block_size + 1), dtype=torch.complex64, device=t.device)
+        _producer_join(t)
+        _native.check(_native.load().neo_hip_uniform_partition(ctypes.c_void_p(t.data_ptr()), C, L, int(block_size),
+                                                               ctypes.c_void_p(out.data_ptr()), 1, t.device.index or 0))
+        return out
     ir = np.ascontiguousarray(np.atleast_2d(np.asarray(impulse_response, dtype=np.float32)))
     C, L = ir.shape
     P = num_partitions(L, block_size)
@@ -143,6 +170,7 @@ def normalize_impulse(impulse_response, device: int = 0):
     if _is_torch(impulse_response):
         t = impulse_response
         C, L = (1, t.shape[0]) if t.dim() == 1 else tuple(t.shape)
+        _producer_join(t)
         _native.check(_native.load().neo_hip_normalize_impulse(ctypes.c_void_p(t.data_ptr()), C, L, 1,
                                                                t.device.index or 0))
         return t
@@ -201,6 +229,7 @@ class UpolsConvolver:
         """uniform_partitioned_convolver::filter(): [C][P][B+1] complex64 (host array or
         CUDA tensor); resets FDL, window and write position."""
         if _is_torch(partitions):
+            _producer_join(partitions)
             _native.check(_native.load().neo_hip_upols_set_filter(self._h, ctypes.c_void_p(partitions.data_ptr()), 1))
             return
         H = np.ascontiguousarray(partitions, dtype=np.complex64)
@@ -214,6 +243,7 @@ class UpolsConvolver:
         """normalize_impulse (optional) + uniform_partition straight into the device filter."""
         if _is_torch(impulse_response):
             t = impulse_response
+            _producer_join(t)
             _native.check(_native.load().neo_hip_upols_set_impulse(self._h, ctypes.c_void_p(t.data_ptr()),
                                                                    t.shape[-1], int(normalize), 1))
             return

@@ -994,7 +994,9 @@ def test_batched_calls_keep_levels_primed(neo_gpu, oracle):
     """process_blocks with batching on and a block count that is not a whole number of
     batches: only whole T-block batches run (they leave the levels to re-prime once), and
     once the levels are primed a call of fewer than 4 T blocks streams them all, so repeated
-    33-block calls do not re-prime every call (ahead_info's window position keeps counting)."""
+    33-block calls do not re-prime every call (ahead_info's window position keeps counting).
+    filter() primes the levels itself (lvl_setup_prime), so the first call streams too; after a
+    reset and one batched call of 128 blocks the next 33-block call runs one batch and primes."""
     torch = pytest.importorskip("torch")
     B, P, C = 64, 300, 2
     L = B * P
@@ -1014,9 +1016,19 @@ def test_batched_calls_keep_levels_primed(neo_gpu, oracle):
         t[:, k * 33 * B:(k + 1) * 33 * B] = seg
         phases.append(conv.ahead_info()[1])
     torch.cuda.synchronize()
-    # call 0: one batch of 32, one streamed block (primes); then 33 streamed blocks per call
-    assert phases == [(1 + 33 * k) % 128 for k in range(6)], phases
+    # primed by filter(): 33 streamed blocks per call from the first
+    assert phases == [(33 * (k + 1)) % 128 for k in range(6)], phases
     assert peak_err(t.cpu().numpy(), ref) <= TOL
+    conv.reset()
+    t = torch.from_numpy(sig).cuda()
+    conv.process_blocks(t[:, : 128 * B].contiguous())  # 4 T blocks: batched passes, the levels re-prime later
+    phases = []
+    for k in range(2):
+        seg = t[:, 128 * B + k * 33 * B:128 * B + (k + 1) * 33 * B].contiguous()
+        conv.process_blocks(seg)
+        phases.append(conv.ahead_info()[1])
+    # call 0: one batch of 32, one streamed block (primes); then 33 streamed blocks
+    assert phases == [1, 34], phases
 
 
 @pytest.mark.parametrize("far", [0, 1])
