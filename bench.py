@@ -462,7 +462,7 @@ def host_io_times(conv, C, B, nblocks, kind, seed=0):
     return dt
 
 
-def group_frames(C, frames, B, L):
+def group_frames(C, frames, B, L, stable=False):
     """tests/cpp/bench_group (C++, NEO_HIP_CONVOLVER_GROUPS): the plugin's processFrame over C
     single-channel convolvers of one owner-registered frame buffer (one launch per frame once
     coalesced), and the dense_convolve<Convolver> harness pattern (one shared scratch block: one
@@ -474,7 +474,8 @@ def group_frames(C, frames, B, L):
     exe = os.path.join(cpp, "bin", "bench_group")
     try:
         subprocess.run(["make", "-s", "-C", cpp, "bin/bench_group"], check=True, capture_output=True, timeout=300)
-        r = subprocess.run([exe, str(C), str(frames), str(B), str(L)], capture_output=True, text=True, timeout=600)
+        r = subprocess.run([exe, str(C), str(frames), str(B), str(L), "1" if stable else "0"], capture_output=True,
+                           text=True, timeout=600)
         d = json.loads(r.stdout.strip().splitlines()[-1])
     except (OSError, subprocess.SubprocessError, ValueError, IndexError) as e:
         return {"error": str(e)[:200]}
@@ -864,8 +865,11 @@ def run_upols(args, world, rank, local):
         del c5
         torch.cuda.empty_cache()
         # the plugin's std::vector<upols_convolver> (group-backed alias, C++) at 256 and 2048 channels
-        for cs_, nf_ in ((256, 64), (2048, 16)):
+        # (frame buffer registered plainly: exact snapshot comparison per member; and with the owner's
+        # frame-stable promise, NEO_HIP_GROUP_FRAME_STABLE: no snapshot, no comparison)
+        for cs_, nf_ in ((256, 64), (2048, 32)):
             host_io[f"group_{cs_}"] = group_frames(cs_, nf_, B, L)
+            host_io[f"group_{cs_}_stable"] = group_frames(cs_, nf_, B, L, stable=True)
         # the plugin's processing class (stereo split_upols_convolver, 10 s IR), both modes
         for lat in (False, True):
             host_io["plugin_stereo" + ("_latency" if lat else "")] = plugin_frames(2, 400, B, L, lat)
@@ -961,16 +965,20 @@ def run_latency_mode(args, conv, feed, C, B, world, C_total):
 
 
 def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world, C_total):
-    """Same convolver and input, blocks available up front (dense_convolve / process_blocks):
-    T blocks share one pass over the filter and the FDL. Not the headline (which is the
-    real-time one-block-per-pass step); reported beside it. 128 blocks per timed run."""
+    """Same convolver and input, blocks available up front (dense_convolve / process_blocks;
+    the reference's offline harness, extra/plugin/src/dsp/DenseConvolution.hpp:39-70 run by
+    extra/plugin/src/ui/BenchmarkTab.hpp:47-66). Not the headline (which is the real-time
+    one-block-per-call step); reported beside it. 256 blocks per timed call: with offline windows
+    (>= 128 partitions) ONE pass of two 128-block windows (k_off_mac: partition-axis transforms of
+    every 128-partition segment), else 8 T-block MAC passes (k_batch_mac)."""
     import torch
 
     if args.no_offline:
         return None
     conv.set_batch(True)
     T, splits = conv.batch_info()
-    nb = 128
+    off, nseg = conv.offline_info()
+    nb = 256
     conv.reset()
     t_warm = time.perf_counter()
     while time.perf_counter() - t_warm < WARM_SECONDS:
@@ -990,12 +998,20 @@ def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world, C_total):
     conv.set_batch(False)
     elapsed = max_over_ranks(t1 - t0, world)
     mac_avg_ms = max_over_ranks(mac_ms / max(launches, 1), world)
-    bytes_pass = C * 16 * P * B  # filter + FDL streamed once per pass of T blocks
+    if off:
+        wp = 2
+        # per column and pass: (nseg + wp) 128 FDL rows, nseg 256-row segment spectra, wp 128 output rows
+        bytes_pass = C * B * 8 * ((nseg + wp) * 128 + nseg * 256 + wp * 128)
+        kernel, per_pass, pmc = f"k_off_mac<{wp}>", wp * 128, "k_off_mac"
+    else:
+        bytes_pass = C * 16 * P * B  # filter + FDL streamed once per pass of T blocks
+        kernel, per_pass, pmc = f"k_batch_mac<{B},{T},1>", T, "k_batch_mac"
     gbs = bytes_pass / (mac_avg_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(_pmc_sfx(pmc_workload(args.workload, C), "_offline"), "k_batch_mac")
-    return {"value": C_total * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": T,
+    traffic = load_pmc_traffic(_pmc_sfx(pmc_workload(args.workload, C), "_offline"), pmc)
+    return {"value": C_total * B * nb / elapsed / 1e6, "unit": "Msamples/s", "blocks": nb, "blocks_per_pass": per_pass,
+            "offline_windows": off, "segments": nseg if off else None,
             "traffic": traffic, "traffic_over_algorithmic": traffic / bytes_pass if traffic else None,
-            "ms_per_block": elapsed * 1e3 / nb, "splits": splits, "kernel": f"k_batch_mac<{B},{T},1>",
+            "ms_per_block": elapsed * 1e3 / nb, "splits": None if off else splits, "kernel": kernel,
             "algorithmic_bytes_per_launch": bytes_pass, "kernel_avg_ms": mac_avg_ms,
             "achieved_gbs": gbs, "frac": gbs / PEAK_HBM_GBS}
 

@@ -405,14 +405,23 @@ public:
     };
     [[nodiscard]] auto scope() -> scope_guard { return scope_guard{*this}; }
 
-    /// [ptr, ptr + samples) stays allocated until unregister_all() (cheap to repeat per frame)
-    auto register_buffer(float const* ptr, std::size_t samples) -> void
+    /// [ptr, ptr + samples) stays allocated until unregister_all() (cheap to repeat per frame).
+    /// frame_stable: nothing but the convolvers' own calls writes it during a frame (the plugin's
+    /// loop over a filled frame): their calls then skip the exact snapshot comparison
+    /// (neo_hip_upols_group_register_ex, NEO_HIP_GROUP_FRAME_STABLE)
+    auto register_buffer(float const* ptr, std::size_t samples, bool frame_stable = false) -> void
     {
         std::lock_guard<std::mutex> lk{_mu};
-        auto const r = std::pair<float const*, std::size_t>{ptr, samples};
-        if (std::find(_ranges.begin(), _ranges.end(), r) == _ranges.end()) _ranges.push_back(r);
+        auto const flags = frame_stable ? NEO_HIP_GROUP_FRAME_STABLE : 0;
+        bool found = false;
+        for (auto& r : _ranges)
+            if (r.ptr == ptr && r.samples == samples) {
+                r.flags = flags;
+                found = true;
+            }
+        if (!found) _ranges.push_back({ptr, samples, flags});
         for (auto& [key, g] : _groups)
-            neo::hip::check(neo_hip_upols_group_register(g.get(), ptr, std::int64_t(samples * sizeof(float))));
+            neo::hip::check(neo_hip_upols_group_register_ex(g.get(), ptr, std::int64_t(samples * sizeof(float)), flags));
     }
     /// before the registered memory is freed or reallocated (e.g. at prepare())
     auto unregister_all() -> void
@@ -429,8 +438,9 @@ public:
         auto const key = std::array<std::size_t, 4>{block, partitions, std::size_t(m == method::upola), std::size_t(device)};
         if (auto it = _groups.find(key); it != _groups.end()) return it->second;
         auto g = make_group(block, partitions, m, device);
-        for (auto const& [p, n] : _ranges)
-            neo::hip::check(neo_hip_upols_group_register(g.get(), p, std::int64_t(n * sizeof(float))));
+        for (auto const& r : _ranges)
+            neo::hip::check(
+                neo_hip_upols_group_register_ex(g.get(), r.ptr, std::int64_t(r.samples * sizeof(float)), r.flags));
         _groups.emplace(key, g);
         return g;
     }
@@ -454,7 +464,12 @@ public:
 private:
     std::mutex _mu;
     std::map<std::array<std::size_t, 4>, std::shared_ptr<neo_hip_upols_group>> _groups;
-    std::vector<std::pair<float const*, std::size_t>> _ranges;
+    struct range {
+        float const* ptr;
+        std::size_t samples;
+        int flags;
+    };
+    std::vector<range> _ranges;
 };
 
 /// Single-channel drop-in for upols_convolver<complex<float>> (uniform_partitioned_convolver.hpp:13-65)
@@ -654,7 +669,7 @@ inline auto dense_convolve(float const* signal, std::size_t channels, std::size_
     // filter and FDL, one download per chunk; the tail block is zero-padded
     std::size_t const nb = (num_samples + block_size - 1) / block_size;
     std::size_t chunk = std::max<std::size_t>(1, (std::size_t(1) << 26) / (channels * block_size));
-    if (chunk >= 32) chunk = chunk / 32 * 32;
+    chunk = std::max<std::size_t>(256, chunk / 256 * 256);  // whole offline passes (two windows of 128 blocks)
     std::vector<float> buf;
     for (std::size_t t0 = 0; t0 < nb; t0 += chunk) {
         std::size_t const t1 = std::min(nb, t0 + chunk), lo = t0 * block_size,

@@ -168,6 +168,18 @@ NEO_HIP_API int neo_hip_upols_process_blocks(neo_hip_upols* h, const float* in, 
 NEO_HIP_API int neo_hip_upols_set_batch(neo_hip_upols* h, int enable);
 /* blocks one process_blocks pass consumes (1 with batching off) and its splits per channel */
 NEO_HIP_API int neo_hip_upols_batch_info(neo_hip_upols* h, int* blocks_per_pass, int* splits);
+/* Offline windows (whole-block handles of >= 128 partitions; on by default): with batching on,
+ * every 256 (or 128) whole blocks of a process_blocks / process_samples call take ONE pass that
+ * computes each 128-block window of every bin as the far level does its band -- DFT256 along the
+ * block axis of each 128-partition segment's FDL rows, times the filter segment's spectrum (made
+ * at the first pass after a filter change), one inverse transform per window -- instead of T-block
+ * MAC passes over all P partitions: ~(nseg + 2) 128 FDL rows and nseg 256 spectrum rows per column
+ * and pass, not 2 P per 32 blocks. Same outputs within float rounding (the blocks are known up
+ * front, as in the reference's offline harness, extra/plugin/src/dsp/DenseConvolution.hpp:39-70,
+ * extra/plugin/src/ui/BenchmarkTab.hpp:47-66). The rest of a call runs the T-block passes. */
+NEO_HIP_API int neo_hip_upols_set_offline(neo_hip_upols* h, int enable);
+/* offline windows on, and the 128-partition segments they transform */
+NEO_HIP_API int neo_hip_upols_get_offline(neo_hip_upols* h, int* enabled, int* segments);
 /* num_samples samples for every channel: channel c at in + c*ld_in / out + c*ld_out
  * (in == out allowed), host (synchronous) or device (asynchronous on `stream`) memory.
  * upola_convolver_v2 handles accept any count, split at block boundaries like
@@ -308,6 +320,15 @@ NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int member);
  * range starting at ptr, unregister(NULL) every range; the group then stops reading them
  * before the call returns (a coalesced group splits at its next frame). */
 NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void* ptr, int64_t bytes);
+/* register_ex with flags: NEO_HIP_GROUP_FRAME_STABLE = the owner also promises that during a frame
+ * (from its first member call until every member has made its call) nothing but those calls writes
+ * the range, as in the plugin's loop over the channels of a filled frame (DenseConvolution.cpp:62-74).
+ * A frame read in place from such a range then skips the leader's snapshot of every member's block
+ * and the members' comparisons with it: a member's call is the copy of its output. Without the flag
+ * (register) each member's block is compared exactly and re-stepped on a difference. Registering the
+ * same range again updates its flags. */
+#define NEO_HIP_GROUP_FRAME_STABLE 1
+NEO_HIP_API int neo_hip_upols_group_register_ex(neo_hip_upols_group* g, const void* ptr, int64_t bytes, int flags);
 NEO_HIP_API int neo_hip_upols_group_unregister(neo_hip_upols_group* g, const void* ptr);
 /* coalesced now; one-launch frame steps, member calls, block re-runs, mode switches so far */
 NEO_HIP_API int neo_hip_upols_group_stats(neo_hip_upols_group* g, int* coalesced, int64_t* frame_steps, int64_t* calls,

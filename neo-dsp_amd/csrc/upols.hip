@@ -612,6 +612,9 @@ void destroy(upols_t* h)
     dfree(h->samples_dev);
     dfree(h->part_b);
     dfree(h->tail);
+    dfree(h->off_hf);
+    dfree(h->off_y);
+    dfree(h->off_tail);
     hfree(h->samples_host);
     delete h;  // h->stream is shared (a group's, or one of the device's four: dmem.hip)
 }
@@ -721,6 +724,14 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
         const float* ip = in + done;
         float* op = out + done;
         int rc;
+        // offline windows: 256 or 128 whole blocks left, every block known (batching on)
+        const int64_t left = (n - done) / B;
+        if (h->off && h->batch && !stream_all && h->in_pos == 0 && a16 && done % 4 == 0 && left >= kFarT) {
+            const int wp = left >= int64_t(kFarT) * kOffMaxWP ? kOffMaxWP : 1;
+            if ((rc = launch_offline(h, ip, ld_in, op, ld_out, wp, s))) return rc;
+            done += int64_t(wp) * kFarT * B;
+            continue;
+        }
         // the largest power-of-two batch (<= T) of whole blocks left, one pass over H + FDL
         int tb = 1;
         while (!stream_all && tb * 2 <= T && n - done >= int64_t(tb) * 2 * B) tb *= 2;
@@ -789,6 +800,11 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     // recomputed: a window's slices read the band's rows back to t_W - 128 (nseg + 2) > t_W - P - 128
     // while blocks up to t_W + 3 may be written beside them (step groups)
     if (h->far_raw) h->ring = std::max(h->ring, partitions + 2 * kFarT);
+    // offline windows (k_off_mac): a pass of 128 wp blocks reads rows back to t_W - 128 nseg while
+    // writing rows t_W .. t_W + 128 wp - 1
+    h->off = !v2 && partitions >= kOffMinP;
+    h->off_nseg = (partitions + kFarT - 1) / kFarT;
+    if (h->off) h->ring = std::max(h->ring, kFarT * (h->off_nseg + kOffMaxWP));
     h->ola = ola || v2;
     h->v2 = v2;
     h->fused = 2.0 * 8.0 * double(channels) * double(partitions) * double(block) < double(kFusedMaxBytes);
@@ -1101,6 +1117,23 @@ NEO_HIP_API int neo_hip_upols_set_batch(neo_hip_upols* h, int enable)
 {
     if (!h) return fail(NEO_HIP_EINVAL, "null handle");
     h->batch = enable != 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_set_offline(neo_hip_upols* h, int enable)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    if (enable && (h->v2 || h->P < kOffMinP))
+        return fail(NEO_HIP_EINVAL, "offline windows take whole-block handles of >= %d partitions", kOffMinP);
+    h->off = enable != 0;
+    return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_get_offline(neo_hip_upols* h, int* enabled, int* segments)
+{
+    if (!h) return fail(NEO_HIP_EINVAL, "null handle");
+    if (enabled) *enabled = h->off;
+    if (segments) *segments = h->off_nseg;
     return NEO_HIP_OK;
 }
 

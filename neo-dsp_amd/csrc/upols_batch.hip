@@ -480,4 +480,57 @@ int launch_batch(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t
     return NEO_HIP_OK;
 }
 
+// Offline windows (k_off_mac, upols_levels.hip): wp windows of 128 blocks -- the window r2c of
+// every block into FDL rows w .. w + 128 wp - 1, the partition-axis transforms of every segment,
+// the per-block finish (one slab: k_off_mac's output spectra), OLA's overlap chain. The ring
+// holds >= 128 (nseg + kOffMaxWP) rows (create), so the new rows overwrite none the pass reads.
+int launch_offline(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int wp, hipStream_t s)
+{
+    const int B = h->B, T = kFarT * wp;
+    if (!h->off_y) {
+        const size_t rows = size_t(h->C) * kFarT * kOffMaxWP * B;
+        if (int rc = dalloc(&h->off_y, rows * sizeof(cf))) return rc;
+        if (dalloc(&h->off_hf, size_t(h->C) * h->off_nseg * 2 * kFarT * B * sizeof(cf)) ||
+            (h->ola && dalloc(&h->off_tail, rows * sizeof(float)))) {
+            dfree(h->off_y);
+            dfree(h->off_hf);
+            h->off_y = nullptr;
+            h->off_hf = nullptr;
+            return fail(NEO_HIP_ENOMEM, "offline window buffers");
+        }
+        h->off_dirty = true;
+    }
+    const unsigned gCT = unsigned(h->C) * unsigned(T);
+    if (int rc = lvl_join(h, s)) return rc;  // step-group slices still reading the FDL ring
+    h->lv_n = -1;  // a streaming step after this re-primes its level windows
+    h->fdl_zero = false;
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, true>), dim3(gCT), dim3(256), 0, s, in, ld_in,
+                                                 h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))
+    } else {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_window<BB, false>), dim3(gCT), dim3(256), 0, s, in, ld_in,
+                                                 h->prev, h->fdl, h->tw, T, h->ring, h->wpos, h->cstride, h->pstride))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    upols_t::ev_group* ev = nullptr;
+    int rc = timing_begin(h, 2, &ev);
+    if (!rc) rc = timing_mark(ev, 0, s);
+    if (!rc) rc = launch_off_mac(h, wp, s);
+    if (!rc) rc = timing_mark(ev, 1, s);
+    if (rc) return rc;
+    if (h->ola) {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_finish<BB, true>), dim3(gCT), dim3(256), 0, s, h->off_y, 1, T,
+                                                 in, ld_in, out, ld_out, h->prev, h->off_tail, h->tw))
+        NEO_HIP_LAUNCH_CHECK();
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_ola<BB>), dim3(unsigned(h->C)), dim3(256), 0, s, out, ld_out,
+                                                 h->off_tail, h->prev, T))
+    } else {
+        NEO_UPOLS_DISPATCH(B, hipLaunchKernelGGL((k_batch_finish<BB, false>), dim3(gCT), dim3(256), 0, s, h->off_y, 1,
+                                                 T, in, ld_in, out, ld_out, h->prev, nullptr, h->tw))
+    }
+    NEO_HIP_LAUNCH_CHECK();
+    h->wpos = (h->wpos + T) % h->ring;
+    return NEO_HIP_OK;
+}
+
 }  // namespace neo_hip

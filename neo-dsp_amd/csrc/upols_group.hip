@@ -100,7 +100,9 @@ struct neo_hip_upols_group {
     std::vector<int> slot_member;     // shared handle channel -> member
     struct range {
         uintptr_t lo, hi;  // owner-registered host range [lo, hi) the leader may read (page-locked: pin_range)
+        bool stable;       // NEO_HIP_GROUP_FRAME_STABLE: not written during a frame but by the members' own calls
     };
+    bool trust = false;  // this frame was read in place from a stable range: members commit without comparing
     std::vector<range> reg;
     float* in_pin = nullptr;          // mapped pinned [C][B]: the frame's input blocks
     float* out_pin = nullptr;         // mapped pinned [C][B]: the frame's output blocks
@@ -224,8 +226,10 @@ void unpin_range(uintptr_t lo, uintptr_t hi)
 // The leader's frame read in place: every live member's block (the leader's own io, the others'
 // buffers of the last frame) at p0 + slot * ld in ONE registered, device-mapped range, 16-byte
 // aligned. Then *in_dev / *ld describe it for the step kernel; false: the leader copies.
-bool inplace_frame(const group_t* g, const member& lead, const float* io, const float** in_dev, int64_t* ld)
+bool inplace_frame(const group_t* g, const member& lead, const float* io, const float** in_dev, int64_t* ld,
+                   bool* stable)
 {
+    *stable = false;
     const int C = int(g->slot_member.size());
     auto ptr = [&](int slot) {
         const member& y = g->m[size_t(g->slot_member[size_t(slot)])];
@@ -246,6 +250,7 @@ bool inplace_frame(const group_t* g, const member& lead, const float* io, const 
             if (!dev) return false;
             *in_dev = dev;
             *ld = d;
+            *stable = r.stable;
             return true;
         }
     return false;
@@ -398,7 +403,9 @@ int call_coalesced(group_t* g, int i, float* io)
         float* spec_in = g->in_pin + int64_t(x.slot) * g->B;
         float* out = g->out_pin + int64_t(x.slot) * g->B;
         NEO_GP_T(tc);
-        const bool differs = std::memcmp(io, spec_in, bb) != 0;
+        // a stable frame (the owner's promise, neo_hip_upols_group_register_ex): the block is the
+        // one the leader's step read in place, no snapshot to compare with
+        const bool differs = !g->trust && std::memcmp(io, spec_in, bb) != 0;
         NEO_GP_ADD(5, tc);
         if (differs) {  // the caller's block differs: this channel's step again
             neo_hip::device_guard dg(g->device);  // the commit path alone makes no HIP call
@@ -439,7 +446,9 @@ int call_coalesced(group_t* g, int i, float* io)
     // leader copies them first into the mapped staging the step reads
     const float* in_dev = g->in_dev;
     int64_t ld_in = g->B;
-    const bool inplace = inplace_frame(g, x, io, &in_dev, &ld_in);
+    bool stable = false;
+    const bool inplace = inplace_frame(g, x, io, &in_dev, &ld_in, &stable);
+    g->trust = inplace && stable;
     auto copy_in = [&] {
         for (const auto& y : g->m)
             if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
@@ -455,7 +464,7 @@ int call_coalesced(group_t* g, int i, float* io)
     int rc = neo_hip::launch_levels(sh, in_dev, ld_in, g->out_dev, g->B, g->stream);
     NEO_GP_ADD(2, t2);
     NEO_GP_T(t3);
-    if (inplace) copy_in();  // beside the step: both read the frame, which nothing writes during this call
+    if (inplace && !stable) copy_in();  // beside the step: both read the frame, which nothing writes during this call
     if (rc || (rc = neo_hip::spin_sync(g->stream))) return rc;
     NEO_GP_ADD(3, t3);
     g->step_n = sh->lv_n - 1;
@@ -620,18 +629,28 @@ NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int id)
     return NEO_HIP_OK;
 }
 
-NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void* ptr, int64_t bytes)
+NEO_HIP_API int neo_hip_upols_group_register_ex(neo_hip_upols_group* g, const void* ptr, int64_t bytes, int flags)
 {
     if (!g || !ptr || bytes <= 0) return fail(NEO_HIP_EINVAL, "null group or empty range");
+    if (flags & ~NEO_HIP_GROUP_FRAME_STABLE) return fail(NEO_HIP_EINVAL, "unknown group register flags %d", flags);
     std::lock_guard<std::mutex> lk(g->mu);
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + uint64_t(bytes);
-    for (const auto& r : g->reg)
-        if (r.lo == lo && r.hi == hi) return NEO_HIP_OK;  // already registered (a per-frame call is cheap)
+    const bool stable = (flags & NEO_HIP_GROUP_FRAME_STABLE) != 0;
+    for (auto& r : g->reg)
+        if (r.lo == lo && r.hi == hi) {  // already registered (a per-frame call is cheap): the flags may change
+            r.stable = stable;
+            return NEO_HIP_OK;
+        }
     neo_hip::device_guard dg(g->device);
     if (dg.rc) return dg.rc;
     pin_range(lo, hi);
-    g->reg.push_back({lo, hi});
+    g->reg.push_back({lo, hi, stable});
     return NEO_HIP_OK;
+}
+
+NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void* ptr, int64_t bytes)
+{
+    return neo_hip_upols_group_register_ex(g, ptr, bytes, 0);
 }
 
 NEO_HIP_API int neo_hip_upols_group_unregister(neo_hip_upols_group* g, const void* ptr)

@@ -26,6 +26,10 @@ constexpr int kBigT = 128;   // big Toeplitz level: window, band [2 kBigT, P) in
 constexpr int kFarT = 128;   // far level: blocks per window (256-point partition-axis transform)
 constexpr int kFarA = 256;   // far level: first partition (2 kFarT)
 constexpr int kFarRing = 2 * kFarA;  // far level: FDL ring rows needed (a slice reads back 383 blocks)
+// offline windows (k_off_mac): batched calls of >= 128 blocks take windows of kFarT blocks through
+// partition-axis transforms of every 128-partition segment, from this many partitions
+constexpr int kOffMinP = 128;
+constexpr int kOffMaxWP = 2;  // windows per pass
 
 // Latency mode (neo_hip_upols_set_persistent, upols_levels.hip): one persistent kernel per handle
 // polls a mailbox in mapped host memory. Step n's record (device addresses of its input and
@@ -210,6 +214,13 @@ struct neo_hip_upols {
     bool bg_busy = false;  // slices enqueued on bg since the last join
     int64_t bg_launches = 0;
     float* tail = nullptr;  // batched OLA tails [C][T][B]
+    // offline windows (k_off_mac, launch_offline): batched calls take 128 or 256 blocks per pass
+    bool off = false;                // eligible (P >= kOffMinP, whole-block handles) and on (neo_hip_upols_set_offline)
+    int off_nseg = 0;                // 128-partition segments from p = 0
+    neo_hip::cf* off_hf = nullptr;   // the filter's segment spectra [C][off_nseg][256][B]
+    bool off_dirty = true;           // off_hf to recompute (filter changed)
+    neo_hip::cf* off_y = nullptr;    // a pass's output spectra [C][128 kOffMaxWP][B]
+    float* off_tail = nullptr;       // OLA: a pass's tails [C][128 kOffMaxWP][B]
     float* samples_dev = nullptr;   // process_samples host staging (device side)
     float* samples_host = nullptr;  // process_samples host staging (pinned)
     size_t samples_cap = 0;
@@ -374,6 +385,12 @@ const char* persist_ineligible(const upols_t* h);
 int lvl_join(upols_t* h, hipStream_t s);
 void lvl_free(upols_t* h);
 void lvl_filter_changed(upols_t* h);
+// offline windows: the segment spectra (if the filter changed) and k_off_mac for wp windows of
+// 128 blocks at h->wpos into h->off_y (buffers allocated by the caller, launch_offline)
+int launch_off_mac(upols_t* h, int wp, hipStream_t s);
+// upols_batch.hip: wp windows of 128 blocks of every channel in one pass (window r2c of every
+// block, k_off_mac, per-block finish), h->wpos advanced
+int launch_offline(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int wp, hipStream_t s);
 // a setup call's last step (set_filter, set_impulse, reset; FDL just zeroed): the level buffers,
 // the far segment spectra and window 0 of every level, on h->stream, so the next call is an
 // ordinary streaming step (no-op without levels and for group handles)

@@ -1239,6 +1239,112 @@ __device__ __forceinline__ void far2r_role(const slice_args& sa, int bid, char* 
         buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
 }
 
+// ---------------------------------------------------------------------------------------
+// Offline windows (process calls with batching on: every block of the call is known up front,
+// dense_convolve / the plugin's offline harness, DenseConvolution.hpp:39-70). The far level's
+// decomposition applied to EVERY partition: per bin, Y[t_W + j] (j < 128) = sum over segments
+// q >= 0 of 128 partitions of samples 128 + j of IDFT256(DFT256(X pair) . DFT256(h_q)), the pair
+// being FDL rows t_W - 128 (q + 1) ... + 255 -- for q = 0 it holds the window's own rows, which
+// k_batch_window inserted before this launch. One workgroup per 16-column unit walks the
+// segments from q = 0 back (each pair's second half is the previous pair's first half: every
+// FDL row of the band read once per pass), multiplies with the filter's segment spectra
+// (k_lvf_filter from partition 0, computed at the first pass after a filter change) and
+// inverse-transforms once per window. WP = 2 windows per pass share every spectrum load: pair
+// q of the first window is pair q + 1 of the second (rows t_W + 128 - 128 (q + 2) ...), so the
+// second window's products reuse the previous segment's transform with this segment's spectrum.
+// Per column and pass: (nseg + WP) 128 FDL rows, nseg 256 spectrum rows, WP 128 output rows,
+// against 2 P rows for the batched MAC's 32 blocks; nseg + WP forward and WP inverse
+// transforms instead of 128 WP P complex MACs.
+struct off_args {
+    const cf* fdl;
+    const cf* hf;  // [C][nseg][256][B]
+    const cf* twf;
+    cf* y;         // [C][128 WP][B]: the windows' output spectra
+    int64_t cstride, pstride;
+    int ring, B, nseg, w;  // w: ring row of the pass's first block
+};
+
+template<int WP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WP == 1 ? 3 : 2))) void k_off_mac(off_args sa)
+{
+    __shared__ cf lds[16 * 16 * 16];  // col_fft transposes
+    __shared__ cf z[kFN];              // bin-0 exchange
+    __shared__ cf tws[kFN];
+    __shared__ cf xh[8 * 256];         // raw rows of the pair before, first half (this pair's second half)
+    const int t = threadIdx.x, a = t >> 4, cp = t & 15;
+    const int gpc = sa.B / 16, u = blockIdx.x, c = u / gpc, g = u - c * gpc, k = g * 16 + cp;
+    const bool unit0 = g == 0;  // uniform per workgroup: the unit holding packed bin 0
+    const int64_t fs = sa.B;
+    const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));
+    tws[t] = sa.twf[t];
+    const __amdgpu_buffer_rsrc_t fres =
+        buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * sa.nseg * kFN * fs, int64_t(sa.nseg) * spec);
+    const int ps8 = int(sa.pstride * int(sizeof(cf))), ko = k * int(sizeof(cf));
+    const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
+    auto z0 = [&](int i) { return unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0; };
+    auto row = [&](int r) { return r >= sa.ring ? r - sa.ring : r; };
+    f2v acc[WP][16];
+#pragma unroll
+    for (int w = 0; w < WP; ++w)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[w][i] = f2v(0.f);
+    // the first pair: rows w + 128 (WP - 2) + r, r < 256 (WP = 1: w - 128; WP = 2: w, the second
+    // window's pair of segment 0); its row a + 16 n
+    int r0 = (sa.w + kFarT * (WP - 2) + a) % sa.ring;
+    r0 = r0 < 0 ? r0 + sa.ring : r0;
+    cf xp[WP > 1 ? 16 : 1];  // WP = 2: the previous pair's spectrum (the second window's segment q)
+    __syncthreads();         // twiddles
+    for (int q = 1 - WP; q < sa.nseg; ++q) {  // uniform per workgroup; q < 0: the second window's pair only
+        cf x[16], hv[16];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) x[n] = buf_ld(fres, row(r0 + 16 * n) * ps8 + ko, 0);
+        if (q == 1 - WP) {
+#pragma unroll
+            for (int n = 8; n < 16; ++n) x[n] = buf_ld(fres, row(r0 + 16 * n) * ps8 + ko, 0);
+        } else {
+#pragma unroll
+            for (int n = 8; n < 16; ++n) x[n] = xh[(n - 8) * 256 + t];  // this lane's own stores
+        }
+        if (q >= 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) hv[i] = buf_ld(hres, vo, q * spec + int(16 * i * fs * int(sizeof(cf))));
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) xh[n * 256 + t] = x[n];
+        r0 = r0 - kFarT < 0 ? r0 - kFarT + sa.ring : r0 - kFarT;
+        col_fft<-1, 16>(x, lds, tws, a, cp, true);
+        if (unit0) bin0_exchange<true>(x, z, a, cp);  // uniform per workgroup; the next col_fft's barriers order z
+        if (q >= 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const pk_coef h(hv[i], z0(i));
+                h.mac(acc[0][i], x[i]);
+                if constexpr (WP > 1) h.mac(acc[1][i], xp[i]);
+            }
+        }
+        if constexpr (WP > 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) xp[i] = x[i];
+        }
+    }
+    constexpr float sc = 1.0f / kFN;
+#pragma unroll
+    for (int w = 0; w < WP; ++w) {
+        cf v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = cf{acc[w][i].x, acc[w][i].y};
+        __syncthreads();  // the last pack exchange's (or the previous window's) reads of z / lds are done
+        if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
+        col_fft<1, 16>(v, lds, tws, a, cp, true);
+        const __amdgpu_buffer_rsrc_t ores =
+            buf_rsrc(sa.y + (int64_t(c) * WP + w) * kFarT * fs, int64_t(kFarT) * fs * int(sizeof(cf)));
+#pragma unroll
+        for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128: block n - 128 of window w
+            buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
+    }
+}
+
 #ifndef NEO_ROLES
 #define NEO_ROLES 63  // diagnostic builds (tools/build_roles.sh): 1 block, 2 Toeplitz T <= 16, 4 T = 32, 8 far 1, 16 far 2a, 32 far 2b
 #endif
@@ -1473,11 +1579,12 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
 }
 
 // Segment spectra (grid C x NSEG x B/16): hf[c][s][f][k] = DFT256 over r < 128 of
-// H[c][128 (s + 2) + r][k] (zero past P); packed bin 0 (two real sequences, DC and Nyquist)
-// in the real-FFT packing of far_role (pack_bin0).
+// H[c][128 (s + seg0) + r][k] (zero past P); packed bin 0 (two real sequences, DC and Nyquist)
+// in the real-FFT packing of far_role (pack_bin0). seg0 = 2: the far level's segments (p >=
+// 256); 0: every segment (offline windows, k_off_mac).
 __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf* __restrict__ hf,
                                                     const cf* __restrict__ twg, int B, int P, int nseg,
-                                                    int64_t cstride, int64_t pstride)
+                                                    int64_t cstride, int64_t pstride, int seg0)
 {
     __shared__ cf lds[16 * 16 * 16];
     __shared__ cf z[kFN];
@@ -1490,7 +1597,7 @@ __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf
     cf v[16];
 #pragma unroll
     for (int n2 = 0; n2 < 16; ++n2) {
-        const int r = a + 16 * n2, p = (s + 2) * kFarT + r;
+        const int r = a + 16 * n2, p = (s + seg0) * kFarT + r;
         v[n2] = (r < kFarT && p < P) ? H[int64_t(c) * cstride + int64_t(p) * pstride + k] : cf{0.f, 0.f};
     }
     col_fft<-1, 16>(v, lds, tw, a, cp, true);
@@ -1675,9 +1782,11 @@ void lvl_free(upols_t* h)
 }
 
 // the filter changed: the far segment spectra are recomputed before the next streaming step
+// (and the offline windows' before the next offline pass)
 void lvl_filter_changed(upols_t* h)
 {
     h->fv_dirty = true;
+    h->off_dirty = true;
     h->lv_n = -1;
 }
 
@@ -2239,7 +2348,7 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     if (lp.nseg && h->fv_dirty && !h->far_raw) {
         const unsigned grid = unsigned(C) * unsigned(lp.nseg) * unsigned(B / 16);
         hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->fv_hf, h->fv_tw, B, h->P, lp.nseg,
-                           h->cstride, h->pstride);
+                           h->cstride, h->pstride, kFarA / kFarT);
         NEO_HIP_LAUNCH_CHECK();
         h->fv_dirty = false;
     }
@@ -2419,6 +2528,25 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     if ((rc = timing_mark(ev, 1, s))) return rc;
     h->wpos = h->wpos + 1 >= h->ring ? 0 : h->wpos + 1;
     h->lv_n = n + 1;
+    return NEO_HIP_OK;
+}
+
+int launch_off_mac(upols_t* h, int wp, hipStream_t s)
+{
+    if (!h->fv_tw)
+        if (int rc = shared_far_tw(&h->fv_tw)) return rc;
+    if (h->off_dirty) {
+        const unsigned grid = unsigned(h->C) * unsigned(h->off_nseg) * unsigned(h->B / 16);
+        hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->off_hf, h->fv_tw, h->B, h->P,
+                           h->off_nseg, h->cstride, h->pstride, 0);
+        NEO_HIP_LAUNCH_CHECK();
+        h->off_dirty = false;
+    }
+    off_args a{h->fdl, h->off_hf, h->fv_tw, h->off_y, h->cstride, h->pstride, h->ring, h->B, h->off_nseg, h->wpos};
+    const unsigned grid = unsigned(h->C) * unsigned(h->B / 16);
+    if (wp == 2) hipLaunchKernelGGL(k_off_mac<2>, dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_off_mac<1>, dim3(grid), dim3(256), 0, s, a);
+    NEO_HIP_LAUNCH_CHECK();
     return NEO_HIP_OK;
 }
 

@@ -60,6 +60,8 @@ SIGNATURES = {
     "neo_hip_upols_process_blocks": (_i, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "neo_hip_upols_reset": (_i, [_vp]),
     "neo_hip_upols_set_ahead": (_i, [_vp, _i]),
+    "neo_hip_upols_set_offline": (_i, [_vp, _i]),
+    "neo_hip_upols_get_offline": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "neo_hip_upols_get_ahead": (_i, [_vp] + [ctypes.POINTER(_i)] * 4),
     "neo_hip_upols_set_timing": (_i, [_vp, _i]),
     "neo_hip_upols_timing": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
@@ -100,6 +102,7 @@ SIGNATURES = {
     "neo_hip_upols_group_reset": (_i, [_vp, _i]),
     "neo_hip_upols_group_stats": (_i, [_vp, ctypes.POINTER(_i)] + [ctypes.POINTER(_i64)] * 4),
     "neo_hip_upols_group_register": (_i, [_vp, _vp, _i64]),
+    "neo_hip_upols_group_register_ex": (_i, [_vp, _vp, _i64, _i]),
     "neo_hip_upols_group_unregister": (_i, [_vp, _vp]),
     "neo_hip_num_partitions": (_i, [_i64, _i, ctypes.POINTER(_i64)]),
     "neo_hip_uniform_partition": (_i, [_vp, _i, _i64, _i, _vp, _i, _i]),

@@ -335,6 +335,17 @@ class UpolsConvolver:
         _native.check(_native.load().neo_hip_upols_batch_info(self._h, ctypes.byref(t), ctypes.byref(s)))
         return t.value, s.value
 
+    def set_offline(self, enable: bool) -> None:
+        """Offline windows for batched calls of >= 128 blocks (neo_hip_upols_set_offline; on by
+        default from 128 partitions): 128-block windows through partition-axis transforms."""
+        _native.check(_native.load().neo_hip_upols_set_offline(self._h, int(bool(enable))))
+
+    def offline_info(self):
+        """(offline windows on, 128-partition segments they transform)"""
+        e, n = ctypes.c_int(), ctypes.c_int()
+        _native.check(_native.load().neo_hip_upols_get_offline(self._h, ctypes.byref(e), ctypes.byref(n)))
+        return bool(e.value), n.value
+
     def set_ahead(self, enable: bool) -> None:
         """Streaming levels for single-block steps (neo_hip_upols_set_ahead)."""
         _native.check(_native.load().neo_hip_upols_set_ahead(self._h, int(bool(enable))))
@@ -685,14 +696,17 @@ class UpolsGroup:
     def reset(self, member: int) -> None:
         _native.check(_native.load().neo_hip_upols_group_reset(self._h, int(member)))
 
-    def register(self, buffer: np.ndarray) -> None:
-        """the group may read `buffer` (host memory the caller keeps alive until unregister)"""
+    def register(self, buffer: np.ndarray, frame_stable: bool = False) -> None:
+        """the group may read `buffer` (host memory the caller keeps alive until unregister).
+        frame_stable: the caller also promises that during a frame nothing but the members' own
+        calls writes it (neo_hip_upols_group_register_ex, NEO_HIP_GROUP_FRAME_STABLE): members then
+        commit without comparing their blocks with a snapshot."""
         if not isinstance(buffer, np.ndarray) or not buffer.flags.c_contiguous:
             raise TypeError("register takes a C-contiguous numpy array")
         self._keep = getattr(self, "_keep", {})
         self._keep[buffer.ctypes.data] = buffer  # keeps the registered array alive on the Python side too
-        _native.check(_native.load().neo_hip_upols_group_register(self._h, ctypes.c_void_p(buffer.ctypes.data),
-                                                                  int(buffer.nbytes)))
+        _native.check(_native.load().neo_hip_upols_group_register_ex(self._h, ctypes.c_void_p(buffer.ctypes.data),
+                                                                     int(buffer.nbytes), 1 if frame_stable else 0))
 
     def unregister(self, buffer=None) -> None:
         """stop reading `buffer` (None: every registered range)"""
@@ -796,7 +810,7 @@ def dense_convolve(signal, impulse_response, block_size: int, device: int = 0, m
     # whole signal in chunks of <= 2^26 samples: one upload, batched passes (T blocks per
     # pass over filter + FDL), one download per chunk; the tail block is zero-padded
     chunk = max(1, (1 << 26) // (C * block_size))
-    chunk = chunk // 32 * 32 or chunk
+    chunk = max(256, chunk // 256 * 256)  # whole offline passes (256 blocks: two windows of 128)
     out = np.empty_like(sig)
     for t0 in range(0, nb, chunk):
         t1 = min(nb, t0 + chunk)

@@ -275,3 +275,35 @@ def test_group_large_frame_in_place(neo_gpu, oracle):
         assert err.max() <= 1e-5, (f, int(err.argmax()), float(err.max()))
     st = g.stats()
     assert st["coalesced"] and st["frame_steps"] == nf - 3 and st["redos"] == len(late) * (nf - 8), st
+
+
+@pytest.mark.parametrize("C", [16, 520])
+def test_group_frame_stable_in_place(neo_gpu, oracle, C):
+    """The owner's frame-stable promise (register(frame, frame_stable=True):
+    NEO_HIP_GROUP_FRAME_STABLE): a coalesced frame read in place takes no snapshot and the members
+    commit without comparing, so the outputs come from the blocks the frame held at the leader's
+    call -- equal to one C-channel handle over the same blocks (to float rounding after the group
+    re-primes), never a redo. Switching the flag off again restores the exact comparison: a member
+    whose block changes after the leader's call is re-stepped and still matches."""
+    B, L, nf = 512, 512 * 100, 16
+    g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 2100 + C)
+    frame = np.zeros((C, B), np.float32)
+    g.register(frame, frame_stable=True)
+    x = np.stack([oracle.noise(2200 + c, B * nf) for c in range(C)])
+    late = (3, C - 1)
+    for f in range(nf):
+        if f == 11:
+            g.register(frame, frame_stable=False)  # the same range again: the flag is updated
+        blk = np.ascontiguousarray(x[:, f * B:(f + 1) * B])
+        expect = ref(blk.copy())
+        frame[:] = blk
+        if f >= 12:  # not stable any more: these blocks change after the leader's call
+            frame[list(late)] = 0.0
+        for c in range(C):
+            if f >= 12 and c in late:
+                frame[c] = blk[c]
+            g(ids[c], frame[c])
+        err = np.abs(frame - expect).max(axis=1) / np.maximum(np.abs(expect).max(axis=1), 1e-3)
+        assert err.max() <= 1e-5, (f, int(err.argmax()), float(err.max()))
+    st = g.stats()
+    assert st["coalesced"] and st["frame_steps"] == nf - 3 and st["redos"] == len(late) * (nf - 12), st

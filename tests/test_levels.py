@@ -520,3 +520,73 @@ def test_part_plan_valid_and_balanced(C, B, P, G):
         assert 0.99 <= min(w5) and max(w5) <= 1.01, (min(w5), max(w5))
         u = np.array(neo.convolution.part_plan(C, B, P, G, uniform=True)["loads"])
         assert u.min() < 0.1 * u.mean()  # the plan before: empty groups
+
+
+def _offline_replay(H, X, R, wp, w0, ring0):
+    """float64 replay of the offline windows (launch_offline + k_off_mac): the FDL ring of R rows
+    holds history (ring0, next write position w0); each pass inserts 128 wp rows at w, then per window walks the pairs from the
+    newest back (pair i = rows w + 128 (wp - 2) - 128 i ... + 255 mod R, i = 0 .. nseg + wp - 2),
+    each pair's second half being the previous pair's first half, multiplies segment q's spectrum
+    with the pair of window j's segment q (pair index q + wp - 1 - j), and keeps samples 128..255
+    of one inverse transform per window."""
+    P, K = H.shape
+    nseg = -(-P // FT)
+    Hp = np.zeros((nseg * FT, K), complex)
+    Hp[:P] = H
+    HF = [np.fft.fft(np.concatenate([Hp[q * FT:(q + 1) * FT], np.zeros((FT, K))]), axis=0) for q in range(nseg)]
+    ring = ring0.copy()
+    w = w0
+    out = []
+    t = 0
+    nb = X.shape[0]
+    while t + FT * wp <= nb:
+        for j in range(FT * wp):  # k_batch_window: rows w .. w + 128 wp - 1
+            ring[(w + j) % R] = X[t + j]
+        acc = [np.zeros((FN, K), complex) for _ in range(wp)]
+        half = None
+        for i in range(nseg + wp - 1):
+            start = w + FT * (wp - 2) - FT * i
+            rows = np.array([(start + r) % R for r in range(FN)])
+            pair = ring[rows].copy()
+            if half is not None:
+                assert np.array_equal(pair[FT:], half)  # the previous pair's first half
+            half = pair[:FT].copy()
+            XF = np.fft.fft(pair, axis=0)
+            for jw in range(wp):
+                q = i - (wp - 1 - jw)
+                if 0 <= q < nseg:
+                    acc[jw] += XF * HF[q]
+        for jw in range(wp):
+            out.append(np.fft.ifft(acc[jw], axis=0)[FT:])
+        w = (w + FT * wp) % R
+        t += FT * wp
+    return np.concatenate(out) if out else np.zeros((0, K))
+
+
+@pytest.mark.parametrize("P,wp", [(128, 1), (129, 2), (300, 2), (300, 1), (700, 2), (938, 2), (1000, 1)])
+def test_offline_windows_match_direct(P, wp):
+    """The offline windows' decomposition and ring arithmetic (upols_levels.hip k_off_mac,
+    upols_batch.hip launch_offline; ring of 128 (nseg + 2) rows, upols.hip create): random
+    spectra with history before the first pass, several passes wrapping the ring, against the
+    direct block-axis convolution Y[t] = sum_p H[p] X[t - p] (uniform_partitioned_convolver.hpp:47-65,
+    fdl_index.hpp:23-36)."""
+    rng = np.random.default_rng(P + wp)
+    K = 3
+    nseg = -(-P // FT)
+    R = max(P + 31, FT * (nseg + 2))
+    H = rng.standard_normal((P, K)) + 1j * rng.standard_normal((P, K))
+    hist = R - FT * 2  # blocks before the first pass (already in the ring)
+    nb = FT * wp * 5
+    Xall = rng.standard_normal((hist + nb, K)) + 1j * rng.standard_normal((hist + nb, K))
+    # direct reference over the whole history
+    Y = np.zeros((hist + nb, K), complex)
+    for t in range(hist + nb):
+        p = np.arange(min(P, t + 1))
+        Y[t] = (H[p] * Xall[t - p]).sum(0)
+    # the ring after `hist` single steps from write position 0: row t mod R holds block t
+    w0 = hist % R
+    ring_hist = np.zeros((R, K), complex)
+    for t in range(hist):
+        ring_hist[t % R] = Xall[t]
+    got = _offline_replay(H, Xall[hist:], R, wp, w0, ring_hist)
+    np.testing.assert_allclose(got, Y[hist:hist + got.shape[0]], rtol=0, atol=1e-9 * np.abs(Y).max())

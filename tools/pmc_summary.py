@@ -87,7 +87,8 @@ def main():
             summarize(tag, w, "k_lvl_step", r["algorithmic_bytes_per_launch"], w)
         summarize(tag, w, "k_upols_step", b["per_block_step"]["algorithmic_bytes_per_launch"], w + "_plain")
         if b.get("offline"):
-            summarize(tag, w, "k_batch_mac", b["offline"]["algorithmic_bytes_per_launch"], w + "_offline")
+            o = b["offline"]
+            summarize(tag, w, o["kernel"].split("<")[0], o["algorithmic_bytes_per_launch"], w + "_offline")
     if not os.path.exists(os.path.join(OUT, f"pmc_c2_FETCH_SIZE_{tag}")):
         return
     b = bench_line(tag, "c2")
