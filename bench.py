@@ -462,7 +462,7 @@ def host_io_times(conv, C, B, nblocks, kind, seed=0):
     return dt
 
 
-def group_frames(C, frames, B, L, stable=False):
+def group_frames(C, frames, B, L, mode=0):
     """tests/cpp/bench_group (C++, NEO_HIP_CONVOLVER_GROUPS): the plugin's processFrame over C
     single-channel convolvers of one owner-registered frame buffer (one launch per frame once
     coalesced), and the dense_convolve<Convolver> harness pattern (one shared scratch block: one
@@ -474,7 +474,7 @@ def group_frames(C, frames, B, L, stable=False):
     exe = os.path.join(cpp, "bin", "bench_group")
     try:
         subprocess.run(["make", "-s", "-C", cpp, "bin/bench_group"], check=True, capture_output=True, timeout=300)
-        r = subprocess.run([exe, str(C), str(frames), str(B), str(L), "1" if stable else "0"], capture_output=True,
+        r = subprocess.run([exe, str(C), str(frames), str(B), str(L), str(mode)], capture_output=True,
                            text=True, timeout=600)
         d = json.loads(r.stdout.strip().splitlines()[-1])
     except (OSError, subprocess.SubprocessError, ValueError, IndexError) as e:
@@ -865,11 +865,12 @@ def run_upols(args, world, rank, local):
         del c5
         torch.cuda.empty_cache()
         # the plugin's std::vector<upols_convolver> (group-backed alias, C++) at 256 and 2048 channels
-        # (frame buffer registered plainly: exact snapshot comparison per member; and with the owner's
-        # frame-stable promise, NEO_HIP_GROUP_FRAME_STABLE: no snapshot, no comparison)
+        # (frame buffer registered plainly: exact snapshot comparison per member; with the owner's
+        # frame-stable promise, NEO_HIP_GROUP_FRAME_STABLE: no snapshot, no comparison; in place,
+        # NEO_HIP_GROUP_FRAME_INPLACE: every output written into the frame by its first call)
         for cs_, nf_ in ((256, 64), (2048, 32)):
-            host_io[f"group_{cs_}"] = group_frames(cs_, nf_, B, L)
-            host_io[f"group_{cs_}_stable"] = group_frames(cs_, nf_, B, L, stable=True)
+            for sfx, mode in (("", 0), ("_stable", 1), ("_inplace", 2)):
+                host_io[f"group_{cs_}{sfx}"] = group_frames(cs_, nf_, B, L, mode)
         # the plugin's processing class (stereo split_upols_convolver, 10 s IR), both modes
         for lat in (False, True):
             host_io["plugin_stereo" + ("_latency" if lat else "")] = plugin_frames(2, 400, B, L, lat)

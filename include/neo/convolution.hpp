@@ -209,6 +209,9 @@ struct upols_multichannel {
     auto paced(bool on) -> void { neo::hip::check(neo_hip_upols_set_paced(_h.get(), on ? 1 : 0)); }
     /// the same with the group's background launch in two pieces (two cross-stream waits per group)
     auto paced_two_pieces() -> void { neo::hip::check(neo_hip_upols_set_paced(_h.get(), 2)); }
+    /// offline windows for batched calls of >= 128 blocks (on by default from 128 partitions;
+    /// neo_hip_upols_set_offline): 128-block windows through partition-axis transforms
+    auto offline(bool on) -> void { neo::hip::check(neo_hip_upols_set_offline(_h.get(), on ? 1 : 0)); }
 
     [[nodiscard]] auto channels() const noexcept { return _C; }
     [[nodiscard]] auto block_size() const noexcept { return _B; }
@@ -405,14 +408,20 @@ public:
     };
     [[nodiscard]] auto scope() -> scope_guard { return scope_guard{*this}; }
 
-    /// [ptr, ptr + samples) stays allocated until unregister_all() (cheap to repeat per frame).
-    /// frame_stable: nothing but the convolvers' own calls writes it during a frame (the plugin's
-    /// loop over a filled frame): their calls then skip the exact snapshot comparison
-    /// (neo_hip_upols_group_register_ex, NEO_HIP_GROUP_FRAME_STABLE)
-    auto register_buffer(float const* ptr, std::size_t samples, bool frame_stable = false) -> void
+    /// what the owner promises about a registered frame buffer (neo_hip_upols_group_register_ex)
+    enum class frame : int {
+        plain = 0,                           ///< allocated until unregister_all(): exact comparison per member
+        stable = NEO_HIP_GROUP_FRAME_STABLE,  ///< + written by nothing but the convolvers' calls during a frame
+        in_place = NEO_HIP_GROUP_FRAME_STABLE | NEO_HIP_GROUP_FRAME_INPLACE,  ///< + read only through them, each
+                                                                              ///< on the same block: outputs in place
+    };
+    /// [ptr, ptr + samples) stays allocated until unregister_all() (cheap to repeat per frame), with
+    /// the owner's promise about it during a frame (the plugin's loop over a filled frame keeps
+    /// frame::in_place; frame::stable skips the members' snapshot comparison)
+    auto register_buffer(float const* ptr, std::size_t samples, frame promise = frame::plain) -> void
     {
         std::lock_guard<std::mutex> lk{_mu};
-        auto const flags = frame_stable ? NEO_HIP_GROUP_FRAME_STABLE : 0;
+        auto const flags = int(promise);
         bool found = false;
         for (auto& r : _ranges)
             if (r.ptr == ptr && r.samples == samples) {

@@ -328,6 +328,13 @@ NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void*
  * (register) each member's block is compared exactly and re-stepped on a difference. Registering the
  * same range again updates its flags. */
 #define NEO_HIP_GROUP_FRAME_STABLE 1
+/* NEO_HIP_GROUP_FRAME_INPLACE (implies STABLE): the owner also reads or writes a member's block only
+ * through that member's call, every member on the same block of the range every frame -- exactly
+ * processFrame's loop. The frame's first call then writes EVERY member's output into its block in
+ * place, and a later member's call has nothing left to do. A member called on another buffer is
+ * still stepped exactly (its own block step again), but its speculative output was written to its
+ * old block: that is the promise the flag makes. */
+#define NEO_HIP_GROUP_FRAME_INPLACE 2
 NEO_HIP_API int neo_hip_upols_group_register_ex(neo_hip_upols_group* g, const void* ptr, int64_t bytes, int flags);
 NEO_HIP_API int neo_hip_upols_group_unregister(neo_hip_upols_group* g, const void* ptr);
 /* coalesced now; one-launch frame steps, member calls, block re-runs, mode switches so far */

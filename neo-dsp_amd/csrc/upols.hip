@@ -759,6 +759,13 @@ int process_samples(upols_t* h, const float* in, int64_t ld_in, float* out, int6
 }  // namespace
 
 
+// The offline windows' ring, 128 (nseg + 2) rows, is a multiple of 256 rows: a channel stride of
+// 5 x 2^20 bytes at B = 512 made the streaming step 4 % slower at c5full (same-box A/B: 9.29-9.49
+// vs 9.68-9.74 Gsamples/s at 20 steps, as with the ring of P + 31 rows); one more row keeps it odd
+// and restores it (9.58-9.83). profiles/r6_ab_ring.json
+#ifndef NEO_OFF_RING_PAD
+#define NEO_OFF_RING_PAD 1  // diagnostic builds (A/B): 0 = the even ring
+#endif
 namespace {
 int create_convolver(int channels, int block, int partitions, int device, bool ola, bool v2,
                      const neo_hip_upols_opts* opt, neo_hip_upols** out, hipStream_t borrow = nullptr)
@@ -804,7 +811,7 @@ int create_convolver(int channels, int block, int partitions, int device, bool o
     // writing rows t_W .. t_W + 128 wp - 1
     h->off = !v2 && partitions >= kOffMinP;
     h->off_nseg = (partitions + kFarT - 1) / kFarT;
-    if (h->off) h->ring = std::max(h->ring, kFarT * (h->off_nseg + kOffMaxWP));
+    if (h->off) h->ring = std::max(h->ring, kFarT * (h->off_nseg + kOffMaxWP) + NEO_OFF_RING_PAD);
     h->ola = ola || v2;
     h->v2 = v2;
     h->fused = 2.0 * 8.0 * double(channels) * double(partitions) * double(block) < double(kFusedMaxBytes);

@@ -100,9 +100,12 @@ struct neo_hip_upols_group {
     std::vector<int> slot_member;     // shared handle channel -> member
     struct range {
         uintptr_t lo, hi;  // owner-registered host range [lo, hi) the leader may read (page-locked: pin_range)
-        bool stable;       // NEO_HIP_GROUP_FRAME_STABLE: not written during a frame but by the members' own calls
+        int flags;         // NEO_HIP_GROUP_FRAME_STABLE: not written during a frame but by the members' own calls;
+                           // NEO_HIP_GROUP_FRAME_INPLACE: also read by the owner only through them, each member on
+                           // the same block every frame (the step writes every output in place)
     };
-    bool trust = false;  // this frame was read in place from a stable range: members commit without comparing
+    bool trust = false;        // this frame was read in place from a stable range: members commit without comparing
+    bool out_inplace = false;  // and its outputs were written in place (FRAME_INPLACE): members have nothing to copy
     std::vector<range> reg;
     float* in_pin = nullptr;          // mapped pinned [C][B]: the frame's input blocks
     float* out_pin = nullptr;         // mapped pinned [C][B]: the frame's output blocks
@@ -227,9 +230,9 @@ void unpin_range(uintptr_t lo, uintptr_t hi)
 // buffers of the last frame) at p0 + slot * ld in ONE registered, device-mapped range, 16-byte
 // aligned. Then *in_dev / *ld describe it for the step kernel; false: the leader copies.
 bool inplace_frame(const group_t* g, const member& lead, const float* io, const float** in_dev, int64_t* ld,
-                   bool* stable)
+                   int* flags)
 {
-    *stable = false;
+    *flags = 0;
     const int C = int(g->slot_member.size());
     auto ptr = [&](int slot) {
         const member& y = g->m[size_t(g->slot_member[size_t(slot)])];
@@ -250,7 +253,7 @@ bool inplace_frame(const group_t* g, const member& lead, const float* io, const 
             if (!dev) return false;
             *in_dev = dev;
             *ld = d;
-            *stable = r.stable;
+            *flags = r.flags;
             return true;
         }
     return false;
@@ -399,13 +402,20 @@ int call_coalesced(group_t* g, int i, float* io)
     member& x = g->m[size_t(i)];
     neo_hip_upols* sh = g->shared;
     const size_t bb = size_t(g->B) * sizeof(float);
+    if (x.pending && g->out_inplace && io == x.io_last) {  // the step wrote this member's output in place
+        x.pending = false;
+        --g->npending;
+        return NEO_HIP_OK;
+    }
     if (x.pending) {
         float* spec_in = g->in_pin + int64_t(x.slot) * g->B;
         float* out = g->out_pin + int64_t(x.slot) * g->B;
         NEO_GP_T(tc);
         // a stable frame (the owner's promise, neo_hip_upols_group_register_ex): the block is the
         // one the leader's step read in place, no snapshot to compare with
-        const bool differs = !g->trust && std::memcmp(io, spec_in, bb) != 0;
+        // (FRAME_INPLACE with another buffer than the frame's: its block was never read, and the
+        // output went to the old one -- the owner broke the promise; this call is still exact)
+        const bool differs = g->out_inplace || (!g->trust && std::memcmp(io, spec_in, bb) != 0);
         NEO_GP_ADD(5, tc);
         if (differs) {  // the caller's block differs: this channel's step again
             neo_hip::device_guard dg(g->device);  // the commit path alone makes no HIP call
@@ -446,9 +456,14 @@ int call_coalesced(group_t* g, int i, float* io)
     // leader copies them first into the mapped staging the step reads
     const float* in_dev = g->in_dev;
     int64_t ld_in = g->B;
-    bool stable = false;
-    const bool inplace = inplace_frame(g, x, io, &in_dev, &ld_in, &stable);
-    g->trust = inplace && stable;
+    int rflags = 0;
+    const bool inplace = inplace_frame(g, x, io, &in_dev, &ld_in, &rflags);
+    const bool stable = inplace && (rflags & (NEO_HIP_GROUP_FRAME_STABLE | NEO_HIP_GROUP_FRAME_INPLACE));
+    g->trust = stable;
+    g->out_inplace = inplace && (rflags & NEO_HIP_GROUP_FRAME_INPLACE);
+    // FRAME_INPLACE: the step writes every member's output into its own block of the frame
+    float* out_dev = g->out_inplace ? const_cast<float*>(in_dev) : g->out_dev;
+    const int64_t ld_out = g->out_inplace ? ld_in : g->B;
     auto copy_in = [&] {
         for (const auto& y : g->m)
             if (y.live) std::memcpy(g->in_pin + int64_t(y.slot) * g->B, &y == &x ? io : y.io_last, bb);
@@ -461,7 +476,7 @@ int call_coalesced(group_t* g, int i, float* io)
     NEO_GP_ADD(1, t1);
     NEO_GP_T(t2);
     g->step_w = sh->wpos;
-    int rc = neo_hip::launch_levels(sh, in_dev, ld_in, g->out_dev, g->B, g->stream);
+    int rc = neo_hip::launch_levels(sh, in_dev, ld_in, out_dev, ld_out, g->stream);
     NEO_GP_ADD(2, t2);
     NEO_GP_T(t3);
     if (inplace && !stable) copy_in();  // beside the step: both read the frame, which nothing writes during this call
@@ -470,7 +485,7 @@ int call_coalesced(group_t* g, int i, float* io)
     g->step_n = sh->lv_n - 1;
     ++g->stat_steps;
     NEO_GP_T(t4);
-    std::memcpy(io, g->out_pin + int64_t(x.slot) * g->B, bb);
+    if (!g->out_inplace) std::memcpy(io, g->out_pin + int64_t(x.slot) * g->B, bb);
     NEO_GP_ADD(4, t4);
     prefetch_output(g, x.slot + 1);  // the next members' outputs, written over PCIe: not in any CPU cache
     prefetch_output(g, x.slot + 2);
@@ -632,19 +647,19 @@ NEO_HIP_API int neo_hip_upols_group_reset(neo_hip_upols_group* g, int id)
 NEO_HIP_API int neo_hip_upols_group_register_ex(neo_hip_upols_group* g, const void* ptr, int64_t bytes, int flags)
 {
     if (!g || !ptr || bytes <= 0) return fail(NEO_HIP_EINVAL, "null group or empty range");
-    if (flags & ~NEO_HIP_GROUP_FRAME_STABLE) return fail(NEO_HIP_EINVAL, "unknown group register flags %d", flags);
+    if (flags & ~(NEO_HIP_GROUP_FRAME_STABLE | NEO_HIP_GROUP_FRAME_INPLACE))
+        return fail(NEO_HIP_EINVAL, "unknown group register flags %d", flags);
     std::lock_guard<std::mutex> lk(g->mu);
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + uint64_t(bytes);
-    const bool stable = (flags & NEO_HIP_GROUP_FRAME_STABLE) != 0;
     for (auto& r : g->reg)
         if (r.lo == lo && r.hi == hi) {  // already registered (a per-frame call is cheap): the flags may change
-            r.stable = stable;
+            r.flags = flags;
             return NEO_HIP_OK;
         }
     neo_hip::device_guard dg(g->device);
     if (dg.rc) return dg.rc;
     pin_range(lo, hi);
-    g->reg.push_back({lo, hi, stable});
+    g->reg.push_back({lo, hi, flags});
     return NEO_HIP_OK;
 }
 

@@ -28,7 +28,10 @@ constexpr int kFarA = 256;   // far level: first partition (2 kFarT)
 constexpr int kFarRing = 2 * kFarA;  // far level: FDL ring rows needed (a slice reads back 383 blocks)
 // offline windows (k_off_mac): batched calls of >= 128 blocks take windows of kFarT blocks through
 // partition-axis transforms of every 128-partition segment, from this many partitions
-constexpr int kOffMinP = 128;
+#ifndef NEO_OFF_MIN_P
+#define NEO_OFF_MIN_P 128  // diagnostic builds (A/B)
+#endif
+constexpr int kOffMinP = NEO_OFF_MIN_P;
 constexpr int kOffMaxWP = 2;  // windows per pass
 
 // Latency mode (neo_hip_upols_set_persistent, upols_levels.hip): one persistent kernel per handle

@@ -1264,6 +1264,9 @@ struct off_args {
     int ring, B, nseg, w;  // w: ring row of the pass's first block
 };
 
+#ifndef NEO_OFF_PF
+#define NEO_OFF_PF 0  // diagnostic builds (A/B): k_off_mac's software prefetch depth
+#endif
 template<int WP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WP == 1 ? 3 : 2))) void k_off_mac(off_args sa)
 {
@@ -1294,25 +1297,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WP == 1 ? 3
     int r0 = (sa.w + kFarT * (WP - 2) + a) % sa.ring;
     r0 = r0 < 0 ? r0 + sa.ring : r0;
     cf xp[WP > 1 ? 16 : 1];  // WP = 2: the previous pair's spectrum (the second window's segment q)
-    __syncthreads();         // twiddles
+    // software prefetch (NEO_OFF_PF): 1 the next pair's new rows, 2 also the next segment's
+    // spectrum, loaded before this segment's transform so their latency hides behind it
+    cf nx[NEO_OFF_PF >= 1 ? 8 : 1], nh[NEO_OFF_PF >= 2 ? 16 : 1];
+    auto load_rows = [&](cf* dst, int n0, int n1) {
+#pragma unroll
+        for (int n = n0; n < n1; ++n) dst[n - n0] = buf_ld(fres, row(r0 + 16 * n) * ps8 + ko, 0);
+    };
+    auto load_spec = [&](cf* dst, int q) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dst[i] = buf_ld(hres, vo, q * spec + int(16 * i * fs * int(sizeof(cf))));
+    };
+    __syncthreads();  // twiddles
     for (int q = 1 - WP; q < sa.nseg; ++q) {  // uniform per workgroup; q < 0: the second window's pair only
         cf x[16], hv[16];
-#pragma unroll
-        for (int n = 0; n < 8; ++n) x[n] = buf_ld(fres, row(r0 + 16 * n) * ps8 + ko, 0);
         if (q == 1 - WP) {
-#pragma unroll
-            for (int n = 8; n < 16; ++n) x[n] = buf_ld(fres, row(r0 + 16 * n) * ps8 + ko, 0);
+            load_rows(x, 0, 16);
         } else {
+            if constexpr (NEO_OFF_PF >= 1) {
+#pragma unroll
+                for (int n = 0; n < 8; ++n) x[n] = nx[n];
+            } else {
+                load_rows(x, 0, 8);
+            }
 #pragma unroll
             for (int n = 8; n < 16; ++n) x[n] = xh[(n - 8) * 256 + t];  // this lane's own stores
         }
         if (q >= 0) {
+            if constexpr (NEO_OFF_PF >= 2) {
+                if (q == 0) load_spec(hv, 0);
+                else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) hv[i] = buf_ld(hres, vo, q * spec + int(16 * i * fs * int(sizeof(cf))));
+                    for (int i = 0; i < 16; ++i) hv[i] = nh[i];
+                }
+            } else {
+                load_spec(hv, q);
+            }
         }
 #pragma unroll
         for (int n = 0; n < 8; ++n) xh[n * 256 + t] = x[n];
         r0 = r0 - kFarT < 0 ? r0 - kFarT + sa.ring : r0 - kFarT;
+        if constexpr (NEO_OFF_PF >= 1)
+            if (q + 1 < sa.nseg) load_rows(nx, 0, 8);  // the next pair's first half
+        if constexpr (NEO_OFF_PF >= 2)
+            if (q + 1 < sa.nseg && q + 1 >= 1) load_spec(nh, q + 1);
         col_fft<-1, 16>(x, lds, tws, a, cp, true);
         if (unit0) bin0_exchange<true>(x, z, a, cp);  // uniform per workgroup; the next col_fft's barriers order z
         if (q >= 0) {

@@ -696,17 +696,20 @@ class UpolsGroup:
     def reset(self, member: int) -> None:
         _native.check(_native.load().neo_hip_upols_group_reset(self._h, int(member)))
 
-    def register(self, buffer: np.ndarray, frame_stable: bool = False) -> None:
+    def register(self, buffer: np.ndarray, frame_stable: bool = False, in_place: bool = False) -> None:
         """the group may read `buffer` (host memory the caller keeps alive until unregister).
         frame_stable: the caller also promises that during a frame nothing but the members' own
         calls writes it (neo_hip_upols_group_register_ex, NEO_HIP_GROUP_FRAME_STABLE): members then
-        commit without comparing their blocks with a snapshot."""
+        commit without comparing their blocks with a snapshot. in_place (NEO_HIP_GROUP_FRAME_INPLACE,
+        implies frame_stable): it also reads each member's block only through that member's call,
+        each member on the same block every frame: the frame's first call writes every output in place."""
         if not isinstance(buffer, np.ndarray) or not buffer.flags.c_contiguous:
             raise TypeError("register takes a C-contiguous numpy array")
         self._keep = getattr(self, "_keep", {})
         self._keep[buffer.ctypes.data] = buffer  # keeps the registered array alive on the Python side too
         _native.check(_native.load().neo_hip_upols_group_register_ex(self._h, ctypes.c_void_p(buffer.ctypes.data),
-                                                                     int(buffer.nbytes), 1 if frame_stable else 0))
+                                                                     int(buffer.nbytes),
+                                                                     3 if in_place else (1 if frame_stable else 0)))
 
     def unregister(self, buffer=None) -> None:
         """stop reading `buffer` (None: every registered range)"""

@@ -6,9 +6,11 @@
 // (DenseConvolution.hpp:56-67: one scratch block shared by every channel), which never coalesces:
 // one launch and one host wait per channel-block, after one frame that switches the group back to
 // a handle per member (switch_frame_us). Prints one JSON line (bench.py host_io.group_*).
-// stable = 1 registers the frame with NEO_HIP_GROUP_FRAME_STABLE (the owner's promise that only the
-// convolvers' calls write it during a frame): members commit without the snapshot comparison.
-//   bench_group <channels> <frames> [block] [taps] [stable]
+// mode = 1 registers the frame with NEO_HIP_GROUP_FRAME_STABLE (the owner's promise that only the
+// convolvers' calls write it during a frame): members commit without the snapshot comparison;
+// mode = 2 with NEO_HIP_GROUP_FRAME_INPLACE too (read only through the calls, each convolver on its
+// own channel): the frame's first call writes every output in place.
+//   bench_group <channels> <frames> [block] [taps] [mode]
 #define NEO_HIP_CONVOLVER_GROUPS 1
 #include <neo/convolution.hpp>
 
@@ -42,7 +44,8 @@ int main(int argc, char** argv)
     std::size_t const nf = argc > 2 ? std::size_t(std::atol(argv[2])) : 64;
     std::size_t const B = argc > 3 ? std::size_t(std::atol(argv[3])) : 512;
     std::size_t const L = argc > 4 ? std::size_t(std::atol(argv[4])) : 480000;
-    bool const stable = argc > 5 && std::atoi(argv[5]) != 0;
+    int const mode = argc > 5 ? std::atoi(argv[5]) : 0;
+    using promise = neo::convolution::convolver_group::frame;
     // one IR for every channel (the frame time does not depend on the filter's values)
     std::vector<float> ir(L);
     oracle_noise(77, ir.data(), L);
@@ -59,7 +62,8 @@ int main(int argc, char** argv)
     double const setup_s = std::chrono::duration<double>(clk::now() - t0).count();
     std::vector<float> src(C * B * 8), frame(C * B);
     oracle_noise(78, src.data(), src.size());
-    owner.register_buffer(frame.data(), frame.size(), stable);
+    owner.register_buffer(frame.data(), frame.size(),
+                          mode == 2 ? promise::in_place : (mode == 1 ? promise::stable : promise::plain));
     auto process_frame = [&](std::size_t f) {
         std::memcpy(frame.data(), src.data() + (f % 8) * C * B, C * B * sizeof(float));  // the host fills the frame
         auto const a = clk::now();
@@ -95,13 +99,13 @@ int main(int argc, char** argv)
     double cmean = 0;
     for (double v : ct) cmean += v;
     cmean /= double(ct.size());
-    std::printf("{\"channels\": %zu, \"block\": %zu, \"partitions\": %zu, \"frames\": %zu, \"frame_stable\": %d, \"coalesced\": %d, "
+    std::printf("{\"channels\": %zu, \"block\": %zu, \"partitions\": %zu, \"frames\": %zu, \"frame_mode\": %d, \"coalesced\": %d, "
                 "\"one_launch_frames\": %lld, \"redos\": %lld, \"frame_p50_us\": %.2f, \"frame_p99_us\": %.2f, "
                 "\"frame_mean_us\": %.2f, \"msamples_s\": %.2f, \"setup_s\": %.2f, "
                 "\"shared_scratch\": {\"channel_blocks\": %zu, \"per_channel_block_p50_us\": %.2f, "
                 "\"per_channel_block_mean_us\": %.2f, \"frame_us\": %.1f, \"msamples_s\": %.2f, "
                 "\"switch_frame_us\": %.1f}}\n",
-                C, B, P, nf, int(stable), coalesced, (long long)steps, (long long)redos, pct(ft, 50), pct(ft, 99), mean,
+                C, B, P, nf, mode, coalesced, (long long)steps, (long long)redos, pct(ft, 50), pct(ft, 99), mean,
                 double(C * B) / mean, setup_s, ct.size(), pct(ct, 50), cmean, cmean * double(C), double(B) / cmean, switch_us);
     return 0;
 }

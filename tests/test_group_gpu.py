@@ -307,3 +307,33 @@ def test_group_frame_stable_in_place(neo_gpu, oracle, C):
         assert err.max() <= 1e-5, (f, int(err.argmax()), float(err.max()))
     st = g.stats()
     assert st["coalesced"] and st["frame_steps"] == nf - 3 and st["redos"] == len(late) * (nf - 12), st
+
+
+@pytest.mark.parametrize("C", [16, 520])
+def test_group_frame_in_place(neo_gpu, oracle, C):
+    """NEO_HIP_GROUP_FRAME_INPLACE (register(frame, in_place=True)): the frame's first call writes
+    every member's output into its own block of the frame, and the later members' calls return at
+    once -- the frame equals one C-channel handle over the same blocks after the last call (to float
+    rounding: the group re-primes when it coalesces), with no redo. A member called once on a
+    buffer outside the frame is still stepped exactly (its own block step again)."""
+    B, L, nf = 512, 512 * 100, 14
+    g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 2400 + C)
+    frame = np.zeros((C, B), np.float32)
+    g.register(frame, in_place=True)
+    x = np.stack([oracle.noise(2500 + c, B * nf) for c in range(C)])
+    odd = np.zeros(B, np.float32)
+    for f in range(nf):
+        blk = np.ascontiguousarray(x[:, f * B:(f + 1) * B])
+        expect = ref(blk.copy())
+        frame[:] = blk
+        for c in range(C):
+            if f == 10 and c == 1:  # one call on another buffer: exact, the frame's block 1 is stale
+                odd[:] = blk[c]
+                g(ids[c], odd)
+                frame[c] = odd
+            else:
+                g(ids[c], frame[c])
+        err = np.abs(frame - expect).max(axis=1) / np.maximum(np.abs(expect).max(axis=1), 1e-3)
+        assert err.max() <= 1e-5, (f, int(err.argmax()), float(err.max()))
+    st = g.stats()
+    assert st["coalesced"] and st["redos"] == 1, st
