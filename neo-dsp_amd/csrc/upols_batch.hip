@@ -490,7 +490,7 @@ int launch_offline(upols_t* h, const float* in, int64_t ld_in, float* out, int64
     if (!h->off_y) {
         const size_t rows = size_t(h->C) * kFarT * kOffMaxWP * B;
         if (int rc = dalloc(&h->off_y, rows * sizeof(cf))) return rc;
-        if (dalloc(&h->off_hf, size_t(h->C) * h->off_nseg * 2 * kFarT * B * sizeof(cf)) ||
+        if (dalloc(&h->off_hf, off_hf_bytes(h)) ||
             (h->ola && dalloc(&h->off_tail, rows * sizeof(float)))) {
             dfree(h->off_y);
             dfree(h->off_hf);

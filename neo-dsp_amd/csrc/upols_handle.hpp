@@ -391,6 +391,7 @@ void lvl_filter_changed(upols_t* h);
 // offline windows: the segment spectra (if the filter changed) and k_off_mac for wp windows of
 // 128 blocks at h->wpos into h->off_y (buffers allocated by the caller, launch_offline)
 int launch_off_mac(upols_t* h, int wp, hipStream_t s);
+size_t off_hf_bytes(const upols_t* h);  // the offline windows' segment spectra (padded channel stride)
 // upols_batch.hip: wp windows of 128 blocks of every channel in one pass (window r2c of every
 // block, k_off_mac, per-block finish), h->wpos advanced
 int launch_offline(upols_t* h, const float* in, int64_t ld_in, float* out, int64_t ld_out, int wp, hipStream_t s);

@@ -90,6 +90,18 @@ void plan_levels(int P, level_plan& lp, int far)
 
 constexpr int kFN = 2 * kFarT;  // far level: partition-axis transform length
 
+// Channel strides (complex units) of the level buffers: kPad rows more than the data, so that no
+// channel stride is a multiple of a large power of two -- every channel's row n of a slab, of the
+// far field or of a segment spectrum would otherwise sit at the same offset modulo 512 KB .. 8 MB
+// (an FDL ring of 1280 rows, 5 x 2^20 bytes per channel at B = 512, cost the c5full step 4 %)
+#ifndef NEO_PAD
+#define NEO_PAD 1  // diagnostic builds (A/B): 0 = unpadded strides
+#endif
+constexpr int kPad = NEO_PAD;
+__host__ __device__ constexpr int64_t slab_cs(int T, int B) { return int64_t(T + kPad) * B; }
+__host__ __device__ constexpr int64_t ff_cs(int B) { return int64_t(kFarT + kPad) * B; }
+__host__ __device__ constexpr int64_t spec_cs(int nseg, int B) { return (int64_t(nseg) * kFN + kPad) * B; }
+
 // 256-point transforms of NC columns held by lanes (a, cp), a < 16, cp < NC: on entry
 // v[n2] = x[a + 16 n2], on exit v[k1] = X[16 k1 + a] (16-point DFTs in registers, twiddle,
 // LDS transpose, 16-point DFTs). Every lane of the workgroup calls it (barriers inside);
@@ -145,6 +157,7 @@ struct toep_arg {
     int tw;             // ring row of the window's first block
     int u0, u1, nwg;    // units (16 columns x one of JH window parts) of this slice, workgroups
     int jh;             // window parts per column group (toep_geom)
+    int64_t cs;         // the slab's channel stride (slab_cs)
 };
 
 struct slice_args {
@@ -174,6 +187,7 @@ struct slice_args {
     toep_arg tp[kLvToep];
     // far level (16-column units), common
     int M, nseg, fnfresh, P;
+    int64_t fsc;  // segment / row-pair spectra channel stride (spec_cs; M = nseg slots)
     const cf* hf;
     cf* xf;
     const cf* twf;
@@ -537,7 +551,7 @@ __device__ __forceinline__ void toep_role(const slice_args& sa, const toep_arg& 
         __syncthreads();
     }
     if (wu == 0 && q4 == 0 && live) {
-        cf* o = ta.slab + (int64_t(c) * T + j0) * sa.B + k;
+        cf* o = ta.slab + int64_t(c) * ta.cs + int64_t(j0) * sa.B + k;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
             f2v v = acc[j];
@@ -698,7 +712,7 @@ __device__ __forceinline__ void toep_lds_role(const slice_args& sa, const toep_a
     }
     __syncthreads();
     if (!grp && live) {
-        cf* o = ta.slab + (int64_t(c) * T + jpart + j0) * sa.B + k;
+        cf* o = ta.slab + int64_t(c) * ta.cs + int64_t(jpart + j0) * sa.B + k;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             f2v v = acc[i];
@@ -779,7 +793,7 @@ __device__ __forceinline__ void toep_big_role(const slice_args& sa, const toep_a
     }
     __syncthreads();
     if (!quarter) {
-        cf* o = ta.slab + (int64_t(c) * kBigT + jpart + 4 * quad) * sa.B + k;
+        cf* o = ta.slab + int64_t(c) * ta.cs + int64_t(jpart + 4 * quad) * sa.B + k;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const f2v v = acc[i] + red[ql * 4 + i] + red[(64 + ql) * 4 + i] + red[(128 + ql) * 4 + i];
@@ -876,8 +890,8 @@ __device__ __forceinline__ void far1_mac(const slice_args& sa, int u, int f0, in
     auto slot = [&](int s) { return ((wn - s - 1) % M + M) % M; };
     const int64_t fs = sa.B, sp = int64_t(kFN) * fs;  // one spectrum
     const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;  // first stored segment (1 when K > 1)
-    const cf* hc = sa.hf + int64_t(c) * nseg * sp + int64_t(f0) * fs + k;
-    const cf* xc = sa.xf + int64_t(c) * M * sp + int64_t(f0) * fs + k;
+    const cf* hc = sa.hf + int64_t(c) * sa.fsc + int64_t(f0) * fs + k;
+    const cf* xc = sa.xf + int64_t(c) * sa.fsc + int64_t(f0) * fs + k;
     f2v acc[K][FPL];             // window wn + j
     cf xp[K > 1 ? K - 1 : 1][FPL];  // xp[d]: segment sb - 1 - d's spectra (the previous rounds)
     bool z0[FPL];                // packed bin 0, f = 0 and 128
@@ -973,7 +987,7 @@ __device__ __forceinline__ void far2a_role(const slice_args& sa, int bid, char* 
     tws[t] = sa.twf[t];
     const __amdgpu_buffer_rsrc_t fres =
         buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
-    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * sa.fsc, int64_t(M) * spec);
     const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
     for (int s = 0; s < s0; ++s) {  // uniform per workgroup (one segment in steady state)
         // rows tw - (s + 3) 128 + a + 16 n (the ring holds >= kFarRing > 256 rows: one wrap at most)
@@ -1013,8 +1027,8 @@ __device__ __forceinline__ void far2b_role(const slice_args& sa, int bid, char* 
     const int spec = int(int64_t(kFN) * fs * int(sizeof(cf)));
     const int s0 = sa.fnfresh < nseg ? sa.fnfresh : nseg;
     tws[t] = sa.twf[t];
-    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
-    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * sa.fsc, int64_t(nseg) * spec);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * sa.fsc, int64_t(M) * spec);
     const __amdgpu_buffer_rsrc_t ares =
         buf_rsrc(sa.f2acc + int64_t((sa.f3wn % sa.fK) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
     const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
@@ -1064,7 +1078,7 @@ __device__ __forceinline__ void far2b_role(const slice_args& sa, int bid, char* 
     if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
     col_fft<1, 16>(v, lds, tws, a, cp, true);
     constexpr float sc = 1.0f / kFN;
-    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * kFarT * fs, spec / 2);
+    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * sa.fcs, spec / 2);
 #pragma unroll
     for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128
         buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
@@ -1090,8 +1104,8 @@ __device__ __forceinline__ void far2c_role(const slice_args& sa, int bid, char* 
     tws[t] = sa.twf[t];
     const __amdgpu_buffer_rsrc_t fres =
         buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
-    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * nseg * kFN * fs, int64_t(nseg) * spec);
-    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * M * kFN * fs, int64_t(M) * spec);
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * sa.fsc, int64_t(nseg) * spec);
+    const __amdgpu_buffer_rsrc_t xres = buf_rsrc(sa.xf + int64_t(c) * sa.fsc, int64_t(M) * spec);
     const __amdgpu_buffer_rsrc_t ares =
         buf_rsrc(sa.f2acc + int64_t((sa.f3wn % sa.fK) * sa.fU + u) * kFN * 16, kFN * 16 * int(sizeof(cf)));
     const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
@@ -1154,7 +1168,7 @@ __device__ __forceinline__ void far2c_role(const slice_args& sa, int bid, char* 
     if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
     col_fft<1, 16>(v, lds, tws, a, cp, true);
     constexpr float sc = 1.0f / kFN;
-    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * kFarT * fs, spec / 2);
+    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * sa.fcs, spec / 2);
 #pragma unroll
     for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128
         buf_st(cscale(v[m], sc), ores, vo, int(16 * (m - 8) * fs * int(sizeof(cf))));
@@ -1232,7 +1246,7 @@ __device__ __forceinline__ void far2r_role(const slice_args& sa, int bid, char* 
     if (unit0) bin0_exchange<false>(v, z, a, cp);  // uniform per workgroup
     col_fft<1, 16>(v, lds, tws, a, cp, true);
     constexpr float sc = 1.0f / kFN;
-    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * kFarT * fs, int(kFN * fs * int(sizeof(cf))) / 2);
+    const __amdgpu_buffer_rsrc_t ores = buf_rsrc(sa.f3ff + int64_t(c) * sa.fcs, int(kFN * fs * int(sizeof(cf))) / 2);
     const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
 #pragma unroll
     for (int m = 8; m < 16; ++m)  // n = 16 m + a >= 128
@@ -1261,6 +1275,7 @@ struct off_args {
     const cf* twf;
     cf* y;         // [C][128 WP][B]: the windows' output spectra
     int64_t cstride, pstride;
+    int64_t hcs;   // hf's channel stride (spec_cs)
     int ring, B, nseg, w;  // w: ring row of the pass's first block
 };
 
@@ -1282,7 +1297,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WP == 1 ? 3
     tws[t] = sa.twf[t];
     const __amdgpu_buffer_rsrc_t fres =
         buf_rsrc(sa.fdl + int64_t(c) * sa.cstride, int64_t(sa.ring) * sa.pstride * int(sizeof(cf)));
-    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * sa.nseg * kFN * fs, int64_t(sa.nseg) * spec);
+    const __amdgpu_buffer_rsrc_t hres = buf_rsrc(sa.hf + int64_t(c) * sa.hcs, int64_t(sa.nseg) * spec);
     const int ps8 = int(sa.pstride * int(sizeof(cf))), ko = k * int(sizeof(cf));
     const int vo = int((int64_t(a) * fs + k) * int(sizeof(cf)));
     auto z0 = [&](int i) { return unit0 && cp == 0 && ((a + 16 * i) & (kFN / 2 - 1)) == 0; };
@@ -1612,7 +1627,7 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
 // 256); 0: every segment (offline windows, k_off_mac).
 __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf* __restrict__ hf,
                                                     const cf* __restrict__ twg, int B, int P, int nseg,
-                                                    int64_t cstride, int64_t pstride, int seg0)
+                                                    int64_t cstride, int64_t pstride, int seg0, int64_t hcs)
 {
     __shared__ cf lds[16 * 16 * 16];
     __shared__ cf z[kFN];
@@ -1643,7 +1658,7 @@ __global__ __launch_bounds__(256) void k_lvf_filter(const cf* __restrict__ H, cf
             }
         }
     }
-    cf* dst = hf + (int64_t(c) * nseg + s) * kFN * B + k;
+    cf* dst = hf + int64_t(c) * hcs + int64_t(s) * kFN * B + k;
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) dst[int64_t(16 * k1 + a) * B] = v[k1];
 }
@@ -1738,7 +1753,7 @@ __host__ __device__ inline void persist_far_args(slice_args& a, int64_t n, int w
         a.f3nwg = int(int64_t(q) * U / ns) - a.f3u0;
         a.f3wn = int(W);
         a.f2grp = K > 1;
-        a.f3ff = ff + (W & 1) * int64_t(a.C) * kFarT * a.B;
+        a.f3ff = ff + (W & 1) * int64_t(a.C) * ff_cs(a.B);
         const int64_t t = (int64_t(w) + W * kFarT - n) % a.ring;
         a.f2tw = int(t < 0 ? t + a.ring : t);
         a.f2comb = 1;
@@ -1765,12 +1780,12 @@ static int lvl_buffers(upols_t* h)
         return fail(NEO_HIP_ENOMEM, "level pipeline: allocation of %s (%zu bytes) failed", what, bytes);
     };
     for (int l = 0; l < lp.n; ++l) {
-        const size_t bytes = 2 * C * size_t(lp.T[l]) * B * sizeof(cf);
+        const size_t bytes = 2 * C * size_t(slab_cs(lp.T[l], int(B))) * sizeof(cf);
         if (!alloc(reinterpret_cast<void**>(&h->lv_slab[l]), bytes)) return undo("level slabs", bytes);
     }
     if (lp.nseg) {
-        const size_t spec = C * size_t(lp.nseg) * kFN * B * sizeof(cf);
-        const size_t ffb = 2 * C * kFarT * B * sizeof(cf);
+        const size_t spec = C * size_t(spec_cs(lp.nseg, int(B))) * sizeof(cf);
+        const size_t ffb = 2 * C * size_t(ff_cs(int(B))) * sizeof(cf);
         if (!h->far_raw) {  // the stored form: segment and row-pair spectra, phase 1 -> 2 partial sums
             if (!alloc(reinterpret_cast<void**>(&h->fv_hf), spec)) return undo("far segment spectra", spec);
             if (!alloc(reinterpret_cast<void**>(&h->fv_xf), spec)) return undo("far FDL spectra", spec);
@@ -1858,6 +1873,8 @@ static slice_args base_args(const upols_t* h)
     if (h->lv.nseg) {
         a.M = h->lv.nseg;
         a.nseg = h->lv.nseg;
+        a.fsc = spec_cs(h->lv.nseg, h->B);
+        a.fcs = ff_cs(h->B);
         a.fnfresh = 1;
         a.fU = int(far_units(h));
         a.fK = far_group(h);
@@ -1981,7 +1998,7 @@ static void far_raw_args(const upols_t* h, int64_t W, int q, int w, int64_t n, s
     a.f3u0 = far_cut(h, q);
     a.f3nwg = far_cut(h, q + 1) - a.f3u0;
     a.f3wn = int(W);
-    a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+    a.f3ff = h->fv_ff + (W & 1) * h->C * ff_cs(h->B);
     a.f2tw = ring_add(w, W * kFarT - n, h->ring);
     a.f2comb = 2;
 }
@@ -2195,12 +2212,12 @@ static void block_part(const upols_t* h, int64_t n, int w, int c0, int nc, const
     for (int l = 0; l < lp.n; ++l) {
         const int T = lp.T[l];
         const int64_t m = n + h->lv_phi[l];  // window m / T, its row m mod T
-        a.sl[a.nsl] = h->lv_slab[l] + ((m / T & 1) * C * T + m % T) * B;
-        a.scs[a.nsl++] = int64_t(T) * B;
+        a.sl[a.nsl] = h->lv_slab[l] + (m / T & 1) * C * slab_cs(T, B) + (m % T) * B;
+        a.scs[a.nsl++] = slab_cs(T, B);
     }
     if (lp.nseg) {
-        a.ff = h->fv_ff + ((n / kFarT & 1) * C * kFarT + n % kFarT) * B;
-        a.fcs = int64_t(kFarT) * B;
+        a.ff = h->fv_ff + (n / kFarT & 1) * C * ff_cs(B) + (n % kFarT) * B;
+        a.fcs = ff_cs(B);
     }
 }
 
@@ -2213,7 +2230,8 @@ static void toep_slice(const upols_t* h, int l, int64_t W, int64_t u0, int64_t u
     toep_arg& ta = a.tp[l];  // slot l = level l (the kernel dispatches on it), empty slices allowed
     ta.u0 = int(u0);
     ta.u1 = int(u1);
-    ta.slab = h->lv_slab[l] + (W & 1) * h->C * T * h->B;
+    ta.slab = h->lv_slab[l] + (W & 1) * h->C * slab_cs(T, h->B);
+    ta.cs = slab_cs(T, h->B);
     ta.T = T;
     ta.a = h->lv.a[l];
     ta.b = h->lv.b[l];
@@ -2279,7 +2297,7 @@ static void block_levels(const upols_t* h, int64_t n, int w, slice_args& a)
             a.f3nwg = far_u(U, q, ns) - a.f3u0;
             a.f3wn = int(W);
             a.f2grp = far_group(h) > 1;
-            a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+            a.f3ff = h->fv_ff + (W & 1) * h->C * ff_cs(h->B);
             a.f2tw = ring_add(w, W * kFarT - n, h->ring);
             a.f2comb = 1;
         }
@@ -2297,7 +2315,7 @@ static void block_levels(const upols_t* h, int64_t n, int w, slice_args& a)
         a.f3nwg = far_u(U, q, ns) - a.f3u0;
         a.f3wn = int(W);
         a.f2grp = far_group(h) > 1;
-        a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+        a.f3ff = h->fv_ff + (W & 1) * h->C * ff_cs(h->B);
     }
 }
 
@@ -2333,7 +2351,7 @@ static void slice_part(const upols_t* h, int64_t n0, int w0, slice_args& a)
             a.f3nwg = far_cut(h, q - 1) - a.f3u0;
             a.f3wn = int(W);
             a.f2grp = far_group(h) > 1;
-            a.f3ff = h->fv_ff + (W & 1) * h->C * kFarT * h->B;
+            a.f3ff = h->fv_ff + (W & 1) * h->C * ff_cs(h->B);
             a.f2tw = ring_add(w0, W * kFarT - n0, h->ring);
             a.f2comb = 1;
         }
@@ -2376,22 +2394,22 @@ static int lvl_prime(upols_t* h, hipStream_t s)
     if (lp.nseg && h->fv_dirty && !h->far_raw) {
         const unsigned grid = unsigned(C) * unsigned(lp.nseg) * unsigned(B / 16);
         hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->fv_hf, h->fv_tw, B, h->P, lp.nseg,
-                           h->cstride, h->pstride, kFarA / kFarT);
+                           h->cstride, h->pstride, kFarA / kFarT, spec_cs(lp.nseg, B));
         NEO_HIP_LAUNCH_CHECK();
         h->fv_dirty = false;
     }
     plan_handle_parts(h);  // window offsets and background part sizes (step groups)
     if (h->fdl_zero) {
         for (int l = 0; l < lp.n; ++l)
-            NEO_HIP_CHECK(hipMemsetAsync(h->lv_slab[l], 0, 2 * size_t(C) * lp.T[l] * B * sizeof(cf), s));
+            NEO_HIP_CHECK(hipMemsetAsync(h->lv_slab[l], 0, 2 * size_t(C) * slab_cs(lp.T[l], B) * sizeof(cf), s));
         if (lp.nseg) {
             if (!h->far_raw) {
-                const size_t spec = size_t(C) * size_t(lp.nseg) * kFN * B * sizeof(cf);
+                const size_t spec = size_t(C) * size_t(spec_cs(lp.nseg, B)) * sizeof(cf);
                 NEO_HIP_CHECK(hipMemsetAsync(h->fv_xf, 0, spec, s));
                 const size_t accb = size_t(far_group(h)) * size_t(far_units(h)) * kFN * 16 * sizeof(cf);
                 NEO_HIP_CHECK(hipMemsetAsync(h->fv_acc, 0, accb, s));
             }
-            NEO_HIP_CHECK(hipMemsetAsync(h->fv_ff, 0, 2 * size_t(C) * kFarT * B * sizeof(cf), s));
+            NEO_HIP_CHECK(hipMemsetAsync(h->fv_ff, 0, 2 * size_t(C) * ff_cs(B) * sizeof(cf), s));
         }
         return NEO_HIP_OK;
     }
@@ -2403,6 +2421,7 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         toep_arg& ta = a.tp[a.ntp++];
         ta.jh = JH;
         ta.slab = h->lv_slab[l];
+        ta.cs = slab_cs(lp.T[l], B);
         ta.T = lp.T[l];
         ta.a = lp.a[l];
         ta.b = lp.b[l];
@@ -2413,7 +2432,7 @@ static int lvl_prime(upols_t* h, hipStream_t s)
         if (h->lv_phi[l]) {  // and window 1 whole: its parts before step 0 never ran (the rest run again)
             toep_arg& t1 = f.tp[l];
             t1 = ta;
-            t1.slab = h->lv_slab[l] + size_t(C) * lp.T[l] * B;
+            t1.slab = h->lv_slab[l] + size_t(C) * slab_cs(lp.T[l], B);
             t1.tw = ring_add(w, lp.T[l] - h->lv_phi[l], h->ring);
             f.ntp = l + 1;
             f_any = true;
@@ -2559,6 +2578,8 @@ int launch_levels(upols_t* h, const float* in, int64_t ld_in, float* out, int64_
     return NEO_HIP_OK;
 }
 
+size_t off_hf_bytes(const upols_t* h) { return size_t(h->C) * size_t(spec_cs(h->off_nseg, h->B)) * sizeof(cf); }
+
 int launch_off_mac(upols_t* h, int wp, hipStream_t s)
 {
     if (!h->fv_tw)
@@ -2566,11 +2587,12 @@ int launch_off_mac(upols_t* h, int wp, hipStream_t s)
     if (h->off_dirty) {
         const unsigned grid = unsigned(h->C) * unsigned(h->off_nseg) * unsigned(h->B / 16);
         hipLaunchKernelGGL(k_lvf_filter, dim3(grid), dim3(256), 0, s, h->H, h->off_hf, h->fv_tw, h->B, h->P,
-                           h->off_nseg, h->cstride, h->pstride, 0);
+                           h->off_nseg, h->cstride, h->pstride, 0, spec_cs(h->off_nseg, h->B));
         NEO_HIP_LAUNCH_CHECK();
         h->off_dirty = false;
     }
-    off_args a{h->fdl, h->off_hf, h->fv_tw, h->off_y, h->cstride, h->pstride, h->ring, h->B, h->off_nseg, h->wpos};
+    off_args a{h->fdl, h->off_hf, h->fv_tw, h->off_y, h->cstride, h->pstride, spec_cs(h->off_nseg, h->B), h->ring, h->B,
+               h->off_nseg, h->wpos};
     const unsigned grid = unsigned(h->C) * unsigned(h->B / 16);
     if (wp == 2) hipLaunchKernelGGL(k_off_mac<2>, dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_off_mac<1>, dim3(grid), dim3(256), 0, s, a);
@@ -2637,15 +2659,15 @@ __device__ __forceinline__ void persist_block(const persist_args& pa, int c, cha
         a.nsl = pa.nlev;
         a.ff = nullptr;
         if (pa.far) {  // this block's far-field row (window n / kFarT, complete two steps before)
-            a.ff = pa.ff + (((n / kFarT) & 1) * a.C * kFarT + n % kFarT) * a.B;
-            a.fcs = int64_t(kFarT) * a.B;
+            a.ff = pa.ff + ((n / kFarT) & 1) * a.C * ff_cs(a.B) + (n % kFarT) * a.B;
+            a.fcs = ff_cs(a.B);
         }
 #pragma unroll
         for (int l = 0; l < kLvToep; ++l) {  // static indices: the slice_args stay in registers
             if (l < pa.nlev) {
                 const int T = pa.T[l];
-                a.sl[l] = pa.slab[l] + (((n >> pa.LT[l]) & 1) * a.C * T + (n & (T - 1))) * a.B;
-                a.scs[l] = int64_t(T) * a.B;
+                a.sl[l] = pa.slab[l] + ((n >> pa.LT[l]) & 1) * a.C * slab_cs(T, a.B) + (n & (T - 1)) * a.B;
+                a.scs[l] = slab_cs(T, a.B);
             }
         }
         if (threadIdx.x == 0) {
@@ -2721,7 +2743,8 @@ __device__ __forceinline__ void persist_slices(const persist_args& pa, int s, ch
                 a.nblk = 0;
                 a.ntp = l + 1;
                 toep_arg ta{};
-                ta.slab = pa.slab[l] + ((cur + 1) & 1) * int64_t(a.C) * T * a.B;
+                ta.slab = pa.slab[l] + ((cur + 1) & 1) * int64_t(a.C) * slab_cs(T, a.B);
+                ta.cs = slab_cs(T, a.B);
                 ta.T = T;
                 ta.a = pa.A[l];
                 ta.b = pa.Bd[l];
