@@ -646,8 +646,11 @@ def run_upols(args, world, rank, local):
         import oracle as O
 
         irn = O.normalize_impulse(irh)
-        parity = {"parity_err": oracle_parity(x, y, feed, irn, B, sorted({0, C // 2, C - 1}), threads=args.cpu_threads),
-                  "channels": sorted({0, C // 2, C - 1}), "blocks": 4,
+        # 16 channels spread over the shard (first and last included), every one of them a different
+        # IR, against the oracle over its input history
+        pch = sorted({0, C - 1} | {(C * i) // 16 + i % 7 for i in range(16) if (C * i) // 16 + i % 7 < C})
+        parity = {"parity_err": oracle_parity(x, y, feed, irn, B, pch, threads=args.cpu_threads),
+                  "channels": pch, "blocks": 4,
                   "what": "last 4 blocks of the timed region vs oracle dense_convolve over their input history "
                           "(peak-normalized; bar 1e-5)"}
     det = instrumented()

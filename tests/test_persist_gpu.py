@@ -286,6 +286,23 @@ def test_latency_mode_far_level_channels_relaunch(neo_gpu, oracle):
     pc.set_persistent(False)
 
 
+@pytest.mark.parametrize("C,B,L,nb", [(16, 128, 128 * 700, 420), (16, 512, 480000, 300)])
+def test_latency_mode_far_level_16_channels(neo_gpu, oracle, C, B, L, nb):
+    """The latency mode's largest channel count with the far level: 16 channels (B = 128 with six
+    far segments; the headline's B = 512 and 10 s IR), one call per block through two far windows,
+    against the oracle on four channels and the normal step bit for bit on all 16."""
+    torch = pytest.importorskip("torch")
+    pc, nc, parts = _far_pair(neo_gpu, oracle, C, B, L, 6800 + B)
+    pc.set_persistent(True, idle_ms=200.0)
+    x = np.stack([oracle.noise(6900 + c, B * nb) for c in range(C)])
+    got = _run(pc, x, B, torch)
+    assert pc.persistent_info()["running"]
+    chans = [0, 5, 10, 15]
+    assert peak_err(got[chans], oracle.dense_convolve(x[chans], parts[chans])) <= TOL
+    assert same_sums(got, _run(nc, x, B, torch))
+    pc.set_persistent(False)
+
+
 @pytest.mark.parametrize("L", [2 ** 11, 2 ** 14, 2 ** 17])
 def test_latency_mode_plain_step_b4096(neo_gpu, oracle, L):
     """The reference benchmark's shape (extra/benchmark/src/convolution.cpp:47-55: one channel,
