@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--json", default="")
+    ap.add_argument("--raw", default="", help="save the first 16 samples' records (start, end, role, cu, xcc) to this .npz")
     ap.add_argument("--part", type=int, default=0, help="0 the one-launch step, 1 the step groups' block launch, "
                     "2 their slices launch (sampled once per step group)")
     args = ap.parse_args()
@@ -58,7 +59,8 @@ def main():
     per_xcc = {}
     spans = []
     per_sample = conv.step_group() if args.part == 2 else 1
-    for _ in range(args.steps):
+    raw = {}
+    for it in range(args.steps):
         feed.run(per_sample)
         fn(buf.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(cnt))
         n = int(cnt.value)
@@ -68,6 +70,9 @@ def main():
         en = (r[:, 1] - t0) / 100.0
         role = r[:, 2] & 0xffffffff
         xcc = (r[:, 2] >> 56) & 15
+        if args.raw and it < 16:
+            raw[f"s{it}"] = np.stack([st, en, role.astype(np.float64), ((r[:, 2] >> 32) & 0xffffff).astype(np.float64),
+                                      xcc.astype(np.float64)], axis=1)
         spans.append(en.max())
         for xc in range(8):
             m = xcc == xc
@@ -108,6 +113,8 @@ def main():
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
+    if args.raw:
+        np.savez_compressed(args.raw, **raw)
 
 
 if __name__ == "__main__":
