@@ -597,7 +597,6 @@ void destroy(upols_t* h)
     hfree(h->ps_mb);
     dfree(h->ps_flags);
     dfree(h->ps_tl);
-    dfree(h->sl_ctr);
     for (auto& g : h->events)
         for (auto& e : g.e) (void)hipEventDestroy(e);
     lvl_free(h);  // joins the background stream first

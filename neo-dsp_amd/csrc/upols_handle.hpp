@@ -216,8 +216,6 @@ struct neo_hip_upols {
     hipEvent_t ev_pc[2] = {};
     bool bg_busy = false;  // slices enqueued on bg since the last join
     int64_t bg_launches = 0;
-    unsigned long long* sl_ctr = nullptr;  // the slices launches' task counter (device; k_lvl_slices)
-    unsigned long long sl_ctr_base = 0;    // its value when the next launch starts
     float* tail = nullptr;  // batched OLA tails [C][T][B]
     // offline windows (k_off_mac, launch_offline): batched calls take 128 or 256 blocks per pass
     bool off = false;                // eligible (P >= kOffMinP, whole-block handles) and on (neo_hip_upols_set_offline)

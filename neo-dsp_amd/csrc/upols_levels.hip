@@ -211,12 +211,6 @@ struct slice_args {
     cf* f3ff;     // 2b's target far window [C][128][B]
     void* tl;     // timeline builds (NEO_TIMELINE): per-workgroup records of the launch
     int bid0;     // paced background pieces: the first workgroup of the launch this piece runs
-    // the slices launch's task queue (k_lvl_slices; null: one task per workgroup, blockIdx order):
-    // resident workgroups take tasks qcnt - qbase = 0, 1, ... (the launch's workgroup indices, in
-    // dispatch order) from the handle's counter until qtotal
-    unsigned long long* qctr;
-    unsigned long long qbase;
-    int qtotal;
 };
 
 // the T = 32 Toeplitz level stages its band in LDS: filter rows [64, 256) and the FDL rows
@@ -1460,14 +1454,14 @@ constexpr int step_wpe() { return B > 512 ? 2 : (KMAX == 1 ? NEO_RAW_WPE : NEO_S
 // the roles of one workgroup, in dispatch order (the longest chains first); returns the role
 // (timeline builds: 1 far 2b, 2 far 2a, 3 block, 4 + L Toeplitz level L, 9 far phase 1)
 #ifndef NEO_ORDER
-#define NEO_ORDER 0  // diagnostic builds: 1 far phase 1 before the Toeplitz levels T <= 16, 2 Toeplitz T >= 32 first,
-                     // 4 far phase 1 first of all
+#define NEO_ORDER 0  // diagnostic builds: 1 far phase 1 before the Toeplitz levels T <= 16, 2 Toeplitz T >= 32 first
 #endif
 // PART: 0 every role (one launch per step), 1 the block role alone, 2 every role but the block
 // (step groups: the block of each call and the level slices of G calls in launches of their own)
 template<int B, bool OLA, int KMAX, int PART = 0>
-__device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem, int bid)
+__device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem)
 {
+    int bid = int(blockIdx.x) + a.bid0;
     auto far2b = [&]() {
         if (bid >= a.f3nwg) {
             bid -= a.f3nwg;
@@ -1531,9 +1525,6 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem, int bi
     if (toep(L4{})) return 8;
     if (toep(L3{})) return 7;
 #endif
-#if NEO_ORDER == 4
-    if (far1()) return 9;
-#endif
     if (far2b()) return 1;
     if (far2a()) return 2;
     if (block()) return 3;
@@ -1566,7 +1557,7 @@ __device__ __forceinline__ int lvl_roles(const slice_args& a, char* smem, int bi
     if (toep(L2{})) return 6;
     if (toep(L1{})) return 5;
     if (toep(L0{})) return 4;
-#if NEO_ORDER != 1 && NEO_ORDER != 4
+#if NEO_ORDER != 1
     if (far1()) return 9;
 #endif
     return 0;
@@ -1587,14 +1578,14 @@ constexpr int block_lds() { return (B + upols_cfg<B>::LL + upols_cfg<B>::TW1 + u
 #endif
 #ifdef NEO_TIMELINE  // diagnostic builds: per-workgroup start / end (100 MHz clock) and role
 template<int WG, class F>
-__device__ __forceinline__ void tl_record(const slice_args& a, F roles, int64_t idx = blockIdx.x)
+__device__ __forceinline__ void tl_record(const slice_args& a, F roles)
 {
     const unsigned long long t0 = wall_clock64();
     const int role = roles();
     if constexpr (WG > 256) return;  // lanes past 256 leave the roles early: no final barrier
     __syncthreads();
     if (threadIdx.x == 0 && a.tl) {
-        unsigned long long* r = static_cast<unsigned long long*>(a.tl) + 4 * idx;
+        unsigned long long* r = static_cast<unsigned long long*>(a.tl) + 4 * int64_t(blockIdx.x);
         r[0] = t0;
         r[1] = wall_clock64();
         const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15;  // HW_REG_XCC_ID
@@ -1611,7 +1602,7 @@ __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_e
 {
     __shared__ __attribute__((aligned(16))) char smem[block_lds<B>()];
     if constexpr (NEO_BLOCK_PRIO > 0) __builtin_amdgcn_s_setprio(NEO_BLOCK_PRIO);
-    NEO_TL_ROLES(lstep_cfg<B>::WG, (lvl_roles<B, OLA, 2, 1>(a, smem, int(blockIdx.x) + a.bid0)));
+    NEO_TL_ROLES(lstep_cfg<B>::WG, (lvl_roles<B, OLA, 2, 1>(a, smem)));
 }
 
 // step groups: every role but the block for the slices of G steps (the background stream);
@@ -1620,33 +1611,14 @@ template<int KMAX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(slices_wpe<KMAX>()))) void k_lvl_slices(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
-    if (!a.qctr) {
-        NEO_TL_ROLES(256, (lvl_roles<512, false, KMAX, 2>(a, smem, int(blockIdx.x) + a.bid0)));
-        return;
-    }
-    // task queue: a resident workgroup runs task after task (the roles' workgroups in their
-    // dispatch order, longest chains first), so short tasks never wait for the dispatcher and
-    // the launch's last tasks spread over every workgroup still running
-    __shared__ int qbid;
-    for (;;) {
-        if (threadIdx.x == 0) qbid = int(atomicAdd(a.qctr, 1ull) - a.qbase);
-        __syncthreads();
-        const int bid = qbid;
-        __syncthreads();  // every lane has read qbid, and the previous task's LDS use is done
-        if (bid >= a.qtotal) break;
-#ifdef NEO_TIMELINE
-        tl_record<256>(a, [&] { return lvl_roles<512, false, KMAX, 2>(a, smem, bid + a.bid0); }, bid);
-#else
-        (void)lvl_roles<512, false, KMAX, 2>(a, smem, bid + a.bid0);
-#endif
-    }
+    NEO_TL_ROLES(256, (lvl_roles<512, false, KMAX, 2>(a, smem)));
 }
 
 template<int B, bool OLA, int KMAX>
 __global__ __launch_bounds__(lstep_cfg<B>::WG) __attribute__((amdgpu_waves_per_eu(step_wpe<B, KMAX>()))) void k_lvl_step(slice_args a)
 {
     __shared__ __attribute__((aligned(16))) char smem[kSliceLds];
-    NEO_TL_ROLES(lstep_cfg<B>::WG, (lvl_roles<B, OLA, KMAX>(a, smem, int(blockIdx.x) + a.bid0)));
+    NEO_TL_ROLES(lstep_cfg<B>::WG, (lvl_roles<B, OLA, KMAX>(a, smem)));
 }
 
 // Segment spectra (grid C x NSEG x B/16): hf[c][s][f][k] = DFT256 over r < 128 of
@@ -1929,9 +1901,6 @@ static unsigned launch_grid(const slice_args& a)
     return t;
 }
 
-#ifndef NEO_SLICE_QUEUE
-#define NEO_SLICE_QUEUE 0  // workgroups per CU of the slices launches' task queue (0: off)
-#endif
 // kernel of a launch: part 0 the step kernel (every role), 1 the block alone, 2 the slices alone
 static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStream_t s, int part = 0,
                               int piece = 0, int pieces = 1)
@@ -1977,23 +1946,9 @@ static int launch_step_kernel(const upols_t* h, const slice_args& a_in, hipStrea
 #else
         const unsigned pad = h->bg_pad;
 #endif
-        // task queue (NEO_SLICE_QUEUE workgroups per CU, resident; 0: one workgroup per task)
-        unsigned qgrid = grid;
-        if (NEO_SLICE_QUEUE > 0 && h->sl_ctr) {
-            static int cus = 0;
-            if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) {
-                (void)hipGetLastError();
-                cus = 256;
-            }
-            a.qctr = h->sl_ctr;
-            a.qbase = h->sl_ctr_base;
-            a.qtotal = int(grid);
-            qgrid = std::min(grid, unsigned(NEO_SLICE_QUEUE * cus));
-            const_cast<upols_t*>(h)->sl_ctr_base += grid + qgrid;  // every task, then one failed fetch per workgroup
-        }
-        if (raw) hipLaunchKernelGGL((k_lvl_slices<1>), dim3(qgrid), dim3(256), pad, s, a);
-        else if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(qgrid), dim3(256), pad, s, a);
-        else hipLaunchKernelGGL((k_lvl_slices<kFarKMax>), dim3(qgrid), dim3(256), pad, s, a);
+        if (raw) hipLaunchKernelGGL((k_lvl_slices<1>), dim3(grid), dim3(256), pad, s, a);
+        else if (pairs) hipLaunchKernelGGL((k_lvl_slices<2>), dim3(grid), dim3(256), pad, s, a);
+        else hipLaunchKernelGGL((k_lvl_slices<kFarKMax>), dim3(grid), dim3(256), pad, s, a);
     } else {
 #define NEO_LVL(OL, KM)                                                                                        \
     NEO_UPOLS_DISPATCH(h->B, if constexpr (BB <= 1024) hipLaunchKernelGGL((k_lvl_step<BB, OL, KM>), dim3(grid), \
@@ -2517,12 +2472,6 @@ static int lvl_prime(upols_t* h, hipStream_t s)
 static int group_streams(upols_t* h)
 {
     if (h->bg) return NEO_HIP_OK;
-    if (NEO_SLICE_QUEUE > 0 && !h->sl_ctr) {  // the slices launches' task counter (monotonic: sl_ctr_base)
-        if (int rc = dalloc(&h->sl_ctr, sizeof(unsigned long long))) return rc;
-        NEO_HIP_CHECK(hipMemsetAsync(h->sl_ctr, 0, sizeof(unsigned long long), h->stream));
-        NEO_HIP_CHECK(hipStreamSynchronize(h->stream));
-        h->sl_ctr_base = 0;
-    }
     int lo = 0, hi = 0;
     NEO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
 #ifdef NEO_BG_PRIO_NORMAL  // diagnostic builds (A/B): the background stream at the default priority
