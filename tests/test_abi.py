@@ -5,6 +5,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -94,3 +95,30 @@ def test_rfftfreq_reference_values():
     assert neo.fft.rfftfreq(2) == pytest.approx([0.0, 0.5])
     assert neo.fft.rfftfreq(2, 1.0 / 20.0) == pytest.approx([0.0, 10.0])
     assert neo.fft.rfftfreq(2, 1.0 / 44100.0) == pytest.approx([0.0, 22050.0])
+
+
+def test_hot_kernels_do_not_spill():
+    """Register spills of the built kernels, read from libneo_hip.so's code objects
+    (tools/spill_check.py, no GPU): the streaming step's kernels, the plain step, the offline
+    windows, the FFT and the latency-mode kernels spill nothing. Only the flat-load batched-MAC
+    fallback (variant 0, used where buffer loads are not available) and the one-window offline
+    pass may; a second inlined copy of the slice roles once made k_lvl_slices spill 104 VGPRs
+    (-12 % at c5full, profiles/r6_ab_slice_queue.json)."""
+    import shutil
+
+    if not shutil.which("/opt/rocm/lib/llvm/bin/llvm-readelf"):
+        pytest.skip("llvm tools not available")
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import spill_check
+
+    k = spill_check.kernels(os.path.join(REPO, "neo-dsp_amd", "lib", "libneo_hip.so"))
+    assert len(k) > 100
+    hot = [n for n in k if any(s in n for s in ("k_lvl_slices", "k_lvl_block", "k_lvl_step", "k_lvl_persist",
+                                                  "k_plain_persist", "k_upols_step", "k_off_macILi2", "k_c2c_lds",
+                                                  "k_lvf_filter", "k_batch_window", "k_batch_finish"))]
+    assert len(hot) > 50
+    bad = {n: k[n] for n in hot if k[n]["vgpr_spill"] or k[n]["scratch"]}
+    assert not bad, bad
+    allowed = ("k_batch_macILi", "k_off_macILi1")
+    other = {n: v for n, v in k.items() if (v["vgpr_spill"] or v["scratch"]) and not any(a in n for a in allowed)}
+    assert not other, other
