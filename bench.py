@@ -982,7 +982,8 @@ def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world, C_total):
     conv.set_batch(True)
     T, splits = conv.batch_info()
     off, nseg = conv.offline_info()
-    nb = 256
+    nb = min(256, ld // B)  # the input buffer's blocks (ref4096: P + 192 = 224)
+    off = off and nb >= 128
     conv.reset()
     t_warm = time.perf_counter()
     while time.perf_counter() - t_warm < WARM_SECONDS:
@@ -1003,7 +1004,7 @@ def run_upols_offline(args, conv, C, B, P, x, y, ld, stream, world, C_total):
     elapsed = max_over_ranks(t1 - t0, world)
     mac_avg_ms = max_over_ranks(mac_ms / max(launches, 1), world)
     if off:
-        wp = 2
+        wp = 2 if nb >= 256 else 1
         # per column and pass: (nseg + wp) 128 FDL rows, nseg 256-row segment spectra, wp 128 output rows
         bytes_pass = C * B * 8 * ((nseg + wp) * 128 + nseg * 256 + wp * 128)
         kernel, per_pass, pmc = f"k_off_mac<{wp}>", wp * 128, "k_off_mac"
