@@ -396,6 +396,22 @@ inline void prefetch_output(const group_t* g, int slot)
     for (size_t k = 0; k < size_t(g->B) * sizeof(float); k += 64) __builtin_prefetch(p + k, 0, 3);
 }
 
+// the block a later member's commit writes (its buffer of the last frame): in this core's cache,
+// writable, ahead of the copy. A frame read in place by the step without the leader's snapshot
+// (FRAME_STABLE) leaves those lines cold: the GPU's reads over PCIe took them out of the caches
+// (the probe build's member copy 0.13 -> 0.03 us at 2048 channels, frame p50 355-363 vs 345-468 us
+// over three same-box runs; 2 and 8 members ahead no better: profiles/r6_ab_group_prefetch.json)
+#ifndef NEO_GROUP_PFW
+#define NEO_GROUP_PFW 4
+#endif
+inline void prefetch_block(const group_t* g, int slot)
+{
+    if (slot >= int(g->slot_member.size())) return;
+    const char* q = reinterpret_cast<const char*>(g->m[size_t(g->slot_member[size_t(slot)])].io_last);
+    if (q)
+        for (size_t k = 0; k < size_t(g->B) * sizeof(float); k += 64) __builtin_prefetch(q + k, 1, 3);
+}
+
 // coalesced mode: the leader's step over every member, or a later member's commit / redo
 int call_coalesced(group_t* g, int i, float* io)
 {
@@ -433,6 +449,7 @@ int call_coalesced(group_t* g, int i, float* io)
         std::memcpy(io, out, bb);
         NEO_GP_ADD(6, tm);
         prefetch_output(g, x.slot + 2);
+        if (g->trust) prefetch_block(g, x.slot + NEO_GROUP_PFW);
         x.pending = false;
         x.io_last = io;
         --g->npending;
@@ -489,6 +506,8 @@ int call_coalesced(group_t* g, int i, float* io)
     NEO_GP_ADD(4, t4);
     prefetch_output(g, x.slot + 1);  // the next members' outputs, written over PCIe: not in any CPU cache
     prefetch_output(g, x.slot + 2);
+    if (g->trust && !g->out_inplace)
+        for (int k = 1; k <= NEO_GROUP_PFW; ++k) prefetch_block(g, x.slot + k);
     x.io_last = io;
     for (auto& y : g->m) {
         if (!y.live) continue;
