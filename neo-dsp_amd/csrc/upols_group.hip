@@ -427,11 +427,12 @@ int call_coalesced(group_t* g, int i, float* io)
         float* spec_in = g->in_pin + int64_t(x.slot) * g->B;
         float* out = g->out_pin + int64_t(x.slot) * g->B;
         NEO_GP_T(tc);
-        // a stable frame (the owner's promise, neo_hip_upols_group_register_ex): the block is the
-        // one the leader's step read in place, no snapshot to compare with
-        // (FRAME_INPLACE with another buffer than the frame's: its block was never read, and the
-        // output went to the old one -- the owner broke the promise; this call is still exact)
-        const bool differs = g->out_inplace || (!g->trust && std::memcmp(io, spec_in, bb) != 0);
+        // a stable frame (the owner's promise, neo_hip_upols_group_register_ex): on the buffer the
+        // leader's step read in place, the block is the one it read (no snapshot to compare with);
+        // on another buffer its block was never read: this channel's step again (FRAME_INPLACE: the
+        // output went to the old buffer -- the owner broke the promise; this call is still exact)
+        const bool differs =
+            g->out_inplace || (g->trust ? io != x.io_last : std::memcmp(io, spec_in, bb) != 0);
         NEO_GP_ADD(5, tc);
         if (differs) {  // the caller's block differs: this channel's step again
             neo_hip::device_guard dg(g->device);  // the commit path alone makes no HIP call

@@ -337,3 +337,33 @@ def test_group_frame_in_place(neo_gpu, oracle, C):
         assert err.max() <= 1e-5, (f, int(err.argmax()), float(err.max()))
     st = g.stats()
     assert st["coalesced"] and st["redos"] == 1, st
+
+
+def test_group_frame_stable_foreign_buffer(neo_gpu, oracle):
+    """Under the frame-stable promise the members skip the comparison only on the buffer the
+    leader's step read in place: a member called once on another buffer, holding another block than
+    its frame block, is stepped again on that block (exact), and the frame's own block is left as it
+    was."""
+    C, B, L, nf = 12, 512, 512 * 100, 12
+    g, ids, parts, ref = _setup(neo_gpu, oracle, C, B, L, 2700)
+    frame = np.zeros((C, B), np.float32)
+    g.register(frame, frame_stable=True)
+    x = np.stack([oracle.noise(2800 + c, B * nf) for c in range(C)])
+    odd = np.zeros(B, np.float32)
+    for f in range(nf):
+        blk = np.ascontiguousarray(x[:, f * B:(f + 1) * B])
+        expect = ref(blk.copy())
+        frame[:] = blk
+        if f == 8:
+            frame[2] = 0.0  # the leader reads zeros for member 2; its call brings the real block
+        for c in range(C):
+            if f == 8 and c == 2:
+                odd[:] = blk[c]
+                g(ids[c], odd)
+                frame[c] = odd
+            else:
+                g(ids[c], frame[c])
+        err = np.abs(frame - expect).max(axis=1) / np.maximum(np.abs(expect).max(axis=1), 1e-3)
+        assert err.max() <= 1e-5, (f, int(err.argmax()), float(err.max()))
+    st = g.stats()
+    assert st["coalesced"] and st["redos"] == 1, st
