@@ -324,7 +324,8 @@ NEO_HIP_API int neo_hip_upols_group_register(neo_hip_upols_group* g, const void*
  * (from its first member call until every member has made its call) nothing but those calls writes
  * the range, as in the plugin's loop over the channels of a filled frame (DenseConvolution.cpp:62-74).
  * A frame read in place from such a range then skips the leader's snapshot of every member's block
- * and the members' comparisons with it: a member's call is the copy of its output. Without the flag
+ * and the members' comparisons with it: a member's call on the buffer the step read is the copy of
+ * its output (a call on another buffer re-runs that member's block step, exact). Without the flag
  * (register) each member's block is compared exactly and re-stepped on a difference. Registering the
  * same range again updates its flags. */
 #define NEO_HIP_GROUP_FRAME_STABLE 1
